@@ -1,0 +1,166 @@
+#!/usr/bin/env python3
+"""Headline benchmark: end-to-end RAG QPS + p50 latency, Llama-3-8B + arctic-embed-l,
+1M-doc index (BASELINE.json ``metric``).
+
+One rank per GPU (``torch.distributed.run``; RCCL for the barrier / max-reduce of the
+timing). Each rank is a full serving replica (data parallel, SURVEY.md §2.E "DP (data /
+replica)", CC9): Llama-3-8B engine + arctic-embed-l encoder + a 1M x 1024 in-HBM flat index
+(2 GB, replicated: cheaper than any per-query collective at this size).
+
+A *step* serves one wave of ``--concurrency`` RAG requests end to end, all inside the timed
+region: query embedding (encoder forward), top-4 cosine search over the 1M-vector index,
+1500-token context cap, prompt assembly with the reference ``rag_template`` + Llama-3 chat
+template, continuous-batched prefill + decode of ``--max-tokens`` tokens (EOS ignored so
+every request does the same work), streaming detokenisation.
+
+Weights are random-init of the real architectures; the corpus is synthetic (index vectors
+are random unit vectors standing in for arctic-embed-l passage embeddings; chunk texts are
+generated prose of ~500 tokens). ``value`` is the whole-job QPS (all ranks).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--concurrency", type=int, default=64, help="requests per rank per step")
+    ap.add_argument("--max-tokens", type=int, default=256)
+    ap.add_argument("--index-size", type=int, default=1_000_000)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--embed-model", default="arctic-embed-l")
+    ap.add_argument("--top-k", type=int, default=4)
+    ap.add_argument("--max-batched-tokens", type=int, default=32768)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
+    ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    from nv_genai_amd.engine.embed_engine import EmbeddingEngine
+    from nv_genai_amd.engine.llm_engine import EngineConfig, LLMEngine, SamplingParams
+    from nv_genai_amd.index.docstore import SyntheticDocStore
+    from nv_genai_amd.index.flat import FlatIndex
+    from nv_genai_amd.parallel import dist as pd
+    from nv_genai_amd.rag.pipeline import RAGPipeline
+    from nv_genai_amd.utils.synthetic import TextGen
+
+    pctx = pd.init_distributed(tp_size=1)
+    world, rank = pctx.world_size, pctx.rank
+    dev = str(pctx.device)
+    gpu = pctx.device.type == "cuda"
+    t_setup = time.time()
+    R = args.concurrency
+    # graphs for the padded decode batch sizes this run can see
+    sizes = tuple(b for b in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256) if b <= R) or (1,)
+    if sizes[-1] < R:
+        sizes = sizes + (R,)
+    ecfg = EngineConfig(model=args.model, max_num_seqs=max(R, 1), max_batched_tokens=args.max_batched_tokens,
+                        max_model_len=8192, use_graphs=gpu and not args.no_graphs,
+                        graph_batch_sizes=sizes, seed=rank, kv_cache_fraction=0.3)
+    llm = LLMEngine(ecfg, device=dev, pctx=pctx)
+    emb = EmbeddingEngine(args.embed_model, device=dev, seed=rank)
+    index = FlatIndex(emb.dim, "cosine", dev, capacity=args.index_size)
+    index.add_random(args.index_size, seed=1234)
+    docs = SyntheticDocStore(args.index_size)
+    rag = RAGPipeline(llm, emb, index, docs, top_k=args.top_k)
+    gen = TextGen(seed=100 + rank)
+    params = SamplingParams(temperature=0.2, top_p=0.7, max_tokens=args.max_tokens, ignore_eos=True)
+    if gpu:
+        torch.cuda.synchronize()
+    setup_s = time.time() - t_setup
+
+    def one_step():
+        qs = [gen.question() for _ in range(R)]
+        return rag.run(qs, params)
+
+    for _ in range(args.warmup):
+        one_step()
+    pd.barrier()
+    if gpu:
+        torch.cuda.synchronize()
+    prof = None
+    if args.profile_dir and rank == 0:
+        from torch.profiler import ProfilerActivity, profile
+
+        prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA])
+        prof.__enter__()
+    llm.stats.update({k: 0 if isinstance(v, int) else 0.0 for k, v in llm.stats.items()})
+    t0 = time.perf_counter()
+    results = []
+    for _ in range(args.steps):
+        results += one_step()
+    if gpu:
+        torch.cuda.synchronize()
+    pd.barrier()
+    elapsed = time.perf_counter() - t0
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        os.makedirs(args.profile_dir, exist_ok=True)
+        prof.export_chrome_trace(os.path.join(args.profile_dir, "trace.json"))
+        with open(os.path.join(args.profile_dir, "top_kernels.txt"), "w") as f:
+            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40))
+    t_max = pd.all_reduce_max(elapsed)
+    n_req = R * args.steps * world
+    qps = n_req / t_max
+    lat = sorted(r.latency for r in results)
+    ttft = sorted(r.ttft for r in results)
+    ptoks = [r.prompt_tokens for r in results]
+    out_tok = sum(len(r.request.output_ids) for r in results) * world
+    p50 = statistics.median(lat)
+    p95 = lat[min(len(lat) - 1, int(0.95 * len(lat)))]
+    line = {
+        "metric": "end-to-end RAG QPS + p50 latency, Llama-3-8B + arctic-embed-l, 1M-doc index",
+        "value": round(qps, 4),
+        "unit": "requests/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * t_max / args.steps, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic: random-init weights; 1M random unit-vector index + generated ~500-token chunks; generated questions",
+        "config": {
+            "model": f"{args.model} + {args.embed_model}",
+            "global_batch": R * world,
+            "seq_len": int(statistics.mean(ptoks)) + args.max_tokens,
+            "parallelism": f"dp{world}",
+            "index_size": args.index_size,
+            "top_k": args.top_k,
+            "max_tokens": args.max_tokens,
+            "concurrency_per_gpu": R,
+        },
+        "p50_latency_ms": round(1000 * p50, 1),
+        "p95_latency_ms": round(1000 * p95, 1),
+        "p50_ttft_ms": round(1000 * statistics.median(ttft), 1),
+        "mean_prompt_tokens": round(statistics.mean(ptoks), 1),
+        "output_tokens_per_s": round(out_tok / t_max, 1),
+        "prefill_s": round(llm.stats["prefill_time"], 3),
+        "decode_s": round(llm.stats["decode_time"], 3),
+        "setup_s": round(setup_s, 1),
+    }
+    if rank == 0:
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(s + "\n")
+    pd.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,301 @@
+// PyTorch bindings for the gfx950 kernels (nv_genai_amd._C).
+// Every entry point validates dtype / device / shape / contiguity against what its kernel
+// and launch grid assume before launching (a malformed launch on the GPU box can fault the
+// device), and launches on PyTorch's current HIP stream so calls are hipGraph-capturable.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include "kernels/kernels.h"
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream(const Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+#define CHECK_DEV(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define CHECK_DT(x, dt) TORCH_CHECK((x).scalar_type() == (dt), #x " must be " #dt)
+#define CHECK_BF16(x) \
+  CHECK_DEV(x);       \
+  CHECK_DT(x, at::kBFloat16)
+
+uint16_t* bfp(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+const uint16_t* cbfp(const c10::optional<Tensor>& t) {
+  return t.has_value() ? reinterpret_cast<const uint16_t*>(t->data_ptr()) : nullptr;
+}
+
+// ------------------------------------------------------------------ norms / activations
+void rmsnorm(Tensor out, Tensor x, Tensor w, double eps) {
+  CHECK_BF16(out); CHECK_BF16(x); CHECK_BF16(w);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2, "rmsnorm expects 2-D [rows, H]");
+  const int H = (int)x.size(1);
+  TORCH_CHECK(H % 8 == 0 && H <= 8192, "rmsnorm: H must be a multiple of 8 and <= 8192");
+  TORCH_CHECK(x.stride(1) == 1 && out.stride(1) == 1 && w.numel() == H && w.is_contiguous());
+  TORCH_CHECK(out.size(0) == x.size(0) && out.size(1) == H);
+  TORCH_CHECK(x.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "rmsnorm: row strides must be 16-B aligned");
+  nga::launch_rmsnorm(bfp(out), bfp(x), nullptr, bfp(w), (float)eps, x.size(0), H, x.stride(0),
+                      out.stride(0), cur_stream(x));
+}
+
+// resid += delta; out = rmsnorm(resid) * w
+void add_rmsnorm(Tensor out, Tensor resid, Tensor delta, Tensor w, double eps) {
+  CHECK_BF16(out); CHECK_BF16(resid); CHECK_BF16(delta); CHECK_BF16(w);
+  CHECK_CONTIG(resid); CHECK_CONTIG(delta); CHECK_CONTIG(out);
+  TORCH_CHECK(resid.dim() == 2 && resid.sizes() == delta.sizes() && resid.sizes() == out.sizes());
+  const int H = (int)resid.size(1);
+  TORCH_CHECK(H % 8 == 0 && H <= 8192 && w.numel() == H);
+  nga::launch_rmsnorm(bfp(out), bfp(resid), bfp(delta), bfp(w), (float)eps, resid.size(0), H, H, H,
+                      cur_stream(resid));
+}
+
+void layernorm(Tensor out, Tensor x, c10::optional<Tensor> resid, Tensor g, Tensor b, double eps) {
+  CHECK_BF16(out); CHECK_BF16(x); CHECK_BF16(g); CHECK_BF16(b);
+  CHECK_CONTIG(out); CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 2 && out.sizes() == x.sizes());
+  const int H = (int)x.size(1);
+  TORCH_CHECK(H % 8 == 0 && H <= 8192 && g.numel() == H && b.numel() == H);
+  if (resid.has_value()) {
+    CHECK_BF16(*resid); CHECK_CONTIG(*resid);
+    TORCH_CHECK(resid->sizes() == x.sizes());
+  }
+  nga::launch_layernorm(bfp(out), bfp(x), cbfp(resid), bfp(g), bfp(b), (float)eps, x.size(0), H,
+                        cur_stream(x));
+}
+
+void silu_mul(Tensor out, Tensor x) {
+  CHECK_BF16(out); CHECK_BF16(x); CHECK_CONTIG(out); CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.size(1) == 2 * out.size(1) && x.size(0) == out.size(0));
+  TORCH_CHECK(out.size(1) % 8 == 0);
+  nga::launch_silu_mul(bfp(out), bfp(x), x.size(0), (int)out.size(1), cur_stream(x));
+}
+
+void bias_gelu(Tensor x, c10::optional<Tensor> bias) {
+  CHECK_BF16(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 8 == 0);
+  if (bias.has_value()) {
+    CHECK_BF16(*bias);
+    TORCH_CHECK(bias->numel() == x.size(1));
+  }
+  nga::launch_bias_gelu(bfp(x), cbfp(bias), x.size(0), (int)x.size(1), cur_stream(x));
+}
+
+// ------------------------------------------------------------------ rope + kv cache
+void rope_cache(Tensor qkv, Tensor pos, Tensor cos_sin, c10::optional<Tensor> slots,
+                c10::optional<Tensor> kc, c10::optional<Tensor> vc, int64_t Hq, int64_t Hkv,
+                int64_t D) {
+  CHECK_BF16(qkv); CHECK_CONTIG(qkv);
+  CHECK_DEV(pos); CHECK_DT(pos, at::kInt);
+  CHECK_DEV(cos_sin); CHECK_DT(cos_sin, at::kFloat); CHECK_CONTIG(cos_sin);
+  TORCH_CHECK(D == 128 || D == 64, "rope_cache: head_dim must be 64 or 128");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == (Hq + 2 * Hkv) * D, "rope_cache: qkv must be [T, (Hq+2Hkv)*D]");
+  TORCH_CHECK(pos.numel() == qkv.size(0));
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D);
+  int BS = 64;
+  const int32_t* sp = nullptr;
+  uint16_t *kp = nullptr, *vp = nullptr;
+  if (slots.has_value()) {
+    TORCH_CHECK(kc.has_value() && vc.has_value());
+    CHECK_DEV(*slots); CHECK_DT(*slots, at::kInt);
+    TORCH_CHECK(slots->numel() == qkv.size(0));
+    CHECK_BF16(*kc); CHECK_BF16(*vc); CHECK_CONTIG(*kc); CHECK_CONTIG(*vc);
+    TORCH_CHECK(kc->dim() == 4 && kc->size(1) == Hkv && kc->size(3) == D, "k cache must be [nb, Hkv, BS, D]");
+    TORCH_CHECK(vc->dim() == 4 && vc->size(1) == Hkv && vc->size(2) == D, "v cache must be [nb, Hkv, D, BS]");
+    BS = (int)kc->size(2);
+    TORCH_CHECK(vc->size(3) == BS && kc->size(0) == vc->size(0));
+    sp = slots->data_ptr<int32_t>();
+    kp = bfp(*kc);
+    vp = bfp(*vc);
+  }
+  nga::launch_rope_cache(bfp(qkv), pos.data_ptr<int32_t>(), cos_sin.data_ptr<float>(), sp, kp, vp,
+                         qkv.size(0), (int)Hq, (int)Hkv, (int)D, BS, cur_stream(qkv));
+}
+
+// ------------------------------------------------------------------ attention
+int64_t decode_pages_per_part(int64_t num_seqs, int64_t Hkv, int64_t max_ctx) {
+  return nga::decode_attn_pages_per_part((int)num_seqs, (int)Hkv, (int)max_ctx);
+}
+
+void decode_attention(Tensor out, Tensor q, Tensor kc, Tensor vc, Tensor block_tables,
+                      Tensor ctx_lens, int64_t Hq, int64_t Hkv, int64_t max_ctx, double scale,
+                      int64_t pages_per_part, Tensor part_ml, Tensor part_o) {
+  CHECK_BF16(out); CHECK_BF16(q); CHECK_BF16(kc); CHECK_BF16(vc);
+  CHECK_CONTIG(kc); CHECK_CONTIG(vc);
+  CHECK_DEV(block_tables); CHECK_DT(block_tables, at::kInt); CHECK_CONTIG(block_tables);
+  CHECK_DEV(ctx_lens); CHECK_DT(ctx_lens, at::kInt);
+  const int64_t B = ctx_lens.numel();
+  TORCH_CHECK(q.dim() == 2 && q.size(0) >= B && q.stride(1) == 1 && q.size(1) >= Hq * 128,
+              "decode_attention: q must be [B, >=Hq*128] with unit inner stride");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) >= B && out.stride(1) == 1 && out.size(1) >= Hq * 128);
+  TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(2) == 64 && kc.size(3) == 128,
+              "decode_attention: k cache must be [nb, Hkv, 64, 128]");
+  TORCH_CHECK(vc.sizes() == at::IntArrayRef({kc.size(0), Hkv, 128, 64}), "v cache must be [nb, Hkv, 128, 64]");
+  TORCH_CHECK(Hq % Hkv == 0 && Hq / Hkv <= 16, "decode_attention: G = Hq/Hkv must be <= 16");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B);
+  TORCH_CHECK(block_tables.size(1) * 64 >= max_ctx, "block table too narrow for max_ctx");
+  TORCH_CHECK(pages_per_part >= 1);
+  const int64_t pages = (max_ctx + 63) / 64;
+  const int64_t nparts = (pages + pages_per_part - 1) / pages_per_part;
+  if (nparts > 1) {
+    CHECK_DEV(part_ml); CHECK_DEV(part_o);
+    TORCH_CHECK(part_ml.numel() >= B * Hq * nparts * 2 && part_o.numel() >= B * Hq * nparts * 128,
+                "decode_attention: partition workspace too small");
+  }
+  nga::launch_decode_attention(bfp(out), out.stride(0), bfp(q), q.stride(0), bfp(kc), bfp(vc),
+                               block_tables.data_ptr<int32_t>(), (int)block_tables.size(1),
+                               ctx_lens.data_ptr<int32_t>(), (int)B, (int)Hq, (int)Hkv,
+                               (int)max_ctx, (float)scale, (int)pages_per_part,
+                               nparts > 1 ? part_ml.data_ptr<float>() : nullptr,
+                               nparts > 1 ? part_o.data_ptr<float>() : nullptr, cur_stream(q));
+}
+
+void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optional<Tensor> v,
+                       c10::optional<Tensor> kc, c10::optional<Tensor> vc,
+                       c10::optional<Tensor> block_tables, Tensor cu_q,
+                       c10::optional<Tensor> ctx_lens, int64_t Hq, int64_t Hkv, int64_t D,
+                       int64_t max_q_len, double scale, bool causal) {
+  CHECK_BF16(out); CHECK_BF16(q);
+  CHECK_DEV(cu_q); CHECK_DT(cu_q, at::kInt); CHECK_CONTIG(cu_q);
+  TORCH_CHECK(D == 64 || D == 128);
+  TORCH_CHECK(Hq % Hkv == 0);
+  TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1 && q.size(1) >= Hq * D && q.stride(0) % 8 == 0);
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) >= Hq * D && out.size(0) == q.size(0));
+  const int64_t B = cu_q.numel() - 1;
+  nga::PrefillParams p{};
+  p.out = bfp(out);
+  p.out_stride = out.stride(0);
+  p.q = bfp(q);
+  p.q_stride = q.stride(0);
+  p.cu_q = cu_q.data_ptr<int32_t>();
+  p.Hq = (int)Hq;
+  p.Hkv = (int)Hkv;
+  p.scale = (float)scale;
+  const bool paged = kc.has_value();
+  if (paged) {
+    TORCH_CHECK(vc.has_value() && block_tables.has_value() && ctx_lens.has_value());
+    CHECK_BF16(*kc); CHECK_BF16(*vc); CHECK_CONTIG(*kc); CHECK_CONTIG(*vc);
+    TORCH_CHECK(kc->dim() == 4 && kc->size(1) == Hkv && kc->size(2) == 64 && kc->size(3) == D);
+    TORCH_CHECK(vc->sizes() == at::IntArrayRef({kc->size(0), Hkv, D, 64}));
+    CHECK_DEV(*block_tables); CHECK_DT(*block_tables, at::kInt); CHECK_CONTIG(*block_tables);
+    CHECK_DEV(*ctx_lens); CHECK_DT(*ctx_lens, at::kInt);
+    TORCH_CHECK(block_tables->dim() == 2 && block_tables->size(0) >= B && ctx_lens->numel() >= B);
+    p.kc = bfp(*kc);
+    p.vc = bfp(*vc);
+    p.block_tables = block_tables->data_ptr<int32_t>();
+    p.max_blocks = (int)block_tables->size(1);
+    p.ctx_lens = ctx_lens->data_ptr<int32_t>();
+  } else {
+    TORCH_CHECK(k.has_value() && v.has_value());
+    CHECK_BF16(*k); CHECK_BF16(*v);
+    TORCH_CHECK(k->dim() == 2 && k->stride(1) == 1 && k->stride(0) == v->stride(0) && k->size(0) == q.size(0));
+    TORCH_CHECK(k->stride(0) % 8 == 0 && k->size(1) >= Hkv * D && v->size(1) >= Hkv * D);
+    p.k = bfp(*k);
+    p.v = bfp(*v);
+    p.kv_stride = k->stride(0);
+  }
+  nga::launch_prefill_attention(p, (int)B, (int)max_q_len, (int)D, paged, causal, cur_stream(q));
+}
+
+// ------------------------------------------------------------------ sampling
+void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p,
+            c10::optional<Tensor> rep_penalty, c10::optional<Tensor> history, Tensor seeds,
+            Tensor steps, Tensor out_tok, Tensor out_logprob) {
+  CHECK_DEV(logits); CHECK_DT(logits, at::kFloat); CHECK_CONTIG(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.size(1) <= 131072, "sample: vocab must be <= 131072");
+  const int64_t B = logits.size(0);
+  CHECK_DT(temperature, at::kFloat); CHECK_DT(top_k, at::kInt); CHECK_DT(top_p, at::kFloat);
+  CHECK_DT(seeds, at::kLong); CHECK_DT(steps, at::kLong);
+  CHECK_DT(out_tok, at::kInt); CHECK_DT(out_logprob, at::kFloat);
+  TORCH_CHECK(temperature.numel() >= B && top_k.numel() >= B && top_p.numel() >= B &&
+              seeds.numel() >= B && steps.numel() >= B && out_tok.numel() >= B && out_logprob.numel() >= B);
+  const float* rp = nullptr;
+  const int32_t* hp = nullptr;
+  int hl = 0;
+  if (rep_penalty.has_value() && history.has_value()) {
+    CHECK_DT(*rep_penalty, at::kFloat); CHECK_DT(*history, at::kInt); CHECK_CONTIG(*history);
+    TORCH_CHECK(history->dim() == 2 && history->size(0) >= B && rep_penalty->numel() >= B);
+    rp = rep_penalty->data_ptr<float>();
+    hp = history->data_ptr<int32_t>();
+    hl = (int)history->size(1);
+  }
+  nga::launch_sample(logits.data_ptr<float>(), (int)B, (int)logits.size(1), temperature.data_ptr<float>(),
+                     top_k.data_ptr<int32_t>(), top_p.data_ptr<float>(), rp, hp, hl,
+                     seeds.data_ptr<int64_t>(), steps.data_ptr<int64_t>(), out_tok.data_ptr<int32_t>(),
+                     out_logprob.data_ptr<float>(), cur_stream(logits));
+}
+
+// ------------------------------------------------------------------ vector search
+void score(Tensor Q, Tensor X, c10::optional<Tensor> row_bias, Tensor S, double dot_scale) {
+  CHECK_BF16(Q); CHECK_BF16(X); CHECK_CONTIG(Q); CHECK_CONTIG(X);
+  CHECK_DEV(S); CHECK_DT(S, at::kFloat); CHECK_CONTIG(S);
+  TORCH_CHECK(Q.dim() == 2 && X.dim() == 2 && Q.size(1) == X.size(1));
+  const int64_t D = X.size(1);
+  TORCH_CHECK(D % 32 == 0 && D <= 1216, "score: D must be a multiple of 32 and <= 1216");
+  TORCH_CHECK(S.size(0) == Q.size(0) && S.size(1) == X.size(0));
+  const float* bp = nullptr;
+  if (row_bias.has_value()) {
+    CHECK_DEV(*row_bias); CHECK_DT(*row_bias, at::kFloat);
+    TORCH_CHECK(row_bias->numel() == X.size(0));
+    bp = row_bias->data_ptr<float>();
+  }
+  nga::launch_score(bfp(Q), (int)Q.size(0), bfp(X), X.size(0), (int)D, bp, S.data_ptr<float>(),
+                    (float)dot_scale, cur_stream(X));
+}
+
+void topk(Tensor in, c10::optional<Tensor> in_idx, int64_t seg_len, int64_t k, Tensor out_v,
+          Tensor out_i) {
+  CHECK_DEV(in); CHECK_DT(in, at::kFloat); CHECK_CONTIG(in);
+  TORCH_CHECK(in.dim() == 2);
+  TORCH_CHECK(k >= 1 && k <= 1024, "topk: k must be in [1, 1024]");
+  const int64_t rows = in.size(0), len = in.size(1);
+  const int64_t nseg = (len + seg_len - 1) / seg_len;
+  CHECK_DT(out_v, at::kFloat); CHECK_DT(out_i, at::kLong); CHECK_CONTIG(out_v); CHECK_CONTIG(out_i);
+  TORCH_CHECK(out_v.numel() == rows * nseg * k && out_i.numel() == rows * nseg * k, "topk: bad output size");
+  const int64_t* ip = nullptr;
+  if (in_idx.has_value()) {
+    CHECK_DT(*in_idx, at::kLong); CHECK_CONTIG(*in_idx);
+    TORCH_CHECK(in_idx->sizes() == in.sizes());
+    ip = in_idx->data_ptr<int64_t>();
+  }
+  nga::launch_topk(in.data_ptr<float>(), ip, rows, len, seg_len, (int)k, out_v.data_ptr<float>(),
+                   out_i.data_ptr<int64_t>(), cur_stream(in));
+}
+
+void pool_l2norm(Tensor hidden, Tensor cu, int64_t mode, bool normalize, Tensor out) {
+  CHECK_BF16(hidden); CHECK_CONTIG(hidden);
+  CHECK_DEV(cu); CHECK_DT(cu, at::kInt);
+  CHECK_DEV(out); CHECK_DT(out, at::kFloat); CHECK_CONTIG(out);
+  const int64_t H = hidden.size(1), B = cu.numel() - 1;
+  TORCH_CHECK(H % 8 == 0 && H <= 8192 && out.size(0) == B && out.size(1) == H);
+  nga::launch_pool_l2norm(bfp(hidden), cu.data_ptr<int32_t>(), (int)B, (int)H, (int)mode,
+                          normalize ? 1 : 0, out.data_ptr<float>(), cur_stream(hidden));
+}
+
+void row_sqnorm(Tensor X, Tensor out) {
+  CHECK_BF16(X); CHECK_CONTIG(X);
+  CHECK_DEV(out); CHECK_DT(out, at::kFloat);
+  TORCH_CHECK(X.dim() == 2 && X.size(1) % 8 == 0 && out.numel() == X.size(0));
+  nga::launch_row_sqnorm(bfp(X), X.size(0), (int)X.size(1), out.data_ptr<float>(), cur_stream(X));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "nv_genai_amd gfx950 HIP kernels";
+  m.def("rmsnorm", &rmsnorm);
+  m.def("add_rmsnorm", &add_rmsnorm);
+  m.def("layernorm", &layernorm);
+  m.def("silu_mul", &silu_mul);
+  m.def("bias_gelu", &bias_gelu);
+  m.def("rope_cache", &rope_cache);
+  m.def("decode_pages_per_part", &decode_pages_per_part);
+  m.def("decode_attention", &decode_attention);
+  m.def("prefill_attention", &prefill_attention);
+  m.def("sample", &sample);
+  m.def("score", &score);
+  m.def("topk", &topk);
+  m.def("pool_l2norm", &pool_l2norm);
+  m.def("row_sqnorm", &row_sqnorm);
+}

@@ -1,0 +1,233 @@
+// Paged decode attention with GQA on MFMA (K2 in SURVEY.md §2.C).
+//
+// One query token per sequence. For a (sequence, kv-head) pair the G = Hq/Hkv query rows
+// that share the kv head form the 16 columns of an MFMA tile (padded with zero rows), so
+// K and V are read from HBM exactly once per (sequence, kv-head) — the kernel is bound by
+// the KV stream, which is ~half the bytes of a Llama-3-8B decode step at RAG context lengths.
+//
+// Per 64-key page (= one KV-cache block, BS = 64) and per wave:
+//   S^T[key, q] = K[key, :] . Q[q, :]^T       4 tiles x 4 d-steps of mfma_f32_16x16x32_bf16
+//   online softmax over keys (exp2 domain), keys of a q column live in 4 lanes x 16 regs
+//   O^T[d, q]  += Vt[d, key] . P^T[key, q]     2 key-groups x 8 d-tiles
+// The S accumulator is consumed as the P^T B-operand with no lane movement: tile rows are
+// mapped to physical keys as key = 32*g + 8*(row>>2) + 4*t1 + (row&3) so that lane group h
+// holds keys 32g+8h .. 32g+8h+7 — exactly the 8 consecutive keys the Vt A-operand load
+// (one 16-B load from the transposed V page) provides.
+//
+// Work split: grid = (seqs, kv_heads, partitions); 4 waves per workgroup stride over the
+// partition's pages; waves combine through LDS; partitions (flash-decoding split-K, used
+// when seqs*kv_heads is too small to fill 256 CUs) combine in a second small kernel.
+#include "common.h"
+#include "kernels.h"
+
+namespace nga {
+
+namespace {
+constexpr int D = 128;
+constexpr int BS = 64;
+constexpr int NW = 4;
+constexpr float LOG2E = 1.4426950408889634f;
+}  // namespace
+
+__global__ void __launch_bounds__(256) decode_attn_kernel(
+    uint16_t* __restrict__ out, int64_t out_stride, const uint16_t* __restrict__ q,
+    int64_t q_stride, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const int32_t* __restrict__ block_tables, int max_blocks,
+    const int32_t* __restrict__ ctx_lens, int Hq, int Hkv, float scale, int pages_per_part,
+    float* __restrict__ part_ml, float* __restrict__ part_o) {
+  const int b = blockIdx.x, kvh = blockIdx.y, part = blockIdx.z, nparts = gridDim.z;
+  const int G = Hq / Hkv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, h = lane >> 4;
+  const int ctx = ctx_lens[b];
+  const int n_pages = (ctx + BS - 1) / BS;
+  const int p_begin = part * pages_per_part;
+  const int p_end = min(n_pages, p_begin + pages_per_part);
+
+  __shared__ float o_s[NW][16][D + 4];
+  __shared__ float m_s[NW][16], l_s[NW][16];
+
+  if (p_begin >= p_end) {
+    // empty partition (or an empty padding sequence, ctx = 0)
+    if (nparts == 1) {
+      for (int i = threadIdx.x; i < G * D; i += blockDim.x)
+        out[(int64_t)b * out_stride + (int64_t)(kvh * G) * D + i] = 0;
+    } else {
+      for (int i = threadIdx.x; i < G; i += blockDim.x) {
+        const int64_t idx = ((int64_t)b * Hq + kvh * G + i) * nparts + part;
+        part_ml[2 * idx] = -INFINITY;
+        part_ml[2 * idx + 1] = 0.f;
+      }
+    }
+    return;
+  }
+
+  // Q^T as the B operand: lane holds Q[q=col][d = 32s + 8h + j]
+  bf16x8 qf[4];
+  {
+    const bool qv = col < G;
+    const uint16_t* qp = q + (int64_t)b * q_stride + (int64_t)(kvh * G + (qv ? col : 0)) * D;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      u16x8 v = load8(qp + 32 * s + 8 * h);
+      if (!qv) v = (u16x8)(0);
+      qf[s] = as_bf16x8(v);
+    }
+  }
+
+  const float sl2 = scale * LOG2E;
+  float m = -INFINITY, l = 0.f;
+  f32x4 o[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o[dt] = (f32x4)(0.f);
+
+  const int32_t* bt = block_tables + (int64_t)b * max_blocks;
+  for (int p = p_begin + w; p < p_end; p += NW) {
+    const int64_t blk = bt[p];
+    const uint16_t* kp = kc + (blk * Hkv + kvh) * (int64_t)(BS * D);
+    const uint16_t* vp = vc + (blk * Hkv + kvh) * (int64_t)(D * BS);
+    // K operand loads: tile tau (g = tau>>1, t1 = tau&1), row = col
+    u16x8 kf[4][4];
+#pragma unroll
+    for (int tau = 0; tau < 4; ++tau) {
+      const int key = 32 * (tau >> 1) + 8 * (col >> 2) + 4 * (tau & 1) + (col & 3);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) kf[tau][s] = load8(kp + key * D + 32 * s + 8 * h);
+    }
+    u16x8 vf[2][8];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) vf[g][dt] = load8(vp + (16 * dt + col) * BS + 32 * g + 8 * h);
+
+    f32x4 sacc[4];
+#pragma unroll
+    for (int tau = 0; tau < 4; ++tau) {
+      sacc[tau] = (f32x4)(0.f);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) sacc[tau] = mfma16(as_bf16x8(kf[tau][s]), qf[s], sacc[tau]);
+    }
+    // scale + mask; lane's keys: 32g + 8h + 4t1 + r for tile tau = 2g + t1, reg r
+    const int kbase = p * BS;
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int tau = 0; tau < 4; ++tau)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kbase + 32 * (tau >> 1) + 8 * h + 4 * (tau & 1) + r;
+        float s = sacc[tau][r] * sl2;
+        s = key < ctx ? s : -INFINITY;
+        sacc[tau][r] = s;
+        mloc = fmaxf(mloc, s);
+      }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float m_new = fmaxf(m, mloc);
+    const float alpha = exp2f(m - m_new);  // m_new finite: every page has >= 1 valid key
+    m = m_new;
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+    bf16x8 pf[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float pv = exp2f(sacc[2 * g + (j >> 2)][j & 3] - m_new);
+        l += pv;
+        pf[g][j] = (__bf16)pv;
+      }
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) o[dt] = mfma16(as_bf16x8(vf[g][dt]), pf[g], o[dt]);
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+
+  // wave partials -> LDS. O^T layout: lane holds O[q=col][d = 16dt + 4h + r]
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o_s[w][col][16 * dt + 4 * h + r] = o[dt][r];
+  if (h == 0) {
+    m_s[w][col] = m;
+    l_s[w][col] = l;
+  }
+  __syncthreads();
+
+  for (int i = threadIdx.x; i < G * D; i += blockDim.x) {
+    const int qi = i / D, d = i % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, m_s[ww][qi]);
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) {
+      const float f = (m_s[ww][qi] == -INFINITY) ? 0.f : exp2f(m_s[ww][qi] - M);
+      L += f * l_s[ww][qi];
+      acc += f * o_s[ww][qi][d];
+    }
+    const int hq = kvh * G + qi;
+    if (nparts == 1) {
+      out[(int64_t)b * out_stride + (int64_t)hq * D + d] = f2bf(acc / L);
+    } else {
+      const int64_t idx = ((int64_t)b * Hq + hq) * nparts + part;
+      part_o[idx * D + d] = acc;
+      if (d == 0) {
+        part_ml[2 * idx] = M;
+        part_ml[2 * idx + 1] = L;
+      }
+    }
+  }
+}
+
+__global__ void decode_attn_reduce_kernel(uint16_t* __restrict__ out, int64_t out_stride,
+                                          const float* __restrict__ part_ml,
+                                          const float* __restrict__ part_o, int Hq, int nparts) {
+  const int b = blockIdx.x, hq = blockIdx.y, d = threadIdx.x;
+  const int64_t base = ((int64_t)b * Hq + hq) * nparts;
+  float M = -INFINITY;
+  for (int p = 0; p < nparts; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
+  float L = 0.f, acc = 0.f;
+  for (int p = 0; p < nparts; ++p) {
+    const float mp = part_ml[2 * (base + p)];
+    if (mp == -INFINITY) continue;
+    const float f = exp2f(mp - M);
+    L += f * part_ml[2 * (base + p) + 1];
+    acc += f * part_o[(base + p) * D + d];
+  }
+  out[(int64_t)b * out_stride + (int64_t)hq * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
+}
+
+int decode_attn_pages_per_part(int num_seqs, int Hkv, int max_ctx) {
+  // Aim for >= ~1024 workgroups (4 per CU) so the KV stream has enough loads in flight.
+  const int pages = (max_ctx + BS - 1) / BS;
+  const int items = num_seqs * Hkv;
+  int want_parts = (1024 + items - 1) / items;
+  if (want_parts < 1) want_parts = 1;
+  int ppp = (pages + want_parts - 1) / want_parts;
+  if (ppp < NW) ppp = NW;  // at least one page per wave
+  return ppp;
+}
+
+void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* q,
+                             int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
+                             const int32_t* block_tables, int max_blocks, const int32_t* ctx_lens,
+                             int num_seqs, int Hq, int Hkv, int max_ctx, float scale,
+                             int pages_per_part, float* part_ml, float* part_o,
+                             hipStream_t stream) {
+  if (num_seqs == 0) return;
+  const int pages = (max_ctx + BS - 1) / BS;
+  const int nparts = (pages + pages_per_part - 1) / pages_per_part;
+  dim3 grid(num_seqs, Hkv, nparts);
+  decode_attn_kernel<<<grid, 256, 0, stream>>>(out, out_stride, q, q_stride, kc, vc, block_tables,
+                                               max_blocks, ctx_lens, Hq, Hkv, scale,
+                                               pages_per_part, part_ml, part_o);
+  if (nparts > 1) {
+    dim3 g2(num_seqs, Hq);
+    decode_attn_reduce_kernel<<<g2, D, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts);
+  }
+}
+
+}  // namespace nga

@@ -1,0 +1,73 @@
+// Host-side launch API of the gfx950 kernels. Every launcher is capture-safe (no
+// allocation, no synchronisation) so decode steps can be recorded into hipGraphs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nga {
+
+// norm.hip
+void launch_rmsnorm(uint16_t* out, uint16_t* resid, const uint16_t* delta, const uint16_t* w,
+                    float eps, int64_t rows, int H, int64_t in_stride, int64_t out_stride,
+                    hipStream_t stream);
+void launch_layernorm(uint16_t* out, const uint16_t* x, const uint16_t* resid, const uint16_t* g,
+                      const uint16_t* b, float eps, int64_t rows, int H, hipStream_t stream);
+
+// activation.hip
+void launch_silu_mul(uint16_t* out, const uint16_t* in, int64_t T, int F, hipStream_t stream);
+void launch_bias_gelu(uint16_t* x, const uint16_t* bias, int64_t T, int F, hipStream_t stream);
+
+// rope.hip
+void launch_rope_cache(uint16_t* qkv, const int32_t* pos, const float* cos_sin,
+                       const int32_t* slots, uint16_t* kc, uint16_t* vc, int64_t T, int Hq,
+                       int Hkv, int D, int BS, hipStream_t stream);
+
+// attention_decode.hip
+int decode_attn_pages_per_part(int num_seqs, int Hkv, int max_ctx);
+void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* q,
+                             int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
+                             const int32_t* block_tables, int max_blocks, const int32_t* ctx_lens,
+                             int num_seqs, int Hq, int Hkv, int max_ctx, float scale,
+                             int pages_per_part, float* part_ml, float* part_o,
+                             hipStream_t stream);
+
+// attention_prefill.hip
+struct PrefillParams {
+  uint16_t* out;
+  int64_t out_stride;
+  const uint16_t* q;
+  int64_t q_stride;
+  const uint16_t* k;  // non-paged K rows (packed like q)
+  const uint16_t* v;
+  int64_t kv_stride;
+  const uint16_t* kc;  // paged caches
+  const uint16_t* vc;
+  const int32_t* block_tables;
+  int max_blocks;
+  const int32_t* cu_q;      // [B+1] offsets of each sequence's query rows
+  const int32_t* ctx_lens;  // [B] total keys (paged)
+  int Hq;
+  int Hkv;
+  float scale;
+};
+void launch_prefill_attention(const PrefillParams& p, int num_seqs, int max_q_len, int D,
+                              bool paged, bool causal, hipStream_t stream);
+
+// sampling.hip
+void launch_sample(float* logits, int B, int V, const float* temperature, const int32_t* top_k,
+                   const float* top_p, const float* rep_penalty, const int32_t* history,
+                   int hist_len, const int64_t* seeds, const int64_t* steps, int32_t* out_tok,
+                   float* out_logprob, hipStream_t stream);
+
+// vector_search.hip
+void launch_score(const uint16_t* Q, int nq, const uint16_t* X, int64_t N, int D,
+                  const float* row_bias, float* S, float dot_scale, hipStream_t stream);
+void launch_topk(const float* in, const int64_t* in_idx, int64_t rows, int64_t row_len,
+                 int64_t seg_len, int k, float* out_v, int64_t* out_i, hipStream_t stream);
+
+// pool.hip
+void launch_pool_l2norm(const uint16_t* hidden, const int32_t* cu, int B, int H, int mode,
+                        int normalize, float* out, hipStream_t stream);
+void launch_row_sqnorm(const uint16_t* X, int64_t N, int D, float* out, hipStream_t stream);
+
+}  // namespace nga

@@ -1,0 +1,437 @@
+// Native serving runtime: paged-KV block manager with prefix caching and the
+// continuous-batching scheduler of the LLM engine (the part of TensorRT-LLM's batch manager
+// the reference relies on through NIM: paged KV, inflight batching, max_batch/max_input/
+// max_output envelopes — SURVEY.md §2.B N1, mistral-7b.yaml:28-39).
+//
+// Python owns the model and the GPU; this object owns sequence state and KV-block
+// accounting, and fills caller-provided int32 buffers (pinned host memory) with the step
+// layout (input ids, positions, slot mapping, cu_seqlens, context lengths, block tables)
+// so one host->device copy per buffer is all the engine does per step.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <deque>
+#include <list>
+#include <stdexcept>
+#include <unordered_map>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace {
+
+uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+uint64_t block_hash(uint64_t prev, const int32_t* toks, int n) {
+  uint64_t h = mix64(prev ^ 0x5bd1e995ull);
+  for (int i = 0; i < n; ++i) h = mix64(h ^ (uint64_t)(uint32_t)toks[i]);
+  return h | 1ull;  // never 0 (0 = "no hash")
+}
+
+class BlockManager {
+ public:
+  BlockManager(int num_blocks, int block_size, bool prefix_caching)
+      : nb_(num_blocks), bs_(block_size), prefix_(prefix_caching), ref_(num_blocks, 0),
+        hash_(num_blocks, 0), lru_pos_(num_blocks) {
+    for (int i = num_blocks - 1; i >= 0; --i) free_.push_back(i);
+  }
+  int block_size() const { return bs_; }
+  int num_blocks() const { return nb_; }
+  int num_free() const { return (int)free_.size() + (int)lru_.size(); }
+  int num_used() const { return nb_ - num_free(); }
+
+  int alloc() {
+    int b;
+    if (!free_.empty()) {
+      b = free_.back();
+      free_.pop_back();
+    } else if (!lru_.empty()) {
+      b = lru_.front();
+      lru_.pop_front();
+      cached_.erase(hash_[b]);
+      hash_[b] = 0;
+    } else {
+      return -1;
+    }
+    ref_[b] = 1;
+    return b;
+  }
+  void release(int b) {
+    if (b < 0 || b >= nb_ || ref_[b] <= 0) throw std::runtime_error("release of a free block");
+    if (--ref_[b] == 0) {
+      if (hash_[b] != 0) {
+        lru_.push_back(b);
+        lru_pos_[b] = std::prev(lru_.end());
+      } else {
+        free_.push_back(b);
+      }
+    }
+  }
+  // Look up a full block by content hash; on hit the block is referenced.
+  int lookup(uint64_t h) {
+    if (!prefix_) return -1;
+    auto it = cached_.find(h);
+    if (it == cached_.end()) return -1;
+    const int b = it->second;
+    if (ref_[b] == 0) lru_.erase(lru_pos_[b]);
+    ref_[b] += 1;
+    ++hits_;
+    return b;
+  }
+  void register_full(int b, uint64_t h) {
+    if (!prefix_ || hash_[b] != 0) return;
+    if (cached_.count(h)) return;  // identical content already cached in another block
+    hash_[b] = h;
+    cached_[h] = b;
+  }
+  int64_t hits() const { return hits_; }
+  void reset_prefix_cache() {
+    for (int b : lru_) {
+      cached_.erase(hash_[b]);
+      hash_[b] = 0;
+      free_.push_back(b);
+    }
+    lru_.clear();
+  }
+
+ private:
+  int nb_, bs_;
+  bool prefix_;
+  std::vector<int> ref_;
+  std::vector<uint64_t> hash_;
+  std::vector<int> free_;
+  std::list<int> lru_;  // ref==0 blocks that still hold reusable (hashed) content
+  std::vector<std::list<int>::iterator> lru_pos_;
+  std::unordered_map<uint64_t, int> cached_;
+  int64_t hits_ = 0;
+};
+
+enum Status { WAITING = 0, RUNNING = 1, FINISHED = 2 };
+
+struct Seq {
+  int64_t id;
+  std::vector<int32_t> toks;  // prompt + generated
+  int prompt_len;
+  int max_new;
+  int computed = 0;            // tokens whose KV is in the cache
+  int cached_prefix = 0;       // tokens served from the prefix cache at admission
+  std::vector<int32_t> blocks;
+  std::vector<uint64_t> hashes;  // hash of each full block
+  int status = WAITING;
+  int64_t arrival;
+  int preemptions = 0;
+};
+
+class Scheduler {
+ public:
+  Scheduler(int num_blocks, int block_size, int max_num_seqs, int max_batched_tokens,
+            int max_model_len, bool prefix_caching)
+      : bm_(num_blocks, block_size, prefix_caching), bs_(block_size), max_seqs_(max_num_seqs),
+        max_tokens_(max_batched_tokens), max_len_(max_model_len) {}
+
+  void add(int64_t id, const std::vector<int32_t>& prompt, int max_new) {
+    if (seqs_.count(id)) throw std::runtime_error("duplicate sequence id");
+    if (prompt.empty()) throw std::runtime_error("empty prompt");
+    if ((int)prompt.size() + max_new > max_len_)
+      throw std::runtime_error("prompt + max_tokens exceeds max_model_len");
+    Seq s;
+    s.id = id;
+    s.toks = prompt;
+    s.prompt_len = (int)prompt.size();
+    s.max_new = max_new;
+    s.arrival = clock_++;
+    seqs_.emplace(id, std::move(s));
+    waiting_.push_back(id);
+  }
+
+  // Fill the step buffers. Returns (kind, num_seqs, num_tokens); kind 0 idle, 1 prefill, 2 decode.
+  // seq_ids[i], cu_q[i..i+1], ctx[i], sample[i] (1 = produce a token), block_tables[i][:] per seq.
+  py::tuple schedule(py::array_t<int32_t> input_ids, py::array_t<int32_t> positions,
+                     py::array_t<int32_t> slots, py::array_t<int32_t> cu_q,
+                     py::array_t<int32_t> ctx, py::array_t<int32_t> block_tables,
+                     py::array_t<int64_t> seq_ids, py::array_t<int32_t> sample) {
+    auto ids = input_ids.mutable_unchecked<1>();
+    auto pos = positions.mutable_unchecked<1>();
+    auto sl = slots.mutable_unchecked<1>();
+    auto cq = cu_q.mutable_unchecked<1>();
+    auto cx = ctx.mutable_unchecked<1>();
+    auto bt = block_tables.mutable_unchecked<2>();
+    auto sid = seq_ids.mutable_unchecked<1>();
+    auto smp = sample.mutable_unchecked<1>();
+    const int max_bt = (int)bt.shape(1);
+    const int cap_tokens = std::min<int>((int)ids.shape(0), max_tokens_);
+    const int cap_seqs = std::min<int>((int)sid.shape(0), max_seqs_);
+
+    // ---- prefill: continue partially prefilled seqs, then admit waiting ones (FCFS)
+    std::vector<int64_t> chosen;
+    std::vector<int> qlen;
+    int budget = cap_tokens;
+    for (int64_t id : running_) {
+      Seq& s = seqs_.at(id);
+      const int todo = (int)s.toks.size() - s.computed;
+      if (todo > 1 || (todo == 1 && s.computed < s.prompt_len)) {
+        if ((int)chosen.size() >= cap_seqs || budget <= 0) break;
+        const int n = std::min(todo, budget);
+        chosen.push_back(id);
+        qlen.push_back(n);
+        budget -= n;
+      }
+    }
+    while (!waiting_.empty() && budget > 0 && (int)chosen.size() < cap_seqs &&
+           (int)running_.size() < max_seqs_) {
+      const int64_t id = waiting_.front();
+      Seq& s = seqs_.at(id);
+      if (!admit(s)) break;
+      waiting_.pop_front();
+      running_.push_back(id);
+      s.status = RUNNING;
+      const int todo = (int)s.toks.size() - s.computed;
+      const int n = std::min(todo, budget);
+      chosen.push_back(id);
+      qlen.push_back(n);
+      budget -= n;
+    }
+    if (!chosen.empty()) {
+      int t = 0;
+      cq(0) = 0;
+      for (size_t i = 0; i < chosen.size(); ++i) {
+        Seq& s = seqs_.at(chosen[i]);
+        const int n = qlen[i];
+        for (int j = 0; j < n; ++j) {
+          const int p = s.computed + j;
+          ids(t) = s.toks[p];
+          pos(t) = p;
+          sl(t) = s.blocks[p / bs_] * bs_ + p % bs_;
+          ++t;
+        }
+        s.computed += n;
+        cq(i + 1) = t;
+        cx(i) = s.computed;
+        sid(i) = s.id;
+        smp(i) = s.computed == (int)s.toks.size() ? 1 : 0;
+        fill_bt(bt, (int)i, s, max_bt);
+        register_full_blocks(s);
+      }
+      return py::make_tuple(1, (int)chosen.size(), t);
+    }
+
+    // ---- decode: every running seq with all tokens but the last computed
+    std::vector<int64_t> dec;
+    for (int64_t id : running_) {
+      Seq& s = seqs_.at(id);
+      if ((int)s.toks.size() - s.computed == 1) dec.push_back(id);
+    }
+    if (dec.empty()) return py::make_tuple(0, 0, 0);
+    // make room: each seq whose next token starts a new block needs one
+    std::sort(dec.begin(), dec.end(),
+              [&](int64_t a, int64_t b) { return seqs_.at(a).arrival < seqs_.at(b).arrival; });
+    std::vector<int64_t> ok;
+    for (size_t i = 0; i < dec.size(); ++i) {
+      Seq& s = seqs_.at(dec[i]);
+      if (s.status != RUNNING) continue;
+      const int p = s.computed;  // position of the token being computed now
+      bool have = p / bs_ < (int)s.blocks.size();
+      while (!have) {
+        const int b = bm_.alloc();
+        if (b >= 0) {
+          s.blocks.push_back(b);
+          have = true;
+          break;
+        }
+        // preempt the latest-arrived running decode seq (recompute later)
+        int64_t victim = -1;
+        for (size_t j = dec.size(); j-- > i + 1;) {
+          if (seqs_.at(dec[j]).status == RUNNING) {
+            victim = dec[j];
+            break;
+          }
+        }
+        if (victim < 0) victim = s.id;
+        preempt(victim);
+        if (victim == s.id) break;
+      }
+      if (have && s.status == RUNNING) ok.push_back(s.id);
+      if ((int)ok.size() >= cap_seqs) break;
+    }
+    cq(0) = 0;
+    for (size_t i = 0; i < ok.size(); ++i) {
+      Seq& s = seqs_.at(ok[i]);
+      const int p = s.computed;
+      ids(i) = s.toks[p];
+      pos(i) = p;
+      sl(i) = s.blocks[p / bs_] * bs_ + p % bs_;
+      s.computed += 1;
+      cq(i + 1) = (int)i + 1;
+      cx(i) = s.computed;
+      sid(i) = s.id;
+      smp(i) = 1;
+      fill_bt(bt, (int)i, s, max_bt);
+      register_full_blocks(s);
+    }
+    return py::make_tuple(ok.empty() ? 0 : 2, (int)ok.size(), (int)ok.size());
+  }
+
+  void append_token(int64_t id, int32_t tok) {
+    Seq& s = seqs_.at(id);
+    s.toks.push_back(tok);
+  }
+
+  void append_tokens(py::array_t<int64_t> ids, py::array_t<int32_t> toks, int n) {
+    auto a = ids.unchecked<1>();
+    auto b = toks.unchecked<1>();
+    for (int i = 0; i < n; ++i) append_token(a(i), b(i));
+  }
+
+  void finish(int64_t id) {
+    auto it = seqs_.find(id);
+    if (it == seqs_.end()) return;
+    Seq& s = it->second;
+    for (int b : s.blocks) bm_.release(b);
+    s.blocks.clear();
+    if (s.status == RUNNING)
+      running_.erase(std::find(running_.begin(), running_.end(), id));
+    else if (s.status == WAITING) {
+      auto w = std::find(waiting_.begin(), waiting_.end(), id);
+      if (w != waiting_.end()) waiting_.erase(w);
+    }
+    seqs_.erase(it);
+  }
+
+  int num_generated(int64_t id) const {
+    const Seq& s = seqs_.at(id);
+    return (int)s.toks.size() - s.prompt_len;
+  }
+  std::vector<int32_t> tokens(int64_t id) const { return seqs_.at(id).toks; }
+  int cached_prefix(int64_t id) const { return seqs_.at(id).cached_prefix; }
+  int num_waiting() const { return (int)waiting_.size(); }
+  int num_running() const { return (int)running_.size(); }
+  bool has_work() const { return !waiting_.empty() || !running_.empty(); }
+  int free_blocks() const { return bm_.num_free(); }
+  int used_blocks() const { return bm_.num_used(); }
+  int total_blocks() const { return bm_.num_blocks(); }
+  int64_t prefix_hits() const { return bm_.hits(); }
+  int64_t preemptions() const { return preempt_count_; }
+  void reset_prefix_cache() { bm_.reset_prefix_cache(); }
+
+ private:
+  bool admit(Seq& s) {
+    // prefix-cache lookup over full blocks, keeping >= 1 token to compute
+    const int n = (int)s.toks.size();
+    std::vector<int32_t> got;
+    std::vector<uint64_t> hs;
+    uint64_t prev = 0;
+    const int max_cached_blocks = (n - 1) / bs_;
+    for (int i = 0; i < max_cached_blocks; ++i) {
+      const uint64_t h = block_hash(prev, s.toks.data() + i * bs_, bs_);
+      const int b = bm_.lookup(h);
+      if (b < 0) break;
+      got.push_back(b);
+      hs.push_back(h);
+      prev = h;
+    }
+    const int need = (n + bs_ - 1) / bs_ - (int)got.size();
+    // keep one spare block per running sequence for decode growth (watermark)
+    if (need > bm_.num_free() - (int)running_.size() / 4) {
+      for (int b : got) bm_.release(b);
+      return false;
+    }
+    for (int i = 0; i < need; ++i) got.push_back(bm_.alloc());
+    s.blocks = got;
+    s.hashes = hs;
+    s.computed = (int)hs.size() * bs_;
+    s.cached_prefix = s.computed;
+    return true;
+  }
+
+  void register_full_blocks(Seq& s) {
+    const int full = s.computed / bs_;
+    while ((int)s.hashes.size() < full) {
+      const int i = (int)s.hashes.size();
+      const uint64_t prev = i ? s.hashes[i - 1] : 0;
+      const uint64_t h = block_hash(prev, s.toks.data() + i * bs_, bs_);
+      s.hashes.push_back(h);
+      bm_.register_full(s.blocks[i], h);
+    }
+  }
+
+  void preempt(int64_t id) {
+    Seq& s = seqs_.at(id);
+    for (int b : s.blocks) bm_.release(b);
+    s.blocks.clear();
+    s.hashes.clear();
+    s.computed = 0;
+    s.status = WAITING;
+    s.preemptions += 1;
+    ++preempt_count_;
+    running_.erase(std::find(running_.begin(), running_.end(), id));
+    waiting_.push_front(id);
+  }
+
+  template <typename BT>
+  void fill_bt(BT& bt, int row, const Seq& s, int max_bt) {
+    if ((int)s.blocks.size() > max_bt) throw std::runtime_error("block table too narrow");
+    for (int j = 0; j < (int)s.blocks.size(); ++j) bt(row, j) = s.blocks[j];
+    for (int j = (int)s.blocks.size(); j < max_bt; ++j) bt(row, j) = 0;
+  }
+
+  BlockManager bm_;
+  int bs_, max_seqs_, max_tokens_, max_len_;
+  std::unordered_map<int64_t, Seq> seqs_;
+  std::deque<int64_t> waiting_;
+  std::vector<int64_t> running_;
+  int64_t clock_ = 0;
+  int64_t preempt_count_ = 0;
+};
+
+}  // namespace
+
+void register_bm25(py::module_& m);
+void register_text(py::module_& m);
+
+PYBIND11_MODULE(_rt, m) {
+  m.doc() = "nv_genai_amd native host runtime";
+  py::class_<BlockManager>(m, "BlockManager")
+      .def(py::init<int, int, bool>(), py::arg("num_blocks"), py::arg("block_size"),
+           py::arg("prefix_caching") = true)
+      .def("alloc", &BlockManager::alloc)
+      .def("release", &BlockManager::release)
+      .def("lookup", &BlockManager::lookup)
+      .def("register_full", &BlockManager::register_full)
+      .def("num_free", &BlockManager::num_free)
+      .def("num_used", &BlockManager::num_used)
+      .def_property_readonly("block_size", &BlockManager::block_size);
+  m.def("block_hash", [](uint64_t prev, const std::vector<int32_t>& toks) {
+    return block_hash(prev, toks.data(), (int)toks.size());
+  });
+  py::class_<Scheduler>(m, "Scheduler")
+      .def(py::init<int, int, int, int, int, bool>(), py::arg("num_blocks"),
+           py::arg("block_size"), py::arg("max_num_seqs"), py::arg("max_batched_tokens"),
+           py::arg("max_model_len"), py::arg("prefix_caching") = true)
+      .def("add", &Scheduler::add)
+      .def("schedule", &Scheduler::schedule)
+      .def("append_token", &Scheduler::append_token)
+      .def("append_tokens", &Scheduler::append_tokens)
+      .def("finish", &Scheduler::finish)
+      .def("num_generated", &Scheduler::num_generated)
+      .def("tokens", &Scheduler::tokens)
+      .def("cached_prefix", &Scheduler::cached_prefix)
+      .def("num_waiting", &Scheduler::num_waiting)
+      .def("num_running", &Scheduler::num_running)
+      .def("has_work", &Scheduler::has_work)
+      .def("free_blocks", &Scheduler::free_blocks)
+      .def("used_blocks", &Scheduler::used_blocks)
+      .def("total_blocks", &Scheduler::total_blocks)
+      .def("prefix_hits", &Scheduler::prefix_hits)
+      .def("preemptions", &Scheduler::preemptions)
+      .def("reset_prefix_cache", &Scheduler::reset_prefix_cache);
+  register_bm25(m);
+  register_text(m);
+}

@@ -1,0 +1,405 @@
+"""LLM serving engine: continuous batching over a paged KV cache, hipGraph-captured decode.
+
+Replaces NIM / TensorRT-LLM. Components:
+
+* :class:`nv_genai_amd._rt.Scheduler` (C++) — FCFS admission against the KV-block budget,
+  chunked prefill under a token budget, preemption-by-recompute when decode runs out of
+  blocks, prefix caching of full 64-token pages (shared RAG templates / system prompts hit).
+* :class:`nv_genai_amd.models.llama.LlamaModel` — the gfx950 kernel forward.
+* Decode steps run from hipGraphs captured per padded batch size (the whole step — 32 layers,
+  LM head and the sampling kernel — replays as one graph launch), prefill runs eagerly
+  (it is GEMM-bound, launch overhead is noise there).
+
+Engine knobs mirror the TRT-LLM envelope the reference configures
+(experimental/fm-asr-streaming-rag/nim/configs/mistral-7b.yaml:28-39): max_batch_size ->
+``max_num_seqs``, max_input_len/max_output_len -> ``max_model_len``,
+kv_cache_free_gpu_mem_fraction -> ``kv_cache_fraction``, tensor_para_size -> ``tp``.
+"""
+from __future__ import annotations
+
+import itertools
+import logging
+import random
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence
+
+import torch
+
+from .. import ops
+from .._native import rt
+from ..models.config import LlamaConfig, llama_config
+from ..models.llama import AttnMeta, LlamaModel
+from ..parallel.dist import ParallelContext, get_context
+from ..utils.tokenizer import IncrementalDetokenizer, LLMTokenizer, llm_tokenizer
+
+log = logging.getLogger(__name__)
+
+
+@dataclass
+class SamplingParams:
+    temperature: float = 0.2        # chain-server defaults (server.py:83-88)
+    top_p: float = 0.7
+    top_k: int = 0
+    max_tokens: int = 1024
+    stop: Sequence[str] = ()
+    stop_token_ids: Sequence[int] = ()
+    ignore_eos: bool = False
+    seed: Optional[int] = None
+    repetition_penalty: float = 1.0
+    logprobs: bool = False
+    min_tokens: int = 0
+
+
+@dataclass
+class Request:
+    id: int
+    prompt_ids: List[int]
+    params: SamplingParams
+    output_ids: List[int] = field(default_factory=list)
+    logprobs: List[float] = field(default_factory=list)
+    text: str = ""
+    finished: bool = False
+    finish_reason: Optional[str] = None
+    arrival: float = 0.0
+    first_token_time: Optional[float] = None
+    finish_time: Optional[float] = None
+    seed: int = 0
+    on_token: Optional[Callable[["Request", str], None]] = None
+    detok: Optional[IncrementalDetokenizer] = None
+    cached_prefix: int = 0
+
+    @property
+    def ttft(self) -> Optional[float]:
+        return None if self.first_token_time is None else self.first_token_time - self.arrival
+
+    @property
+    def latency(self) -> Optional[float]:
+        return None if self.finish_time is None else self.finish_time - self.arrival
+
+
+@dataclass
+class EngineConfig:
+    model: str = "llama3-8b"
+    max_num_seqs: int = 256
+    max_batched_tokens: int = 16384
+    max_model_len: int = 8192
+    block_size: int = 64
+    kv_cache_fraction: float = 0.3
+    kv_cache_blocks: Optional[int] = None
+    enable_prefix_caching: bool = True
+    use_graphs: bool = True
+    graph_batch_sizes: Sequence[int] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256)
+    decode_pages_per_part: int = 16
+    seed: int = 0
+    detokenize: bool = True
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig = EngineConfig(), device: Optional[str] = None,
+                 pctx: Optional[ParallelContext] = None, model: Optional[LlamaModel] = None,
+                 tokenizer: Optional[LLMTokenizer] = None, model_cfg: Optional[LlamaConfig] = None):
+        self.cfg = cfg
+        self.p = pctx or get_context()
+        if device is None:
+            device = str(self.p.device) if self.p.device.type == "cuda" else (
+                "cuda" if torch.cuda.is_available() else "cpu")
+        self.device = torch.device(device)
+        self.mcfg = model_cfg or llama_config(cfg.model, max_position=max(cfg.max_model_len, 256))
+        self.model = model or LlamaModel(self.mcfg, self.device, pctx=self.p, seed=cfg.seed)
+        self.tok = tokenizer or llm_tokenizer()
+        self.stop_ids = set(self.tok.stop_ids) | set(self.mcfg.eos_ids)
+        self.gpu = self.device.type == "cuda"
+        # ---- KV cache
+        nb = cfg.kv_cache_blocks
+        if nb is None:
+            if self.gpu:
+                free, _ = torch.cuda.mem_get_info(self.device)
+                nb = int(free * cfg.kv_cache_fraction) // self.model.kv_block_bytes(cfg.block_size)
+            else:
+                nb = 256
+        self.num_blocks = int(nb)
+        self.model.allocate_kv_cache(self.num_blocks, cfg.block_size)
+        self.max_blocks = (cfg.max_model_len + cfg.block_size - 1) // cfg.block_size
+        self.sched = rt.Scheduler(self.num_blocks, cfg.block_size, cfg.max_num_seqs,
+                                  cfg.max_batched_tokens, cfg.max_model_len,
+                                  cfg.enable_prefix_caching)
+        # ---- host step buffers (pinned) filled by the native scheduler
+        pin = self.gpu
+        T, S = max(cfg.max_batched_tokens, cfg.max_num_seqs), cfg.max_num_seqs
+
+        def hbuf(*shape, dtype=torch.int32):
+            return torch.zeros(*shape, dtype=dtype, pin_memory=pin)
+
+        self.h_ids, self.h_pos, self.h_slots = hbuf(T), hbuf(T), hbuf(T)
+        self.h_cu, self.h_ctx = hbuf(S + 1), hbuf(S)
+        self.h_bt = hbuf(S, self.max_blocks)
+        self.h_sid = hbuf(S, dtype=torch.int64)
+        self.h_smp = hbuf(S)
+        self.h_temp = hbuf(S, dtype=torch.float32)
+        self.h_topk = hbuf(S)
+        self.h_topp = hbuf(S, dtype=torch.float32)
+        self.h_seed = hbuf(S, dtype=torch.int64)
+        self.h_step = hbuf(S, dtype=torch.int64)
+        self.h_pen = hbuf(S, dtype=torch.float32)
+        self._np = [b.numpy() for b in (self.h_ids, self.h_pos, self.h_slots, self.h_cu,
+                                         self.h_ctx, self.h_bt, self.h_sid, self.h_smp)]
+        dev = self.device
+
+        def dbuf(*shape, dtype=torch.int32):
+            return torch.zeros(*shape, dtype=dtype, device=dev)
+
+        self.d_ids, self.d_pos, self.d_slots = dbuf(T), dbuf(T), dbuf(T)
+        self.d_cu, self.d_ctx = dbuf(S + 1), dbuf(S)
+        self.d_bt = dbuf(S, self.max_blocks)
+        self.d_temp = dbuf(S, dtype=torch.float32)
+        self.d_topk = dbuf(S)
+        self.d_topp = dbuf(S, dtype=torch.float32)
+        self.d_seed = dbuf(S, dtype=torch.int64)
+        self.d_step = dbuf(S, dtype=torch.int64)
+        self.d_pen = dbuf(S, dtype=torch.float32)
+        self.d_tok = dbuf(S)
+        self.d_lp = dbuf(S, dtype=torch.float32)
+        self.decode_ws = ops.DecodeWorkspace(S, self.model.hq, self.model.hkv, cfg.max_model_len,
+                                             dev, cfg.decode_pages_per_part) if self.gpu else None
+        self.requests: Dict[int, Request] = {}
+        self._ids = itertools.count(1)
+        self._rng = random.Random(cfg.seed)
+        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.stats = {"prefill_steps": 0, "decode_steps": 0, "prefill_tokens": 0,
+                      "decode_tokens": 0, "prefill_time": 0.0, "decode_time": 0.0}
+        self.lock = threading.RLock()
+        if self.gpu and cfg.use_graphs:
+            self._capture_graphs()
+
+    # ------------------------------------------------------------------ requests
+    def add_request(self, prompt_ids: List[int], params: Optional[SamplingParams] = None,
+                    request_id: Optional[int] = None,
+                    on_token: Optional[Callable[[Request, str], None]] = None) -> Request:
+        params = params or SamplingParams()
+        rid = request_id if request_id is not None else next(self._ids)
+        max_new = max(1, min(params.max_tokens, self.cfg.max_model_len - len(prompt_ids)))
+        if len(prompt_ids) >= self.cfg.max_model_len:
+            raise ValueError(f"prompt of {len(prompt_ids)} tokens exceeds max_model_len "
+                             f"{self.cfg.max_model_len}")
+        req = Request(rid, list(prompt_ids), params, arrival=time.perf_counter(),
+                      seed=params.seed if params.seed is not None else self._rng.getrandbits(62),
+                      on_token=on_token)
+        req.params = SamplingParams(**{**params.__dict__, "max_tokens": max_new})
+        if self.cfg.detokenize:
+            req.detok = IncrementalDetokenizer(self.tok)
+        with self.lock:
+            self.sched.add(rid, req.prompt_ids, max_new)
+            self.requests[rid] = req
+        return req
+
+    def abort(self, rid: int):
+        with self.lock:
+            req = self.requests.pop(rid, None)
+            self.sched.finish(rid)
+            if req is not None and not req.finished:
+                req.finished, req.finish_reason = True, "abort"
+                req.finish_time = time.perf_counter()
+
+    def has_work(self) -> bool:
+        return self.sched.has_work()
+
+    # ------------------------------------------------------------------ step
+    def step(self) -> List[Request]:
+        """Run one scheduler step; returns requests that finished in it."""
+        with self.lock:
+            ids, pos, sl, cu, ctx, bt, sid, smp = self._np
+            kind, n, ntok = self.sched.schedule(ids, pos, sl, cu, ctx, bt, sid, smp)
+            if kind == 0:
+                return []
+            t0 = time.perf_counter()
+            reqs = [self.requests[int(sid[i])] for i in range(n)]
+            for i, r in enumerate(reqs):
+                p = r.params
+                self.h_temp[i] = p.temperature
+                self.h_topk[i] = p.top_k
+                self.h_topp[i] = p.top_p
+                self.h_seed[i] = r.seed
+                self.h_step[i] = len(r.output_ids)
+                self.h_pen[i] = p.repetition_penalty
+            if kind == 2:
+                toks, lps = self._decode(n)
+                self.stats["decode_steps"] += 1
+                self.stats["decode_tokens"] += n
+                key = "decode_time"
+            else:
+                toks, lps = self._prefill(n, ntok)
+                self.stats["prefill_steps"] += 1
+                self.stats["prefill_tokens"] += ntok
+                key = "prefill_time"
+            toks = toks.tolist()
+            lps = lps.tolist()
+            self.stats[key] += time.perf_counter() - t0
+            now = time.perf_counter()
+            done = []
+            for i, r in enumerate(reqs):
+                if not smp[i]:
+                    continue
+                if self._emit(r, toks[i], lps[i], now):
+                    done.append(r)
+            return done
+
+    def _emit(self, r: Request, tok: int, lp: float, now: float) -> bool:
+        if r.first_token_time is None:
+            r.first_token_time = now
+            r.cached_prefix = self.sched.cached_prefix(r.id)
+        r.output_ids.append(tok)
+        if r.params.logprobs:
+            r.logprobs.append(lp)
+        self.sched.append_token(r.id, tok)
+        delta = ""
+        n = len(r.output_ids)
+        reason = None
+        is_stop_tok = (tok in self.stop_ids and not r.params.ignore_eos) or tok in r.params.stop_token_ids
+        if is_stop_tok and n > r.params.min_tokens:
+            reason = "stop"
+        elif r.detok is not None:
+            delta = r.detok.push(tok)
+            r.text += delta
+            if r.params.stop:
+                for s in r.params.stop:
+                    idx = r.text.find(s, max(0, len(r.text) - len(delta) - len(s)))
+                    if s and idx >= 0:
+                        delta = delta[: max(0, len(delta) - (len(r.text) - idx))]
+                        r.text = r.text[:idx]
+                        reason = "stop"
+                        break
+        if reason is None and n >= r.params.max_tokens:
+            reason = "length"
+        if r.on_token is not None and (delta or reason):
+            try:
+                r.on_token(r, delta)
+            except Exception:  # noqa: BLE001 - a consumer error must not kill the engine
+                log.exception("on_token callback failed")
+        if reason is not None:
+            r.finished, r.finish_reason, r.finish_time = True, reason, now
+            self.sched.finish(r.id)
+            self.requests.pop(r.id, None)
+            if r.on_token is not None:
+                try:
+                    r.on_token(r, "")
+                except Exception:  # noqa: BLE001
+                    log.exception("on_token callback failed")
+            return True
+        return False
+
+    def _meta(self, kind, n, ntok, max_q, max_ctx) -> AttnMeta:
+        return AttnMeta(kind=kind, slots=self.d_slots[:ntok], cu_q=self.d_cu[: n + 1],
+                        ctx_lens=self.d_ctx[:n], block_tables=self.d_bt[:n], max_q_len=max_q,
+                        max_ctx=max_ctx, decode_ws=self.decode_ws)
+
+    def _upload(self, n, ntok):
+        nb = non_blocking = self.gpu
+        self.d_ids[:ntok].copy_(self.h_ids[:ntok], non_blocking=nb)
+        self.d_pos[:ntok].copy_(self.h_pos[:ntok], non_blocking=nb)
+        self.d_slots[:ntok].copy_(self.h_slots[:ntok], non_blocking=nb)
+        self.d_cu[: n + 1].copy_(self.h_cu[: n + 1], non_blocking=nb)
+        self.d_ctx[:n].copy_(self.h_ctx[:n], non_blocking=nb)
+        self.d_bt[:n].copy_(self.h_bt[:n], non_blocking=nb)
+        for h, d in ((self.h_temp, self.d_temp), (self.h_topk, self.d_topk), (self.h_topp, self.d_topp),
+                     (self.h_seed, self.d_seed), (self.h_step, self.d_step), (self.h_pen, self.d_pen)):
+            d[:n].copy_(h[:n], non_blocking=non_blocking)
+
+    def _sample(self, logits, n):
+        rep = self.d_pen[:n] if self._needs_penalty(n) else None
+        hist = self._history(n) if rep is not None else None
+        return ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n],
+                          self.d_seed[:n], self.d_step[:n], rep, hist,
+                          out_tok=self.d_tok[:n], out_lp=self.d_lp[:n])
+
+    def _needs_penalty(self, n) -> bool:
+        return bool((self.h_pen[:n] != 1.0).any())
+
+    def _history(self, n):
+        rows = [self.sched.tokens(int(self.h_sid[i])) for i in range(n)]
+        L = max(len(r) for r in rows)
+        h = torch.full((n, L), -1, dtype=torch.int32)
+        for i, r in enumerate(rows):
+            h[i, : len(r)] = torch.tensor(r, dtype=torch.int32)
+        return h.to(self.device)
+
+    def _prefill(self, n, ntok):
+        self._upload(n, ntok)
+        cu = self.h_cu[: n + 1]
+        max_q = int((cu[1:] - cu[:-1]).max())
+        meta = self._meta("prefill", n, ntok, max_q, int(self.h_ctx[:n].max()))
+        sample_idx = (self.d_cu[1: n + 1] - 1).long()
+        h = self.model.forward(self.d_ids[:ntok], self.d_pos[:ntok], meta, sample_idx)
+        logits = self.model.logits(h)
+        tok, lp = self._sample(logits, n)
+        return tok[:n].cpu(), lp[:n].cpu()
+
+    def _decode(self, n):
+        if self.graphs and not self._needs_penalty(n):
+            bs = next((b for b in sorted(self.graphs) if b >= n), None)
+            if bs is not None:
+                # padding rows: no cache write, empty context, greedy
+                self.h_slots[n:bs] = -1
+                self.h_ctx[n:bs] = 0
+                self.h_ids[n:bs] = 0
+                self.h_pos[n:bs] = 0
+                self.h_temp[n:bs] = 0.0
+                self.h_topk[n:bs] = 0
+                self.h_topp[n:bs] = 1.0
+                self.h_step[n:bs] = 0
+                self.h_seed[n:bs] = 0
+                self._upload(bs, bs)
+                self.graphs[bs].replay()
+                return self.d_tok[:n].cpu(), self.d_lp[:n].cpu()
+        self._upload(n, n)
+        meta = self._meta("decode", n, n, 1, self.cfg.max_model_len)
+        h = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta)
+        logits = self.model.logits(h)
+        tok, lp = self._sample(logits, n)
+        return tok[:n].cpu(), lp[:n].cpu()
+
+    def _decode_body(self, bs):
+        meta = self._meta("decode", bs, bs, 1, self.cfg.max_model_len)
+        h = self.model.forward(self.d_ids[:bs], self.d_pos[:bs], meta)
+        logits = self.model.logits(h)
+        ops.sample(logits, self.d_temp[:bs], self.d_topk[:bs], self.d_topp[:bs],
+                   self.d_seed[:bs], self.d_step[:bs], None, None,
+                   out_tok=self.d_tok[:bs], out_lp=self.d_lp[:bs])
+
+    def _capture_graphs(self):
+        sizes = [b for b in self.cfg.graph_batch_sizes if b <= self.cfg.max_num_seqs]
+        # inert inputs for capture: no cache writes, empty contexts
+        self.d_slots.fill_(-1)
+        self.d_ctx.zero_()
+        self.d_temp.zero_()
+        self.d_topp.fill_(1.0)
+        pool = None
+        stream = torch.cuda.Stream(self.device)
+        stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(stream):
+            for bs in sorted(sizes, reverse=True):
+                for _ in range(2):
+                    self._decode_body(bs)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool, stream=stream):
+                    self._decode_body(bs)
+                pool = g.pool()
+                self.graphs[bs] = g
+        torch.cuda.current_stream(self.device).wait_stream(stream)
+        torch.cuda.synchronize(self.device)
+
+    # ------------------------------------------------------------------ convenience
+    def run_until_done(self, reqs: Optional[List[Request]] = None) -> None:
+        while self.has_work():
+            self.step()
+            if reqs is not None and all(r.finished for r in reqs):
+                break
+
+    def generate(self, prompts: List[List[int]], params: Optional[SamplingParams] = None) -> List[Request]:
+        reqs = [self.add_request(p, params) for p in prompts]
+        self.run_until_done(reqs)
+        return reqs
+
+    def kv_usage(self) -> float:
+        return self.sched.used_blocks() / max(1, self.sched.total_blocks())

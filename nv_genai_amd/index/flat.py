@@ -1,0 +1,181 @@
+"""In-HBM brute-force vector index (kernel K13).
+
+Replaces Milvus-GPU (GPU_IVF_FLAT / FLAT), FAISS ``IndexFlatL2`` and pgvector for the
+reference's retrieval path. Vectors live in one preallocated bf16 [capacity, dim] tensor in
+HBM (1M x 1024 = 2 GB; a 288 GB MI355X holds >100M at this width), scored by the MFMA
+``score`` kernel with the per-row bias channel doing double duty:
+
+* ``l2``: bias = -|x|^2 so the kernel's ``2 q.x - |x|^2`` ranks like -||q - x||^2 (|q|^2 is
+  added back on the host so returned scores are true negative squared distances);
+* deletes: bias = -inf tombstones (no re-packing on delete; compaction is lazy).
+
+Metrics: ``ip`` (inner product), ``cosine`` (vectors/queries pre-normalised, then ip),
+``l2``. Search returns (scores [nq, k], ids [nq, k]) with external int64 ids.
+"""
+from __future__ import annotations
+
+import json
+import os
+from pathlib import Path
+from typing import Optional, Tuple
+
+import torch
+
+from .. import ops
+
+
+class FlatIndex:
+    def __init__(self, dim: int, metric: str = "cosine", device: Optional[str] = None,
+                 capacity: int = 1024, dtype=torch.bfloat16):
+        if metric not in ("ip", "cosine", "l2"):
+            raise ValueError(f"unknown metric {metric}")
+        self.dim, self.metric, self.dtype = dim, metric, dtype
+        self.device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+        self.n = 0
+        self.n_deleted = 0
+        self._alloc(max(capacity, 1))
+        self._id2row = {}
+
+    def _alloc(self, cap: int):
+        X = torch.zeros(cap, self.dim, dtype=self.dtype, device=self.device)
+        bias = torch.full((cap,), float("-inf"), dtype=torch.float32, device=self.device)
+        ids = torch.full((cap,), -1, dtype=torch.int64, device=self.device)
+        if getattr(self, "X", None) is not None and self.n:
+            X[: self.n] = self.X[: self.n]
+            bias[: self.n] = self.bias[: self.n]
+            ids[: self.n] = self.ids[: self.n]
+        self.X, self.bias, self.ids = X, bias, ids
+        self.capacity = cap
+
+    def __len__(self) -> int:
+        return self.n - self.n_deleted
+
+    def _prep(self, v: torch.Tensor) -> torch.Tensor:
+        v = v.to(self.device, torch.float32)
+        if self.metric == "cosine":
+            v = v / v.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+        return v
+
+    def add(self, vecs: torch.Tensor, ids: Optional[torch.Tensor] = None) -> torch.Tensor:
+        vecs = self._prep(vecs)
+        m = vecs.shape[0]
+        if ids is None:
+            start = max(self._id2row.keys(), default=-1) + 1
+            ids = torch.arange(start, start + m, dtype=torch.int64)
+        ids = ids.to(torch.int64).cpu()
+        if self.n + m > self.capacity:
+            cap = self.capacity
+            while cap < self.n + m:
+                cap *= 2
+            self._alloc(cap)
+        r0 = self.n
+        self.X[r0:r0 + m] = vecs.to(self.dtype)
+        if self.metric == "l2":
+            self.bias[r0:r0 + m] = -ops.row_sqnorm(self.X[r0:r0 + m])
+        else:
+            self.bias[r0:r0 + m] = 0.0
+        self.ids[r0:r0 + m] = ids.to(self.device)
+        for j, i in enumerate(ids.tolist()):
+            if i in self._id2row:
+                self._delete_row(self._id2row[i])
+            self._id2row[i] = r0 + j
+        self.n += m
+        return ids
+
+    def add_random(self, n: int, seed: int = 0, chunk: int = 1 << 18) -> None:
+        """Fill with n random unit vectors (synthetic corpus embeddings for benchmarks)."""
+        g = torch.Generator(device=self.device)
+        g.manual_seed(seed)
+        start = max(self._id2row.keys(), default=-1) + 1
+        if self.n + n > self.capacity:
+            self._alloc(self.n + n)
+        for c in range(0, n, chunk):
+            m = min(chunk, n - c)
+            v = torch.randn(m, self.dim, device=self.device, generator=g)
+            v = v / v.norm(dim=-1, keepdim=True)
+            r0 = self.n
+            self.X[r0:r0 + m] = v.to(self.dtype)
+            self.bias[r0:r0 + m] = (-ops.row_sqnorm(self.X[r0:r0 + m])) if self.metric == "l2" else 0.0
+            self.ids[r0:r0 + m] = torch.arange(start + c, start + c + m, device=self.device)
+            self.n += m
+        base = self.n - n
+        self._id2row.update(zip(range(start, start + n), range(base, base + n)))
+
+    def _delete_row(self, r: int):
+        if self.bias[r].item() != float("-inf"):
+            self.bias[r] = float("-inf")
+            self.n_deleted += 1
+
+    def remove(self, ids) -> int:
+        cnt = 0
+        for i in (ids.tolist() if torch.is_tensor(ids) else list(ids)):
+            r = self._id2row.pop(int(i), None)
+            if r is not None:
+                self._delete_row(r)
+                cnt += 1
+        if self.n_deleted > max(1024, self.n // 4):
+            self.compact()
+        return cnt
+
+    def compact(self):
+        keep = torch.nonzero(self.bias[: self.n] != float("-inf")).flatten()
+        m = keep.numel()
+        self.X[:m] = self.X[keep]
+        self.bias[:m] = self.bias[keep]
+        self.ids[:m] = self.ids[keep]
+        self.bias[m: self.n] = float("-inf")
+        self.ids[m: self.n] = -1
+        self.n, self.n_deleted = m, 0
+        self._id2row = {int(i): r for r, i in enumerate(self.ids[:m].tolist())}
+
+    @torch.inference_mode()
+    def search(self, q: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        if q.dim() == 1:
+            q = q.unsqueeze(0)
+        q = self._prep(q)
+        if self.n == 0:
+            nq = q.shape[0]
+            return (torch.empty(nq, 0, device=self.device), torch.empty(nq, 0, dtype=torch.int64, device=self.device))
+        qb = q.to(self.dtype).contiguous()
+        X = self.X[: self.n]
+        if self.metric == "l2":
+            S = ops.score(qb, X, self.bias[: self.n], 2.0)
+        else:
+            S = ops.score(qb, X, self.bias[: self.n], 1.0)
+        k = min(k, self.n)
+        vals, rows = ops.topk(S, k)
+        if self.metric == "l2":
+            vals = vals - q.float().pow(2).sum(-1, keepdim=True)
+        ids = torch.where(rows >= 0, self.ids[rows.clamp_min(0)], torch.full_like(rows, -1))
+        ids = torch.where(torch.isfinite(vals), ids, torch.full_like(ids, -1))
+        return vals, ids
+
+    # ------------------------------------------------------------------ persistence
+    def save(self, path: str) -> None:
+        from safetensors.torch import save_file
+
+        p = Path(path)
+        p.mkdir(parents=True, exist_ok=True)
+        tmp = p / "vectors.safetensors.tmp"
+        save_file({"X": self.X[: self.n].cpu(), "bias": self.bias[: self.n].cpu(),
+                   "ids": self.ids[: self.n].cpu()}, str(tmp))
+        os.replace(tmp, p / "vectors.safetensors")
+        meta = {"dim": self.dim, "metric": self.metric, "n": self.n, "kind": "flat"}
+        (p / "index.json").write_text(json.dumps(meta))
+
+    @classmethod
+    def load(cls, path: str, device: Optional[str] = None) -> "FlatIndex":
+        from safetensors.torch import load_file
+
+        p = Path(path)
+        meta = json.loads((p / "index.json").read_text())
+        t = load_file(str(p / "vectors.safetensors"))
+        idx = cls(meta["dim"], meta["metric"], device, capacity=max(1, meta["n"]))
+        n = meta["n"]
+        idx.X[:n] = t["X"].to(idx.device)
+        idx.bias[:n] = t["bias"].to(idx.device)
+        idx.ids[:n] = t["ids"].to(idx.device)
+        idx.n = n
+        idx.n_deleted = int((t["bias"] == float("-inf")).sum())
+        idx._id2row = {int(i): r for r, i in enumerate(t["ids"].tolist()) if t["bias"][r] != float("-inf")}
+        return idx

@@ -1,0 +1,216 @@
+"""Llama-3 decoder (8B / 70B) on the gfx950 kernel set, tensor-parallel over RCCL.
+
+This is the MI355X-native replacement for the TensorRT-LLM engine inside NIM
+(SURVEY.md §2.B N1). Per layer:
+
+    x_norm = rmsnorm(resid)                          K3  (fused with the residual add)
+    qkv    = x_norm @ Wqkv^T                         K6  hipBLASLt (column-parallel)
+    rope + paged K/V^T cache write                   K4 + K9 (one kernel)
+    attn   = prefill (MFMA flash, paged) | decode (MFMA paged GQA, split-K)   K1 / K2
+    resid += all_reduce(attn @ Wo^T)                 K6 row-parallel + CC1
+    x_norm = rmsnorm(resid)
+    h      = silu(x_norm @ Wg^T) * (x_norm @ Wu^T)   K6 (fused gate|up GEMM) + K5
+    resid += all_reduce(h @ Wd^T)                    K6 row-parallel + CC2
+
+Only the rows that produce a token (the last prompt position of each sequence, every decode
+row) go through the final norm and the vocab-parallel LM head (+ all-gather, CC4).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+
+from .. import ops
+from ..parallel.dist import ParallelContext, get_context, tp_all_gather, tp_all_reduce
+from .config import LlamaConfig
+
+
+@dataclass
+class AttnMeta:
+    """Per-step attention/cache layout (built by the engine from the native scheduler)."""
+
+    kind: str                      # "prefill" | "decode"
+    slots: torch.Tensor            # [T] int32 cache slot of each token (-1 = no write)
+    cu_q: torch.Tensor             # [B+1] int32
+    ctx_lens: torch.Tensor         # [B] int32 keys visible to each sequence
+    block_tables: torch.Tensor     # [B, max_blocks] int32
+    max_q_len: int
+    max_ctx: int
+    decode_ws: Optional[ops.DecodeWorkspace] = None
+
+
+class LlamaModel:
+    def __init__(self, cfg: LlamaConfig, device="cuda", dtype=torch.bfloat16,
+                 pctx: Optional[ParallelContext] = None, seed: int = 0,
+                 weights: Optional[Dict[str, torch.Tensor]] = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.p = pctx or get_context()
+        tp = self.p.tp_size
+        if cfg.heads % tp or cfg.kv_heads % tp or cfg.ffn % tp or cfg.vocab_size % tp:
+            raise ValueError(f"{cfg.name}: dims not divisible by tp={tp}")
+        self.hq = cfg.heads // tp
+        self.hkv = cfg.kv_heads // tp
+        self.D = cfg.head_dim
+        self.ffn = cfg.ffn // tp
+        self.vocab_local = cfg.vocab_size // tp
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        if weights is None:
+            self._random_init(seed)
+        else:
+            self._load(weights)
+        self.cos_sin = ops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta,
+                                        cfg.rope_scaling).to(self.device)
+
+    # ------------------------------------------------------------------ weights
+    def _random_init(self, seed: int):
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed * 1000 + self.p.tp_rank)
+        H = cfg.hidden
+
+        def rnd(*shape, std=0.02):
+            t = torch.empty(*shape, device=dev, dtype=dt)
+            t.normal_(0.0, std, generator=g)
+            return t
+
+        out_std = 0.02 / math.sqrt(2 * cfg.layers)
+        self.embed = rnd(self.vocab_local, H)
+        self.layers: List[Dict[str, torch.Tensor]] = []
+        for _ in range(cfg.layers):
+            self.layers.append({
+                "attn_norm": torch.ones(H, device=dev, dtype=dt),
+                "wqkv": rnd((self.hq + 2 * self.hkv) * self.D, H),
+                "wo": rnd(H, self.hq * self.D, std=out_std),
+                "mlp_norm": torch.ones(H, device=dev, dtype=dt),
+                "wgu": rnd(2 * self.ffn, H),
+                "wd": rnd(H, self.ffn, std=out_std),
+            })
+        self.final_norm = torch.ones(H, device=dev, dtype=dt)
+        self.lm_head = rnd(self.vocab_local, H)
+
+    def _load(self, w: Dict[str, torch.Tensor]):
+        """Load HF-named Llama weights (model.layers.N.self_attn.q_proj.weight, ...),
+        fusing q/k/v and gate/up, and slicing this rank's TP shard."""
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        tp, r = self.p.tp_size, self.p.tp_rank
+
+        def rows(t, n):  # column-parallel shard (output rows)
+            c = t.shape[0] // tp
+            return t[r * c:(r + 1) * c]
+
+        def cols(t):  # row-parallel shard (input columns)
+            c = t.shape[1] // tp
+            return t[:, r * c:(r + 1) * c]
+
+        def get(name):
+            return w[name].to(dev, dt)
+
+        self.embed = rows(get("model.embed_tokens.weight"), 0).contiguous()
+        self.layers = []
+        for i in range(cfg.layers):
+            p = f"model.layers.{i}."
+            q, k, v = get(p + "self_attn.q_proj.weight"), get(p + "self_attn.k_proj.weight"), get(p + "self_attn.v_proj.weight")
+            gt, up = get(p + "mlp.gate_proj.weight"), get(p + "mlp.up_proj.weight")
+            self.layers.append({
+                "attn_norm": get(p + "input_layernorm.weight"),
+                "wqkv": torch.cat([rows(q, 0), rows(k, 0), rows(v, 0)]).contiguous(),
+                "wo": cols(get(p + "self_attn.o_proj.weight")).contiguous(),
+                "mlp_norm": get(p + "post_attention_layernorm.weight"),
+                "wgu": torch.cat([rows(gt, 0), rows(up, 0)]).contiguous(),
+                "wd": cols(get(p + "mlp.down_proj.weight")).contiguous(),
+            })
+        self.final_norm = get("model.norm.weight")
+        head = w.get("lm_head.weight", w["model.embed_tokens.weight"]).to(dev, dt)
+        self.lm_head = rows(head, 0).contiguous()
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        """HF-named weights of this rank (unfused; TP shards are local slices)."""
+        out = {"model.embed_tokens.weight": self.embed, "model.norm.weight": self.final_norm,
+               "lm_head.weight": self.lm_head}
+        qd, kd = self.hq * self.D, self.hkv * self.D
+        for i, L in enumerate(self.layers):
+            p = f"model.layers.{i}."
+            out[p + "input_layernorm.weight"] = L["attn_norm"]
+            out[p + "self_attn.q_proj.weight"] = L["wqkv"][:qd]
+            out[p + "self_attn.k_proj.weight"] = L["wqkv"][qd:qd + kd]
+            out[p + "self_attn.v_proj.weight"] = L["wqkv"][qd + kd:]
+            out[p + "self_attn.o_proj.weight"] = L["wo"]
+            out[p + "post_attention_layernorm.weight"] = L["mlp_norm"]
+            out[p + "mlp.gate_proj.weight"] = L["wgu"][: self.ffn]
+            out[p + "mlp.up_proj.weight"] = L["wgu"][self.ffn:]
+            out[p + "mlp.down_proj.weight"] = L["wd"]
+        return out
+
+    # ------------------------------------------------------------------ cache
+    def allocate_kv_cache(self, num_blocks: int, block_size: int = 64):
+        if block_size != 64:
+            raise ValueError("the gfx950 attention kernels use 64-token KV pages")
+        shape_k = (self.cfg.layers, num_blocks, self.hkv, block_size, self.D)
+        shape_v = (self.cfg.layers, num_blocks, self.hkv, self.D, block_size)
+        # zero-filled: masked keys of a partially filled page must stay finite
+        self.k_cache = torch.zeros(shape_k, device=self.device, dtype=self.dtype)
+        self.v_cache = torch.zeros(shape_v, device=self.device, dtype=self.dtype)
+        return self.k_cache, self.v_cache
+
+    def kv_block_bytes(self, block_size: int = 64) -> int:
+        return 2 * self.cfg.layers * self.hkv * self.D * block_size * torch.finfo(self.dtype).bits // 8
+
+    # ------------------------------------------------------------------ forward
+    def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
+        if self.p.tp_size == 1:
+            return torch.nn.functional.embedding(ids.long(), self.embed)
+        lo = self.p.tp_rank * self.vocab_local
+        local = ids.long() - lo
+        ok = (local >= 0) & (local < self.vocab_local)
+        h = torch.nn.functional.embedding(local.clamp(0, self.vocab_local - 1), self.embed)
+        h = h * ok.unsqueeze(-1).to(h.dtype)
+        return tp_all_reduce(h, self.p)
+
+    def forward(self, ids: torch.Tensor, pos: torch.Tensor, meta: AttnMeta,
+                sample_idx: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Returns the final-normed hidden rows selected by ``sample_idx`` (all rows if None)."""
+        cfg = self.cfg
+        hq, hkv, D = self.hq, self.hkv, self.D
+        resid = self.embed_tokens(ids)
+        T = resid.shape[0]
+        x = ops.rmsnorm(resid, self.layers[0]["attn_norm"], cfg.eps)
+        qdim = hq * D
+        for li, L in enumerate(self.layers):
+            qkv = x @ L["wqkv"].t()
+            ops.rope_cache_(qkv, pos, self.cos_sin, meta.slots, self.k_cache[li],
+                            self.v_cache[li], hq, hkv, D)
+            q = qkv[:, :qdim]
+            if meta.kind == "decode":
+                attn = ops.decode_attention(q, self.k_cache[li], self.v_cache[li],
+                                            meta.block_tables, meta.ctx_lens, hq, hkv,
+                                            meta.max_ctx, self.scale, ws=meta.decode_ws)
+            else:
+                attn = ops.prefill_attention_paged(q, self.k_cache[li], self.v_cache[li],
+                                                   meta.block_tables, meta.cu_q, meta.ctx_lens,
+                                                   hq, hkv, D, meta.max_q_len, self.scale)
+            o = attn @ L["wo"].t()
+            tp_all_reduce(o, self.p)
+            x = ops.add_rmsnorm(resid, o, L["mlp_norm"], cfg.eps)
+            h = ops.silu_mul(x @ L["wgu"].t())
+            d = h @ L["wd"].t()
+            tp_all_reduce(d, self.p)
+            nxt = self.layers[li + 1]["attn_norm"] if li + 1 < len(self.layers) else None
+            if nxt is not None:
+                x = ops.add_rmsnorm(resid, d, nxt, cfg.eps)
+            else:
+                # only rows that sample need the final norm
+                if sample_idx is not None:
+                    rows = resid.index_select(0, sample_idx) + d.index_select(0, sample_idx)
+                    return ops.rmsnorm(rows.contiguous(), self.final_norm, cfg.eps)
+                return ops.add_rmsnorm(resid, d, self.final_norm, cfg.eps)
+        raise RuntimeError("unreachable")
+
+    def logits(self, h: torch.Tensor) -> torch.Tensor:
+        """fp32 logits over the full vocabulary (vocab-parallel head + all-gather)."""
+        lg = (h @ self.lm_head.t()).float()
+        return tp_all_gather(lg, dim=-1, ctx=self.p)

@@ -1,0 +1,234 @@
+"""Operator layer: GPU tensors run the hand-written gfx950 HIP kernels of ``nv_genai_amd._C``;
+CPU tensors run the fp32 PyTorch references in :mod:`nv_genai_amd.ops.reference`.
+
+There is no silent fallback on the GPU: if the extension is missing or fails to load, every
+GPU call raises (so a GPU test can never pass on an eager-PyTorch substitute).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+
+from . import reference as ref
+
+_C = None
+_C_ERR: Optional[BaseException] = None
+try:  # pragma: no cover - depends on the built artefact
+    from .. import _C as _C  # type: ignore
+except BaseException as e:  # noqa: BLE001
+    _C_ERR = e
+
+
+def kernels():
+    """The loaded HIP extension; raises loudly when it is unavailable."""
+    if _C is None:
+        raise RuntimeError(
+            "nv_genai_amd._C (gfx950 HIP kernels) is not loadable: "
+            f"{_C_ERR!r}. Build it with `python -m nv_genai_amd._build`.")
+    return _C
+
+
+def have_kernels() -> bool:
+    return _C is not None
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ------------------------------------------------------------------------- norms
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None):
+    if not _gpu(x):
+        r = ref.rmsnorm(x, w, eps)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    if out is None:
+        out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+    kernels().rmsnorm(out, x, w, float(eps))
+    return out
+
+
+def add_rmsnorm(resid: torch.Tensor, delta: torch.Tensor, w: torch.Tensor, eps: float,
+                out: Optional[torch.Tensor] = None):
+    """resid += delta (in place); returns rmsnorm(resid) * w."""
+    if not _gpu(resid):
+        r = ref.add_rmsnorm(resid, delta, w, eps)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    if out is None:
+        out = torch.empty_like(resid)
+    kernels().add_rmsnorm(out, resid, delta, w, float(eps))
+    return out
+
+
+def layernorm(x, g, b, eps, resid=None, out=None):
+    if not _gpu(x):
+        return ref.layernorm(x, g, b, eps, resid)
+    if out is None:
+        out = torch.empty_like(x)
+    kernels().layernorm(out, x, resid, g, b, float(eps))
+    return out
+
+
+def silu_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None):
+    if not _gpu(x):
+        return ref.silu_mul(x)
+    if out is None:
+        out = torch.empty(x.shape[0], x.shape[1] // 2, dtype=x.dtype, device=x.device)
+    kernels().silu_mul(out, x)
+    return out
+
+
+def bias_gelu_(x: torch.Tensor, bias: Optional[torch.Tensor]):
+    if not _gpu(x):
+        return ref.bias_gelu_(x, bias)
+    kernels().bias_gelu(x, bias)
+    return x
+
+
+# ------------------------------------------------------------------------- rope / kv
+def rope_cache_(qkv, pos, cos_sin, slots, kc, vc, Hq: int, Hkv: int, D: int):
+    if not _gpu(qkv):
+        return ref.rope_cache_(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, D)
+    kernels().rope_cache(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, D)
+    return qkv
+
+
+# ------------------------------------------------------------------------- attention
+class DecodeWorkspace:
+    """Split-K partition buffers for decode attention, sized for (max_seqs, Hq, max_ctx)."""
+
+    def __init__(self, max_seqs: int, Hq: int, Hkv: int, max_ctx: int, device,
+                 pages_per_part: Optional[int] = None):
+        pages = (max_ctx + 63) // 64
+        if pages_per_part is None:
+            pages_per_part = 16
+        self.pages_per_part = max(1, pages_per_part)
+        self.max_ctx = max_ctx
+        nparts = (pages + self.pages_per_part - 1) // self.pages_per_part
+        self.ml = torch.empty(max_seqs * Hq * nparts * 2, dtype=torch.float32, device=device)
+        self.o = torch.empty(max_seqs * Hq * nparts * 128, dtype=torch.float32, device=device)
+
+
+def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, max_ctx, scale,
+                     out=None, ws: Optional[DecodeWorkspace] = None):
+    if not _gpu(q):
+        r = ref.decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, scale, D=kc.shape[3])
+        if out is not None:
+            out[: r.shape[0], : r.shape[1]].copy_(r)
+            return out
+        return r
+    B = ctx_lens.numel()
+    if out is None:
+        out = torch.empty(B, Hq * 128, dtype=q.dtype, device=q.device)
+    if ws is None:
+        ws = DecodeWorkspace(B, Hq, Hkv, max_ctx, q.device,
+                             kernels().decode_pages_per_part(B, Hkv, max_ctx))
+    assert max_ctx <= ws.max_ctx
+    kernels().decode_attention(out, q, kc, vc, block_tables, ctx_lens, Hq, Hkv, int(max_ctx),
+                               float(scale), ws.pages_per_part, ws.ml, ws.o)
+    return out
+
+
+def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D, max_q_len,
+                            scale, out=None, causal=True):
+    if not _gpu(q):
+        r = ref.prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
+                                        scale, causal)
+        if out is not None:
+            out[:, : r.shape[1]].copy_(r)
+            return out
+        return r
+    if out is None:
+        out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
+    kernels().prefill_attention(out, q, None, None, kc, vc, block_tables, cu_q, ctx_lens, Hq,
+                                Hkv, D, int(max_q_len), float(scale), bool(causal))
+    return out
+
+
+def varlen_attention(q, k, v, cu, Hq, Hkv, D, max_len, scale, causal=False, out=None):
+    """Packed variable-length attention (no paging): q/k/v rows share the cu offsets."""
+    if not _gpu(q):
+        return ref.varlen_attention(q, k, v, cu, Hq, Hkv, D, scale, causal)
+    if out is None:
+        out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
+    kernels().prefill_attention(out, q, k, v, None, None, None, cu, None, Hq, Hkv, D,
+                                int(max_len), float(scale), bool(causal))
+    return out
+
+
+# ------------------------------------------------------------------------- sampling
+def sample(logits, temperature, top_k, top_p, seeds, steps, rep_penalty=None, history=None,
+           out_tok=None, out_lp=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Sample one token per row. ``logits`` (fp32, [B, V]) may be modified in place."""
+    if not _gpu(logits):
+        return ref.sample(logits, temperature, top_k, top_p, seeds, steps, rep_penalty, history)
+    B = logits.shape[0]
+    if out_tok is None:
+        out_tok = torch.empty(B, dtype=torch.int32, device=logits.device)
+    if out_lp is None:
+        out_lp = torch.empty(B, dtype=torch.float32, device=logits.device)
+    kernels().sample(logits, temperature, top_k, top_p, rep_penalty, history, seeds, steps,
+                     out_tok, out_lp)
+    return out_tok, out_lp
+
+
+# ------------------------------------------------------------------------- vector search
+def score(Q, X, row_bias=None, dot_scale: float = 1.0, out=None):
+    if not _gpu(X):
+        return ref.score(Q, X, row_bias, dot_scale)
+    if out is None:
+        out = torch.empty(Q.shape[0], X.shape[0], dtype=torch.float32, device=X.device)
+    kernels().score(Q, X, row_bias, out, float(dot_scale))
+    return out
+
+
+TOPK_SEG = 4096
+
+
+def topk(S: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Exact row-wise top-k (descending) of a fp32 score matrix: per-4096 segment select,
+    then a merge select over the segment winners."""
+    k = int(min(k, S.shape[1]))
+    if not _gpu(S):
+        return ref.topk(S, k)
+    C = kernels()
+    rows, n = S.shape
+    nseg = (n + TOPK_SEG - 1) // TOPK_SEG
+    v1 = torch.empty(rows, nseg * k, dtype=torch.float32, device=S.device)
+    i1 = torch.empty(rows, nseg * k, dtype=torch.int64, device=S.device)
+    C.topk(S, None, TOPK_SEG, k, v1, i1)
+    if nseg == 1:
+        return v1, i1
+    v2 = torch.empty(rows, k, dtype=torch.float32, device=S.device)
+    i2 = torch.empty(rows, k, dtype=torch.int64, device=S.device)
+    C.topk(v1, i1, nseg * k, k, v2, i2)
+    return v2, i2
+
+
+def pool_l2norm(hidden, cu, mode: int = 0, normalize: bool = True, out=None):
+    if not _gpu(hidden):
+        return ref.pool_l2norm(hidden, cu, mode, normalize)
+    B = cu.numel() - 1
+    if out is None:
+        out = torch.empty(B, hidden.shape[1], dtype=torch.float32, device=hidden.device)
+    kernels().pool_l2norm(hidden, cu, int(mode), bool(normalize), out)
+    return out
+
+
+def row_sqnorm(X, out=None):
+    if not _gpu(X):
+        return ref.row_sqnorm(X)
+    if out is None:
+        out = torch.empty(X.shape[0], dtype=torch.float32, device=X.device)
+    kernels().row_sqnorm(X, out)
+    return out
+
+
+rope_cos_sin = ref.rope_cos_sin

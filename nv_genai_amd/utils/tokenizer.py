@@ -1,0 +1,180 @@
+"""Tokenizers for the random-init models.
+
+No model hub is reachable, so the framework trains its own tokenizers once, from the
+deterministic synthetic corpus, with HF ``tokenizers`` and caches them under
+``nv_genai_amd/assets/``:
+
+* ``llm_tokenizer.json`` — byte-level BPE (32768 ids) with the Llama-3 chat special tokens
+  (<|begin_of_text|>, <|start_header_id|>, <|end_header_id|>, <|eot_id|>, <|end_of_text|>);
+* ``embed_tokenizer.json`` — BERT WordPiece (30522 ids, [CLS]/[SEP]/[PAD]/[UNK]/[MASK]).
+
+The LLM's embedding / LM-head keep the real Llama-3 vocabulary (128256 rows): ids the
+tokenizer never emits are valid model inputs, and sampled ids >= the tokenizer size are
+folded into range for detokenisation (weights are random, text is synthetic either way).
+"""
+from __future__ import annotations
+
+import os
+import threading
+from functools import lru_cache
+from pathlib import Path
+from typing import Iterable, List, Optional
+
+from tokenizers import Tokenizer, decoders, models, normalizers, pre_tokenizers, processors, trainers
+
+from .synthetic import corpus
+
+ASSETS = Path(__file__).resolve().parent.parent / "assets"
+LLM_SPECIALS = ["<|begin_of_text|>", "<|end_of_text|>", "<|start_header_id|>",
+                "<|end_header_id|>", "<|eot_id|>"]
+BERT_SPECIALS = ["[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]"]
+_LOCK = threading.Lock()
+
+
+def _train_corpus() -> Iterable[str]:
+    return corpus(3000, seed=7)
+
+
+def _build_llm(path: Path, vocab: int = 32768) -> Tokenizer:
+    tok = Tokenizer(models.BPE())
+    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tok.decoder = decoders.ByteLevel()
+    tr = trainers.BpeTrainer(vocab_size=vocab, special_tokens=LLM_SPECIALS,
+                             initial_alphabet=pre_tokenizers.ByteLevel.alphabet(),
+                             show_progress=False)
+    tok.train_from_iterator(_train_corpus(), tr)
+    path.parent.mkdir(parents=True, exist_ok=True)
+    tok.save(str(path))
+    return tok
+
+
+def _build_bert(path: Path, vocab: int = 30522) -> Tokenizer:
+    tok = Tokenizer(models.WordPiece(unk_token="[UNK]"))
+    tok.normalizer = normalizers.BertNormalizer(lowercase=True)
+    tok.pre_tokenizer = pre_tokenizers.BertPreTokenizer()
+    tok.decoder = decoders.WordPiece()
+    tr = trainers.WordPieceTrainer(vocab_size=vocab, special_tokens=BERT_SPECIALS,
+                                   show_progress=False)
+    tok.train_from_iterator(_train_corpus(), tr)
+    cls, sep = tok.token_to_id("[CLS]"), tok.token_to_id("[SEP]")
+    tok.post_processor = processors.TemplateProcessing(
+        single="[CLS] $A [SEP]", pair="[CLS] $A [SEP] $B:1 [SEP]:1",
+        special_tokens=[("[CLS]", cls), ("[SEP]", sep)])
+    path.parent.mkdir(parents=True, exist_ok=True)
+    tok.save(str(path))
+    return tok
+
+
+class LLMTokenizer:
+    """Text <-> ids plus the Llama-3 chat template."""
+
+    def __init__(self, tok: Optional[Tokenizer] = None):
+        if tok is None:
+            p = ASSETS / "llm_tokenizer.json"
+            with _LOCK:
+                tok = Tokenizer.from_file(str(p)) if p.exists() else _build_llm(p)
+        self.tok = tok
+        self.n = tok.get_vocab_size()
+        self.bos_id = tok.token_to_id("<|begin_of_text|>")
+        self.eot_id = tok.token_to_id("<|eot_id|>")
+        self.eos_id = tok.token_to_id("<|end_of_text|>")
+        self.header_start = tok.token_to_id("<|start_header_id|>")
+        self.header_end = tok.token_to_id("<|end_header_id|>")
+
+    @property
+    def stop_ids(self):
+        return (self.eot_id, self.eos_id)
+
+    def encode(self, text: str) -> List[int]:
+        return self.tok.encode(text, add_special_tokens=False).ids
+
+    def encode_batch(self, texts: List[str]) -> List[List[int]]:
+        return [e.ids for e in self.tok.encode_batch(texts, add_special_tokens=False)]
+
+    def decode(self, ids: List[int], skip_special: bool = True) -> str:
+        ids = [i % self.n for i in ids]
+        return self.tok.decode(ids, skip_special_tokens=skip_special)
+
+    def apply_chat_template(self, messages: List[dict], add_generation_prompt: bool = True) -> List[int]:
+        """Llama-3 instruct format:
+        <|begin_of_text|><|start_header_id|>role<|end_header_id|>\n\ncontent<|eot_id|>..."""
+        ids = [self.bos_id]
+        for m in messages:
+            ids.append(self.header_start)
+            ids += self.encode(m.get("role", "user"))
+            ids.append(self.header_end)
+            ids += self.encode("\n\n" + str(m.get("content", "")))
+            ids.append(self.eot_id)
+        if add_generation_prompt:
+            ids.append(self.header_start)
+            ids += self.encode("assistant")
+            ids.append(self.header_end)
+            ids += self.encode("\n\n")
+        return ids
+
+
+class IncrementalDetokenizer:
+    """Streams text for a growing id list without re-decoding from scratch every token:
+    decodes a small window and emits only complete (non-replacement-char) text."""
+
+    def __init__(self, tok: LLMTokenizer, prompt_tail: Optional[List[int]] = None):
+        self.tok = tok
+        self.ids: List[int] = []
+        self.prefix_off = 0
+        self.read_off = 0
+
+    def push(self, tid: int) -> str:
+        self.ids.append(tid)
+        prefix = self.tok.decode(self.ids[self.prefix_off:self.read_off])
+        full = self.tok.decode(self.ids[self.prefix_off:])
+        if full.endswith("�"):
+            return ""
+        delta = full[len(prefix):]
+        self.prefix_off = self.read_off
+        self.read_off = len(self.ids)
+        return delta
+
+
+class EmbedTokenizer:
+    def __init__(self, tok: Optional[Tokenizer] = None, max_len: int = 512):
+        if tok is None:
+            p = ASSETS / "embed_tokenizer.json"
+            with _LOCK:
+                tok = Tokenizer.from_file(str(p)) if p.exists() else _build_bert(p)
+        self.tok = tok
+        self.max_len = max_len
+        self.cls_id = tok.token_to_id("[CLS]")
+        self.sep_id = tok.token_to_id("[SEP]")
+
+    def encode(self, text: str, truncate: str = "END") -> List[int]:
+        ids = self.tok.encode(text).ids
+        return self._trunc(ids, truncate)
+
+    def encode_batch(self, texts: List[str], truncate: str = "END") -> List[List[int]]:
+        return [self._trunc(e.ids, truncate) for e in self.tok.encode_batch(texts)]
+
+    def encode_pair(self, a: str, b: str, truncate: str = "END") -> List[int]:
+        return self._trunc(self.tok.encode(a, b).ids, truncate)
+
+    def _trunc(self, ids: List[int], truncate: str) -> List[int]:
+        if len(ids) <= self.max_len:
+            return ids
+        t = (truncate or "NONE").upper()
+        if t == "END":
+            return ids[: self.max_len - 1] + [self.sep_id]
+        if t == "START":
+            return [self.cls_id] + ids[-(self.max_len - 1):]
+        raise ValueError(f"input of {len(ids)} tokens exceeds {self.max_len} and truncate=NONE")
+
+    def count(self, text: str) -> int:
+        return len(self.tok.encode(text).ids)
+
+
+@lru_cache(maxsize=1)
+def llm_tokenizer() -> LLMTokenizer:
+    return LLMTokenizer()
+
+
+@lru_cache(maxsize=1)
+def embed_tokenizer() -> EmbedTokenizer:
+    return EmbedTokenizer()

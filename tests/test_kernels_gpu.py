@@ -1,0 +1,219 @@
+"""Numerics of every gfx950 HIP kernel against the plain-PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+from nv_genai_amd import ops
+from nv_genai_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(*shape, dev, scale=1.0):
+    return (torch.randn(*shape, device=dev) * scale).to(torch.bfloat16)
+
+
+def _close(a, b, atol, rtol=0.0):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    lim = atol + rtol * b.abs().max().item()
+    assert err <= lim, f"max err {err} > {lim}"
+
+
+@pytest.mark.parametrize("H", [1024, 4096, 8192])
+def test_rmsnorm(gpu, H):
+    torch.manual_seed(0)
+    x, w = _bf(37, H, dev=gpu), _bf(H, dev=gpu)
+    _close(ops.rmsnorm(x, w, 1e-5), ref.rmsnorm(x.cpu(), w.cpu(), 1e-5), 0.05, 0.01)
+    r, d = _bf(37, H, dev=gpu), _bf(37, H, dev=gpu)
+    r_ref = r.cpu().clone()
+    y = ops.add_rmsnorm(r, d, w, 1e-5)
+    y_ref = ref.add_rmsnorm(r_ref, d.cpu(), w.cpu(), 1e-5)
+    _close(r, r_ref, 0.02, 0.01)
+    _close(y, y_ref, 0.05, 0.01)
+
+
+def test_layernorm_gelu_silu(gpu):
+    torch.manual_seed(1)
+    x, r, g, b = _bf(33, 1024, dev=gpu), _bf(33, 1024, dev=gpu), _bf(1024, dev=gpu), _bf(1024, dev=gpu)
+    _close(ops.layernorm(x, g, b, 1e-12, resid=r), ref.layernorm(x.cpu(), g.cpu(), b.cpu(), 1e-12, r.cpu()), 0.06, 0.01)
+    h = _bf(17, 4096, dev=gpu)
+    bias = _bf(4096, dev=gpu)
+    h_ref = h.cpu().clone()
+    ops.bias_gelu_(h, bias)
+    ref.bias_gelu_(h_ref, bias.cpu())
+    _close(h, h_ref, 0.03, 0.01)
+    gu = _bf(19, 2 * 14336, dev=gpu)
+    _close(ops.silu_mul(gu), ref.silu_mul(gu.cpu()), 0.05, 0.01)
+
+
+def _make_cache(nb, Hkv, D, dev):
+    kc = _bf(nb, Hkv, 64, D, dev=dev)
+    vc = _bf(nb, Hkv, D, 64, dev=dev)
+    return kc, vc
+
+
+def test_rope_cache(gpu):
+    torch.manual_seed(2)
+    Hq, Hkv, D, T = 32, 8, 128, 70
+    qkv = _bf(T, (Hq + 2 * Hkv) * D, dev=gpu)
+    pos = torch.randint(0, 4000, (T,), dtype=torch.int32, device=gpu)
+    cs = ops.rope_cos_sin(4096, D).to(gpu)
+    nb = 8
+    kc, vc = _make_cache(nb, Hkv, D, gpu)
+    slots = torch.randperm(nb * 64, device=gpu)[:T].to(torch.int32)
+    slots[5] = -1
+    qkv_r, kc_r, vc_r = qkv.cpu().clone(), kc.cpu().clone(), vc.cpu().clone()
+    ops.rope_cache_(qkv, pos, cs, slots, kc, vc, Hq, Hkv, D)
+    ref.rope_cache_(qkv_r, pos.cpu(), cs.cpu(), slots.cpu(), kc_r, vc_r, Hq, Hkv, D)
+    _close(qkv, qkv_r, 0.03, 0.01)
+    _close(kc, kc_r, 0.03, 0.01)
+    _close(vc, vc_r, 1e-6)
+
+
+def _paged_setup(ctxs, Hkv, D, dev, seed=0):
+    torch.manual_seed(seed)
+    pages = [(c + 63) // 64 for c in ctxs]
+    nb = sum(pages) + 3
+    kc, vc = _make_cache(nb, Hkv, D, dev)
+    perm = torch.randperm(nb).tolist()
+    maxp = max(pages)
+    bt = torch.zeros(len(ctxs), maxp, dtype=torch.int32)
+    k = 0
+    for i, p in enumerate(pages):
+        for j in range(p):
+            bt[i, j] = perm[k]
+            k += 1
+    return kc, vc, bt.to(dev)
+
+
+@pytest.mark.parametrize("G", [4, 8])
+@pytest.mark.parametrize("ppp", [None, 2])
+def test_decode_attention(gpu, G, ppp):
+    Hkv, D = 8 if G == 4 else 1, 128
+    Hq = Hkv * G
+    ctxs = [1, 63, 64, 65, 700, 3001, 128]
+    kc, vc, bt = _paged_setup(ctxs, Hkv, D, gpu)
+    B = len(ctxs)
+    q = _bf(B, Hq * D, dev=gpu)
+    ctx = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
+    scale = 1 / math.sqrt(D)
+    ws = ops.DecodeWorkspace(B, Hq, Hkv, max(ctxs), gpu, ppp)
+    out = ops.decode_attention(q, kc, vc, bt, ctx, Hq, Hkv, max(ctxs), scale, ws=ws)
+    o_ref = ref.decode_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), ctx.cpu(), Hq, Hkv, scale)
+    _close(out, o_ref, 0.02)
+
+
+def test_decode_attention_empty_rows(gpu):
+    Hkv, G, D = 8, 4, 128
+    Hq = Hkv * G
+    kc, vc, bt = _paged_setup([100, 1], Hkv, D, gpu)
+    ctx = torch.tensor([100, 0], dtype=torch.int32, device=gpu)
+    q = _bf(2, Hq * D, dev=gpu)
+    out = ops.decode_attention(q, kc, vc, bt, ctx, Hq, Hkv, 100, 1 / math.sqrt(D))
+    assert torch.isfinite(out.float()).all()
+    assert out[1].abs().max().item() == 0.0
+
+
+def test_prefill_attention_paged(gpu):
+    Hkv, G, D = 8, 4, 128
+    Hq = Hkv * G
+    ctxs = [100, 700, 64, 1, 1500]
+    qls = [100, 300, 64, 1, 129]  # second and last: chunked prefill after a cached prefix
+    kc, vc, bt = _paged_setup(ctxs, Hkv, D, gpu, seed=3)
+    cu = [0]
+    for ql in qls:
+        cu.append(cu[-1] + ql)
+    T = cu[-1]
+    q = _bf(T, Hq * D, dev=gpu)
+    cu_t = torch.tensor(cu, dtype=torch.int32, device=gpu)
+    ctx_t = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
+    scale = 1 / math.sqrt(D)
+    out = ops.prefill_attention_paged(q, kc, vc, bt, cu_t, ctx_t, Hq, Hkv, D, max(qls), scale)
+    o_ref = ref.prefill_attention_paged(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cu_t.cpu(), ctx_t.cpu(), Hq, Hkv, D, scale)
+    _close(out, o_ref, 0.02)
+
+
+@pytest.mark.parametrize("D,H,causal", [(64, 16, False), (128, 8, True)])
+def test_varlen_attention(gpu, D, H, causal):
+    torch.manual_seed(4)
+    lens = [5, 64, 130, 512, 1]
+    cu = [0]
+    for n in lens:
+        cu.append(cu[-1] + n)
+    T = cu[-1]
+    qkv = _bf(T, 3 * H * D, dev=gpu)
+    q, k, v = qkv[:, : H * D], qkv[:, H * D: 2 * H * D], qkv[:, 2 * H * D:]
+    cu_t = torch.tensor(cu, dtype=torch.int32, device=gpu)
+    scale = 1 / math.sqrt(D)
+    out = ops.varlen_attention(q, k, v, cu_t, H, H, D, max(lens), scale, causal)
+    o_ref = ref.varlen_attention(q.cpu(), k.cpu(), v.cpu(), cu_t.cpu(), H, H, D, scale, causal)
+    _close(out, o_ref, 0.02)
+
+
+def test_sample(gpu):
+    torch.manual_seed(5)
+    B, V = 24, 128256
+    logits = torch.randn(B, V, device=gpu) * 3
+    temp = torch.tensor([0.0, 1.0, 0.7, 1.3] * 6, device=gpu)
+    topk = torch.tensor([0, 0, 50, 1, 0, 10] * 4, dtype=torch.int32, device=gpu)
+    topp = torch.tensor([1.0, 0.9, 1.0, 0.5, 0.7, 1.0] * 4, device=gpu)
+    seeds = torch.arange(B, dtype=torch.int64, device=gpu) * 7919
+    steps = torch.arange(B, dtype=torch.int64, device=gpu)
+    lg_cpu = logits.cpu().clone()
+    tok, lp = ops.sample(logits.clone(), temp, topk, topp, seeds, steps)
+    tok_r, lp_r = ref.sample(lg_cpu, temp.cpu(), topk.cpu(), topp.cpu(), seeds.cpu(), steps.cpu())
+    agree = (tok.cpu() == tok_r).float().mean().item()
+    assert agree >= 0.9, f"only {agree:.2f} of draws agree with the reference"
+    same = tok.cpu() == tok_r
+    assert torch.allclose(lp.cpu()[same], lp_r[same], atol=1e-3)
+    # every draw respects its own truncation
+    for b in range(B):
+        xs = lg_cpu[b] / (temp[b].item() if temp[b] > 0 else 1.0)
+        t = int(tok[b])
+        if int(topk[b]) > 0:
+            assert xs[t] >= torch.topk(xs, int(topk[b])).values[-1]
+        if temp[b] <= 0 or int(topk[b]) == 1:
+            assert t == int(torch.argmax(xs))
+
+
+def test_sample_repetition_penalty(gpu):
+    B, V = 2, 1000
+    logits = torch.zeros(B, V, device=gpu)
+    logits[:, 7] = 5.0
+    logits[:, 9] = 4.0
+    hist = torch.tensor([[7, -1], [3, 3]], dtype=torch.int32, device=gpu)
+    pen = torch.tensor([2.0, 2.0], device=gpu)
+    tok, _ = ops.sample(logits, torch.zeros(B, device=gpu), torch.zeros(B, dtype=torch.int32, device=gpu),
+                        torch.ones(B, device=gpu), torch.zeros(B, dtype=torch.int64, device=gpu),
+                        torch.zeros(B, dtype=torch.int64, device=gpu), pen, hist)
+    assert tok.tolist() == [9, 7]
+
+
+@pytest.mark.parametrize("nq,N,D", [(1, 5000, 1024), (37, 70000, 1024), (64, 12345, 384), (130, 4096, 256)])
+def test_score_topk(gpu, nq, N, D):
+    torch.manual_seed(6)
+    Q = _bf(nq, D, dev=gpu)
+    X = _bf(N, D, dev=gpu)
+    bias = torch.randn(N, device=gpu)
+    S = ops.score(Q, X, bias, 0.5)
+    S_ref = ref.score(Q.cpu(), X.cpu(), bias.cpu(), 0.5)
+    _close(S, S_ref, 2e-3, 1e-4)
+    for k in (1, 4, 100):
+        v, i = ops.topk(S, k)
+        v_ref, _ = torch.topk(S.cpu(), k, dim=1)
+        _close(v, v_ref, 0.0)
+        # indices point at the reported scores
+        assert torch.equal(torch.gather(S.cpu(), 1, i.cpu()), v.cpu())
+
+
+def test_pool(gpu):
+    torch.manual_seed(7)
+    lens = [3, 1, 77]
+    cu = torch.tensor([0, 3, 4, 81], dtype=torch.int32, device=gpu)
+    h = _bf(81, 1024, dev=gpu)
+    for mode in (0, 1):
+        _close(ops.pool_l2norm(h, cu, mode, True), ref.pool_l2norm(h.cpu(), cu.cpu(), mode, True), 1e-4)
+    X = _bf(1000, 1024, dev=gpu)
+    _close(ops.row_sqnorm(X), ref.row_sqnorm(X.cpu()), 0.05, 1e-4)
