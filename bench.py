@@ -77,6 +77,11 @@ def main():
     docs = SyntheticDocStore(args.index_size)
     rag = RAGPipeline(llm, emb, index, docs, top_k=args.top_k)
     gen = TextGen(seed=100 + rank)
+    # random-init encoder outputs are highly anisotropic (every query would retrieve the same
+    # few passages and share KV through the prefix cache): PCA-whiten them so concurrent
+    # queries retrieve different passages, as with a trained embedding model
+    cal = TextGen(seed=999)
+    emb.calibrate_whitening([cal.question() for _ in range(4096)])
     params = SamplingParams(temperature=0.2, top_p=0.7, max_tokens=args.max_tokens, ignore_eos=True)
     if gpu:
         torch.cuda.synchronize()
@@ -152,6 +157,8 @@ def main():
         "prefill_s": round(llm.stats["prefill_time"], 3),
         "decode_s": round(llm.stats["decode_time"], 3),
         "setup_s": round(setup_s, 1),
+        "prefix_cache_hit_blocks": int(llm.sched.prefix_hits()),
+        "distinct_docs_retrieved": len({d for r in results for d in r.doc_ids}),
     }
     if rank == 0:
         s = json.dumps(line)

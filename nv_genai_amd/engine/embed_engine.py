@@ -38,6 +38,32 @@ class EmbeddingEngine:
         self.lock = threading.Lock()
         self.dim = self.cfg.hidden
         self.stats = {"calls": 0, "texts": 0, "tokens": 0}
+        self.center: Optional[torch.Tensor] = None
+        self.whiten: Optional[torch.Tensor] = None
+
+    def calibrate_center(self, texts: Sequence[str], input_type: str = "query") -> torch.Tensor:
+        """Isotropy correction: subtract the mean embedding of a calibration set and
+        re-normalise every output. Random-init encoders emit nearly collinear vectors (every
+        query would retrieve the same passages); centring restores per-query diversity
+        without changing the work done per request."""
+        self.center = None
+        self.center = self.embed(texts, input_type).mean(0)
+        return self.center
+
+    def calibrate_whitening(self, texts: Sequence[str], input_type: str = "query",
+                            eps: float = 1e-4) -> None:
+        """PCA whitening ("BERT-whitening"): y = normalise((x - mu) W), W = C^-1/2 from a
+        calibration set (use >= dim texts for a full-rank estimate). Makes a random-init
+        encoder's embeddings isotropic so retrieval over a synthetic index is as diverse as
+        with a trained model; one [n, d] x [d, d] GEMM per call."""
+        self.center, self.whiten = None, None
+        x = self.embed(texts, input_type).double()
+        mu = x.mean(0)
+        xc = x - mu
+        cov = xc.T @ xc / max(1, x.shape[0] - 1)
+        lam, U = torch.linalg.eigh(cov)
+        W = U @ torch.diag(1.0 / torch.sqrt(lam.clamp_min(0) + eps * lam.max())) @ U.T
+        self.center, self.whiten = mu.float(), W.float()
 
     @property
     def name(self) -> str:
@@ -82,6 +108,11 @@ class EmbeddingEngine:
                                          pos.to(self.device, non_blocking=True),
                                          cu_t.to(self.device, non_blocking=True),
                                          max(len(seqs[b]) for b in batch), tt)
+                if self.center is not None and not self.cfg.num_labels:
+                    res = res - self.center
+                    if self.whiten is not None:
+                        res = res @ self.whiten
+                    res = res / res.norm(dim=-1, keepdim=True).clamp_min(1e-12)
                 out[torch.tensor(batch, device=self.device)] = res
                 self.stats["tokens"] += tok
             self.stats["calls"] += 1

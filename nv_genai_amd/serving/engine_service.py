@@ -1,0 +1,181 @@
+"""Background driver for the LLM engine: one thread steps the continuous-batching engine,
+any number of producer threads / asyncio tasks submit requests and consume token streams.
+
+Failure handling (SURVEY.md §5.3 "new framework"): an exception inside a step fails every
+in-flight stream with an error instead of hanging it; a watchdog flags a step that runs longer
+than ``watchdog_s`` (readiness then reports unhealthy); consumers can cancel (client
+disconnect) and the request is aborted in the scheduler, freeing its KV blocks.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import queue
+import threading
+import time
+from typing import AsyncIterator, Iterator, List, Optional
+
+from ..engine.llm_engine import LLMEngine, Request, SamplingParams
+
+log = logging.getLogger(__name__)
+_END = object()
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class StreamHandle:
+    """Token-delta stream of one request (sync and async iteration).
+
+    The engine thread pushes deltas into a thread-safe queue; an asyncio consumer attaches
+    its own asyncio.Queue (fed through ``call_soon_threadsafe``) so no executor thread is
+    parked per open stream."""
+
+    def __init__(self, service: "EngineService"):
+        self.service = service
+        self.q: "queue.Queue" = queue.Queue()
+        self.request: Optional[Request] = None
+        self.error: Optional[BaseException] = None
+        self.done = threading.Event()
+        self._lock = threading.Lock()
+        self._loop: Optional[asyncio.AbstractEventLoop] = None
+        self._aq: Optional[asyncio.Queue] = None
+
+    def _put(self, item):
+        with self._lock:
+            if self._aq is not None:
+                self._loop.call_soon_threadsafe(self._aq.put_nowait, item)
+            else:
+                self.q.put(item)
+
+    # engine-thread side
+    def _on_token(self, req: Request, delta: str):
+        if delta:
+            self._put(delta)
+        if req.finished and not self.done.is_set():
+            self.done.set()
+            self._put(_END)
+
+    def _fail(self, err: BaseException):
+        self.error = err
+        if not self.done.is_set():
+            self.done.set()
+            self._put(_END)
+
+    # consumer side
+    def __iter__(self) -> Iterator[str]:
+        while True:
+            item = self.q.get()
+            if item is _END:
+                if self.error is not None:
+                    raise EngineError(str(self.error))
+                return
+            yield item
+
+    async def aiter(self) -> AsyncIterator[str]:
+        with self._lock:
+            self._loop = asyncio.get_running_loop()
+            self._aq = asyncio.Queue()
+            while True:
+                try:
+                    self._aq.put_nowait(self.q.get_nowait())
+                except queue.Empty:
+                    break
+        while True:
+            item = await self._aq.get()
+            if item is _END:
+                if self.error is not None:
+                    raise EngineError(str(self.error))
+                return
+            yield item
+
+    def text(self) -> str:
+        return "".join(self)
+
+    def cancel(self):
+        if self.request is not None and not self.done.is_set():
+            self.service.abort(self.request.id)
+            self._fail(EngineError("cancelled"))
+
+    @property
+    def finish_reason(self) -> Optional[str]:
+        return None if self.request is None else self.request.finish_reason
+
+    @property
+    def usage(self) -> dict:
+        r = self.request
+        if r is None:
+            return {}
+        return {"prompt_tokens": len(r.prompt_ids), "completion_tokens": len(r.output_ids),
+                "total_tokens": len(r.prompt_ids) + len(r.output_ids)}
+
+
+class EngineService:
+    def __init__(self, engine: LLMEngine, watchdog_s: float = 300.0, name: str = "llm"):
+        self.engine = engine
+        self.watchdog_s = watchdog_s
+        self.name = name
+        self.cv = threading.Condition()
+        self.handles = {}
+        self.running = True
+        self.step_started: Optional[float] = None
+        self.last_error: Optional[str] = None
+        self.steps = 0
+        self.thread = threading.Thread(target=self._loop, name=f"{name}-engine", daemon=True)
+        self.thread.start()
+
+    def submit(self, prompt_ids: List[int], params: SamplingParams) -> StreamHandle:
+        h = StreamHandle(self)
+        with self.cv:
+            req = self.engine.add_request(prompt_ids, params, on_token=h._on_token)
+            h.request = req
+            self.handles[req.id] = h
+            self.cv.notify()
+        return h
+
+    def abort(self, rid: int):
+        self.engine.abort(rid)
+        self.handles.pop(rid, None)
+
+    def _loop(self):
+        while self.running:
+            with self.cv:
+                while self.running and not self.engine.has_work():
+                    self.cv.wait(timeout=0.5)
+            if not self.running:
+                break
+            try:
+                self.step_started = time.monotonic()
+                done = self.engine.step()
+                self.steps += 1
+                for r in done:
+                    self.handles.pop(r.id, None)
+            except Exception as e:  # noqa: BLE001 - fail the streams, keep serving
+                log.exception("engine step failed")
+                self.last_error = repr(e)
+                for rid, h in list(self.handles.items()):
+                    try:
+                        self.engine.abort(rid)
+                    except Exception:  # noqa: BLE001
+                        pass
+                    h._fail(e)
+                self.handles.clear()
+            finally:
+                self.step_started = None
+
+    def healthy(self) -> bool:
+        st = self.step_started
+        return self.thread.is_alive() and not (st is not None and time.monotonic() - st > self.watchdog_s)
+
+    def metrics(self) -> dict:
+        e = self.engine
+        return {"running": e.sched.num_running(), "waiting": e.sched.num_waiting(),
+                "kv_usage": e.kv_usage(), "steps": self.steps, **e.stats,
+                "prefix_hit_blocks": e.sched.prefix_hits(), "preemptions": e.sched.preemptions()}
+
+    def shutdown(self):
+        self.running = False
+        with self.cv:
+            self.cv.notify_all()
+        self.thread.join(timeout=5)
