@@ -1,0 +1,133 @@
+"""HTTP connectors speaking the OpenAI / NIM wire protocol (SURVEY.md §2.B N1-N3 contracts):
+
+* :class:`ChatClient`  — ``POST {base}/chat/completions`` (``stream=true`` -> SSE
+  ``data: {...}`` chunks terminated by ``data: [DONE]``), temperature / top_p / max_tokens /
+  stop / seed forwarded (RetrievalAugmentedGeneration/common/utils.py:265-290);
+* :class:`EmbeddingsClient` — ``POST {base}/embeddings`` with ``input_type`` query|passage and
+  ``truncate`` (experimental/fm-asr-streaming-rag/chain-server/common.py:64-101);
+* :class:`RerankClient` — ``POST {base}/ranking`` ``{query:{text}, passages:[{text}]}`` ->
+  ``rankings[{index, logit}]`` (experimental/fm-asr-streaming-rag/chain-server/retriever.py:287-306).
+
+They work against this framework's model server and against any OpenAI-compatible endpoint.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Iterator, List, Optional, Sequence
+
+import requests
+
+from .local import Messages, normalize_messages
+
+
+def _base(url: str) -> str:
+    url = url.rstrip("/")
+    if not url.startswith("http"):
+        url = "http://" + url
+    if not url.endswith("/v1"):
+        url += "/v1"
+    return url
+
+
+def _headers(api_key: Optional[str]):
+    h = {"Content-Type": "application/json", "Accept": "application/json"}
+    key = api_key or os.environ.get("NVIDIA_API_KEY") or os.environ.get("OPENAI_API_KEY")
+    if key:
+        h["Authorization"] = f"Bearer {key}"
+    return h
+
+
+class ChatClient:
+    def __init__(self, base_url: str, model: str = "meta/llama3-8b-instruct",
+                 temperature: float = 0.2, top_p: float = 0.7, max_tokens: int = 1024,
+                 stop: Sequence[str] = (), seed: Optional[int] = None,
+                 api_key: Optional[str] = None, timeout: float = 600.0, headers: Optional[dict] = None):
+        self.base = _base(base_url)
+        self.model = model
+        self.defaults = dict(temperature=temperature, top_p=top_p, max_tokens=max_tokens,
+                             stop=list(stop), seed=seed)
+        self.api_key = api_key
+        self.timeout = timeout
+        self.extra_headers = headers or {}
+
+    def _body(self, messages: Messages, stream: bool, **kw) -> dict:
+        b = {"model": self.model, "messages": normalize_messages(messages), "stream": stream}
+        for k, v in {**self.defaults, **{k: v for k, v in kw.items() if v is not None}}.items():
+            if v is None or (k == "stop" and not v):
+                continue
+            b[k] = v
+        return b
+
+    def stream(self, messages: Messages, **kw) -> Iterator[str]:
+        with requests.post(f"{self.base}/chat/completions", json=self._body(messages, True, **kw),
+                           headers={**_headers(self.api_key), **self.extra_headers},
+                           stream=True, timeout=self.timeout) as r:
+            r.raise_for_status()
+            for line in r.iter_lines(decode_unicode=True):
+                if not line or not line.startswith("data:"):
+                    continue
+                payload = line[5:].strip()
+                if payload == "[DONE]":
+                    break
+                chunk = json.loads(payload)
+                for ch in chunk.get("choices", []):
+                    delta = ch.get("delta", {}).get("content")
+                    if delta:
+                        yield delta
+
+    def invoke(self, messages: Messages, **kw) -> str:
+        r = requests.post(f"{self.base}/chat/completions", json=self._body(messages, False, **kw),
+                          headers={**_headers(self.api_key), **self.extra_headers}, timeout=self.timeout)
+        r.raise_for_status()
+        return r.json()["choices"][0]["message"]["content"]
+
+    __call__ = invoke
+
+
+class EmbeddingsClient:
+    def __init__(self, base_url: str, model: str = "snowflake/arctic-embed-l", truncate: str = "END",
+                 api_key: Optional[str] = None, timeout: float = 120.0, batch_size: int = 256):
+        self.base = _base(base_url)
+        self.model = model
+        self.truncate = truncate
+        self.api_key = api_key
+        self.timeout = timeout
+        self.batch_size = batch_size
+
+    def _embed(self, texts: Sequence[str], input_type: str) -> List[List[float]]:
+        out: List[List[float]] = []
+        for i in range(0, len(texts), self.batch_size):
+            body = {"input": list(texts[i:i + self.batch_size]), "model": self.model,
+                    "input_type": input_type, "truncate": self.truncate,
+                    "encoding_format": "float"}
+            r = requests.post(f"{self.base}/embeddings", json=body, headers=_headers(self.api_key),
+                              timeout=self.timeout)
+            r.raise_for_status()
+            data = sorted(r.json()["data"], key=lambda d: d["index"])
+            out += [d["embedding"] for d in data]
+        return out
+
+    def embed_query(self, text: str) -> List[float]:
+        return self._embed([text], "query")[0]
+
+    def embed_documents(self, texts: Sequence[str]) -> List[List[float]]:
+        return self._embed(texts, "passage")
+
+
+class RerankClient:
+    def __init__(self, base_url: str, model: str = "nv-rerank-qa-mistral-4b:1", top_n: int = 4,
+                 api_key: Optional[str] = None, timeout: float = 120.0):
+        self.base = _base(base_url)
+        self.model = model
+        self.top_n = top_n
+        self.api_key = api_key
+        self.timeout = timeout
+
+    def rank(self, query: str, passages: Sequence[str]) -> List[dict]:
+        body = {"model": self.model, "query": {"text": query},
+                "passages": [{"text": p} for p in passages]}
+        r = requests.post(f"{self.base}/ranking", json=body, headers=_headers(self.api_key),
+                          timeout=self.timeout)
+        r.raise_for_status()
+        return r.json()["rankings"]

@@ -1,0 +1,77 @@
+"""Vision-language client (Neva-22B "is it a graph?", DePlot chart->table,
+examples/multimodal_rag/llm/llm_client.py:37-42).
+
+Images go as ``HumanMessage`` content with an ``image_url`` base64 JPEG data URI to any
+OpenAI-compatible vision endpoint (``VLM_SERVER_URL`` / ``APP_VLM_SERVERURL``), with the Neva
+steer labels (creativity / quality / complexity / verbosity) in the text. Without a configured
+endpoint :class:`ImageHeuristics` answers locally from the image bytes alone (format, size,
+a colour-histogram "chart-likeness" guess), so ingestion still produces searchable text.
+"""
+from __future__ import annotations
+
+import base64
+import os
+import struct
+from typing import Optional
+
+import requests
+
+
+def image_size(data: bytes):
+    """(format, width, height) for PNG / JPEG / GIF bytes, else (fmt, 0, 0)."""
+    if data[:8] == b"\x89PNG\r\n\x1a\n" and len(data) >= 24:
+        w, h = struct.unpack(">II", data[16:24])
+        return "png", w, h
+    if data[:2] == b"\xff\xd8":
+        i = 2
+        while i + 9 < len(data):
+            if data[i] != 0xFF:
+                i += 1
+                continue
+            marker = data[i + 1]
+            if marker in (0xC0, 0xC1, 0xC2):
+                h, w = struct.unpack(">HH", data[i + 5:i + 9])
+                return "jpeg", w, h
+            seg = struct.unpack(">H", data[i + 2:i + 4])[0]
+            i += 2 + seg
+        return "jpeg", 0, 0
+    if data[:6] in (b"GIF87a", b"GIF89a"):
+        w, h = struct.unpack("<HH", data[6:10])
+        return "gif", w, h
+    return "unknown", 0, 0
+
+
+class VisionClient:
+    def __init__(self, base_url: str, model: str = "ai-neva-22b", timeout: float = 120.0):
+        from .http import _base
+
+        self.base = _base(base_url)
+        self.model = model
+        self.timeout = timeout
+
+    def describe(self, image: bytes, prompt: str = "Describe this image in detail", **steer) -> str:
+        fmt, _, _ = image_size(image)
+        b64 = base64.b64encode(image).decode()
+        labels = ",".join(f"{k}:{v}" for k, v in steer.items())
+        text = prompt + (f" [labels: {labels}]" if labels else "")
+        body = {"model": self.model, "max_tokens": 1024, "messages": [{"role": "user", "content": [
+            {"type": "text", "text": text},
+            {"type": "image_url", "image_url": {"url": f"data:image/{'jpeg' if fmt != 'png' else 'png'};base64,{b64}"}}]}]}
+        r = requests.post(f"{self.base}/chat/completions", json=body, timeout=self.timeout)
+        r.raise_for_status()
+        return r.json()["choices"][0]["message"]["content"]
+
+
+class ImageHeuristics:
+    """Endpoint-free fallback."""
+
+    model = "local-image-heuristics"
+
+    def describe(self, image: bytes, prompt: str = "", **steer) -> str:
+        fmt, w, h = image_size(image)
+        return f"An embedded {fmt} image of {w}x{h} pixels ({len(image)} bytes)."
+
+
+def get_vision_client(model: str = "ai-neva-22b"):
+    url = os.environ.get("VLM_SERVER_URL") or os.environ.get("APP_VLM_SERVERURL")
+    return VisionClient(url, model) if url else ImageHeuristics()

@@ -99,7 +99,8 @@ class EngineConfig:
 class LLMEngine:
     def __init__(self, cfg: EngineConfig = EngineConfig(), device: Optional[str] = None,
                  pctx: Optional[ParallelContext] = None, model: Optional[LlamaModel] = None,
-                 tokenizer: Optional[LLMTokenizer] = None, model_cfg: Optional[LlamaConfig] = None):
+                 tokenizer: Optional[LLMTokenizer] = None, model_cfg: Optional[LlamaConfig] = None,
+                 weights: Optional[dict] = None):
         self.cfg = cfg
         self.p = pctx or get_context()
         if device is None:
@@ -107,7 +108,8 @@ class LLMEngine:
                 "cuda" if torch.cuda.is_available() else "cpu")
         self.device = torch.device(device)
         self.mcfg = model_cfg or llama_config(cfg.model, max_position=max(cfg.max_model_len, 256))
-        self.model = model or LlamaModel(self.mcfg, self.device, pctx=self.p, seed=cfg.seed)
+        self.model = model or LlamaModel(self.mcfg, self.device, pctx=self.p, seed=cfg.seed,
+                                         weights=weights)
         self.tok = tokenizer or llm_tokenizer()
         self.stop_ids = set(self.tok.stop_ids) | set(self.mcfg.eos_ids)
         self.gpu = self.device.type == "cuda"

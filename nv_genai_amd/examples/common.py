@@ -1,0 +1,72 @@
+"""Helpers shared by the example chains: traced LLM streaming, ingestion, retrieval."""
+from __future__ import annotations
+
+import logging
+import os
+import uuid
+from typing import Iterator, List, Optional, Sequence
+
+from ..chain_server import utils
+from ..index.vectorstore import Document
+from ..observability.tracing import TracingCallback, get_tracer
+from ..rag.loaders import load_file
+
+log = logging.getLogger(__name__)
+NO_CONTEXT = "No response generated from LLM, make sure your query is relavent to the ingested document."
+NO_DOCS = "No response generated from LLM, make sure you have ingested document from the Knowledge Base Tab."
+
+
+class TracedExample:
+    """Gives every example a callback handler (the reference's
+    ``langchain_instrumentation_class_wrapper`` sets ``self.cb_handler``)."""
+
+    def __init__(self):
+        self.cb_handler = TracingCallback(get_tracer("chain-server"))
+
+    def stream_llm(self, messages, **kwargs) -> Iterator[str]:
+        llm = utils.get_llm(**kwargs)
+        rid = uuid.uuid4().hex
+        self.cb_handler.on_llm_start(rid, messages, **{k: v for k, v in kwargs.items() if v is not None})
+        out: List[str] = []
+        try:
+            for chunk in llm.stream(messages):
+                self.cb_handler.on_llm_new_token(rid, chunk)
+                out.append(chunk)
+                yield chunk
+        except Exception as e:
+            self.cb_handler.on_llm_error(rid, e)
+            raise
+        self.cb_handler.on_llm_end(rid, "".join(out))
+
+    def invoke_llm(self, messages, **kwargs) -> str:
+        return "".join(self.stream_llm(messages, **kwargs))
+
+    def retrieve(self, vs, query: str, k: int, threshold: Optional[float] = None):
+        rid = uuid.uuid4().hex
+        self.cb_handler.on_retriever_start(rid, query)
+        if threshold is None:
+            res = vs.similarity_search_with_score(query, k)
+        else:
+            res = vs.similarity_search_with_relevance_scores(query, k, threshold)
+        self.cb_handler.on_retriever_end(rid, res)
+        return res
+
+
+def ingest_file(vs, filepath: str, filename: str, splitter=None, metadata: Optional[dict] = None,
+                allowed: Optional[Sequence[str]] = None) -> int:
+    if allowed is not None and not filename.lower().endswith(tuple(allowed)):
+        raise ValueError(f"{filename} is not a valid Text, PDF or Markdown file")
+    docs = load_file(filepath, filename)
+    if not docs:
+        log.warning("No documents available to process!")
+        return 0
+    for d in docs:
+        d.metadata.update(metadata or {})
+    splitter = splitter or utils.get_text_splitter()
+    chunks = splitter.split_documents(docs)
+    vs.add_documents(chunks)
+    return len(chunks)
+
+
+def context_from(docs, sep: str = "\n\n") -> str:
+    return "".join(d.page_content + sep for d in docs)

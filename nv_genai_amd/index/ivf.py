@@ -1,0 +1,181 @@
+"""IVF-Flat index (SURVEY.md §2.B N4 / kernel K14): the Milvus ``GPU_IVF_FLAT`` the
+reference configures (nlist 64, nprobe 16 — RetrievalAugmentedGeneration/common/
+configuration.py:38-47, utils.py:198-203).
+
+* training: k-means on the GPU — assignment is the MFMA ``score`` kernel + exact top-1
+  (``topk`` kernel) against the centroids, centroid update is a scatter-add;
+* storage: vectors re-ordered by list into one contiguous bf16 slab with per-list offsets,
+  so a probe scans contiguous HBM;
+* search: coarse top-nprobe over centroids (batched over queries), then per query a
+  gather-free scan of its probed list ranges with the same score + top-k kernels.
+
+Flat search of a batch of queries reads the whole index once for the batch; IVF reads
+nprobe/nlist of it per query — so IVF wins for small batches / latency, flat for big batches.
+"""
+from __future__ import annotations
+
+import json
+import os
+from pathlib import Path
+from typing import Optional, Tuple
+
+import torch
+
+from .. import ops
+
+
+def kmeans(X: torch.Tensor, k: int, iters: int = 10, seed: int = 0, metric: str = "cosine") -> torch.Tensor:
+    """k-means (spherical for cosine/ip) over bf16 rows X [n, d]; returns fp32 centroids [k, d]."""
+    n = X.shape[0]
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    C = X[torch.randperm(n, generator=g)[:k].to(X.device)].float()
+    for _ in range(iters):
+        a = assign(X, C, metric)
+        sums = torch.zeros_like(C).index_add_(0, a, X.float())
+        cnt = torch.bincount(a, minlength=k).float().unsqueeze(1)
+        empty = cnt.squeeze(1) == 0
+        C = torch.where(empty.unsqueeze(1), C, sums / cnt.clamp_min(1))
+        if metric in ("cosine", "ip"):
+            C = C / C.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+    return C
+
+
+def assign(X: torch.Tensor, C: torch.Tensor, metric: str = "cosine", chunk: int = 1 << 18) -> torch.Tensor:
+    """Nearest centroid of every row (MFMA score kernel with centroids as the 'queries')."""
+    Cb = C.to(X.dtype).contiguous()
+    bias = -ops.row_sqnorm(Cb) if metric == "l2" else None
+    out = []
+    for s in range(0, X.shape[0], chunk):
+        xs = X[s:s + chunk].contiguous()
+        # rows of xs are the queries: S[i, c] = <x_i, c> (- |c|^2/2 via bias for l2)
+        S = ops.score(xs, Cb, None if bias is None else bias * 0.5, 1.0)
+        out.append(ops.topk(S, 1)[1][:, 0])
+    return torch.cat(out)
+
+
+class IVFFlatIndex:
+    def __init__(self, dim: int, nlist: int = 64, nprobe: int = 16, metric: str = "cosine",
+                 device: Optional[str] = None, dtype=torch.bfloat16):
+        self.dim, self.nlist, self.nprobe, self.metric, self.dtype = dim, nlist, nprobe, metric, dtype
+        self.device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+        self.centroids: Optional[torch.Tensor] = None
+        self.X = torch.zeros(0, dim, dtype=dtype, device=self.device)
+        self.ids = torch.zeros(0, dtype=torch.int64, device=self.device)
+        self.bias = torch.zeros(0, dtype=torch.float32, device=self.device)
+        self.offsets = torch.zeros(nlist + 1, dtype=torch.int64)
+        self._pending = []  # vectors added before training
+
+    def __len__(self):
+        return int(torch.isfinite(self.bias).sum().item()) + sum(v.shape[0] for v, _ in self._pending)
+
+    def _prep(self, v: torch.Tensor) -> torch.Tensor:
+        v = v.to(self.device, torch.float32)
+        if self.metric == "cosine":
+            v = v / v.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+        return v
+
+    @property
+    def is_trained(self) -> bool:
+        return self.centroids is not None
+
+    def train(self, vecs: torch.Tensor, iters: int = 10, seed: int = 0):
+        X = self._prep(vecs).to(self.dtype)
+        k = min(self.nlist, X.shape[0])
+        self.nlist = k
+        self.centroids = kmeans(X, k, iters, seed, self.metric)
+        self.offsets = torch.zeros(k + 1, dtype=torch.int64)
+        pend, self._pending = self._pending, []
+        for v, i in pend:
+            self.add(v, i)
+
+    def add(self, vecs: torch.Tensor, ids: torch.Tensor) -> None:
+        if not self.is_trained:
+            self._pending.append((vecs, ids))
+            if sum(v.shape[0] for v, _ in self._pending) >= 39 * self.nlist:
+                allv = torch.cat([self._prep(v) for v, _ in self._pending])
+                self.train(allv)
+            return
+        X = self._prep(vecs).to(self.dtype)
+        a = assign(X, self.centroids, self.metric)
+        # merge into the list-sorted slab
+        cur_list = torch.repeat_interleave(torch.arange(self.nlist), self.offsets[1:] - self.offsets[:-1]).to(self.device)
+        allX = torch.cat([self.X, X])
+        allI = torch.cat([self.ids, ids.to(self.device, torch.int64)])
+        allB = torch.cat([self.bias, (-ops.row_sqnorm(X)) if self.metric == "l2" else torch.zeros(X.shape[0], device=self.device)])
+        lists = torch.cat([cur_list, a])
+        order = torch.argsort(lists, stable=True)
+        self.X, self.ids, self.bias = allX[order].contiguous(), allI[order], allB[order]
+        cnt = torch.bincount(lists, minlength=self.nlist).cpu()
+        self.offsets = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(cnt, 0)])
+
+    def remove(self, ids) -> int:
+        ids_t = torch.as_tensor(list(ids) if not torch.is_tensor(ids) else ids, dtype=torch.int64, device=self.device)
+        hit = torch.isin(self.ids, ids_t) & torch.isfinite(self.bias)
+        self.bias[hit] = float("-inf")
+        return int(hit.sum().item())
+
+    @torch.inference_mode()
+    def search(self, q: torch.Tensor, k: int, nprobe: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        if q.dim() == 1:
+            q = q.unsqueeze(0)
+        q = self._prep(q)
+        nq = q.shape[0]
+        if not self.is_trained:
+            # brute force over pending vectors
+            from .flat import FlatIndex
+
+            f = FlatIndex(self.dim, self.metric, str(self.device))
+            for v, i in self._pending:
+                f.add(v, i)
+            return f.search(q, k)
+        nprobe = min(nprobe or self.nprobe, self.nlist)
+        qb = q.to(self.dtype).contiguous()
+        cS = ops.score(qb, self.centroids.to(self.dtype).contiguous(), None, 1.0)
+        _, probes = ops.topk(cS, nprobe)
+        probes = probes.cpu()
+        off = self.offsets
+        vals = torch.full((nq, k), float("-inf"), device=self.device)
+        out_ids = torch.full((nq, k), -1, dtype=torch.int64, device=self.device)
+        for i in range(nq):
+            rng = [(int(off[p]), int(off[p + 1])) for p in probes[i].tolist() if off[p + 1] > off[p]]
+            if not rng:
+                continue
+            rows = torch.cat([torch.arange(a, b) for a, b in rng]).to(self.device)
+            Xs = self.X.index_select(0, rows)
+            scale = 2.0 if self.metric == "l2" else 1.0
+            S = ops.score(qb[i:i + 1], Xs, self.bias.index_select(0, rows), scale)
+            kk = min(k, rows.numel())
+            v, r = ops.topk(S, kk)
+            if self.metric == "l2":
+                v = v - q[i].pow(2).sum()
+            vals[i, :kk] = v[0]
+            out_ids[i, :kk] = torch.where(torch.isfinite(v[0]), self.ids[rows[r[0]]], torch.full_like(r[0], -1))
+        return vals, out_ids
+
+    def save(self, path: str):
+        from safetensors.torch import save_file
+
+        p = Path(path)
+        p.mkdir(parents=True, exist_ok=True)
+        t = {"X": self.X.cpu(), "ids": self.ids.cpu(), "bias": self.bias.cpu(), "offsets": self.offsets}
+        if self.centroids is not None:
+            t["centroids"] = self.centroids.cpu()
+        tmp = p / "vectors.safetensors.tmp"
+        save_file(t, str(tmp))
+        os.replace(tmp, p / "vectors.safetensors")
+        (p / "index.json").write_text(json.dumps({"kind": "ivf_flat", "dim": self.dim, "nlist": self.nlist,
+                                                   "nprobe": self.nprobe, "metric": self.metric}))
+
+    @classmethod
+    def load(cls, path: str, device: Optional[str] = None) -> "IVFFlatIndex":
+        from safetensors.torch import load_file
+
+        p = Path(path)
+        m = json.loads((p / "index.json").read_text())
+        t = load_file(str(p / "vectors.safetensors"))
+        idx = cls(m["dim"], m["nlist"], m["nprobe"], m["metric"], device)
+        idx.X, idx.ids, idx.bias = t["X"].to(idx.device), t["ids"].to(idx.device), t["bias"].to(idx.device)
+        idx.offsets = t["offsets"]
+        if "centroids" in t:
+            idx.centroids = t["centroids"].to(idx.device)
+        return idx

@@ -1,0 +1,208 @@
+"""LangChain-``VectorStore``-shaped facade over the in-HBM index + docstore: the surface the
+reference's chains call (``add_documents``, ``similarity_search*``, ``as_retriever`` with
+``similarity_score_threshold``, ``delete``; RetrievalAugmentedGeneration/common/utils.py:211-468,
+examples/nvidia_api_catalog/chains.py:117-127), with named collections
+(``COLLECTION_NAME`` / ``conv_store``), filename bookkeeping and snapshot persistence.
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple
+
+import torch
+
+from .docstore import DocStore
+from .flat import FlatIndex
+from .ivf import IVFFlatIndex
+
+
+@dataclass
+class Document:
+    page_content: str
+    metadata: Dict[str, Any] = field(default_factory=dict)
+
+
+def _embed_docs(embedder, texts: Sequence[str]) -> torch.Tensor:
+    if hasattr(embedder, "embed_documents_tensor"):
+        return embedder.embed_documents_tensor(texts)
+    if hasattr(embedder, "embed") and hasattr(embedder, "dim"):
+        return embedder.embed(texts, "passage")
+    return torch.tensor(embedder.embed_documents(list(texts)), dtype=torch.float32)
+
+
+def _embed_queries(embedder, texts: Sequence[str]) -> torch.Tensor:
+    if hasattr(embedder, "embed_query_tensor"):
+        return embedder.embed_query_tensor(texts)
+    if hasattr(embedder, "embed") and hasattr(embedder, "dim"):
+        return embedder.embed(texts, "query")
+    return torch.tensor([embedder.embed_query(t) for t in texts], dtype=torch.float32)
+
+
+class VectorStore:
+    def __init__(self, embedder, dim: int, index_type: str = "flat", metric: str = "cosine",
+                 device: Optional[str] = None, nlist: int = 64, nprobe: int = 16,
+                 name: str = "default", persist_dir: Optional[str] = None):
+        self.embedder = embedder
+        self.dim = dim
+        self.name = name
+        self.metric = metric
+        self.index_type = index_type
+        if index_type == "ivf_flat":
+            self.index = IVFFlatIndex(dim, nlist, nprobe, metric, device)
+        else:
+            self.index = FlatIndex(dim, metric, device)
+        self.docs = DocStore()
+        self.lock = threading.RLock()
+        self.persist_dir = persist_dir
+        if persist_dir and (Path(persist_dir) / "index.json").exists():
+            self.load(persist_dir)
+
+    def __len__(self):
+        return len(self.docs)
+
+    # ------------------------------------------------------------------ write
+    def add_texts(self, texts: Sequence[str], metadatas: Optional[Sequence[dict]] = None,
+                  embeddings: Optional[torch.Tensor] = None) -> List[int]:
+        texts = list(texts)
+        if not texts:
+            return []
+        vecs = embeddings if embeddings is not None else _embed_docs(self.embedder, texts)
+        with self.lock:
+            ids = self.docs.new_ids(len(texts))
+            self.index.add(vecs, torch.tensor(ids, dtype=torch.int64))
+            self.docs.add(ids, texts, metadatas)
+        if self.persist_dir:
+            self.save(self.persist_dir)
+        return ids
+
+    def add_documents(self, documents: Sequence[Document]) -> List[int]:
+        return self.add_texts([d.page_content for d in documents], [d.metadata for d in documents])
+
+    def delete(self, ids: Iterable[int]) -> int:
+        ids = list(ids)
+        with self.lock:
+            n = self.index.remove(ids)
+            self.docs.remove(ids)
+        if self.persist_dir:
+            self.save(self.persist_dir)
+        return n
+
+    def delete_by_filename(self, filename: str) -> bool:
+        ids = self.docs.ids_for("filename", filename) or self.docs.ids_for("source", filename)
+        if not ids:
+            return False
+        self.delete(ids)
+        return True
+
+    def get_filenames(self) -> List[str]:
+        out = self.docs.filenames()
+        if not out:
+            seen = []
+            for m in self.docs.meta.values():
+                s = m.get("source")
+                if s and s not in seen:
+                    seen.append(s)
+            out = [os.path.basename(s) for s in seen]
+        return out
+
+    # ------------------------------------------------------------------ read
+    def similarity_search_with_score_batch(self, queries: Sequence[str], k: int = 4
+                                           ) -> List[List[Tuple[Document, float]]]:
+        if len(self.docs) == 0:
+            return [[] for _ in queries]
+        q = _embed_queries(self.embedder, queries)
+        with self.lock:
+            vals, ids = self.index.search(q, k)
+            vals, ids = vals.cpu().tolist(), ids.cpu().tolist()
+            out = []
+            for vs, ds in zip(vals, ids):
+                row = []
+                for v, d in zip(vs, ds):
+                    if d < 0 or d not in self.docs.texts:
+                        continue
+                    row.append((Document(self.docs.get(d), dict(self.docs.metadata(d), doc_id=d)), float(v)))
+                out.append(row)
+        return out
+
+    def similarity_search_with_score(self, query: str, k: int = 4) -> List[Tuple[Document, float]]:
+        return self.similarity_search_with_score_batch([query], k)[0]
+
+    def similarity_search(self, query: str, k: int = 4) -> List[Document]:
+        return [d for d, _ in self.similarity_search_with_score(query, k)]
+
+    def relevance(self, score: float) -> float:
+        """Map a raw score to relevance like LangChain's euclidean relevance function for
+        unit vectors, 1 - ||q - x|| / sqrt(2) (FAISS default store in the reference)."""
+        if self.metric == "l2":
+            return 1.0 - max(0.0, -score) ** 0.5 / 2 ** 0.5
+        if self.metric == "cosine":
+            return 1.0 - max(0.0, 2.0 - 2.0 * score) ** 0.5 / 2 ** 0.5
+        return score
+
+    def similarity_search_with_relevance_scores(self, query: str, k: int = 4,
+                                                score_threshold: Optional[float] = None):
+        res = [(d, self.relevance(s)) for d, s in self.similarity_search_with_score(query, k)]
+        if score_threshold is not None:
+            res = [(d, s) for d, s in res if s >= score_threshold]
+        return res
+
+    def as_retriever(self, search_type: str = "similarity", search_kwargs: Optional[dict] = None):
+        return Retriever(self, search_type, search_kwargs or {})
+
+    # ------------------------------------------------------------------ persistence
+    def save(self, path: str):
+        with self.lock:
+            self.index.save(path)
+            self.docs.save(path)
+            (Path(path) / "store.json").write_text(json.dumps(
+                {"name": self.name, "dim": self.dim, "metric": self.metric, "index_type": self.index_type}))
+
+    def load(self, path: str):
+        p = Path(path)
+        kind = json.loads((p / "index.json").read_text()).get("kind", "flat")
+        dev = str(self.index.device)
+        self.index = IVFFlatIndex.load(path, dev) if kind == "ivf_flat" else FlatIndex.load(path, dev)
+        self.docs = DocStore.load(path)
+
+
+class Retriever:
+    """``vs.as_retriever(search_type=..., search_kwargs={k, score_threshold})``."""
+
+    def __init__(self, store: VectorStore, search_type: str, search_kwargs: dict):
+        self.store = store
+        self.search_type = search_type
+        self.k = int(search_kwargs.get("k", 4))
+        self.score_threshold = search_kwargs.get("score_threshold")
+
+    def invoke(self, query: str) -> List[Document]:
+        if self.search_type == "similarity_score_threshold":
+            return [d for d, _ in self.store.similarity_search_with_relevance_scores(
+                query, self.k, self.score_threshold)]
+        return self.store.similarity_search(query, self.k)
+
+    get_relevant_documents = invoke
+
+    def invoke_with_scores(self, query: str):
+        return self.store.similarity_search_with_score(query, self.k)
+
+
+_STORES: Dict[str, VectorStore] = {}
+_STORES_LOCK = threading.Lock()
+
+
+def get_store(name: str, factory) -> VectorStore:
+    with _STORES_LOCK:
+        vs = _STORES.get(name)
+        if vs is None:
+            vs = factory(name)
+            _STORES[name] = vs
+        return vs
+
+
+def reset_stores():
+    with _STORES_LOCK:
+        _STORES.clear()

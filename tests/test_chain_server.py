@@ -1,0 +1,145 @@
+"""Contract tests of the chain server against the reference's golden wire format, with
+deterministic fake backends (hash embedder + fake LLM) on CPU."""
+import json
+import os
+from pathlib import Path
+
+import pytest
+
+GOLDEN = Path(__file__).parent / "fixtures" / "golden"
+
+
+@pytest.fixture()
+def client(tmp_path, monkeypatch):
+    monkeypatch.setenv("APP_LLM_MODELENGINE", "fake")
+    monkeypatch.setenv("APP_EMBEDDINGS_MODELENGINE", "hash")
+    monkeypatch.setenv("APP_EMBEDDINGS_DIMENSIONS", "256")
+    monkeypatch.setenv("EXAMPLE_NAME", os.environ.get("TEST_EXAMPLE", "developer_rag"))
+    monkeypatch.setenv("INGESTED_CSV_FILES_LIST", str(tmp_path / "ingested_csv_files.txt"))
+    from fastapi.testclient import TestClient
+
+    from nv_genai_amd.chain_server import server, utils
+
+    utils.reset()
+    monkeypatch.setattr(server, "UPLOAD_DIR", str(tmp_path / "uploads"))
+    server.app.example = None
+    with TestClient(server.app) as c:
+        yield c
+    utils.reset()
+    server.app.example = None
+
+
+def _frames(text):
+    assert text.endswith("\n\n")
+    parts = text.split("\n\n")[:-1]
+    for p in parts:
+        assert p.startswith("data: ")
+    return [json.loads(p[6:]) for p in parts]
+
+
+def _upload(client, name, content):
+    return client.post("/documents", files={"file": (name, content.encode(), "text/plain")})
+
+
+def test_health(client):
+    r = client.get("/health")
+    assert r.status_code == 200 and r.json() == {"message": "Service is up."}
+
+
+def test_golden_frame_shape_matches_reference():
+    ref = _frames(open(GOLDEN / "rag_response.json").read().strip() + "\n\n")
+    assert ref[-1]["choices"][0]["finish_reason"] == "[DONE]"
+    assert set(ref[0]) == {"id", "choices"}
+    assert set(ref[0]["choices"][0]) == {"index", "message", "finish_reason"}
+
+
+def test_generate_llm_chain_sse_format(client):
+    body = {"messages": [{"role": "user", "content": "Tell me about Paris"}], "use_knowledge_base": False}
+    r = client.post("/generate", json=body)
+    assert r.status_code == 200
+    assert r.headers["content-type"].startswith("text/event-stream")
+    frames = _frames(r.text)
+    ref = _frames(open(GOLDEN / "llm_response.json").read().strip() + "\n\n")
+    assert len({f["id"] for f in frames}) == 1
+    for f, g in zip(frames, ref):
+        assert f.keys() == g.keys() and f["choices"][0].keys() == g["choices"][0].keys()
+    assert frames[-1]["choices"][0] == {"index": 0, "message": {"role": "assistant", "content": ""},
+                                        "finish_reason": "[DONE]"}
+    assert "".join(f["choices"][0]["message"]["content"] for f in frames)
+    # compact separators exactly like pydantic v2 / the golden file
+    assert r.text.startswith('data: {"id":"')
+
+
+def test_ingest_search_list_delete(client):
+    text = ("The Eiffel Tower is located in Paris and was completed in 1889. "
+            "It is made of wrought iron and is 330 metres tall.\n\n" * 3)
+    r = _upload(client, "eiffel.txt", text)
+    assert r.status_code == 200 and r.json() == json.load(open(GOLDEN / "documents_ingest-docs.json"))
+    r = _upload(client, "other.txt", "Completely unrelated text about ocean tides and the moon.")
+    assert r.status_code == 200
+    r = client.get("/documents")
+    assert r.status_code == 200
+    # developer_rag keeps the reference quirk: filename minus its last 4 characters
+    assert sorted(r.json()["documents"]) == ["eiffel", "other"]
+    r = client.post("/search", json={"query": "How tall is the Eiffel Tower in Paris?", "top_k": 4})
+    assert r.status_code == 200
+    chunks = r.json()["chunks"]
+    assert chunks and set(chunks[0]) == {"content", "filename", "score"}
+    assert "Eiffel" in chunks[0]["content"]
+    r = client.post("/generate", json={"messages": [{"role": "user", "content": "How tall is the Eiffel Tower?"}],
+                                       "use_knowledge_base": True, "max_tokens": 8})
+    frames = _frames(r.text)
+    assert frames[-1]["choices"][0]["finish_reason"] == "[DONE]"
+    r = client.delete("/documents", params={"filename": "eiffel"})
+    assert r.status_code == 200 and r.json() == {"message": "Document eiffel deleted successfully"}
+    assert client.get("/documents").json()["documents"] == ["other"]
+    r = client.delete("/documents", params={"filename": "missing"})
+    assert r.status_code == 500
+
+
+@pytest.mark.parametrize("patch,status", [
+    ({"temperature": 0.0}, 422), ({"temperature": 1.5}, 422), ({"top_p": 0.05}, 422),
+    ({"max_tokens": 2000}, 422), ({"max_tokens": -1}, 422), ({"stop": ["x" * 300]}, 422),
+    ({"use_knowledge_base": "maybe"}, 422), ({"messages": [{"role": "robot", "content": "hi"}]}, 422),
+    ({"messages": [{"role": "user", "content": "x" * 131073}]}, 422),
+    ({"temperature": 1.0, "top_p": 0.1, "max_tokens": 0, "stop": ["a"]}, 200),
+])
+def test_prompt_limits(client, patch, status):
+    body = {"messages": [{"role": "user", "content": "hi"}], "use_knowledge_base": False}
+    body.update(patch)
+    r = client.post("/generate", json=body)
+    assert r.status_code == status
+    if status == 422:
+        for err in r.json()["detail"]:
+            assert "input" not in err  # the 422 handler strips the echoed input
+
+
+def test_search_limits(client):
+    assert client.post("/search", json={"query": "q", "top_k": 26}).status_code == 422
+    assert client.post("/search", json={"query": "q", "top_k": 0}).status_code == 200
+
+
+def test_sanitize_html(client):
+    from nv_genai_amd.chain_server.sanitize import clean
+
+    assert clean("<script>alert(1)</script>hello") == "alert(1)hello"
+    assert clean("<b>bold</b> & <i>it</i>") == "<b>bold</b> &amp; <i>it</i>"
+    assert clean("plain text") == "plain text"
+
+
+def test_error_frame_when_llm_fails(client, monkeypatch):
+    from nv_genai_amd.chain_server import utils
+    from nv_genai_amd.connectors.fake import FakeChatModel
+
+    utils.register_runtime("fake_llm", FakeChatModel(fail=True))
+    r = client.post("/generate", json={"messages": [{"role": "user", "content": "hi"}], "use_knowledge_base": False})
+    frames = _frames(r.text)
+    assert frames[-1]["choices"][0]["finish_reason"] == "[DONE]"
+    assert "Error from chain server" in frames[-1]["choices"][0]["message"]["content"]
+
+
+def test_metrics_and_ready(client):
+    client.post("/generate", json={"messages": [{"role": "user", "content": "hi"}], "use_knowledge_base": False})
+    r = client.get("/metrics")
+    assert r.status_code == 200 and "chain_server_generate_requests_total" in r.text
+    assert client.get("/health/ready").json()["ready"] is True
