@@ -147,6 +147,8 @@ class LLMEngine:
         self.h_pen = hbuf(S, dtype=torch.float32)
         self._np = [b.numpy() for b in (self.h_ids, self.h_pos, self.h_slots, self.h_cu,
                                          self.h_ctx, self.h_bt, self.h_sid, self.h_smp)]
+        (self.n_temp, self.n_topk, self.n_topp, self.n_seed, self.n_step, self.n_pen) = (
+            b.numpy() for b in (self.h_temp, self.h_topk, self.h_topp, self.h_seed, self.h_step, self.h_pen))
         dev = self.device
 
         def dbuf(*shape, dtype=torch.int32):
@@ -216,15 +218,13 @@ class LLMEngine:
             if kind == 0:
                 return []
             t0 = time.perf_counter()
-            reqs = [self.requests[int(sid[i])] for i in range(n)]
-            for i, r in enumerate(reqs):
-                p = r.params
-                self.h_temp[i] = p.temperature
-                self.h_topk[i] = p.top_k
-                self.h_topp[i] = p.top_p
-                self.h_seed[i] = r.seed
-                self.h_step[i] = len(r.output_ids)
-                self.h_pen[i] = p.repetition_penalty
+            reqs = [self.requests[int(s)] for s in sid[:n].tolist()]
+            self.n_temp[:n] = [r.params.temperature for r in reqs]
+            self.n_topk[:n] = [r.params.top_k for r in reqs]
+            self.n_topp[:n] = [r.params.top_p for r in reqs]
+            self.n_seed[:n] = [r.seed for r in reqs]
+            self.n_step[:n] = [len(r.output_ids) for r in reqs]
+            self.n_pen[:n] = [r.params.repetition_penalty for r in reqs]
             if kind == 2:
                 toks, lps = self._decode(n)
                 self.stats["decode_steps"] += 1
@@ -240,12 +240,78 @@ class LLMEngine:
             self.stats[key] += time.perf_counter() - t0
             now = time.perf_counter()
             done = []
-            for i, r in enumerate(reqs):
-                if not smp[i]:
-                    continue
-                if self._emit(r, toks[i], lps[i], now):
+            for i, (r, s) in enumerate(zip(reqs, smp[:n].tolist())):
+                if s and self._emit(r, toks[i], lps[i], now):
                     done.append(r)
             return done
+
+    # ------------------------------------------------------------------ tensor parallel
+    # Rank 0 of a TP group drives: it schedules, then broadcasts the step layout (one int32
+    # payload over RCCL) so every rank runs the same forward; the collectives inside the
+    # model (row-parallel all-reduces, vocab all-gather) then line up. Followers loop in
+    # run_follower() until the driver broadcasts a stop header.
+    @property
+    def is_driver(self) -> bool:
+        return self.p.tp_size == 1 or self.p.tp_rank == 0
+
+    def _tp_src(self) -> int:
+        return self.p.rank - self.p.tp_rank
+
+    def _bcast(self, t: torch.Tensor) -> torch.Tensor:
+        import torch.distributed as dist
+
+        dev = self.device if self.p.backend == "nccl" else torch.device("cpu")
+        x = t.to(dev)
+        dist.broadcast(x, src=self._tp_src(), group=self.p.tp_group)
+        return x
+
+    def _sync_step(self, kind: int, n: int, ntok: int, max_q: int, max_ctx: int, bs: int) -> None:
+        """Driver: publish the step (header + packed int buffers) to the TP group."""
+        if self.p.tp_size == 1:
+            return
+        hdr = torch.tensor([kind, n, ntok, max_q, max_ctx, bs, 0, 0], dtype=torch.int64)
+        self._bcast(hdr)
+        if kind < 0:
+            return
+        rows = max(n, bs)
+        toks = max(ntok, bs)
+        payload = torch.cat([self.h_ids[:toks], self.h_pos[:toks], self.h_slots[:toks],
+                             self.h_cu[: rows + 1], self.h_ctx[:rows], self.h_bt[:rows].reshape(-1)])
+        self._bcast(payload)
+
+    def _recv_step(self):
+        hdr = self._bcast(torch.zeros(8, dtype=torch.int64)).cpu().tolist()
+        kind, n, ntok, max_q, max_ctx, bs = hdr[:6]
+        if kind < 0:
+            return kind, 0, 0, 0, 0, 0
+        rows, toks = max(n, bs), max(ntok, bs)
+        size = 3 * toks + (rows + 1) + rows + rows * self.max_blocks
+        payload = self._bcast(torch.zeros(size, dtype=torch.int32)).cpu()
+        o = 0
+        for buf, m in ((self.h_ids, toks), (self.h_pos, toks), (self.h_slots, toks), (self.h_cu, rows + 1),
+                       (self.h_ctx, rows)):
+            buf[:m] = payload[o:o + m]
+            o += m
+        self.h_bt[:rows] = payload[o:o + rows * self.max_blocks].view(rows, self.max_blocks)
+        return kind, n, ntok, max_q, max_ctx, bs
+
+    def run_follower(self) -> None:
+        """Non-driver TP ranks: execute every step the driver publishes."""
+        while True:
+            kind, n, ntok, max_q, max_ctx, bs = self._recv_step()
+            if kind < 0:
+                return
+            if kind == 1:
+                self._prefill_compute(n, ntok, max_q, max_ctx)
+            elif bs:
+                self._upload(bs, bs)
+                self.graphs[bs].replay()
+            else:
+                self._decode_eager(n)
+
+    def stop_followers(self) -> None:
+        if self.p.tp_size > 1 and self.is_driver:
+            self._sync_step(-1, 0, 0, 0, 0, 0)
 
     def _emit(self, r: Request, tok: int, lp: float, now: float) -> bool:
         if r.first_token_time is None:
@@ -327,15 +393,20 @@ class LLMEngine:
         return h.to(self.device)
 
     def _prefill(self, n, ntok):
-        self._upload(n, ntok)
-        cu = self.h_cu[: n + 1]
+        cu = self._np[3][: n + 1]
         max_q = int((cu[1:] - cu[:-1]).max())
-        meta = self._meta("prefill", n, ntok, max_q, int(self.h_ctx[:n].max()))
-        sample_idx = (self.d_cu[1: n + 1] - 1).long()
-        h = self.model.forward(self.d_ids[:ntok], self.d_pos[:ntok], meta, sample_idx)
-        logits = self.model.logits(h)
+        max_ctx = int(self._np[4][:n].max())
+        self._sync_step(1, n, ntok, max_q, max_ctx, 0)
+        logits = self._prefill_compute(n, ntok, max_q, max_ctx)
         tok, lp = self._sample(logits, n)
         return tok[:n].cpu(), lp[:n].cpu()
+
+    def _prefill_compute(self, n, ntok, max_q, max_ctx):
+        self._upload(n, ntok)
+        meta = self._meta("prefill", n, ntok, max_q, max_ctx)
+        sample_idx = (self.d_cu[1: n + 1] - 1).long()
+        h = self.model.forward(self.d_ids[:ntok], self.d_pos[:ntok], meta, sample_idx)
+        return self.model.logits(h)
 
     def _decode(self, n):
         if self.graphs and not self._needs_penalty(n):
@@ -351,15 +422,20 @@ class LLMEngine:
                 self.h_topp[n:bs] = 1.0
                 self.h_step[n:bs] = 0
                 self.h_seed[n:bs] = 0
+                self._sync_step(2, n, n, 1, self.cfg.max_model_len, bs)
                 self._upload(bs, bs)
                 self.graphs[bs].replay()
                 return self.d_tok[:n].cpu(), self.d_lp[:n].cpu()
+        self._sync_step(2, n, n, 1, self.cfg.max_model_len, 0)
+        logits = self._decode_eager(n)
+        tok, lp = self._sample(logits, n)
+        return tok[:n].cpu(), lp[:n].cpu()
+
+    def _decode_eager(self, n):
         self._upload(n, n)
         meta = self._meta("decode", n, n, 1, self.cfg.max_model_len)
         h = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta)
-        logits = self.model.logits(h)
-        tok, lp = self._sample(logits, n)
-        return tok[:n].cpu(), lp[:n].cpu()
+        return self.model.logits(h)
 
     def _decode_body(self, bs):
         meta = self._meta("decode", bs, bs, 1, self.cfg.max_model_len)

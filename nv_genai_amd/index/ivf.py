@@ -108,7 +108,15 @@ class IVFFlatIndex:
         cnt = torch.bincount(lists, minlength=self.nlist).cpu()
         self.offsets = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(cnt, 0)])
 
+    def _ensure_trained(self):
+        """Train on whatever was added so far (k-means wants ~39 points per list, so adds
+        are buffered until then; a search / save / remove forces training earlier)."""
+        if not self.is_trained and self._pending:
+            allv = torch.cat([self._prep(v) for v, _ in self._pending])
+            self.train(allv)
+
     def remove(self, ids) -> int:
+        self._ensure_trained()
         ids_t = torch.as_tensor(list(ids) if not torch.is_tensor(ids) else ids, dtype=torch.int64, device=self.device)
         hit = torch.isin(self.ids, ids_t) & torch.isfinite(self.bias)
         self.bias[hit] = float("-inf")
@@ -120,14 +128,9 @@ class IVFFlatIndex:
             q = q.unsqueeze(0)
         q = self._prep(q)
         nq = q.shape[0]
+        self._ensure_trained()
         if not self.is_trained:
-            # brute force over pending vectors
-            from .flat import FlatIndex
-
-            f = FlatIndex(self.dim, self.metric, str(self.device))
-            for v, i in self._pending:
-                f.add(v, i)
-            return f.search(q, k)
+            return (torch.empty(nq, 0, device=self.device), torch.empty(nq, 0, dtype=torch.int64, device=self.device))
         nprobe = min(nprobe or self.nprobe, self.nlist)
         qb = q.to(self.dtype).contiguous()
         cS = ops.score(qb, self.centroids.to(self.dtype).contiguous(), None, 1.0)
@@ -155,6 +158,7 @@ class IVFFlatIndex:
     def save(self, path: str):
         from safetensors.torch import save_file
 
+        self._ensure_trained()
         p = Path(path)
         p.mkdir(parents=True, exist_ok=True)
         t = {"X": self.X.cpu(), "ids": self.ids.cpu(), "bias": self.bias.cpu(), "offsets": self.offsets}

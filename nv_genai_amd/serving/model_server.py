@@ -1,0 +1,310 @@
+"""OpenAI / NIM-compatible model server (SURVEY.md §7.1 ``model_server``): the endpoints the
+reference's connectors (ChatNVIDIA, NVIDIAEmbeddings, NeMo Retriever reranking) call, served
+by this framework's engines on MI355X.
+
+* ``POST /v1/chat/completions`` — Llama-3 chat template, SSE streaming (``chat.completion.chunk``
+  frames then ``data: [DONE]``) or one JSON response; temperature / top_p / top_k / max_tokens /
+  stop / seed / repetition_penalty / ignore_eos / logprobs;
+* ``POST /v1/completions`` — raw prompt completion (same knobs);
+* ``POST /v1/embeddings`` — ``input`` str|list, ``input_type`` query|passage, ``truncate``
+  END|START|NONE, float or base64 encoding; requests are merged by a dynamic batcher;
+* ``POST /v1/ranking`` — ``{query:{text}, passages:[{text}]}`` -> ``rankings[{index, logit}]``;
+* ``GET /v1/models``, ``GET /v1/health/ready``, ``GET /v1/health/live``, ``GET /metrics``.
+
+``python -m nv_genai_amd.serving.model_server --llm llama3-8b --embed arctic-embed-l --port 8000``
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import base64
+import json
+import logging
+import os
+import struct
+import time
+import uuid
+from typing import Any, Dict, List, Optional, Union
+
+from fastapi import FastAPI, Request
+from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
+from pydantic import BaseModel, Field
+
+from ..engine.llm_engine import SamplingParams
+from ..observability.metrics import Registry
+from ..observability.tracing import get_tracer
+
+log = logging.getLogger(__name__)
+
+
+class ChatMessage(BaseModel):
+    role: str = "user"
+    content: Union[str, List[Dict[str, Any]]] = ""
+
+
+class ChatRequest(BaseModel):
+    model: str = ""
+    messages: List[ChatMessage]
+    temperature: float = Field(0.2, ge=0.0, le=2.0)
+    top_p: float = Field(0.7, gt=0.0, le=1.0)
+    top_k: int = Field(0, ge=0)
+    max_tokens: int = Field(1024, ge=1)
+    stop: Optional[Union[str, List[str]]] = None
+    seed: Optional[int] = None
+    stream: bool = False
+    repetition_penalty: float = Field(1.0, gt=0.0)
+    ignore_eos: bool = False
+    logprobs: bool = False
+
+
+class CompletionRequest(BaseModel):
+    model: str = ""
+    prompt: Union[str, List[str]]
+    temperature: float = Field(0.2, ge=0.0, le=2.0)
+    top_p: float = Field(0.7, gt=0.0, le=1.0)
+    top_k: int = Field(0, ge=0)
+    max_tokens: int = Field(16, ge=1)
+    stop: Optional[Union[str, List[str]]] = None
+    seed: Optional[int] = None
+    stream: bool = False
+    repetition_penalty: float = Field(1.0, gt=0.0)
+    ignore_eos: bool = False
+
+
+class EmbeddingRequest(BaseModel):
+    input: Union[str, List[str]]
+    model: str = ""
+    input_type: str = "passage"
+    truncate: str = "END"
+    encoding_format: str = "float"
+
+
+class RankText(BaseModel):
+    text: str
+
+
+class RankingRequest(BaseModel):
+    model: str = ""
+    query: RankText
+    passages: List[RankText]
+    truncate: str = "END"
+
+
+def _params(r) -> SamplingParams:
+    stop = [r.stop] if isinstance(r.stop, str) else list(r.stop or [])
+    return SamplingParams(temperature=r.temperature, top_p=r.top_p, top_k=r.top_k, max_tokens=r.max_tokens,
+                          stop=stop, seed=r.seed, repetition_penalty=r.repetition_penalty,
+                          ignore_eos=r.ignore_eos, logprobs=getattr(r, "logprobs", False))
+
+
+def _content_text(c) -> str:
+    if isinstance(c, str):
+        return c
+    return "".join(p.get("text", "") for p in c if isinstance(p, dict) and p.get("type", "text") == "text")
+
+
+def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name: str = "meta/llama3-8b-instruct",
+               embed_name: str = "snowflake/arctic-embed-l", rerank_name: str = "nv-rerank-qa-mistral-4b:1",
+               batch_delay_s: float = 0.002) -> FastAPI:
+    app = FastAPI(title="nv_genai_amd model server")
+    metrics = Registry()
+    tracer = get_tracer("model-server")
+    batcher = None
+    if embed_engine is not None:
+        from .batcher import DynamicBatcher
+
+        batcher = DynamicBatcher(embed_engine, batch_delay_s)
+    app.state.llm, app.state.embed, app.state.rerank, app.state.batcher = llm_service, embed_engine, rerank_engine, batcher
+
+    def _need(x, what):
+        if x is None:
+            raise RuntimeError(f"no {what} model loaded on this server")
+        return x
+
+    async def _run_stream(handle, rid: str, model: str, obj: str, chat: bool, t0: float):
+        first = True
+        try:
+            async for delta in handle.aiter():
+                if first:
+                    metrics.observe("ttft_seconds", time.perf_counter() - t0)
+                    first = False
+                if chat:
+                    ch = {"index": 0, "delta": {"role": "assistant", "content": delta}, "finish_reason": None}
+                else:
+                    ch = {"index": 0, "text": delta, "finish_reason": None}
+                yield "data: " + json.dumps({"id": rid, "object": obj, "created": int(time.time()),
+                                             "model": model, "choices": [ch]}) + "\n\n"
+            fin = {"index": 0, "finish_reason": handle.finish_reason or "stop"}
+            fin.update({"delta": {}} if chat else {"text": ""})
+            yield "data: " + json.dumps({"id": rid, "object": obj, "created": int(time.time()), "model": model,
+                                         "choices": [fin], "usage": handle.usage}) + "\n\n"
+            yield "data: [DONE]\n\n"
+        except asyncio.CancelledError:  # client went away: free the sequence
+            handle.cancel()
+            raise
+        except Exception as e:  # noqa: BLE001
+            yield "data: " + json.dumps({"error": {"message": str(e), "type": "engine_error"}}) + "\n\n"
+        finally:
+            metrics.observe("request_seconds", time.perf_counter() - t0)
+            r = handle.request
+            if r is not None and r.output_ids and r.first_token_time and r.finish_time and len(r.output_ids) > 1:
+                metrics.observe("tpot_seconds", (r.finish_time - r.first_token_time) / (len(r.output_ids) - 1))
+
+    async def _complete(handle, t0: float) -> str:
+        out = []
+        async for d in handle.aiter():
+            out.append(d)
+        metrics.observe("request_seconds", time.perf_counter() - t0)
+        return "".join(out)
+
+    @app.post("/v1/chat/completions")
+    async def chat(req: ChatRequest, request: Request):
+        svc = _need(app.state.llm, "LLM")
+        t0 = time.perf_counter()
+        metrics.inc("chat_requests_total")
+        msgs = [{"role": m.role, "content": _content_text(m.content)} for m in req.messages]
+        with tracer.span("chat.completions", {"model": req.model}, request.headers.get("traceparent")):
+            ids = svc.engine.tok.apply_chat_template(msgs)
+            handle = svc.submit(ids, _params(req))
+        rid = f"chatcmpl-{uuid.uuid4().hex}"
+        model = req.model or llm_name
+        if req.stream:
+            return StreamingResponse(_run_stream(handle, rid, model, "chat.completion.chunk", True, t0),
+                                     media_type="text/event-stream")
+        text = await _complete(handle, t0)
+        choice = {"index": 0, "message": {"role": "assistant", "content": text},
+                  "finish_reason": handle.finish_reason}
+        if req.logprobs and handle.request is not None:
+            choice["logprobs"] = {"content": [{"logprob": lp} for lp in handle.request.logprobs]}
+        return {"id": rid, "object": "chat.completion", "created": int(time.time()), "model": model,
+                "choices": [choice], "usage": handle.usage}
+
+    @app.post("/v1/completions")
+    async def completions(req: CompletionRequest, request: Request):
+        svc = _need(app.state.llm, "LLM")
+        t0 = time.perf_counter()
+        metrics.inc("completion_requests_total")
+        prompts = [req.prompt] if isinstance(req.prompt, str) else req.prompt
+        tok = svc.engine.tok
+        model = req.model or llm_name
+        rid = f"cmpl-{uuid.uuid4().hex}"
+        handles = [svc.submit([tok.bos_id] + tok.encode(p), _params(req)) for p in prompts]
+        if req.stream:
+            if len(handles) != 1:
+                return JSONResponse({"error": "stream supports a single prompt"}, status_code=400)
+            return StreamingResponse(_run_stream(handles[0], rid, model, "text_completion", False, t0),
+                                     media_type="text/event-stream")
+        texts = [await _complete(h, t0) for h in handles]
+        usage = {"prompt_tokens": sum(h.usage.get("prompt_tokens", 0) for h in handles),
+                 "completion_tokens": sum(h.usage.get("completion_tokens", 0) for h in handles)}
+        usage["total_tokens"] = usage["prompt_tokens"] + usage["completion_tokens"]
+        return {"id": rid, "object": "text_completion", "created": int(time.time()), "model": model,
+                "choices": [{"index": i, "text": t, "finish_reason": h.finish_reason}
+                            for i, (t, h) in enumerate(zip(texts, handles))], "usage": usage}
+
+    @app.post("/v1/embeddings")
+    async def embeddings(req: EmbeddingRequest):
+        eng = _need(app.state.embed, "embedding")
+        t0 = time.perf_counter()
+        texts = [req.input] if isinstance(req.input, str) else list(req.input)
+        if req.input_type not in ("query", "passage"):
+            return JSONResponse({"error": "input_type must be 'query' or 'passage'"}, status_code=400)
+        try:
+            seqs = eng.tokenize(texts, req.input_type, req.truncate)
+        except ValueError as e:
+            return JSONResponse({"error": str(e)}, status_code=400)
+        fut = app.state.batcher.submit_ids(seqs)
+        vecs = await asyncio.wrap_future(fut)
+        vecs = vecs.cpu()
+        metrics.observe("embed_seconds", time.perf_counter() - t0)
+        metrics.inc("embed_texts_total", len(texts))
+        data = []
+        for i, v in enumerate(vecs):
+            if req.encoding_format == "base64":
+                emb: Any = base64.b64encode(struct.pack(f"<{v.numel()}f", *v.tolist())).decode()
+            else:
+                emb = v.tolist()
+            data.append({"object": "embedding", "index": i, "embedding": emb})
+        ntok = sum(len(s) for s in seqs)
+        return {"object": "list", "data": data, "model": req.model or embed_name,
+                "usage": {"prompt_tokens": ntok, "total_tokens": ntok}}
+
+    @app.post("/v1/ranking")
+    async def ranking(req: RankingRequest):
+        eng = app.state.rerank or _need(app.state.embed, "reranking")
+        t0 = time.perf_counter()
+        logits = await asyncio.to_thread(eng.rerank, req.query.text, [p.text for p in req.passages], req.truncate)
+        metrics.observe("rank_seconds", time.perf_counter() - t0)
+        order = sorted(range(len(logits)), key=lambda i: -logits[i])
+        return {"rankings": [{"index": i, "logit": float(logits[i])} for i in order]}
+
+    @app.get("/v1/models")
+    def models():
+        out = []
+        if app.state.llm is not None:
+            out.append({"id": llm_name, "object": "model", "owned_by": "nv_genai_amd"})
+        if app.state.embed is not None:
+            out.append({"id": embed_name, "object": "model", "owned_by": "nv_genai_amd"})
+        if app.state.rerank is not None:
+            out.append({"id": rerank_name, "object": "model", "owned_by": "nv_genai_amd"})
+        return {"object": "list", "data": out}
+
+    @app.get("/v1/health/live")
+    def live():
+        return {"object": "health-response", "message": "Service is live."}
+
+    @app.get("/v1/health/ready")
+    def ready():
+        ok = app.state.llm is None or app.state.llm.healthy()
+        return JSONResponse({"object": "health-response", "message": "Service is ready." if ok else "not ready"},
+                            status_code=200 if ok else 503)
+
+    @app.get("/metrics")
+    def prom():
+        g = app.state.llm.metrics() if app.state.llm is not None else {}
+        if app.state.batcher is not None:
+            g["embed_batches"] = app.state.batcher.batches
+        return PlainTextResponse(metrics.render(g, prefix="model_server"), media_type="text/plain; version=0.0.4")
+
+    return app
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--llm", default="llama3-8b", help="LLM preset ('' to disable)")
+    ap.add_argument("--embed", default="arctic-embed-l", help="encoder preset ('' to disable)")
+    ap.add_argument("--rerank", default="", help="reranker preset ('' to disable)")
+    ap.add_argument("--weights", default="", help="safetensors dir for the LLM")
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--max-num-seqs", type=int, default=256)
+    ap.add_argument("--max-model-len", type=int, default=8192)
+    ap.add_argument("--kv-cache-fraction", type=float, default=0.3)
+    ap.add_argument("--device", default=None)
+    args = ap.parse_args(argv)
+    import uvicorn
+
+    from ..engine.embed_engine import EmbeddingEngine
+    from ..engine.llm_engine import EngineConfig, LLMEngine
+    from .engine_service import EngineService
+
+    svc = emb = rr = None
+    if args.llm:
+        weights = None
+        if args.weights:
+            from ..utils.checkpoint import load_weights
+
+            weights = load_weights(args.weights)
+        eng = LLMEngine(EngineConfig(model=args.llm, max_num_seqs=args.max_num_seqs, max_model_len=args.max_model_len,
+                                     kv_cache_fraction=args.kv_cache_fraction), device=args.device, weights=weights)
+        svc = EngineService(eng)
+    if args.embed:
+        emb = EmbeddingEngine(args.embed, device=args.device)
+    if args.rerank:
+        rr = EmbeddingEngine(args.rerank, device=args.device)
+    app = create_app(svc, emb, rr)
+    uvicorn.run(app, host=args.host, port=args.port, log_level=os.environ.get("LOGLEVEL", "info").lower())
+
+
+if __name__ == "__main__":
+    main()

@@ -113,26 +113,53 @@ class LLMTokenizer:
         return ids
 
 
+def _byte_decoder() -> dict:
+    """Inverse of the GPT-2 byte-level alphabet (printable stand-ins for the 256 bytes)."""
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1)) + list(range(ord("®"), ord("ÿ") + 1))
+    cs = bs[:]
+    n = 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    return {chr(c): b for b, c in zip(bs, cs)}
+
+
 class IncrementalDetokenizer:
-    """Streams text for a growing id list without re-decoding from scratch every token:
-    decodes a small window and emits only complete (non-replacement-char) text."""
+    """Streams text for a growing id list at O(1) per token: every id maps to its raw bytes
+    (precomputed once per tokenizer from the byte-level vocabulary) and an incremental UTF-8
+    decoder emits only complete characters — no re-decoding of a window per token."""
 
     def __init__(self, tok: LLMTokenizer, prompt_tail: Optional[List[int]] = None):
+        import codecs
+
         self.tok = tok
-        self.ids: List[int] = []
-        self.prefix_off = 0
-        self.read_off = 0
+        self.table = token_bytes_table(tok)
+        self.dec = codecs.getincrementaldecoder("utf-8")(errors="replace")
 
     def push(self, tid: int) -> str:
-        self.ids.append(tid)
-        prefix = self.tok.decode(self.ids[self.prefix_off:self.read_off])
-        full = self.tok.decode(self.ids[self.prefix_off:])
-        if full.endswith("�"):
-            return ""
-        delta = full[len(prefix):]
-        self.prefix_off = self.read_off
-        self.read_off = len(self.ids)
-        return delta
+        b = self.table[tid % len(self.table)]
+        return self.dec.decode(b) if b else ""
+
+
+_TABLES: dict = {}
+
+
+def token_bytes_table(tok: LLMTokenizer) -> List[bytes]:
+    t = _TABLES.get(id(tok))
+    if t is None:
+        inv = _byte_decoder()
+        specials = {tok.bos_id, tok.eot_id, tok.eos_id, tok.header_start, tok.header_end}
+        t = []
+        for i in range(tok.n):
+            s = tok.tok.id_to_token(i)
+            if s is None or i in specials:
+                t.append(b"")
+            else:
+                t.append(bytes(inv.get(ch, 32) for ch in s))
+        _TABLES[id(tok)] = t
+    return t
 
 
 class EmbedTokenizer:

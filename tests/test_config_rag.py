@@ -1,0 +1,147 @@
+"""Config wizard (APP_* parity), loaders / splitters, vector store / IVF / persistence,
+tracing propagation."""
+import io
+import json
+import os
+import zipfile
+
+import pytest
+import torch
+
+from nv_genai_amd.chain_server.configuration import AppConfig
+
+
+def test_env_names_match_reference_scheme():
+    names = {n for n, _, _ in AppConfig.envvars()}
+    for n in ("APP_VECTORSTORE_URL", "APP_VECTORSTORE_NLIST", "APP_LLM_MODELNAME", "APP_LLM_SERVERURL",
+              "APP_TEXTSPLITTER_CHUNKSIZE", "APP_TEXTSPLITTER_CHUNKOVERLAP", "APP_EMBEDDINGS_DIMENSIONS",
+              "APP_RETRIEVER_SCORETHRESHOLD", "APP_RETRIEVER_TOPK", "APP_PROMPTS_RAGTEMPLATE",
+              "APP_PROMPTS_CHATTEMPLATE", "APP_EMBEDDINGS_SERVERURL", "APP_ENGINE_TPSIZE", "APP_INDEX_TYPE"):
+        assert n in names
+
+
+def test_defaults():
+    c = AppConfig.from_dict({})
+    assert c.vector_store.nlist == 64 and c.vector_store.nprobe == 16
+    assert c.text_splitter.chunk_size == 510 and c.text_splitter.chunk_overlap == 200
+    assert c.retriever.top_k == 4 and c.retriever.score_threshold == 0.25
+    assert c.embeddings.dimensions == 1024
+    assert "{context_str}" in c.prompts.rag_template
+
+
+def test_env_json_decoding_and_file_precedence(tmp_path, monkeypatch):
+    monkeypatch.setenv("APP_RETRIEVER_TOPK", "7")
+    monkeypatch.setenv("APP_LLM_MODELNAME", "meta/llama3-70b-instruct")
+    monkeypatch.setenv("APP_VECTORSTORE_URL", "http://other:1")
+    f = tmp_path / "cfg.yaml"
+    f.write_text("vectorStore:\n  url: http://file:19530\nretriever:\n  scoreThreshold: 0.5\n")
+    c = AppConfig.from_file(str(f))
+    assert c.retriever.top_k == 7                       # env fills an unset key (JSON-decoded to int)
+    assert c.llm.model_name == "meta/llama3-70b-instruct"
+    assert c.vector_store.url == "http://file:19530"    # file wins over env (reference quirk)
+    assert c.retriever.score_threshold == 0.5
+    jf = tmp_path / "cfg.json"
+    jf.write_text(json.dumps({"llm": {"model_engine": "local"}}))
+    assert AppConfig.from_file(str(jf)).llm.model_engine == "local"
+    bad = tmp_path / "bad.yaml"
+    bad.write_text("{:::")
+    assert AppConfig.from_file(str(bad)) is None
+    assert AppConfig.from_file(str(tmp_path / "missing.yaml")) is None
+
+
+def test_print_help():
+    out = []
+    AppConfig.print_help(out.append)
+    text = "".join(out)
+    assert "ENV Variable: APP_VECTORSTORE_URL" in text and "chunkSize: 510" in text
+
+
+def test_loaders_pdf_pptx_html(tmp_path):
+    from nv_genai_amd.rag.loaders import load_file, make_pdf
+
+    p = tmp_path / "doc.pdf"
+    p.write_bytes(make_pdf(["Alpha page text", "Beta page (with parens)"]))
+    docs = load_file(str(p))
+    assert [d.page_content for d in docs] == ["Alpha page text", "Beta page (with parens)"]
+    assert docs[1].metadata["page"] == 2
+    pp = tmp_path / "deck.pptx"
+    with zipfile.ZipFile(pp, "w") as z:
+        for i, t in enumerate(["Slide one", "Slide two"], 1):
+            z.writestr(f"ppt/slides/slide{i}.xml",
+                       f'<p:sld xmlns:p="p" xmlns:a="a"><a:t>{t}</a:t></p:sld>')
+    assert [d.page_content for d in load_file(str(pp))] == ["Slide one", "Slide two"]
+    h = tmp_path / "x.html"
+    h.write_text("<html><script>bad()</script><p>Hello</p><p>World</p></html>")
+    assert load_file(str(h))[0].page_content.split() == ["Hello", "World"]
+    with pytest.raises(ValueError):
+        load_file(str(tmp_path / "file.xyz"))
+
+
+def test_token_splitter_overlap():
+    from nv_genai_amd.rag.splitters import TokenTextSplitter
+
+    s = TokenTextSplitter(tokens_per_chunk=20, chunk_overlap=5)
+    text = " ".join(f"word{i}" for i in range(200))
+    chunks = s.split_text(text)
+    assert len(chunks) > 5 and all(s.count_tokens(c) <= 22 for c in chunks)
+    assert chunks[0].split()[-1] in chunks[1]  # overlap carries context forward
+
+
+def test_vectorstore_flat_ivf_and_persistence(tmp_path):
+    from nv_genai_amd.connectors.fake import HashEmbeddings
+    from nv_genai_amd.index.vectorstore import VectorStore
+
+    emb = HashEmbeddings(128)
+    texts = [f"document about topic {i} with keyword k{i % 7}" for i in range(300)]
+    metas = [{"filename": f"f{i % 3}.txt"} for i in range(300)]
+    for itype in ("flat", "ivf_flat"):
+        vs = VectorStore(emb, 128, itype, "cosine", "cpu", nlist=8, nprobe=8, persist_dir=str(tmp_path / itype))
+        vs.add_texts(texts, metas)
+        hits = vs.similarity_search_with_score("topic 42 keyword k0", 3)
+        assert "topic 42 " in hits[0][0].page_content
+        assert sorted(vs.get_filenames()) == ["f0.txt", "f1.txt", "f2.txt"]
+        assert vs.delete_by_filename("f0.txt")
+        assert all(d.metadata["filename"] != "f0.txt" for d, _ in vs.similarity_search_with_score("topic 42 k0", 20))
+        vs2 = VectorStore(emb, 128, itype, "cosine", "cpu", persist_dir=str(tmp_path / itype))
+        assert len(vs2) == 200
+        assert vs2.similarity_search("topic 43 keyword k1", 1)[0].page_content == texts[43]
+        rel = vs2.similarity_search_with_relevance_scores("topic 43 keyword k1", 4, score_threshold=0.25)
+        assert rel and all(s >= 0.25 for _, s in rel)
+
+
+def test_flat_l2_and_ip_metrics():
+    from nv_genai_amd.index.flat import FlatIndex
+
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(500, 32, generator=g)
+    q = torch.randn(3, 32, generator=g)
+    for metric in ("l2", "ip"):
+        idx = FlatIndex(32, metric, "cpu")
+        idx.add(X, torch.arange(500) + 1000)
+        v, i = idx.search(q, 5)
+        qb = q.bfloat16().float()  # queries are scored in bf16, like the stored vectors
+        if metric == "l2":
+            d = (qb * qb).sum(1, keepdim=True) - 2 * qb @ X.bfloat16().float().T \
+                + X.bfloat16().float().pow(2).sum(1)[None]
+            rv, ri = torch.topk(-d, 5)
+        else:
+            rv, ri = torch.topk(qb @ X.bfloat16().float().T, 5)
+        assert torch.equal(i, ri + 1000)
+        assert torch.allclose(v, rv, atol=0.1)  # |q|^2 is added back from the fp32 query
+
+
+def test_tracing_traceparent_propagation():
+    from nv_genai_amd.observability.tracing import InMemoryExporter, Tracer, inject_context
+
+    exp = InMemoryExporter()
+    fe = Tracer("frontend", exp, enabled=True)
+    cs = Tracer("chain-server", exp, enabled=True)
+    with fe.span("predict") as s:
+        hdr = inject_context()
+    with cs.span("POST /generate", traceparent=hdr["traceparent"]) as c:
+        with cs.span("retriever"):
+            pass
+    names = {sp.name: sp for sp in exp.spans}
+    assert names["POST /generate"].trace_id == names["predict"].trace_id
+    assert names["POST /generate"].parent_id == names["predict"].span_id
+    assert names["retriever"].parent_id == names["POST /generate"].span_id

@@ -1,0 +1,101 @@
+"""Multi-process tests on CPU (gloo, world_size 2): tensor-parallel Llama matches TP=1
+token-for-token, and the sharded vector index matches single-process search."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _tp_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    from nv_genai_amd.engine.llm_engine import EngineConfig, LLMEngine, SamplingParams
+    from nv_genai_amd.models.config import llama_config
+    from nv_genai_amd.models.llama import LlamaModel
+    from nv_genai_amd.parallel import dist as pd
+
+    single = pd.ParallelContext()
+    cfg = llama_config("llama-tiny")
+    full = LlamaModel(cfg, "cpu", pctx=single, seed=7).state_dict()
+    ecfg = EngineConfig(model="llama-tiny", max_num_seqs=4, max_batched_tokens=256, max_model_len=512,
+                        kv_cache_blocks=32)
+    prompts = [[5, 6, 7, 8] * 20, [9, 10, 11] * 11]
+    params = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
+    ref = None
+    if rank == 0:
+        e1 = LLMEngine(ecfg, device="cpu", pctx=single, weights=full)
+        ref = [r.output_ids for r in e1.generate(prompts, params)]
+    pctx = pd.init_distributed(tp_size=2, backend="gloo", device="cpu")
+    eng = LLMEngine(ecfg, device="cpu", pctx=pctx, weights=full)
+    if eng.is_driver:
+        out = [r.output_ids for r in eng.generate(prompts, params)]
+        eng.stop_followers()
+        q.put((out, ref))
+    else:
+        eng.run_follower()
+    pd.destroy()
+
+
+def test_tensor_parallel_matches_single():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out, ref = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out == ref
+
+
+def _shard_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    from nv_genai_amd.index.flat import FlatIndex
+    from nv_genai_amd.index.sharded import ShardedIndex
+    from nv_genai_amd.parallel import dist as pd
+
+    pctx = pd.init_distributed(tp_size=1, backend="gloo", device="cpu")
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(3000, 64, generator=g)
+    Q = torch.randn(5, 64, generator=g)
+    ids = torch.arange(3000) * 3
+    sh = ShardedIndex(64, "cosine", "cpu", pctx=pctx)
+    sh.add(X, ids)  # every rank passes the full set; each keeps its own stripe
+    vals, out_ids = sh.search(Q if rank == 0 else torch.zeros(5, 64), 7)
+    if rank == 0:
+        full = FlatIndex(64, "cosine", "cpu")
+        full.add(X, ids)
+        rv, ri = full.search(Q, 7)
+        q.put((vals, out_ids, rv, ri, len(sh.local)))
+    pd.destroy()
+
+
+def test_sharded_index_matches_flat():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    vals, ids, rv, ri, nlocal = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert nlocal == 1500
+    assert torch.allclose(vals, rv, atol=1e-5)
+    assert torch.equal(ids, ri)

@@ -1,0 +1,104 @@
+"""LLM / embedding engine behaviour on CPU (reference ops): continuous batching equals
+sequential greedy decoding, stop handling, chunked prefill, prefix caching, sampling."""
+import pytest
+import torch
+
+from nv_genai_amd.engine.llm_engine import EngineConfig, LLMEngine, SamplingParams
+from nv_genai_amd.ops import reference as ref
+
+
+@pytest.fixture(scope="module")
+def model():
+    from nv_genai_amd.models.config import llama_config
+    from nv_genai_amd.models.llama import LlamaModel
+    from nv_genai_amd.parallel.dist import ParallelContext
+
+    return LlamaModel(llama_config("llama-tiny"), "cpu", pctx=ParallelContext(), seed=3)
+
+
+def _engine(model, **kw):
+    cfg = dict(model="llama-tiny", max_num_seqs=8, max_batched_tokens=96, max_model_len=512, kv_cache_blocks=64)
+    cfg.update(kw)
+    return LLMEngine(EngineConfig(**cfg), device="cpu", model=model)
+
+
+PROMPTS = [[3, 4, 5, 6] * 25, [7, 8] * 40, [9] * 5]
+
+
+def test_batched_equals_sequential(model):
+    p = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True)
+    batched = [r.output_ids for r in _engine(model).generate(PROMPTS, p)]
+    for prompt, out in zip(PROMPTS, batched):
+        solo = _engine(model, max_batched_tokens=512).generate([prompt], p)[0].output_ids
+        assert solo == out
+
+
+def test_chunked_prefill_matches_unchunked(model):
+    p = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
+    a = _engine(model, max_batched_tokens=32).generate([PROMPTS[0]], p)[0].output_ids
+    b = _engine(model, max_batched_tokens=512).generate([PROMPTS[0]], p)[0].output_ids
+    assert a == b
+
+
+def test_prefix_cache_reuse_is_exact(model):
+    e = _engine(model)
+    p = SamplingParams(temperature=0.0, max_tokens=5, ignore_eos=True)
+    first = e.generate([PROMPTS[0]], p)[0]
+    second = e.generate([PROMPTS[0]], p)[0]
+    assert second.cached_prefix >= 64 and first.output_ids == second.output_ids
+
+
+def test_seeded_sampling_reproducible(model):
+    p = SamplingParams(temperature=0.9, top_p=0.95, top_k=50, max_tokens=8, ignore_eos=True, seed=1234)
+    a = _engine(model).generate([PROMPTS[1]], p)[0].output_ids
+    b = _engine(model).generate([PROMPTS[1]], p)[0].output_ids
+    assert a == b
+
+
+def test_stop_token_and_length(model):
+    e = _engine(model)
+    p = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True)
+    out = e.generate([PROMPTS[2]], p)[0]
+    tok = out.output_ids[2]
+    r = e.generate([PROMPTS[2]], SamplingParams(temperature=0.0, max_tokens=10, stop_token_ids=[tok]))[0]
+    assert r.finish_reason == "stop" and r.output_ids[-1] == tok and len(r.output_ids) == 3
+    assert out.finish_reason == "length" and len(out.output_ids) == 10
+
+
+def test_abort_frees_blocks(model):
+    e = _engine(model)
+    used0 = e.sched.used_blocks()
+    r = e.add_request(PROMPTS[0], SamplingParams(max_tokens=50, ignore_eos=True))
+    e.step()
+    assert e.sched.used_blocks() > used0
+    e.abort(r.id)
+    assert r.finish_reason == "abort" and not e.has_work()
+
+
+def test_reference_sampler_truncation():
+    torch.manual_seed(0)
+    lg = torch.randn(4, 1000)
+    t, _ = ref.sample(lg.clone(), torch.tensor([1.0] * 4), torch.tensor([5, 0, 1, 0]), torch.tensor([1.0, 0.3, 1.0, 1.0]),
+                      torch.arange(4), torch.zeros(4, dtype=torch.int64))
+    assert lg[0, t[0]] >= torch.topk(lg[0], 5).values[-1]
+    assert t[2] == torch.argmax(lg[2])
+    probs = torch.softmax(lg[1], 0)
+    order = torch.argsort(probs, descending=True)
+    cs = torch.cumsum(probs[order], 0)
+    nucleus = set(order[: int((cs < 0.3).sum()) + 1].tolist())
+    assert int(t[1]) in nucleus
+
+
+def test_embedding_engine_packing_order_and_truncation():
+    from nv_genai_amd.engine.embed_engine import EmbeddingEngine
+
+    e = EmbeddingEngine("encoder-tiny", device="cpu", max_batch_tokens=64)
+    texts = ["short", "a much longer piece of text " * 5, "mid length text here"]
+    together = e.embed(texts)
+    alone = torch.cat([e.embed([t]) for t in texts])
+    assert torch.allclose(together, alone, atol=1e-4)
+    assert torch.allclose(together.norm(dim=1), torch.ones(3), atol=1e-4)
+    ids = e.tokenize(["x " * 1000], truncate="END")[0]
+    assert len(ids) == 512
+    with pytest.raises(ValueError):
+        e.tokenize(["x " * 1000], truncate="NONE")

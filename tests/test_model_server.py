@@ -1,0 +1,130 @@
+"""OpenAI/NIM-compatible model server on CPU with tiny models, exercised both through the
+ASGI test client and through the real HTTP connectors (uvicorn on a loopback port)."""
+import json
+import socket
+import threading
+import time
+
+import pytest
+import torch
+
+
+@pytest.fixture(scope="module")
+def server():
+    from nv_genai_amd.engine.embed_engine import EmbeddingEngine
+    from nv_genai_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from nv_genai_amd.serving.engine_service import EngineService
+    from nv_genai_amd.serving.model_server import create_app
+
+    eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=8, max_batched_tokens=512, max_model_len=512,
+                                 kv_cache_blocks=64), device="cpu")
+    svc = EngineService(eng)
+    emb = EmbeddingEngine("encoder-tiny", device="cpu")
+    rr = EmbeddingEngine("reranker-tiny", device="cpu")
+    app = create_app(svc, emb, rr, llm_name="tiny-llm", embed_name="tiny-embed", rerank_name="tiny-rerank")
+    yield app
+    svc.shutdown()
+
+
+@pytest.fixture(scope="module")
+def client(server):
+    from fastapi.testclient import TestClient
+
+    with TestClient(server) as c:
+        yield c
+
+
+@pytest.fixture(scope="module")
+def http_url(server):
+    import uvicorn
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cfg = uvicorn.Config(server, host="127.0.0.1", port=port, log_level="error")
+    srv = uvicorn.Server(cfg)
+    t = threading.Thread(target=srv.run, daemon=True)
+    t.start()
+    for _ in range(200):
+        if srv.started:
+            break
+        time.sleep(0.05)
+    yield f"http://127.0.0.1:{port}"
+    srv.should_exit = True
+    t.join(timeout=5)
+
+
+def test_models_and_health(client):
+    ids = [m["id"] for m in client.get("/v1/models").json()["data"]]
+    assert ids == ["tiny-llm", "tiny-embed", "tiny-rerank"]
+    assert client.get("/v1/health/ready").status_code == 200
+    assert client.get("/v1/health/live").status_code == 200
+
+
+def test_chat_nonstream_deterministic(client):
+    body = {"messages": [{"role": "user", "content": "hello there"}], "max_tokens": 6, "temperature": 0.0,
+            "ignore_eos": True}
+    a = client.post("/v1/chat/completions", json=body).json()
+    b = client.post("/v1/chat/completions", json=body).json()
+    assert a["object"] == "chat.completion"
+    assert a["choices"][0]["message"]["content"] == b["choices"][0]["message"]["content"]
+    assert a["usage"]["completion_tokens"] == 6
+    assert a["choices"][0]["finish_reason"] == "length"
+
+
+def test_chat_stream_frames(client):
+    body = {"messages": [{"role": "user", "content": "stream please"}], "max_tokens": 5, "stream": True,
+            "ignore_eos": True, "seed": 3}
+    r = client.post("/v1/chat/completions", json=body)
+    frames = [ln[6:] for ln in r.text.split("\n\n") if ln.startswith("data: ")]
+    assert frames[-1] == "[DONE]"
+    objs = [json.loads(f) for f in frames[:-1]]
+    assert all(o["object"] == "chat.completion.chunk" for o in objs)
+    assert objs[-1]["choices"][0]["finish_reason"] == "length"
+    assert objs[-1]["usage"]["completion_tokens"] == 5
+
+
+def test_completions(client):
+    r = client.post("/v1/completions", json={"prompt": ["a b c", "d e"], "max_tokens": 3, "ignore_eos": True}).json()
+    assert len(r["choices"]) == 2 and r["usage"]["completion_tokens"] == 6
+
+
+def test_embeddings_query_passage_and_truncate(client):
+    r = client.post("/v1/embeddings", json={"input": ["alpha beta", "gamma"], "input_type": "query"}).json()
+    v = torch.tensor([d["embedding"] for d in r["data"]])
+    assert v.shape == (2, 128)
+    assert torch.allclose(v.norm(dim=1), torch.ones(2), atol=1e-4)
+    p = client.post("/v1/embeddings", json={"input": "alpha beta", "input_type": "passage"}).json()
+    assert not torch.allclose(torch.tensor(p["data"][0]["embedding"]), v[0])  # asymmetric prefix
+    long = "word " * 2000
+    assert client.post("/v1/embeddings", json={"input": long, "truncate": "NONE"}).status_code == 400
+    assert client.post("/v1/embeddings", json={"input": long, "truncate": "END"}).status_code == 200
+    b64 = client.post("/v1/embeddings", json={"input": "alpha", "encoding_format": "base64"}).json()
+    assert isinstance(b64["data"][0]["embedding"], str)
+
+
+def test_ranking(client):
+    r = client.post("/v1/ranking", json={"query": {"text": "q"}, "passages": [{"text": "a"}, {"text": "b"}, {"text": "c"}]}).json()
+    assert sorted(x["index"] for x in r["rankings"]) == [0, 1, 2]
+    logits = [x["logit"] for x in r["rankings"]]
+    assert logits == sorted(logits, reverse=True)
+
+
+def test_http_connectors_roundtrip(http_url):
+    from nv_genai_amd.connectors.http import ChatClient, EmbeddingsClient, RerankClient
+
+    chat = ChatClient(http_url, "tiny-llm", max_tokens=4, temperature=0.0)
+    streamed = "".join(chat.stream([("user", "hi")], ignore_eos=True))
+    whole = chat.invoke([("user", "hi")], ignore_eos=True)
+    assert streamed == whole
+    emb = EmbeddingsClient(http_url, "tiny-embed")
+    assert len(emb.embed_query("hello")) == 128
+    assert len(emb.embed_documents(["a", "b", "c"])) == 3
+    rk = RerankClient(http_url, "tiny-rerank").rank("q", ["x", "y"])
+    assert len(rk) == 2
+
+
+def test_metrics_exposed(client):
+    t = client.get("/metrics").text
+    assert "model_server_chat_requests_total" in t and "model_server_kv_usage" in t
