@@ -290,6 +290,36 @@ class Scheduler {
     for (int i = 0; i < n; ++i) append_token(a(i), b(i));
   }
 
+  // Pipelined decode: the token a sequence will sample in the in-flight step is not known
+  // yet; a placeholder (-1) lets the next step be scheduled now (its input id is gathered
+  // on the GPU from the previous step's output) and is replaced once the step completes.
+  void append_placeholders(const std::vector<int64_t>& ids) {
+    for (int64_t id : ids) seqs_.at(id).toks.push_back(-1);
+  }
+
+  void set_last_token(int64_t id, int32_t tok) {
+    auto it = seqs_.find(id);
+    if (it == seqs_.end()) return;  // finished / aborted meanwhile
+    Seq& s = it->second;
+    if (s.toks.empty() || s.toks.back() != -1) throw std::runtime_error("no placeholder to fill");
+    s.toks.back() = tok;
+  }
+
+  bool has_placeholder(int64_t id) const {
+    auto it = seqs_.find(id);
+    return it != seqs_.end() && !it->second.toks.empty() && it->second.toks.back() == -1;
+  }
+
+  void drop_placeholder(int64_t id) {
+    auto it = seqs_.find(id);
+    if (it == seqs_.end()) return;
+    Seq& s = it->second;
+    if (!s.toks.empty() && s.toks.back() == -1) {
+      s.toks.pop_back();
+      if (s.computed > (int)s.toks.size()) s.computed = (int)s.toks.size();
+    }
+  }
+
   void finish(int64_t id) {
     auto it = seqs_.find(id);
     if (it == seqs_.end()) return;
@@ -355,6 +385,9 @@ class Scheduler {
     const int full = s.computed / bs_;
     while ((int)s.hashes.size() < full) {
       const int i = (int)s.hashes.size();
+      bool pending = false;
+      for (int j = 0; j < bs_; ++j) pending |= s.toks[i * bs_ + j] < 0;
+      if (pending) break;  // hash once the placeholder has its real token
       const uint64_t prev = i ? s.hashes[i - 1] : 0;
       const uint64_t h = block_hash(prev, s.toks.data() + i * bs_, bs_);
       s.hashes.push_back(h);
@@ -419,6 +452,10 @@ PYBIND11_MODULE(_rt, m) {
       .def("schedule", &Scheduler::schedule)
       .def("append_token", &Scheduler::append_token)
       .def("append_tokens", &Scheduler::append_tokens)
+      .def("append_placeholders", &Scheduler::append_placeholders)
+      .def("set_last_token", &Scheduler::set_last_token)
+      .def("has_placeholder", &Scheduler::has_placeholder)
+      .def("drop_placeholder", &Scheduler::drop_placeholder)
       .def("finish", &Scheduler::finish)
       .def("num_generated", &Scheduler::num_generated)
       .def("tokens", &Scheduler::tokens)

@@ -94,6 +94,7 @@ class EngineConfig:
     decode_pages_per_part: int = 16
     seed: int = 0
     detokenize: bool = True
+    async_decode: bool = True  # pipeline decode steps (host work overlaps the GPU)
 
 
 class LLMEngine:
@@ -174,6 +175,13 @@ class LLMEngine:
         self.stats = {"prefill_steps": 0, "decode_steps": 0, "prefill_tokens": 0,
                       "decode_tokens": 0, "prefill_time": 0.0, "decode_time": 0.0}
         self.lock = threading.RLock()
+        self._pending: Optional[dict] = None
+        self._tok_flip = 0
+        self._tok_host = [(hbuf(S), hbuf(S, dtype=torch.float32)) for _ in range(2)]
+        if self.p.tp_size > 1:
+            # followers replay from broadcast host buffers; the device-side id gather of the
+            # pipelined path is not replicated, so TP steps run synchronously
+            self.cfg = cfg = type(cfg)(**{**cfg.__dict__, "async_decode": False})
         if self.gpu and cfg.use_graphs:
             self._capture_graphs()
 
@@ -210,21 +218,66 @@ class LLMEngine:
         return self.sched.has_work()
 
     # ------------------------------------------------------------------ step
+    def _fill_params(self, reqs, pending_ids=()):
+        n = len(reqs)
+        self.n_temp[:n] = [r.params.temperature for r in reqs]
+        self.n_topk[:n] = [r.params.top_k for r in reqs]
+        self.n_topp[:n] = [r.params.top_p for r in reqs]
+        self.n_seed[:n] = [r.seed for r in reqs]
+        self.n_step[:n] = [len(r.output_ids) + (r.id in pending_ids) for r in reqs]
+        self.n_pen[:n] = [r.params.repetition_penalty for r in reqs]
+
     def step(self) -> List[Request]:
-        """Run one scheduler step; returns requests that finished in it."""
+        """Run one scheduler step; returns requests that finished in it.
+
+        Decode steps are pipelined when possible: step k+1 is scheduled and launched before
+        step k's tokens are read back (its input ids are gathered on the GPU from step k's
+        output), so host work — reading tokens, detokenising, stop checks, scheduling —
+        overlaps the GPU instead of serialising with it."""
         with self.lock:
+            pend = self._pending
+            done: List[Request] = []
+            if pend is not None:
+                cont = [r.id for r in pend["reqs"] if len(r.output_ids) + 1 < r.params.max_tokens
+                        and r.id in self.requests]
+                self.sched.append_placeholders(cont)
             ids, pos, sl, cu, ctx, bt, sid, smp = self._np
             kind, n, ntok = self.sched.schedule(ids, pos, sl, cu, ctx, bt, sid, smp)
-            if kind == 0:
+            if pend is not None:
+                rows = pend["rows"]
+                sids = sid[:n].tolist()
+                if (kind == 2 and all(s in rows for s in sids)
+                        and not self._needs_penalty_reqs(pend["reqs"])):
+                    t0 = time.perf_counter()
+                    reqs = [self.requests[s] for s in sids]
+                    self._fill_params(reqs, pending_ids=rows)
+                    src = torch.tensor([rows[s] for s in sids], dtype=torch.int64)
+                    nxt = self._decode_launch(n, src)
+                    done += self._finalize(pend)
+                    self.stats["decode_steps"] += 1
+                    self.stats["decode_tokens"] += n
+                    self.stats["decode_time"] += time.perf_counter() - t0
+                    self._pending = nxt
+                    return done
+                # cannot pipeline: settle the in-flight step first, then run this one normally
+                done += self._finalize(pend)
+                self._pending = None
+                for i in range(n):
+                    if ids[i] < 0:
+                        ids[i] = self.sched.tokens(int(sid[i]))[pos[i]]
+                if kind == 0:
+                    return done
+            elif kind == 0:
                 return []
             t0 = time.perf_counter()
             reqs = [self.requests[int(s)] for s in sid[:n].tolist()]
-            self.n_temp[:n] = [r.params.temperature for r in reqs]
-            self.n_topk[:n] = [r.params.top_k for r in reqs]
-            self.n_topp[:n] = [r.params.top_p for r in reqs]
-            self.n_seed[:n] = [r.seed for r in reqs]
-            self.n_step[:n] = [len(r.output_ids) for r in reqs]
-            self.n_pen[:n] = [r.params.repetition_penalty for r in reqs]
+            self._fill_params(reqs)
+            if kind == 2 and self.cfg.async_decode and not self._needs_penalty(n):
+                self._pending = self._decode_launch(n, None)
+                self.stats["decode_steps"] += 1
+                self.stats["decode_tokens"] += n
+                self.stats["decode_time"] += time.perf_counter() - t0
+                return done
             if kind == 2:
                 toks, lps = self._decode(n)
                 self.stats["decode_steps"] += 1
@@ -239,11 +292,80 @@ class LLMEngine:
             lps = lps.tolist()
             self.stats[key] += time.perf_counter() - t0
             now = time.perf_counter()
-            done = []
             for i, (r, s) in enumerate(zip(reqs, smp[:n].tolist())):
                 if s and self._emit(r, toks[i], lps[i], now):
                     done.append(r)
             return done
+
+    def _needs_penalty_reqs(self, reqs) -> bool:
+        return any(r.params.repetition_penalty != 1.0 for r in reqs)
+
+    def _decode_launch(self, n: int, src_rows: Optional[torch.Tensor]) -> dict:
+        """Replay the decode graph for n rows without waiting for it. ``src_rows`` (row of
+        each sequence in the previous in-flight step) gathers the input ids on the device
+        from that step's sampled tokens. Tokens are copied to pinned host memory right after
+        the graph so the next step may overwrite the device buffer."""
+        bs = next((b for b in sorted(self.graphs) if b >= n), None)
+        if bs is not None:
+            self.h_slots[n:bs] = -1
+            self.h_ctx[n:bs] = 0
+            self.h_ids[n:bs] = 0
+            self.h_pos[n:bs] = 0
+            self.h_temp[n:bs] = 0.0
+            self.h_topk[n:bs] = 0
+            self.h_topp[n:bs] = 1.0
+            self.h_step[n:bs] = 0
+            self.h_seed[n:bs] = 0
+        self._sync_step(2, n, n, 1, self.cfg.max_model_len, bs or 0)
+        self._upload(bs or n, bs or n)
+        if src_rows is not None:
+            idx = src_rows.to(self.device, non_blocking=True)
+            self.d_ids[:n] = self.d_tok.index_select(0, idx)
+        if bs is not None:
+            self.graphs[bs].replay()
+        else:
+            meta = self._meta("decode", n, n, 1, self.cfg.max_model_len)
+            logits = self.model.logits(self.model.forward(self.d_ids[:n], self.d_pos[:n], meta))
+            tok, lp = self._sample(logits, n)
+            if tok.data_ptr() != self.d_tok.data_ptr():
+                self.d_tok[:n].copy_(tok[:n])
+                self.d_lp[:n].copy_(lp[:n])
+        buf = self._tok_host[self._tok_flip]
+        self._tok_flip ^= 1
+        buf[0][:n].copy_(self.d_tok[:n], non_blocking=self.gpu)
+        buf[1][:n].copy_(self.d_lp[:n], non_blocking=self.gpu)
+        ev = None
+        if self.gpu:
+            ev = torch.cuda.Event()
+            ev.record()
+        reqs = [self.requests[int(s)] for s in self._np[6][:n].tolist()]
+        return {"reqs": reqs, "rows": {r.id: i for i, r in enumerate(reqs)}, "n": n, "buf": buf, "ev": ev}
+
+    def _finalize(self, pend: dict) -> List[Request]:
+        if pend["ev"] is not None:
+            pend["ev"].synchronize()
+        n = pend["n"]
+        toks = pend["buf"][0][:n].tolist()
+        lps = pend["buf"][1][:n].tolist()
+        now = time.perf_counter()
+        done = []
+        for r, t, lp in zip(pend["reqs"], toks, lps):
+            if r.finished:
+                continue
+            had = self.sched.has_placeholder(r.id)
+            if had:
+                self.sched.set_last_token(r.id, t)
+            if self._emit(r, t, lp, now, appended=had):
+                done.append(r)
+        return done
+
+    def drain(self) -> List[Request]:
+        """Settle the in-flight pipelined step (if any)."""
+        with self.lock:
+            if self._pending is None:
+                return []
+            pend, self._pending = self._pending, None
+            return self._finalize(pend)
 
     # ------------------------------------------------------------------ tensor parallel
     # Rank 0 of a TP group drives: it schedules, then broadcasts the step layout (one int32
@@ -313,14 +435,15 @@ class LLMEngine:
         if self.p.tp_size > 1 and self.is_driver:
             self._sync_step(-1, 0, 0, 0, 0, 0)
 
-    def _emit(self, r: Request, tok: int, lp: float, now: float) -> bool:
+    def _emit(self, r: Request, tok: int, lp: float, now: float, appended: bool = False) -> bool:
         if r.first_token_time is None:
             r.first_token_time = now
             r.cached_prefix = self.sched.cached_prefix(r.id)
         r.output_ids.append(tok)
         if r.params.logprobs:
             r.logprobs.append(lp)
-        self.sched.append_token(r.id, tok)
+        if not appended:
+            self.sched.append_token(r.id, tok)
         delta = ""
         n = len(r.output_ids)
         reason = None

@@ -102,3 +102,18 @@ def test_embedding_engine_packing_order_and_truncation():
     assert len(ids) == 512
     with pytest.raises(ValueError):
         e.tokenize(["x " * 1000], truncate="NONE")
+
+
+def test_pipelined_decode_matches_synchronous(model):
+    p = SamplingParams(temperature=0.8, top_p=0.9, max_tokens=12, ignore_eos=True, seed=5)
+    a = [r.output_ids for r in _engine(model, async_decode=True).generate(PROMPTS, p)]
+    b = [r.output_ids for r in _engine(model, async_decode=False).generate(PROMPTS, p)]
+    assert a == b
+    # mixed lengths: sequences leave the batch at different steps
+    ps = [SamplingParams(temperature=0.0, max_tokens=m, ignore_eos=True) for m in (3, 9, 6)]
+    for async_ in (True, False):
+        e = _engine(model, async_decode=async_)
+        reqs = [e.add_request(pr, pp) for pr, pp in zip(PROMPTS, ps)]
+        e.run_until_done(reqs)
+        assert [len(r.output_ids) for r in reqs] == [3, 9, 6]
+        assert e.sched.used_blocks() == 0 or not e.has_work()
