@@ -34,7 +34,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--concurrency", type=int, default=64, help="requests per rank per step")
+    ap.add_argument("--concurrency", type=int, default=256, help="requests per rank per step")
     ap.add_argument("--max-tokens", type=int, default=256)
     ap.add_argument("--index-size", type=int, default=1_000_000)
     ap.add_argument("--model", default="llama3-8b")

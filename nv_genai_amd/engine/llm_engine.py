@@ -95,6 +95,7 @@ class EngineConfig:
     seed: int = 0
     detokenize: bool = True
     async_decode: bool = True  # pipeline decode steps (host work overlaps the GPU)
+    tuned_gemms: bool = True   # load the per-shape hipBLASLt/rocBLAS table (ops/gemm_tuning.py)
 
 
 class LLMEngine:
@@ -114,6 +115,10 @@ class LLMEngine:
         self.tok = tokenizer or llm_tokenizer()
         self.stop_ids = set(self.tok.stop_ids) | set(self.mcfg.eos_ids)
         self.gpu = self.device.type == "cuda"
+        if self.gpu and cfg.tuned_gemms:
+            from ..ops.gemm_tuning import use_tuned_gemms
+
+            self.tuned_gemms = use_tuned_gemms()
         # ---- KV cache
         nb = cfg.kv_cache_blocks
         if nb is None:
@@ -177,6 +182,7 @@ class LLMEngine:
         self.lock = threading.RLock()
         self._pending: Optional[dict] = None
         self._tok_flip = 0
+        self._up_ev = None  # marks the last host->device upload of the pinned step buffers
         self._tok_host = [(hbuf(S), hbuf(S, dtype=torch.float32)) for _ in range(2)]
         if self.p.tp_size > 1:
             # followers replay from broadcast host buffers; the device-side id gather of the
@@ -242,6 +248,10 @@ class LLMEngine:
                         and r.id in self.requests]
                 self.sched.append_placeholders(cont)
             ids, pos, sl, cu, ctx, bt, sid, smp = self._np
+            if self._up_ev is not None:
+                # the in-flight step's upload may still be queued behind the GPU's previous
+                # graph: the pinned buffers must not be rewritten before the DMA has read them
+                self._up_ev.synchronize()
             kind, n, ntok = self.sched.schedule(ids, pos, sl, cu, ctx, bt, sid, smp)
             if pend is not None:
                 rows = pend["rows"]
@@ -409,6 +419,8 @@ class LLMEngine:
         rows, toks = max(n, bs), max(ntok, bs)
         size = 3 * toks + (rows + 1) + rows + rows * self.max_blocks
         payload = self._bcast(torch.zeros(size, dtype=torch.int32)).cpu()
+        if self._up_ev is not None:
+            self._up_ev.synchronize()
         o = 0
         for buf, m in ((self.h_ids, toks), (self.h_pos, toks), (self.h_slots, toks), (self.h_cu, rows + 1),
                        (self.h_ctx, rows)):
@@ -496,6 +508,9 @@ class LLMEngine:
         for h, d in ((self.h_temp, self.d_temp), (self.h_topk, self.d_topk), (self.h_topp, self.d_topp),
                      (self.h_seed, self.d_seed), (self.h_step, self.d_step), (self.h_pen, self.d_pen)):
             d[:n].copy_(h[:n], non_blocking=non_blocking)
+        if self.gpu:
+            self._up_ev = torch.cuda.Event()
+            self._up_ev.record()
 
     def _sample(self, logits, n):
         rep = self.d_pen[:n] if self._needs_penalty(n) else None

@@ -238,6 +238,48 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
         order = sorted(range(len(logits)), key=lambda i: -logits[i])
         return {"rankings": [{"index": i, "logit": float(logits[i])} for i in order]}
 
+    # Triton "generate" extension (the TRT-LLM ensemble contract of
+    # experimental/AzureML/trt_llm_azureml.py:282-320): text_input + sampling knobs.
+    def _triton_params(b: dict) -> SamplingParams:
+        if int(b.get("beam_width", 1)) != 1:
+            raise ValueError("beam_width > 1 is not supported; use sampling")
+        stop = b.get("stop_words") or []
+        return SamplingParams(temperature=float(b.get("temperature", 1.0)), top_p=float(b.get("top_p", 1.0)),
+                              top_k=int(b.get("top_k", 0)), max_tokens=int(b.get("max_tokens", 64)),
+                              repetition_penalty=float(b.get("repetition_penalty", 1.0)),
+                              seed=b.get("random_seed"), stop=[stop] if isinstance(stop, str) else list(stop),
+                              ignore_eos=bool(b.get("ignore_eos", False)))
+
+    @app.post("/v2/models/{model}/generate")
+    async def triton_generate(model: str, request: Request):
+        svc = _need(app.state.llm, "LLM")
+        b = await request.json()
+        try:
+            params = _triton_params(b)
+        except ValueError as e:
+            return JSONResponse({"error": str(e)}, status_code=400)
+        tok = svc.engine.tok
+        h = svc.submit([tok.bos_id] + tok.encode(b.get("text_input", "")), params)
+        text = await _complete(h, time.perf_counter())
+        return {"model_name": model, "model_version": "1", "text_output": text}
+
+    @app.post("/v2/models/{model}/generate_stream")
+    async def triton_generate_stream(model: str, request: Request):
+        svc = _need(app.state.llm, "LLM")
+        b = await request.json()
+        try:
+            params = _triton_params(b)
+        except ValueError as e:
+            return JSONResponse({"error": str(e)}, status_code=400)
+        tok = svc.engine.tok
+        h = svc.submit([tok.bos_id] + tok.encode(b.get("text_input", "")), params)
+
+        async def gen():
+            async for d in h.aiter():
+                yield "data: " + json.dumps({"model_name": model, "model_version": "1", "text_output": d}) + "\n\n"
+
+        return StreamingResponse(gen(), media_type="text/event-stream")
+
     @app.get("/v1/models")
     def models():
         out = []

@@ -128,3 +128,30 @@ def test_http_connectors_roundtrip(http_url):
 def test_metrics_exposed(client):
     t = client.get("/metrics").text
     assert "model_server_chat_requests_total" in t and "model_server_kv_usage" in t
+
+
+def test_triton_generate_connector(http_url):
+    from nv_genai_amd.connectors.triton import TritonLLM
+
+    llm = TritonLLM(http_url.replace("http://", ""), model_name="ensemble", tokens=4, temperature=0.0)
+    whole = llm.invoke("tell me", ignore_eos=True)
+    streamed = "".join(llm.stream("tell me", ignore_eos=True))
+    assert whole == streamed and isinstance(whole, str)
+
+
+def test_router_proxies_and_balances(http_url):
+    from fastapi.testclient import TestClient
+
+    from nv_genai_amd.serving.router import create_router
+
+    app = create_router([http_url, http_url + "/"])
+    with TestClient(app) as c:
+        assert [m["id"] for m in c.get("/v1/models").json()["data"]][0] == "tiny-llm"
+        body = {"messages": [{"role": "user", "content": "hi"}], "max_tokens": 3, "ignore_eos": True,
+                "temperature": 0.0}
+        a = c.post("/v1/chat/completions", json=body).json()
+        s = c.post("/v1/chat/completions", json=dict(body, stream=True)).text
+        assert a["usage"]["completion_tokens"] == 3
+        assert s.rstrip().endswith("data: [DONE]")
+        st = c.get("/router/status").json()
+        assert all(v == 0 for v in st["inflight"].values())
