@@ -103,3 +103,97 @@ def test_kg_rag_modes(tmp_path):
     c = rag.context("what memory does the MI355X have?", mode="combined")
     assert "facts" in c and "Passages" in c
     assert rag.answer("MI355X memory?").startswith("answer:")
+
+
+class ListLLM:
+    """Answers multi-query prompts with a list, everything else with a fixed string."""
+
+    def __init__(self):
+        self.prompts = []
+
+    def stream(self, messages, **kw):
+        yield self.invoke(messages)
+
+    def invoke(self, messages, **kw):
+        text = messages[-1][1]
+        self.prompts.append(text)
+        if "different versions" in text:
+            return "Here are the questions:\n1. hbm3e capacity of mi355x\n2) xgmi links between gpus\n\n- llamas"
+        if "summarize" in text:
+            return "summary: user asked about gpus"
+        if "[[RESPONSE]]" in text:
+            return "**:green[TRUE]** supported"
+        if "rewrite" in messages[0][1] if len(messages) > 1 else False:
+            return "rewritten: how much memory does the mi355x have"
+        return "the gpu memory is large"
+
+
+def test_parse_lines_and_dedupe():
+    from nv_genai_amd.rag.advanced import dedupe, parse_lines, sources_of
+    from nv_genai_amd.index.vectorstore import Document
+
+    assert parse_lines("Here are:\n1. a\n2) b\n\n- c\n") == ["a", "b", "c"]
+    docs = [Document("x", {"source": "s1"}), Document("x", {"source": "s2"}), Document("y", {"source": "s1"})]
+    d = dedupe(docs)
+    assert [x.metadata["source"] for x in d] == ["s1", "s1"]
+    assert sources_of(d)["s1"]["doc_content"] == "x\n\ny"
+
+
+def test_advanced_retriever_modes():
+    from nv_genai_amd.rag.advanced import AdvancedRetriever
+
+    class Rev:
+        def rank(self, q, texts):
+            return [{"index": i, "logit": -i} for i in range(len(texts))][::-1]
+
+    st = _store()
+    llm = ListLLM()
+    r = AdvancedRetriever(st, llm, Rev(), k=4, score_threshold=0.0, top_n=2)
+    d0, ctx0, _ = r.retrieve("hbm3e memory of the mi355x", 0)
+    assert len(d0) == 4 and ctx0.count("\n\n") == 4
+    d1, _, src1 = r.retrieve("hbm3e memory", 1)
+    assert len(d1) == 2 and len({x.page_content for x in d1}) == 2          # deduped + reranked top-2
+    d2, _, _ = r.retrieve("hbm3e memory", 2)
+    assert any("the gpu memory is large" in p for p in llm.prompts) or len(d2) == 2
+    with pytest.raises(ValueError):
+        r.retrieve("q", 9)
+
+
+def test_merger_and_embedding_filters():
+    from nv_genai_amd.index.vectorstore import Document
+    from nv_genai_amd.rag.advanced import (ContextualCompressionRetriever, EmbeddingsFilter,
+                                           EmbeddingsRedundantFilter, MergerRetriever)
+
+    class R:
+        def __init__(self, docs):
+            self.docs = docs
+
+        def invoke(self, q):
+            return self.docs
+
+    a = [Document("gpu memory hbm3e"), Document("llamas")]
+    b = [Document("gpu memory hbm3e"), Document("xgmi links"), Document("weather")]
+    merged = MergerRetriever([R(a), R(b)]).invoke("q")
+    assert [d.page_content for d in merged] == ["gpu memory hbm3e", "gpu memory hbm3e", "llamas", "xgmi links",
+                                                "weather"]
+    emb = HashEmbeddings(dim=128)
+    uniq = EmbeddingsRedundantFilter(emb).transform_documents(merged)
+    assert len(uniq) == 4
+    comp = ContextualCompressionRetriever(MergerRetriever([R(a), R(b)]),
+                                          [EmbeddingsRedundantFilter(emb), EmbeddingsFilter(emb, 0.99)])
+    assert [d.page_content for d in comp.invoke("gpu memory hbm3e")] == ["gpu memory hbm3e"]
+
+
+def test_advanced_chat_turn_memory_factcheck_feedback(tmp_path):
+    from nv_genai_amd.rag.advanced import AdvancedRAGChat, AdvancedRetriever, FeedbackLog
+
+    llm = ListLLM()
+    chat = AdvancedRAGChat(AdvancedRetriever(_store(), llm, None, k=2, score_threshold=0.0), llm, "You are ORAN bot")
+    out = chat.ask("what memory does the mi355x have")
+    assert out["answer"] == "the gpu memory is large" and out["fact_check"].startswith("**:green[TRUE]**")
+    assert chat.memory.buffer.startswith("summary")
+    out2 = chat.ask("and how fast is it?")                 # follow-up is rewritten against the summary
+    assert out2["query"].startswith("rewritten")
+    fb = FeedbackLog(str(tmp_path / "fb.jsonl"))
+    row = fb.submit({"score": "🙂", "text": "ok"}, "q", "r")
+    assert row["score"] == 4 and json.loads((tmp_path / "fb.jsonl").read_text())["comment"] == "Score: 4/5. Feedback: ok"
