@@ -7,11 +7,21 @@ timing). Each rank is a full serving replica (data parallel, SURVEY.md §2.E "DP
 replica)", CC9): Llama-3-8B engine + arctic-embed-l encoder + a 1M x 1024 in-HBM flat index
 (2 GB, replicated: cheaper than any per-query collective at this size).
 
-A *step* serves one wave of ``--concurrency`` RAG requests end to end, all inside the timed
-region: query embedding (encoder forward), top-4 cosine search over the 1M-vector index,
-1500-token context cap, prompt assembly with the reference ``rag_template`` + Llama-3 chat
-template, continuous-batched prefill + decode of ``--max-tokens`` tokens (EOS ignored so
-every request does the same work), streaming detokenisation.
+Every request is served end to end inside the timed region: query embedding (encoder
+forward), top-4 cosine search over the 1M-vector index, 1500-token context cap, prompt
+assembly with the reference ``rag_template`` + Llama-3 chat template, continuous-batched
+prefill + decode of ``--max-tokens`` tokens (EOS ignored so every request does the same
+work), streaming detokenisation.
+
+Load model (``--mode``):
+* ``closed`` (default): ``--concurrency`` closed-loop clients per GPU — each client sends
+  its next question as soon as its previous answer completes (the usual serving-benchmark
+  load). Clients ramp up one request lifetime apart so the run reaches steady state; a
+  *step* is ``--concurrency`` completed requests, so ``--steps K`` times K·C completions
+  after ``--warmup W``·C warm-up completions. Steady state is what mixed prefill/decode
+  batching is built for: each engine step decodes every running request and prefills the
+  newly arrived ones in the same GEMMs.
+* ``wave``: a step is one synchronized wave of C requests submitted together.
 
 Weights are random-init of the real architectures; the corpus is synthetic (index vectors
 are random unit vectors standing in for arctic-embed-l passage embeddings; chunk texts are
@@ -44,6 +54,8 @@ def parse():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    ap.add_argument("--mode", choices=("closed", "wave"), default="closed")
+    ap.add_argument("--mixed-prefill-tokens", type=int, default=2048)
     return ap.parse_args()
 
 
@@ -69,7 +81,8 @@ def main():
         sizes = sizes + (R,)
     ecfg = EngineConfig(model=args.model, max_num_seqs=max(R, 1), max_batched_tokens=args.max_batched_tokens,
                         max_model_len=8192, use_graphs=gpu and not args.no_graphs,
-                        graph_batch_sizes=sizes, seed=rank, kv_cache_fraction=0.3)
+                        graph_batch_sizes=sizes, seed=rank, kv_cache_fraction=0.3,
+                        mixed_prefill_tokens=args.mixed_prefill_tokens)
     llm = LLMEngine(ecfg, device=dev, pctx=pctx)
     emb = EmbeddingEngine(args.embed_model, device=dev, seed=rank)
     index = FlatIndex(emb.dim, "cosine", dev, capacity=args.index_size)
@@ -91,8 +104,31 @@ def main():
         qs = [gen.question() for _ in range(R)]
         return rag.run(qs, params)
 
-    for _ in range(args.warmup):
-        one_step()
+    active = {}                     # request id -> RAGResult of the closed-loop clients
+    ramp = max(1, -(-R // max(1, args.max_tokens)))  # new clients per engine step while ramping
+
+    def closed_loop(n_done: int, ramping: bool):
+        """Serve until ``n_done`` requests complete; a completed client re-submits at once."""
+        out = []
+        while len(out) < n_done:
+            need = R - len(active)
+            if ramping:
+                need = min(need, ramp)
+            if need > 0:
+                for res in rag.submit([gen.question() for _ in range(need)], params):
+                    active[res.request.id] = res
+            for req in llm.step():
+                res = active.pop(req.id, None)
+                if res is not None:
+                    out.append(res)
+            ramping = ramping and len(active) < R
+        return out
+
+    if args.mode == "wave":
+        for _ in range(args.warmup):
+            one_step()
+    else:
+        closed_loop(max(1, args.warmup) * R, ramping=True)
     pd.barrier()
     if gpu:
         torch.cuda.synchronize()
@@ -105,8 +141,11 @@ def main():
     llm.stats.update({k: 0 if isinstance(v, int) else 0.0 for k, v in llm.stats.items()})
     t0 = time.perf_counter()
     results = []
-    for _ in range(args.steps):
-        results += one_step()
+    if args.mode == "wave":
+        for _ in range(args.steps):
+            results += one_step()
+    else:
+        results = closed_loop(args.steps * R, ramping=False)
     if gpu:
         torch.cuda.synchronize()
     pd.barrier()
@@ -148,6 +187,8 @@ def main():
             "top_k": args.top_k,
             "max_tokens": args.max_tokens,
             "concurrency_per_gpu": R,
+            "load": args.mode,
+            "mixed_prefill_tokens": args.mixed_prefill_tokens,
         },
         "p50_latency_ms": round(1000 * p50, 1),
         "p95_latency_ms": round(1000 * p95, 1),
@@ -156,6 +197,8 @@ def main():
         "output_tokens_per_s": round(out_tok / t_max, 1),
         "prefill_s": round(llm.stats["prefill_time"], 3),
         "decode_s": round(llm.stats["decode_time"], 3),
+        "steps_prefill_decode_mixed": [llm.stats["prefill_steps"] - llm.stats["mixed_steps"],
+                                       llm.stats["decode_steps"], llm.stats["mixed_steps"]],
         "setup_s": round(setup_s, 1),
         "prefix_cache_hit_blocks": int(llm.sched.prefix_hits()),
         "distinct_docs_retrieved": len({d for r in results for d in r.doc_ids}),

@@ -152,131 +152,63 @@ class Scheduler {
     waiting_.push_back(id);
   }
 
-  // Fill the step buffers. Returns (kind, num_seqs, num_tokens); kind 0 idle, 1 prefill, 2 decode.
+  // Mixed steps (SARATHI-style piggybacking): when > 0, a step that has decode-ready
+  // sequences also carries up to this many prefill tokens, so the decode rows ride along the
+  // prefill GEMMs instead of re-reading every weight in a separate skinny decode step.
+  void set_mixed_prefill_tokens(int n) { mixed_tokens_ = std::max(0, n); }
+  int last_num_decode() const { return last_nd_; }
+
+  // Fill the step buffers. Returns (kind, num_seqs, num_tokens); kind 0 idle, 1 prefill,
+  // 2 decode, 3 mixed (rows [0, last_num_decode()) decode one token each, the rest prefill).
   // seq_ids[i], cu_q[i..i+1], ctx[i], sample[i] (1 = produce a token), block_tables[i][:] per seq.
   py::tuple schedule(py::array_t<int32_t> input_ids, py::array_t<int32_t> positions,
                      py::array_t<int32_t> slots, py::array_t<int32_t> cu_q,
                      py::array_t<int32_t> ctx, py::array_t<int32_t> block_tables,
                      py::array_t<int64_t> seq_ids, py::array_t<int32_t> sample) {
-    auto ids = input_ids.mutable_unchecked<1>();
-    auto pos = positions.mutable_unchecked<1>();
-    auto sl = slots.mutable_unchecked<1>();
-    auto cq = cu_q.mutable_unchecked<1>();
-    auto cx = ctx.mutable_unchecked<1>();
-    auto bt = block_tables.mutable_unchecked<2>();
-    auto sid = seq_ids.mutable_unchecked<1>();
-    auto smp = sample.mutable_unchecked<1>();
-    const int max_bt = (int)bt.shape(1);
-    const int cap_tokens = std::min<int>((int)ids.shape(0), max_tokens_);
-    const int cap_seqs = std::min<int>((int)sid.shape(0), max_seqs_);
+    Bufs B{input_ids.mutable_unchecked<1>(), positions.mutable_unchecked<1>(),
+           slots.mutable_unchecked<1>(), cu_q.mutable_unchecked<1>(), ctx.mutable_unchecked<1>(),
+           block_tables.mutable_unchecked<2>(), seq_ids.mutable_unchecked<1>(),
+           sample.mutable_unchecked<1>()};
+    const int cap_tokens = std::min<int>((int)B.ids.shape(0), max_tokens_);
+    const int cap_seqs = std::min<int>((int)B.sid.shape(0), max_seqs_);
+    last_nd_ = 0;
+
+    if (mixed_tokens_ > 0) {
+      std::vector<int64_t> dec = decode_ready();
+      if (!dec.empty()) {
+        std::vector<int64_t> ok = prepare_decode(dec, cap_seqs);
+        std::vector<int64_t> chosen;
+        std::vector<int> qlen;
+        pick_prefill(std::min(cap_tokens - (int)ok.size(), mixed_tokens_), cap_seqs - (int)ok.size(),
+                     chosen, qlen);
+        const std::vector<int> ones(ok.size(), 1);
+        B.cq(0) = 0;
+        int t = fill_rows(B, ok, ones, 0, 0);
+        if (chosen.empty()) return py::make_tuple(ok.empty() ? 0 : 2, (int)ok.size(), t);
+        last_nd_ = (int)ok.size();
+        t = fill_rows(B, chosen, qlen, (int)ok.size(), t);
+        return py::make_tuple(ok.empty() ? 1 : 3, (int)(ok.size() + chosen.size()), t);
+      }
+    }
 
     // ---- prefill: continue partially prefilled seqs, then admit waiting ones (FCFS)
     std::vector<int64_t> chosen;
     std::vector<int> qlen;
-    int budget = cap_tokens;
-    for (int64_t id : running_) {
-      Seq& s = seqs_.at(id);
-      const int todo = (int)s.toks.size() - s.computed;
-      if (todo > 1 || (todo == 1 && s.computed < s.prompt_len)) {
-        if ((int)chosen.size() >= cap_seqs || budget <= 0) break;
-        const int n = std::min(todo, budget);
-        chosen.push_back(id);
-        qlen.push_back(n);
-        budget -= n;
-      }
-    }
-    while (!waiting_.empty() && budget > 0 && (int)chosen.size() < cap_seqs &&
-           (int)running_.size() < max_seqs_) {
-      const int64_t id = waiting_.front();
-      Seq& s = seqs_.at(id);
-      if (!admit(s)) break;
-      waiting_.pop_front();
-      running_.push_back(id);
-      s.status = RUNNING;
-      const int todo = (int)s.toks.size() - s.computed;
-      const int n = std::min(todo, budget);
-      chosen.push_back(id);
-      qlen.push_back(n);
-      budget -= n;
-    }
+    pick_prefill(cap_tokens, cap_seqs, chosen, qlen);
     if (!chosen.empty()) {
-      int t = 0;
-      cq(0) = 0;
-      for (size_t i = 0; i < chosen.size(); ++i) {
-        Seq& s = seqs_.at(chosen[i]);
-        const int n = qlen[i];
-        for (int j = 0; j < n; ++j) {
-          const int p = s.computed + j;
-          ids(t) = s.toks[p];
-          pos(t) = p;
-          sl(t) = s.blocks[p / bs_] * bs_ + p % bs_;
-          ++t;
-        }
-        s.computed += n;
-        cq(i + 1) = t;
-        cx(i) = s.computed;
-        sid(i) = s.id;
-        smp(i) = s.computed == (int)s.toks.size() ? 1 : 0;
-        fill_bt(bt, (int)i, s, max_bt);
-        register_full_blocks(s);
-      }
+      B.cq(0) = 0;
+      const int t = fill_rows(B, chosen, qlen, 0, 0);
       return py::make_tuple(1, (int)chosen.size(), t);
     }
 
     // ---- decode: every running seq with all tokens but the last computed
-    std::vector<int64_t> dec;
-    for (int64_t id : running_) {
-      Seq& s = seqs_.at(id);
-      if ((int)s.toks.size() - s.computed == 1) dec.push_back(id);
-    }
+    std::vector<int64_t> dec = decode_ready();
     if (dec.empty()) return py::make_tuple(0, 0, 0);
-    // make room: each seq whose next token starts a new block needs one
-    std::sort(dec.begin(), dec.end(),
-              [&](int64_t a, int64_t b) { return seqs_.at(a).arrival < seqs_.at(b).arrival; });
-    std::vector<int64_t> ok;
-    for (size_t i = 0; i < dec.size(); ++i) {
-      Seq& s = seqs_.at(dec[i]);
-      if (s.status != RUNNING) continue;
-      const int p = s.computed;  // position of the token being computed now
-      bool have = p / bs_ < (int)s.blocks.size();
-      while (!have) {
-        const int b = bm_.alloc();
-        if (b >= 0) {
-          s.blocks.push_back(b);
-          have = true;
-          break;
-        }
-        // preempt the latest-arrived running decode seq (recompute later)
-        int64_t victim = -1;
-        for (size_t j = dec.size(); j-- > i + 1;) {
-          if (seqs_.at(dec[j]).status == RUNNING) {
-            victim = dec[j];
-            break;
-          }
-        }
-        if (victim < 0) victim = s.id;
-        preempt(victim);
-        if (victim == s.id) break;
-      }
-      if (have && s.status == RUNNING) ok.push_back(s.id);
-      if ((int)ok.size() >= cap_seqs) break;
-    }
-    cq(0) = 0;
-    for (size_t i = 0; i < ok.size(); ++i) {
-      Seq& s = seqs_.at(ok[i]);
-      const int p = s.computed;
-      ids(i) = s.toks[p];
-      pos(i) = p;
-      sl(i) = s.blocks[p / bs_] * bs_ + p % bs_;
-      s.computed += 1;
-      cq(i + 1) = (int)i + 1;
-      cx(i) = s.computed;
-      sid(i) = s.id;
-      smp(i) = 1;
-      fill_bt(bt, (int)i, s, max_bt);
-      register_full_blocks(s);
-    }
-    return py::make_tuple(ok.empty() ? 0 : 2, (int)ok.size(), (int)ok.size());
+    std::vector<int64_t> ok = prepare_decode(dec, cap_seqs);
+    const std::vector<int> ones(ok.size(), 1);
+    B.cq(0) = 0;
+    const int t = fill_rows(B, ok, ones, 0, 0);
+    return py::make_tuple(ok.empty() ? 0 : 2, (int)ok.size(), t);
   }
 
   void append_token(int64_t id, int32_t tok) {
@@ -352,6 +284,112 @@ class Scheduler {
   void reset_prefix_cache() { bm_.reset_prefix_cache(); }
 
  private:
+  struct Bufs {
+    py::detail::unchecked_mutable_reference<int32_t, 1> ids, pos, sl, cq, cx;
+    py::detail::unchecked_mutable_reference<int32_t, 2> bt;
+    py::detail::unchecked_mutable_reference<int64_t, 1> sid;
+    py::detail::unchecked_mutable_reference<int32_t, 1> smp;
+  };
+
+  // Prefill candidates: partially prefilled running seqs first, then FCFS admission.
+  void pick_prefill(int budget, int cap_seqs, std::vector<int64_t>& chosen, std::vector<int>& qlen) {
+    if (budget <= 0 || cap_seqs <= 0) return;
+    for (int64_t id : running_) {
+      Seq& s = seqs_.at(id);
+      const int todo = (int)s.toks.size() - s.computed;
+      if (todo > 1 || (todo == 1 && s.computed < s.prompt_len)) {
+        if ((int)chosen.size() >= cap_seqs || budget <= 0) break;
+        const int n = std::min(todo, budget);
+        chosen.push_back(id);
+        qlen.push_back(n);
+        budget -= n;
+      }
+    }
+    while (!waiting_.empty() && budget > 0 && (int)chosen.size() < cap_seqs &&
+           (int)running_.size() < max_seqs_) {
+      const int64_t id = waiting_.front();
+      Seq& s = seqs_.at(id);
+      if (!admit(s)) break;
+      waiting_.pop_front();
+      running_.push_back(id);
+      s.status = RUNNING;
+      const int todo = (int)s.toks.size() - s.computed;
+      const int n = std::min(todo, budget);
+      chosen.push_back(id);
+      qlen.push_back(n);
+      budget -= n;
+    }
+  }
+
+  std::vector<int64_t> decode_ready() {
+    std::vector<int64_t> dec;
+    for (int64_t id : running_) {
+      Seq& s = seqs_.at(id);
+      if ((int)s.toks.size() - s.computed == 1 && s.computed >= s.prompt_len) dec.push_back(id);
+    }
+    return dec;
+  }
+
+  // Give every decode seq whose next token starts a new block that block, preempting the
+  // latest arrivals (recompute later) when the pool is exhausted.
+  std::vector<int64_t> prepare_decode(std::vector<int64_t> dec, int cap_seqs) {
+    std::sort(dec.begin(), dec.end(),
+              [&](int64_t a, int64_t b) { return seqs_.at(a).arrival < seqs_.at(b).arrival; });
+    std::vector<int64_t> ok;
+    for (size_t i = 0; i < dec.size(); ++i) {
+      Seq& s = seqs_.at(dec[i]);
+      if (s.status != RUNNING) continue;
+      const int p = s.computed;  // position of the token being computed now
+      bool have = p / bs_ < (int)s.blocks.size();
+      while (!have) {
+        const int b = bm_.alloc();
+        if (b >= 0) {
+          s.blocks.push_back(b);
+          have = true;
+          break;
+        }
+        int64_t victim = -1;
+        for (size_t j = dec.size(); j-- > i + 1;) {
+          if (seqs_.at(dec[j]).status == RUNNING) {
+            victim = dec[j];
+            break;
+          }
+        }
+        if (victim < 0) victim = s.id;
+        preempt(victim);
+        if (victim == s.id) break;
+      }
+      if (have && s.status == RUNNING) ok.push_back(s.id);
+      if ((int)ok.size() >= cap_seqs) break;
+    }
+    return ok;
+  }
+
+  // Lay out rows [row0, row0 + ids.size()) starting at token t; returns the next token index.
+  int fill_rows(Bufs& B, const std::vector<int64_t>& ids, const std::vector<int>& qlen, int row0, int t) {
+    const int max_bt = (int)B.bt.shape(1);
+    for (size_t i = 0; i < ids.size(); ++i) {
+      Seq& s = seqs_.at(ids[i]);
+      const int n = qlen[i];
+      for (int j = 0; j < n; ++j) {
+        const int p = s.computed + j;
+        B.ids(t) = s.toks[p];
+        B.pos(t) = p;
+        B.sl(t) = s.blocks[p / bs_] * bs_ + p % bs_;
+        ++t;
+      }
+      s.computed += n;
+      const int r = row0 + (int)i;
+      B.cq(r + 1) = t;
+      B.cx(r) = s.computed;
+      B.sid(r) = s.id;
+      B.smp(r) = s.computed == (int)s.toks.size() ? 1 : 0;
+      fill_bt(B.bt, r, s, max_bt);
+      register_full_blocks(s);
+    }
+    return t;
+  }
+
   bool admit(Seq& s) {
     // prefix-cache lookup over full blocks, keeping >= 1 token to compute
     const int n = (int)s.toks.size();
@@ -422,6 +460,8 @@ class Scheduler {
   std::vector<int64_t> running_;
   int64_t clock_ = 0;
   int64_t preempt_count_ = 0;
+  int mixed_tokens_ = 0;
+  int last_nd_ = 0;
 };
 
 }  // namespace
@@ -468,7 +508,9 @@ PYBIND11_MODULE(_rt, m) {
       .def("total_blocks", &Scheduler::total_blocks)
       .def("prefix_hits", &Scheduler::prefix_hits)
       .def("preemptions", &Scheduler::preemptions)
-      .def("reset_prefix_cache", &Scheduler::reset_prefix_cache);
+      .def("reset_prefix_cache", &Scheduler::reset_prefix_cache)
+      .def("set_mixed_prefill_tokens", &Scheduler::set_mixed_prefill_tokens)
+      .def("last_num_decode", &Scheduler::last_num_decode);
   register_bm25(m);
   register_text(m);
 }

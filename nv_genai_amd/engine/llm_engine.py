@@ -25,6 +25,7 @@ import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence
 
+import numpy as np
 import torch
 
 from .. import ops
@@ -94,8 +95,12 @@ class EngineConfig:
     decode_pages_per_part: int = 16
     seed: int = 0
     detokenize: bool = True
-    async_decode: bool = True  # pipeline decode steps (host work overlaps the GPU)
+    async_decode: bool = True  # pipeline steps (host work overlaps the GPU)
+    mixed_prefill_tokens: int = 2048  # prefill tokens that ride along a decode step (0 = off)
     tuned_gemms: bool = True   # load the per-shape hipBLASLt/rocBLAS table (ops/gemm_tuning.py)
+
+
+_INERT = Request(id=-1, prompt_ids=[0], params=SamplingParams(temperature=0.0))
 
 
 class LLMEngine:
@@ -133,6 +138,7 @@ class LLMEngine:
         self.sched = rt.Scheduler(self.num_blocks, cfg.block_size, cfg.max_num_seqs,
                                   cfg.max_batched_tokens, cfg.max_model_len,
                                   cfg.enable_prefix_caching)
+        self.sched.set_mixed_prefill_tokens(cfg.mixed_prefill_tokens)
         # ---- host step buffers (pinned) filled by the native scheduler
         pin = self.gpu
         T, S = max(cfg.max_batched_tokens, cfg.max_num_seqs), cfg.max_num_seqs
@@ -177,7 +183,7 @@ class LLMEngine:
         self._ids = itertools.count(1)
         self._rng = random.Random(cfg.seed)
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
-        self.stats = {"prefill_steps": 0, "decode_steps": 0, "prefill_tokens": 0,
+        self.stats = {"prefill_steps": 0, "decode_steps": 0, "mixed_steps": 0, "prefill_tokens": 0,
                       "decode_tokens": 0, "prefill_time": 0.0, "decode_time": 0.0}
         self.lock = threading.RLock()
         self._pending: Optional[dict] = None
@@ -225,6 +231,10 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ step
     def _fill_params(self, reqs, pending_ids=()):
+        """Per-row sampling parameters. A row whose request finished while its step was being
+        settled (None) samples greedily and is ignored."""
+        if any(r is None for r in reqs):
+            reqs = [r if r is not None else _INERT for r in reqs]
         n = len(reqs)
         self.n_temp[:n] = [r.params.temperature for r in reqs]
         self.n_topk[:n] = [r.params.top_k for r in reqs]
@@ -236,110 +246,102 @@ class LLMEngine:
     def step(self) -> List[Request]:
         """Run one scheduler step; returns requests that finished in it.
 
-        Decode steps are pipelined when possible: step k+1 is scheduled and launched before
-        step k's tokens are read back (its input ids are gathered on the GPU from step k's
-        output), so host work — reading tokens, detokenising, stop checks, scheduling —
-        overlaps the GPU instead of serialising with it."""
+        Steps are pipelined when possible: step k+1 is scheduled and launched before step k's
+        tokens are read back (input ids that step k is still producing are gathered on the
+        GPU from its output), so host work — reading tokens, detokenising, stop checks,
+        scheduling — overlaps the GPU instead of serialising with it. With mixed batching
+        (``mixed_prefill_tokens``) a step carries the decode rows of every running sequence
+        plus a prefill chunk, so decode rows ride on the prefill GEMMs."""
         with self.lock:
             pend = self._pending
             done: List[Request] = []
             if pend is not None:
-                cont = [r.id for r in pend["reqs"] if len(r.output_ids) + 1 < r.params.max_tokens
-                        and r.id in self.requests]
+                cont = [r.id for r, s in zip(pend["reqs"], pend["smp"]) if s and r is not None
+                        and len(r.output_ids) + 1 < r.params.max_tokens and r.id in self.requests]
                 self.sched.append_placeholders(cont)
             ids, pos, sl, cu, ctx, bt, sid, smp = self._np
             if self._up_ev is not None:
                 # the in-flight step's upload may still be queued behind the GPU's previous
-                # graph: the pinned buffers must not be rewritten before the DMA has read them
+                # step: the pinned buffers must not be rewritten before the DMA has read them
                 self._up_ev.synchronize()
             kind, n, ntok = self.sched.schedule(ids, pos, sl, cu, ctx, bt, sid, smp)
+            nd = n if kind == 2 else (self.sched.last_num_decode() if kind == 3 else 0)
+            src = None
             if pend is not None:
+                ph = np.flatnonzero(ids[:ntok] < 0) if kind else np.empty(0, dtype=np.int64)
                 rows = pend["rows"]
-                sids = sid[:n].tolist()
-                if (kind == 2 and all(s in rows for s in sids)
-                        and not self._needs_penalty_reqs(pend["reqs"])):
-                    t0 = time.perf_counter()
-                    reqs = [self.requests[s] for s in sids]
-                    self._fill_params(reqs, pending_ids=rows)
-                    src = torch.tensor([rows[s] for s in sids], dtype=torch.int64)
-                    nxt = self._decode_launch(n, src)
+                ok = (kind != 0 and self.cfg.async_decode and not self._needs_penalty_reqs(pend["reqs"])
+                      and all(i < nd and int(sid[i]) in rows for i in ph.tolist()))
+                if ok:
+                    src = (ph, [rows[int(sid[i])] for i in ph.tolist()])
+                else:
+                    # cannot pipeline: settle the in-flight step, then run this one normally
                     done += self._finalize(pend)
-                    self.stats["decode_steps"] += 1
-                    self.stats["decode_tokens"] += n
-                    self.stats["decode_time"] += time.perf_counter() - t0
-                    self._pending = nxt
-                    return done
-                # cannot pipeline: settle the in-flight step first, then run this one normally
-                done += self._finalize(pend)
-                self._pending = None
-                for i in range(n):
-                    if ids[i] < 0:
-                        ids[i] = self.sched.tokens(int(sid[i]))[pos[i]]
-                if kind == 0:
-                    return done
-            elif kind == 0:
-                return []
+                    pend = self._pending = None
+                    for i in ph.tolist():
+                        r = int(np.searchsorted(cu[1:n + 1], i, side="right"))
+                        try:
+                            ids[i] = self.sched.tokens(int(sid[r]))[pos[i]]
+                        except (IndexError, KeyError):  # finished meanwhile: row is inert
+                            ids[i] = 0
+            if kind == 0:
+                return done
             t0 = time.perf_counter()
-            reqs = [self.requests[int(s)] for s in sid[:n].tolist()]
-            self._fill_params(reqs)
-            if kind == 2 and self.cfg.async_decode and not self._needs_penalty(n):
-                self._pending = self._decode_launch(n, None)
-                self.stats["decode_steps"] += 1
-                self.stats["decode_tokens"] += n
-                self.stats["decode_time"] += time.perf_counter() - t0
+            reqs = [self.requests.get(int(s)) for s in sid[:n].tolist()]
+            pending_ids = pend["sampled"] if pend is not None else ()
+            self._fill_params(reqs, pending_ids=pending_ids)
+            key = "decode_time" if kind == 2 else "prefill_time"
+            self._count(kind, n, ntok, nd)
+            if self.cfg.async_decode and not self._needs_penalty(n):
+                nxt = self._launch(kind, n, ntok, nd, src)
+                if pend is not None:
+                    done += self._finalize(pend)
+                self._pending = nxt
+                self.stats[key] += time.perf_counter() - t0
                 return done
             if kind == 2:
                 toks, lps = self._decode(n)
-                self.stats["decode_steps"] += 1
-                self.stats["decode_tokens"] += n
-                key = "decode_time"
             else:
-                toks, lps = self._prefill(n, ntok)
-                self.stats["prefill_steps"] += 1
-                self.stats["prefill_tokens"] += ntok
-                key = "prefill_time"
+                toks, lps = self._prefill(n, ntok, nd)
             toks = toks.tolist()
             lps = lps.tolist()
             self.stats[key] += time.perf_counter() - t0
             now = time.perf_counter()
             for i, (r, s) in enumerate(zip(reqs, smp[:n].tolist())):
-                if s and self._emit(r, toks[i], lps[i], now):
+                if s and r is not None and not r.finished and self._emit(r, toks[i], lps[i], now):
                     done.append(r)
             return done
 
-    def _needs_penalty_reqs(self, reqs) -> bool:
-        return any(r.params.repetition_penalty != 1.0 for r in reqs)
-
-    def _decode_launch(self, n: int, src_rows: Optional[torch.Tensor]) -> dict:
-        """Replay the decode graph for n rows without waiting for it. ``src_rows`` (row of
-        each sequence in the previous in-flight step) gathers the input ids on the device
-        from that step's sampled tokens. Tokens are copied to pinned host memory right after
-        the graph so the next step may overwrite the device buffer."""
-        bs = next((b for b in sorted(self.graphs) if b >= n), None)
-        if bs is not None:
-            self.h_slots[n:bs] = -1
-            self.h_ctx[n:bs] = 0
-            self.h_ids[n:bs] = 0
-            self.h_pos[n:bs] = 0
-            self.h_temp[n:bs] = 0.0
-            self.h_topk[n:bs] = 0
-            self.h_topp[n:bs] = 1.0
-            self.h_step[n:bs] = 0
-            self.h_seed[n:bs] = 0
-        self._sync_step(2, n, n, 1, self.cfg.max_model_len, bs or 0)
-        self._upload(bs or n, bs or n)
-        if src_rows is not None:
-            idx = src_rows.to(self.device, non_blocking=True)
-            self.d_ids[:n] = self.d_tok.index_select(0, idx)
-        if bs is not None:
-            self.graphs[bs].replay()
+    def _count(self, kind, n, ntok, nd):
+        if kind == 2:
+            self.stats["decode_steps"] += 1
+            self.stats["decode_tokens"] += n
         else:
-            meta = self._meta("decode", n, n, 1, self.cfg.max_model_len)
-            logits = self.model.logits(self.model.forward(self.d_ids[:n], self.d_pos[:n], meta))
-            tok, lp = self._sample(logits, n)
-            if tok.data_ptr() != self.d_tok.data_ptr():
-                self.d_tok[:n].copy_(tok[:n])
-                self.d_lp[:n].copy_(lp[:n])
+            self.stats["prefill_steps"] += 1
+            self.stats["prefill_tokens"] += ntok - nd
+            if nd:
+                self.stats["mixed_steps"] += 1
+                self.stats["decode_tokens"] += nd
+
+    def _needs_penalty_reqs(self, reqs) -> bool:
+        return any(r is not None and r.params.repetition_penalty != 1.0 for r in reqs)
+
+    def _launch(self, kind: int, n: int, ntok: int, nd: int, src) -> dict:
+        """Launch a step without waiting for it. ``src = (token_idx, prev_rows)`` gathers the
+        input ids the previous in-flight step is still producing from its device output.
+        Tokens are copied to pinned host memory right after sampling, so the next step may
+        overwrite the device buffers."""
+        if kind == 2:
+            self._decode_launch(n, src)
+        else:
+            cu = self._np[3][: n + 1]
+            max_q = int((cu[1:] - cu[:-1]).max())
+            max_ctx = int(self._np[4][:n].max())
+            self._sync_step(kind, n, ntok, max_q, max_ctx, 0, nd)
+            self._upload(n, ntok)
+            self._gather_ids(src)
+            logits = self._prefill_forward(n, ntok, max_q, max_ctx, nd)
+            self._sample(logits, n)
         buf = self._tok_host[self._tok_flip]
         self._tok_flip ^= 1
         buf[0][:n].copy_(self.d_tok[:n], non_blocking=self.gpu)
@@ -348,8 +350,49 @@ class LLMEngine:
         if self.gpu:
             ev = torch.cuda.Event()
             ev.record()
-        reqs = [self.requests[int(s)] for s in self._np[6][:n].tolist()]
-        return {"reqs": reqs, "rows": {r.id: i for i, r in enumerate(reqs)}, "n": n, "buf": buf, "ev": ev}
+        reqs = [self.requests.get(int(s)) for s in self._np[6][:n].tolist()]
+        smp = self._np[7][:n].tolist()
+        return {"reqs": reqs, "smp": smp, "rows": {int(s): i for i, s in enumerate(self._np[6][:n].tolist())},
+                "sampled": {r.id for r, m in zip(reqs, smp) if m and r is not None},
+                "n": n, "buf": buf, "ev": ev}
+
+    def _gather_ids(self, src) -> None:
+        if src is None or len(src[0]) == 0:
+            return
+        idx = torch.as_tensor(src[0], dtype=torch.int64).to(self.device, non_blocking=True)
+        prev = torch.as_tensor(src[1], dtype=torch.int64).to(self.device, non_blocking=True)
+        self.d_ids.index_copy_(0, idx, self.d_tok.index_select(0, prev))
+
+    def _decode_launch(self, n: int, src) -> None:
+        """Replay the decode graph for n rows (padded to the captured bucket)."""
+        bs = next((b for b in sorted(self.graphs) if b >= n), None)
+        if bs is not None:
+            self._pad_rows(n, bs)
+        self._sync_step(2, n, n, 1, self.cfg.max_model_len, bs or 0)
+        self._upload(bs or n, bs or n)
+        if src is not None and len(src[0]) == n:
+            prev = torch.as_tensor(src[1], dtype=torch.int64).to(self.device, non_blocking=True)
+            self.d_ids[:n] = self.d_tok.index_select(0, prev)
+        else:
+            self._gather_ids(src)
+        if bs is not None:
+            self.graphs[bs].replay()
+        else:
+            meta = self._meta("decode", n, n, 1, self.cfg.max_model_len)
+            logits = self.model.logits(self.model.forward(self.d_ids[:n], self.d_pos[:n], meta))
+            self._sample(logits, n)
+
+    def _pad_rows(self, n: int, bs: int) -> None:
+        """Padding rows of a graph bucket: no cache write, empty context, greedy."""
+        self.h_slots[n:bs] = -1
+        self.h_ctx[n:bs] = 0
+        self.h_ids[n:bs] = 0
+        self.h_pos[n:bs] = 0
+        self.h_temp[n:bs] = 0.0
+        self.h_topk[n:bs] = 0
+        self.h_topp[n:bs] = 1.0
+        self.h_step[n:bs] = 0
+        self.h_seed[n:bs] = 0
 
     def _finalize(self, pend: dict) -> List[Request]:
         if pend["ev"] is not None:
@@ -359,8 +402,8 @@ class LLMEngine:
         lps = pend["buf"][1][:n].tolist()
         now = time.perf_counter()
         done = []
-        for r, t, lp in zip(pend["reqs"], toks, lps):
-            if r.finished:
+        for r, s, t, lp in zip(pend["reqs"], pend["smp"], toks, lps):
+            if not s or r is None or r.finished:
                 continue
             had = self.sched.has_placeholder(r.id)
             if had:
@@ -397,11 +440,11 @@ class LLMEngine:
         dist.broadcast(x, src=self._tp_src(), group=self.p.tp_group)
         return x
 
-    def _sync_step(self, kind: int, n: int, ntok: int, max_q: int, max_ctx: int, bs: int) -> None:
+    def _sync_step(self, kind: int, n: int, ntok: int, max_q: int, max_ctx: int, bs: int, nd: int = 0) -> None:
         """Driver: publish the step (header + packed int buffers) to the TP group."""
         if self.p.tp_size == 1:
             return
-        hdr = torch.tensor([kind, n, ntok, max_q, max_ctx, bs, 0, 0], dtype=torch.int64)
+        hdr = torch.tensor([kind, n, ntok, max_q, max_ctx, bs, nd, 0], dtype=torch.int64)
         self._bcast(hdr)
         if kind < 0:
             return
@@ -413,9 +456,9 @@ class LLMEngine:
 
     def _recv_step(self):
         hdr = self._bcast(torch.zeros(8, dtype=torch.int64)).cpu().tolist()
-        kind, n, ntok, max_q, max_ctx, bs = hdr[:6]
+        kind, n, ntok, max_q, max_ctx, bs, nd = hdr[:7]
         if kind < 0:
-            return kind, 0, 0, 0, 0, 0
+            return kind, 0, 0, 0, 0, 0, 0
         rows, toks = max(n, bs), max(ntok, bs)
         size = 3 * toks + (rows + 1) + rows + rows * self.max_blocks
         payload = self._bcast(torch.zeros(size, dtype=torch.int32)).cpu()
@@ -427,16 +470,17 @@ class LLMEngine:
             buf[:m] = payload[o:o + m]
             o += m
         self.h_bt[:rows] = payload[o:o + rows * self.max_blocks].view(rows, self.max_blocks)
-        return kind, n, ntok, max_q, max_ctx, bs
+        return kind, n, ntok, max_q, max_ctx, bs, nd
 
     def run_follower(self) -> None:
         """Non-driver TP ranks: execute every step the driver publishes."""
         while True:
-            kind, n, ntok, max_q, max_ctx, bs = self._recv_step()
+            kind, n, ntok, max_q, max_ctx, bs, nd = self._recv_step()
             if kind < 0:
                 return
-            if kind == 1:
-                self._prefill_compute(n, ntok, max_q, max_ctx)
+            if kind in (1, 3):
+                self._upload(n, ntok)
+                self._prefill_forward(n, ntok, max_q, max_ctx, nd)
             elif bs:
                 self._upload(bs, bs)
                 self.graphs[bs].replay()
@@ -445,7 +489,7 @@ class LLMEngine:
 
     def stop_followers(self) -> None:
         if self.p.tp_size > 1 and self.is_driver:
-            self._sync_step(-1, 0, 0, 0, 0, 0)
+            self._sync_step(-1, 0, 0, 0, 0, 0, 0)
 
     def _emit(self, r: Request, tok: int, lp: float, now: float, appended: bool = False) -> bool:
         if r.first_token_time is None:
@@ -492,10 +536,15 @@ class LLMEngine:
             return True
         return False
 
-    def _meta(self, kind, n, ntok, max_q, max_ctx) -> AttnMeta:
-        return AttnMeta(kind=kind, slots=self.d_slots[:ntok], cu_q=self.d_cu[: n + 1],
-                        ctx_lens=self.d_ctx[:n], block_tables=self.d_bt[:n], max_q_len=max_q,
-                        max_ctx=max_ctx, decode_ws=self.decode_ws)
+    def _meta(self, kind, n, ntok, max_q, max_ctx, nd: int = 0) -> AttnMeta:
+        m = AttnMeta(kind=kind, slots=self.d_slots[:ntok], cu_q=self.d_cu[: n + 1],
+                     ctx_lens=self.d_ctx[:n], block_tables=self.d_bt[:n], max_q_len=max_q,
+                     max_ctx=max_ctx, decode_ws=self.decode_ws)
+        if nd:
+            # mixed step: rows [0, nd) decode, the rest prefill with its own cu_seqlens
+            m.kind, m.n_decode, m.max_ctx = "mixed", nd, self.cfg.max_model_len
+            m.cu_q_prefill = self.d_cu[nd: n + 1] - nd
+        return m
 
     def _upload(self, n, ntok):
         nb = non_blocking = self.gpu
@@ -515,9 +564,13 @@ class LLMEngine:
     def _sample(self, logits, n):
         rep = self.d_pen[:n] if self._needs_penalty(n) else None
         hist = self._history(n) if rep is not None else None
-        return ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n],
-                          self.d_seed[:n], self.d_step[:n], rep, hist,
-                          out_tok=self.d_tok[:n], out_lp=self.d_lp[:n])
+        tok, lp = ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n],
+                             self.d_seed[:n], self.d_step[:n], rep, hist,
+                             out_tok=self.d_tok[:n], out_lp=self.d_lp[:n])
+        if tok.data_ptr() != self.d_tok.data_ptr():   # reference path returns fresh tensors
+            self.d_tok[:n].copy_(tok[:n])
+            self.d_lp[:n].copy_(lp[:n])
+        return self.d_tok[:n], self.d_lp[:n]
 
     def _needs_penalty(self, n) -> bool:
         return bool((self.h_pen[:n] != 1.0).any())
@@ -530,18 +583,19 @@ class LLMEngine:
             h[i, : len(r)] = torch.tensor(r, dtype=torch.int32)
         return h.to(self.device)
 
-    def _prefill(self, n, ntok):
+    def _prefill(self, n, ntok, nd: int = 0):
+        """Synchronous prefill (nd = 0) or mixed step (rows [0, nd) decode)."""
         cu = self._np[3][: n + 1]
-        max_q = int((cu[1:] - cu[:-1]).max())
+        max_q = int((cu[nd + 1:] - cu[nd:-1]).max())
         max_ctx = int(self._np[4][:n].max())
-        self._sync_step(1, n, ntok, max_q, max_ctx, 0)
-        logits = self._prefill_compute(n, ntok, max_q, max_ctx)
+        self._sync_step(3 if nd else 1, n, ntok, max_q, max_ctx, 0, nd)
+        self._upload(n, ntok)
+        logits = self._prefill_forward(n, ntok, max_q, max_ctx, nd)
         tok, lp = self._sample(logits, n)
         return tok[:n].cpu(), lp[:n].cpu()
 
-    def _prefill_compute(self, n, ntok, max_q, max_ctx):
-        self._upload(n, ntok)
-        meta = self._meta("prefill", n, ntok, max_q, max_ctx)
+    def _prefill_forward(self, n, ntok, max_q, max_ctx, nd: int = 0):
+        meta = self._meta("prefill", n, ntok, max_q, max_ctx, nd)
         sample_idx = (self.d_cu[1: n + 1] - 1).long()
         h = self.model.forward(self.d_ids[:ntok], self.d_pos[:ntok], meta, sample_idx)
         return self.model.logits(h)
@@ -550,16 +604,7 @@ class LLMEngine:
         if self.graphs and not self._needs_penalty(n):
             bs = next((b for b in sorted(self.graphs) if b >= n), None)
             if bs is not None:
-                # padding rows: no cache write, empty context, greedy
-                self.h_slots[n:bs] = -1
-                self.h_ctx[n:bs] = 0
-                self.h_ids[n:bs] = 0
-                self.h_pos[n:bs] = 0
-                self.h_temp[n:bs] = 0.0
-                self.h_topk[n:bs] = 0
-                self.h_topp[n:bs] = 1.0
-                self.h_step[n:bs] = 0
-                self.h_seed[n:bs] = 0
+                self._pad_rows(n, bs)
                 self._sync_step(2, n, n, 1, self.cfg.max_model_len, bs)
                 self._upload(bs, bs)
                 self.graphs[bs].replay()

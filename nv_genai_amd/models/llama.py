@@ -40,6 +40,8 @@ class AttnMeta:
     max_q_len: int
     max_ctx: int
     decode_ws: Optional[ops.DecodeWorkspace] = None
+    n_decode: int = 0                          # mixed steps: rows [0, n_decode) are decode rows
+    cu_q_prefill: Optional[torch.Tensor] = None  # mixed steps: cu_seqlens of the prefill rows
 
 
 class LlamaModel:
@@ -189,6 +191,16 @@ class LlamaModel:
                 attn = ops.decode_attention(q, self.k_cache[li], self.v_cache[li],
                                             meta.block_tables, meta.ctx_lens, hq, hkv,
                                             meta.max_ctx, self.scale, ws=meta.decode_ws)
+            elif meta.kind == "mixed":
+                nd = meta.n_decode
+                attn = torch.empty(T, qdim, dtype=qkv.dtype, device=qkv.device)
+                ops.decode_attention(q[:nd], self.k_cache[li], self.v_cache[li],
+                                     meta.block_tables[:nd], meta.ctx_lens[:nd], hq, hkv,
+                                     meta.max_ctx, self.scale, out=attn[:nd], ws=meta.decode_ws)
+                ops.prefill_attention_paged(q[nd:], self.k_cache[li], self.v_cache[li],
+                                            meta.block_tables[nd:], meta.cu_q_prefill,
+                                            meta.ctx_lens[nd:], hq, hkv, D, meta.max_q_len,
+                                            self.scale, out=attn[nd:])
             else:
                 attn = ops.prefill_attention_paged(q, self.k_cache[li], self.v_cache[li],
                                                    meta.block_tables, meta.cu_q, meta.ctx_lens,

@@ -73,6 +73,10 @@ class RAGPipeline:
         self.max_ctx = max_context_tokens
         self.score_threshold = score_threshold
         self.set_template(template)
+        # retrieval runs on its own HIP stream so query embedding + search of newly arriving
+        # requests overlap the LLM step in flight instead of queueing behind it
+        dev = getattr(embedder, "device", torch.device("cpu"))
+        self.stream = torch.cuda.Stream(dev) if torch.device(dev).type == "cuda" else None
 
     def set_template(self, template: str):
         tok = self.llm.tok
@@ -85,9 +89,14 @@ class RAGPipeline:
             [tok.header_end] + tok.encode("\n\n")
 
     def retrieve(self, questions: Sequence[str]):
-        q = self.embedder.embed(questions, input_type="query")
-        scores, ids = self.index.search(q, self.top_k)
-        return scores.cpu(), ids.cpu()
+        if self.stream is None:
+            q = self.embedder.embed(questions, input_type="query")
+            scores, ids = self.index.search(q, self.top_k)
+            return scores.cpu(), ids.cpu()
+        with torch.cuda.stream(self.stream):
+            q = self.embedder.embed(questions, input_type="query")
+            scores, ids = self.index.search(q, self.top_k)
+            return scores.cpu(), ids.cpu()
 
     def context_ids(self, doc_ids: Sequence[int], scores: Sequence[float]) -> tuple:
         out: List[int] = []

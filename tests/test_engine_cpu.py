@@ -117,3 +117,25 @@ def test_pipelined_decode_matches_synchronous(model):
         e.run_until_done(reqs)
         assert [len(r.output_ids) for r in reqs] == [3, 9, 6]
         assert e.sched.used_blocks() == 0 or not e.has_work()
+
+
+@pytest.mark.parametrize("async_", [True, False])
+def test_mixed_prefill_decode_steps_exact(model, async_):
+    """Staggered arrivals: later prompts are prefilled inside steps that also decode the
+    running ones (mixed steps); greedy outputs equal the unmixed engine's."""
+    p = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
+    outs = []
+    for mixed in (0, 40):
+        e = _engine(model, mixed_prefill_tokens=mixed, async_decode=async_)
+        reqs = [e.add_request(PROMPTS[0], p)]
+        for i, pr in enumerate(PROMPTS[1:] + [[5, 6, 7] * 30]):
+            for _ in range(3):
+                e.step()
+            reqs.append(e.add_request(pr, p))
+        e.run_until_done(reqs)
+        outs.append([r.output_ids for r in reqs])
+        if mixed:
+            assert e.stats["mixed_steps"] > 0
+        else:
+            assert e.stats["mixed_steps"] == 0
+    assert outs[0] == outs[1]

@@ -43,7 +43,8 @@ def test_gpu_forward_matches_reference(gpu, weights):
         ids, pos, sl, cu, ctx, bt, sid, smp = eng._np
         kind, n, ntok = eng.sched.schedule(ids, pos, sl, cu, ctx, bt, sid, smp)
         cu_ = eng._np[3][: n + 1]
-        eng._logits = eng._prefill_compute(n, ntok, int((cu_[1:] - cu_[:-1]).max()), int(eng._np[4][:n].max()))
+        eng._upload(n, ntok)
+        eng._logits = eng._prefill_forward(n, ntok, int((cu_[1:] - cu_[:-1]).max()), int(eng._np[4][:n].max()))
     lg, lc = g._logits.float().cpu(), c._logits.float()
     rel = (lg - lc).norm() / lc.norm()
     assert rel < 0.03, f"relative logit error {rel:.4f}"
@@ -120,3 +121,37 @@ def test_flat_and_ivf_index_gpu(gpu):
     assert fg.remove([5, 6]) == 2
     _, i2 = fg.search(X[:2], 3)
     assert 5 not in i2.cpu().tolist()[0] and 6 not in i2.cpu().tolist()[1]
+
+
+def test_mixed_step_logits_match_separate_steps(gpu, weights):
+    """A mixed step (decode rows + a prefill chunk in one forward, decode kernel on the
+    first rows, paged prefill kernel on the rest) gives the same logits as running the
+    decode step and the prefill step separately."""
+    from nv_genai_amd.engine.llm_engine import SamplingParams
+
+    p = SamplingParams(temperature=0.0, max_tokens=4, ignore_eos=True)
+    seen = {}
+    for mixed in (0, 2048):
+        e = _engine(weights, "cuda", mixed_prefill_tokens=mixed, async_decode=False, use_graphs=False)
+        cap = {}
+        orig = e._sample
+
+        def sample(logits, n, e=e, cap=cap, orig=orig):
+            for i, s in enumerate(e._np[6][:n].tolist()):
+                cap.setdefault(int(s), []).append(logits[i].float().cpu())
+            return orig(logits, n)
+
+        e._sample = sample
+        a = e.add_request(PROMPTS[1], p)
+        e.step()                      # prefill A
+        e.step()                      # decode A
+        b = e.add_request(PROMPTS[0], p)
+        e.run_until_done([a, b])
+        if mixed:
+            assert e.stats["mixed_steps"] >= 1
+        seen[mixed] = (cap[a.id], cap[b.id], a.output_ids, b.output_ids)
+    for k in (0, 1):
+        for x, y in zip(seen[0][k][:2], seen[2048][k][:2]):
+            cos = torch.nn.functional.cosine_similarity(x, y, dim=0)
+            assert cos > 0.999, cos
+    assert seen[0][2][:3] == seen[2048][2][:3] and seen[0][3][:2] == seen[2048][3][:2]
