@@ -217,3 +217,16 @@ def test_pool(gpu):
         _close(ops.pool_l2norm(h, cu, mode, True), ref.pool_l2norm(h.cpu(), cu.cpu(), mode, True), 1e-4)
     X = _bf(1000, 1024, dev=gpu)
     _close(ops.row_sqnorm(X), ref.row_sqnorm(X.cpu()), 0.05, 1e-4)
+
+
+def test_hard_negative_mining_gpu_matches_cpu(gpu):
+    from nv_genai_amd.training.hard_negatives import mine_hard_negatives
+
+    g = torch.Generator().manual_seed(0)
+    q = torch.nn.functional.normalize(torch.randn(300, 128, generator=g), dim=1).bfloat16().float()
+    p = torch.nn.functional.normalize(torch.randn(9000, 128, generator=g), dim=1).bfloat16().float()
+    pos = [[i, (i * 13) % 9000] for i in range(300)]
+    cpu = mine_hard_negatives(q, p, pos, margin=0.9, num_negs=8)
+    gpu_ = mine_hard_negatives(q.cuda(), p.cuda(), pos, margin=0.9, num_negs=8, block=128)
+    agree = sum(len(set(a) & set(b)) for a, b in zip(cpu, gpu_)) / sum(len(a) for a in cpu)
+    assert agree > 0.97, agree
