@@ -107,21 +107,29 @@ def main():
     active = {}                     # request id -> RAGResult of the closed-loop clients
     ramp = max(1, -(-R // max(1, args.max_tokens)))  # new clients per engine step while ramping
 
+    pending = []                    # retrievals in flight on the retrieval stream
+    clients = [0]                   # clients with a question in the system (retrieving or generating)
+
     def closed_loop(n_done: int, ramping: bool):
-        """Serve until ``n_done`` requests complete; a completed client re-submits at once."""
+        """Serve until ``n_done`` requests complete; a completed client re-submits at once.
+        Each iteration launches the next engine step first, then does the host work for
+        retrieval (non-blocking) while that step runs on the GPU."""
         out = []
         while len(out) < n_done:
-            need = R - len(active)
-            if ramping:
-                need = min(need, ramp)
-            if need > 0:
-                for res in rag.submit([gen.question() for _ in range(need)], params):
-                    active[res.request.id] = res
             for req in llm.step():
                 res = active.pop(req.id, None)
                 if res is not None:
                     out.append(res)
-            ramping = ramping and len(active) < R
+                    clients[0] -= 1
+            for res in rag.poll(pending, block=not llm.has_work()):
+                active[res.request.id] = res
+            need = R - clients[0]
+            if ramping:
+                need = min(need, ramp)
+            if need > 0:
+                pending.append(rag.submit_async([gen.question() for _ in range(need)], params))
+                clients[0] += need
+            ramping = ramping and clients[0] < R
         return out
 
     if args.mode == "wave":

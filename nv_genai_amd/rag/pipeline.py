@@ -64,6 +64,17 @@ class RAGResult:
         return None if ft is None else ft - self.t_start
 
 
+@dataclass
+class PendingRetrieval:
+    questions: List[str]
+    params: SamplingParams
+    scores: torch.Tensor
+    ids: torch.Tensor
+    event: Optional["torch.cuda.Event"]
+    t0: float
+    keep: tuple = ()     # device tensors kept alive until the copies complete
+
+
 class RAGPipeline:
     def __init__(self, llm: LLMEngine, embedder: EmbeddingEngine, index, docstore: DocStore,
                  top_k: int = 4, max_context_tokens: int = DEFAULT_MAX_CONTEXT,
@@ -131,6 +142,48 @@ class RAGPipeline:
             req = self.llm.add_request(prompt, params)
             results.append(RAGResult(qtext, req, used, scores[i].tolist(), t0, t1, len(prompt)))
         return results
+
+    # ------------------------------------------------------------------ non-blocking path
+    def submit_async(self, questions: Sequence[str], params: SamplingParams) -> "PendingRetrieval":
+        """Launch query embedding + index search on the retrieval stream and return at once;
+        the top-k ids land in pinned host memory. ``poll`` turns finished retrievals into
+        LLM requests. A serving loop calls ``llm.step()`` (which launches the next GPU step)
+        and then ``poll()``/``submit_async()``, so neither the retrieval kernels nor the host
+        work of building prompts ever leaves the GPU idle."""
+        t0 = time.perf_counter()
+        if self.stream is None:
+            scores, ids = self.retrieve(questions)
+            return PendingRetrieval(list(questions), params, scores, ids, None, t0)
+        with torch.cuda.stream(self.stream):
+            q = self.embedder.embed(questions, input_type="query")
+            scores, ids = self.index.search(q, self.top_k)
+            hs = torch.empty(scores.shape, dtype=scores.dtype, pin_memory=True)
+            hi = torch.empty(ids.shape, dtype=ids.dtype, pin_memory=True)
+            hs.copy_(scores, non_blocking=True)
+            hi.copy_(ids, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        return PendingRetrieval(list(questions), params, hs, hi, ev, t0, keep=(scores, ids))
+
+    def poll(self, pending: List["PendingRetrieval"], block: bool = False) -> List[RAGResult]:
+        """Turn every finished retrieval of ``pending`` into LLM requests (removed from the
+        list); with ``block`` wait for all of them."""
+        out: List[RAGResult] = []
+        still = []
+        for pr in pending:
+            if pr.event is not None and not block and not pr.event.query():
+                still.append(pr)
+                continue
+            if pr.event is not None:
+                pr.event.synchronize()
+            t1 = time.perf_counter()
+            sc, ix = pr.scores.tolist(), pr.ids.tolist()
+            for i, qtext in enumerate(pr.questions):
+                prompt, used = self.build_prompt(qtext, ix[i], sc[i])
+                req = self.llm.add_request(prompt, pr.params)
+                out.append(RAGResult(qtext, req, used, sc[i], pr.t0, t1, len(prompt)))
+        pending[:] = still
+        return out
 
     def run(self, questions: Sequence[str], params: SamplingParams) -> List[RAGResult]:
         res = self.submit(questions, params)
