@@ -280,6 +280,57 @@ void row_sqnorm(Tensor X, Tensor out) {
   nga::launch_row_sqnorm(bfp(X), X.size(0), (int)X.size(1), out.data_ptr<float>(), cur_stream(X));
 }
 
+// ---- DSP (FM-ASR front end)
+void fir_c64(Tensor x, Tensor taps, c10::optional<Tensor> hist, Tensor y) {
+  CHECK_DEV(x); CHECK_DT(x, at::kComplexFloat); CHECK_CONTIG(x);
+  CHECK_DEV(taps); CHECK_DT(taps, at::kFloat); CHECK_CONTIG(taps);
+  CHECK_DEV(y); CHECK_DT(y, at::kComplexFloat); CHECK_CONTIG(y);
+  const int64_t n = x.numel(), nt = taps.numel();
+  TORCH_CHECK(nt >= 1 && nt <= nga::kFirMaxTaps, "fir_c64: 1..1024 taps");
+  TORCH_CHECK(y.numel() == n, "fir_c64: output size");
+  const float* hp = nullptr;
+  if (hist.has_value()) {
+    CHECK_DEV(*hist); CHECK_DT(*hist, at::kComplexFloat); CHECK_CONTIG(*hist);
+    TORCH_CHECK(hist->numel() == nt - 1, "fir_c64: history must hold ntaps-1 samples");
+    hp = reinterpret_cast<const float*>(hist->data_ptr());
+  }
+  nga::launch_fir_c64(reinterpret_cast<const float*>(x.data_ptr()), (int)n, taps.data_ptr<float>(), (int)nt, hp,
+                      reinterpret_cast<float*>(y.data_ptr()), cur_stream(x));
+}
+
+void fm_demod(Tensor x, double prev_re, double prev_im, bool has_prev, Tensor y) {
+  CHECK_DEV(x); CHECK_DT(x, at::kComplexFloat); CHECK_CONTIG(x);
+  CHECK_DEV(y); CHECK_DT(y, at::kFloat); CHECK_CONTIG(y);
+  const int64_t n = x.numel();
+  TORCH_CHECK(y.numel() == (has_prev ? n : std::max<int64_t>(0, n - 1)), "fm_demod: output size");
+  nga::launch_fm_demod(reinterpret_cast<const float*>(x.data_ptr()), (int)n, (float)prev_re, (float)prev_im,
+                       has_prev ? 1 : 0, y.data_ptr<float>(), cur_stream(x));
+}
+
+void resample_pcm(Tensor x, Tensor h, int64_t down, int64_t pre, double gain, c10::optional<Tensor> yf,
+                  c10::optional<Tensor> yi) {
+  CHECK_DEV(x); CHECK_DT(x, at::kFloat); CHECK_CONTIG(x);
+  CHECK_DEV(h); CHECK_DT(h, at::kFloat); CHECK_CONTIG(h);
+  TORCH_CHECK(down >= 1 && pre >= 0, "resample_pcm: bad down/pre");
+  int64_t nout = -1;
+  float* fp = nullptr;
+  int16_t* ip = nullptr;
+  if (yf.has_value()) {
+    CHECK_DEV(*yf); CHECK_DT(*yf, at::kFloat); CHECK_CONTIG(*yf);
+    nout = yf->numel();
+    fp = yf->data_ptr<float>();
+  }
+  if (yi.has_value()) {
+    CHECK_DEV(*yi); CHECK_DT(*yi, at::kShort); CHECK_CONTIG(*yi);
+    TORCH_CHECK(nout < 0 || yi->numel() == nout, "resample_pcm: outputs differ in size");
+    nout = yi->numel();
+    ip = yi->data_ptr<int16_t>();
+  }
+  TORCH_CHECK(nout >= 0, "resample_pcm: need an output");
+  nga::launch_resample_pcm(x.data_ptr<float>(), (int)x.numel(), h.data_ptr<float>(), (int)h.numel(), (int)down,
+                           (int)pre, (int)nout, (float)gain, fp, ip, cur_stream(x));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -298,4 +349,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("topk", &topk);
   m.def("pool_l2norm", &pool_l2norm);
   m.def("row_sqnorm", &row_sqnorm);
+  m.def("fir_c64", &fir_c64);
+  m.def("fm_demod", &fm_demod);
+  m.def("resample_pcm", &resample_pcm);
 }

@@ -70,4 +70,13 @@ void launch_pool_l2norm(const uint16_t* hidden, const int32_t* cu, int B, int H,
                         int normalize, float* out, hipStream_t stream);
 void launch_row_sqnorm(const uint16_t* X, int64_t N, int D, float* out, hipStream_t stream);
 
+// dsp.hip (complex64 passed as interleaved float pairs)
+constexpr int kFirMaxTaps = 1024;
+void launch_fir_c64(const float* x, int n, const float* taps, int ntaps, const float* hist, float* y,
+                    hipStream_t stream);
+void launch_fm_demod(const float* x, int n, float prev_re, float prev_im, int has_prev, float* y,
+                     hipStream_t stream);
+void launch_resample_pcm(const float* x, int n, const float* h, int nh, int down, int pre, int nout,
+                         float gain, float* yf, int16_t* yi, hipStream_t stream);
+
 }  // namespace nga

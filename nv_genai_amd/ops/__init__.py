@@ -232,3 +232,32 @@ def row_sqnorm(X, out=None):
 
 
 rope_cos_sin = ref.rope_cos_sin
+
+
+# ---------------------------------------------------------------- DSP (FM-ASR front end)
+def fir_c64(x: torch.Tensor, taps: torch.Tensor, hist: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _gpu(x):
+        return ref.fir_c64(x, taps, hist)
+    y = torch.empty_like(x)
+    kernels().fir_c64(x, taps, hist, y)
+    return y
+
+
+def fm_demod(x: torch.Tensor, prev: Optional[complex] = None) -> torch.Tensor:
+    if not _gpu(x):
+        return ref.fm_demod(x, prev)
+    n = x.numel() if prev is not None else max(0, x.numel() - 1)
+    y = torch.empty(n, dtype=torch.float32, device=x.device)
+    p = prev if prev is not None else 0j
+    kernels().fm_demod(x, float(p.real), float(p.imag), prev is not None, y)
+    return y
+
+
+def resample_pcm(x: torch.Tensor, h: torch.Tensor, down: int, pre: int, nout: int, gain: float = 1.0):
+    """-> (float32 samples, int16 PCM)."""
+    if not _gpu(x):
+        return ref.resample_pcm(x, h, down, pre, nout, gain)
+    yf = torch.empty(nout, dtype=torch.float32, device=x.device)
+    yi = torch.empty(nout, dtype=torch.int16, device=x.device)
+    kernels().resample_pcm(x, h, int(down), int(pre), float(gain), yf, yi)
+    return yf, yi

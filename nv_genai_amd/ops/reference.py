@@ -256,3 +256,36 @@ def pool_l2norm(hidden, cu, mode: int, normalize: bool):
 
 def row_sqnorm(X):
     return X.float().pow(2).sum(-1)
+
+
+# ---------------------------------------------------------------- DSP (FM-ASR front end)
+def fir_c64(x, taps, hist=None):
+    """y[i] = sum_k taps[k] x[i-k] (complex x, real taps); x[<0] from ``hist`` or zeros."""
+    nt = taps.numel()
+    pre = hist if hist is not None else torch.zeros(nt - 1, dtype=x.dtype, device=x.device)
+    xx = torch.cat([pre.to(x.dtype), x])
+    w = taps.flip(0).to(torch.float64)
+    re = torch.nn.functional.conv1d(xx.real.double().view(1, 1, -1), w.view(1, 1, -1)).view(-1)
+    im = torch.nn.functional.conv1d(xx.imag.double().view(1, 1, -1), w.view(1, 1, -1)).view(-1)
+    return torch.complex(re.float(), im.float())
+
+
+def fm_demod(x, prev=None):
+    if prev is not None:
+        x = torch.cat([torch.tensor([prev], dtype=x.dtype, device=x.device), x])
+    d = x[1:] * x[:-1].conj()
+    return torch.atan2(d.imag, d.real).float()
+
+
+def resample_pcm(x, h, down, pre, nout, gain):
+    """Decimating FIR y[m] = gain * sum_k h[k] x[(m + pre) * down - k]; returns (float, int16)."""
+    full = torch.nn.functional.conv1d(
+        torch.nn.functional.pad(x.double().view(1, 1, -1), (h.numel() - 1, h.numel() - 1)),
+        h.double().flip(0).view(1, 1, -1)).view(-1)
+    idx = (torch.arange(nout, dtype=torch.int64) + pre) * down
+    y = torch.zeros(nout, dtype=torch.float64)
+    ok = idx < full.numel()
+    y[ok] = full[idx[ok]]
+    y = (gain * y).float()
+    pcm = (y * 32768.0).clamp(-32768.0, 32767.0).to(torch.int16)
+    return y, pcm
