@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--mode", choices=("closed", "wave"), default="closed")
     ap.add_argument("--mixed-prefill-tokens", type=int, default=2048)
+    ap.add_argument("--retrieval-batch", type=int, default=8,
+                    help="queries per embedding+search launch (dynamic batching, like the reference's Triton embedder)")
+    ap.add_argument("--retrieval-delay-ms", type=float, default=50.0,
+                    help="max time a query waits for its retrieval batch to fill (Triton max_queue_delay)")
     return ap.parse_args()
 
 
@@ -108,6 +112,7 @@ def main():
     ramp = max(1, -(-R // max(1, args.max_tokens)))  # new clients per engine step while ramping
 
     pending = []                    # retrievals in flight on the retrieval stream
+    queued = []                     # (question, arrival time) waiting for a retrieval batch
     clients = [0]                   # clients with a question in the system (retrieving or generating)
 
     def closed_loop(n_done: int, ramping: bool):
@@ -127,8 +132,15 @@ def main():
             if ramping:
                 need = min(need, ramp)
             if need > 0:
-                pending.append(rag.submit_async([gen.question() for _ in range(need)], params))
+                now = time.perf_counter()
+                queued.extend((gen.question(), now) for _ in range(need))
                 clients[0] += need
+            if queued and (len(queued) >= args.retrieval_batch or not llm.has_work()
+                           or time.perf_counter() - queued[0][1] >= args.retrieval_delay_ms / 1e3):
+                pr = rag.submit_async([q for q, _ in queued], params)
+                pr.t0 = [t for _, t in queued]        # latency counts the batching wait
+                pending.append(pr)
+                queued.clear()
             ramping = ramping and clients[0] < R
         return out
 

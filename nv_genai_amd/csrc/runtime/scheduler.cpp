@@ -156,6 +156,10 @@ class Scheduler {
   // sequences also carries up to this many prefill tokens, so the decode rows ride along the
   // prefill GEMMs instead of re-reading every weight in a separate skinny decode step.
   void set_mixed_prefill_tokens(int n) { mixed_tokens_ = std::max(0, n); }
+  // Round the token count of prefill/mixed steps down to a multiple of `a` by shortening the
+  // last prefill chunks (the remainder runs next step): the projection GEMMs then always see
+  // M in a small set of tile-aligned sizes, which the per-shape GEMM table covers.
+  void set_token_alignment(int a) { align_ = std::max(1, a); }
   int last_num_decode() const { return last_nd_; }
 
   // Fill the step buffers. Returns (kind, num_seqs, num_tokens); kind 0 idle, 1 prefill,
@@ -181,6 +185,7 @@ class Scheduler {
         std::vector<int> qlen;
         pick_prefill(std::min(cap_tokens - (int)ok.size(), mixed_tokens_), cap_seqs - (int)ok.size(),
                      chosen, qlen);
+        align_tokens((int)ok.size(), chosen, qlen);
         const std::vector<int> ones(ok.size(), 1);
         B.cq(0) = 0;
         int t = fill_rows(B, ok, ones, 0, 0);
@@ -195,6 +200,7 @@ class Scheduler {
     std::vector<int64_t> chosen;
     std::vector<int> qlen;
     pick_prefill(cap_tokens, cap_seqs, chosen, qlen);
+    align_tokens(0, chosen, qlen);
     if (!chosen.empty()) {
       B.cq(0) = 0;
       const int t = fill_rows(B, chosen, qlen, 0, 0);
@@ -318,6 +324,24 @@ class Scheduler {
       chosen.push_back(id);
       qlen.push_back(n);
       budget -= n;
+    }
+  }
+
+  void align_tokens(int nd, std::vector<int64_t>& chosen, std::vector<int>& qlen) {
+    if (align_ <= 1 || chosen.empty()) return;
+    int total = nd;
+    for (int q : qlen) total += q;
+    const int target = total - total % align_;
+    if (target <= nd || target == total) return;  // too small to align without starving prefill
+    int cut = total - target;
+    while (cut > 0 && !chosen.empty()) {
+      const int take = std::min(cut, qlen.back());
+      qlen.back() -= take;
+      cut -= take;
+      if (qlen.back() == 0) {
+        chosen.pop_back();
+        qlen.pop_back();
+      }
     }
   }
 
@@ -461,6 +485,7 @@ class Scheduler {
   int64_t clock_ = 0;
   int64_t preempt_count_ = 0;
   int mixed_tokens_ = 0;
+  int align_ = 1;
   int last_nd_ = 0;
 };
 
@@ -510,6 +535,7 @@ PYBIND11_MODULE(_rt, m) {
       .def("preemptions", &Scheduler::preemptions)
       .def("reset_prefix_cache", &Scheduler::reset_prefix_cache)
       .def("set_mixed_prefill_tokens", &Scheduler::set_mixed_prefill_tokens)
+      .def("set_token_alignment", &Scheduler::set_token_alignment)
       .def("last_num_decode", &Scheduler::last_num_decode);
   register_bm25(m);
   register_text(m);

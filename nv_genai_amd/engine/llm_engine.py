@@ -97,6 +97,7 @@ class EngineConfig:
     detokenize: bool = True
     async_decode: bool = True  # pipeline steps (host work overlaps the GPU)
     mixed_prefill_tokens: int = 2048  # prefill tokens that ride along a decode step (0 = off)
+    token_alignment: int = 256   # prefill/mixed steps carry a multiple of this many tokens
     tuned_gemms: bool = True   # load the per-shape hipBLASLt/rocBLAS table (ops/gemm_tuning.py)
 
 
@@ -139,6 +140,7 @@ class LLMEngine:
                                   cfg.max_batched_tokens, cfg.max_model_len,
                                   cfg.enable_prefix_caching)
         self.sched.set_mixed_prefill_tokens(cfg.mixed_prefill_tokens)
+        self.sched.set_token_alignment(cfg.token_alignment)
         # ---- host step buffers (pinned) filled by the native scheduler
         pin = self.gpu
         T, S = max(cfg.max_batched_tokens, cfg.max_num_seqs), cfg.max_num_seqs

@@ -181,7 +181,8 @@ class RAGPipeline:
             for i, qtext in enumerate(pr.questions):
                 prompt, used = self.build_prompt(qtext, ix[i], sc[i])
                 req = self.llm.add_request(prompt, pr.params)
-                out.append(RAGResult(qtext, req, used, sc[i], pr.t0, t1, len(prompt)))
+                t0 = pr.t0[i] if isinstance(pr.t0, list) else pr.t0
+                out.append(RAGResult(qtext, req, used, sc[i], t0, t1, len(prompt)))
         pending[:] = still
         return out
 
