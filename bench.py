@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--mode", choices=("closed", "wave"), default="closed")
     ap.add_argument("--mixed-prefill-tokens", type=int, default=2048)
+    ap.add_argument("--mixed-min-tokens", type=int, default=0,
+                    help="accumulate this many prompt tokens before forming a mixed step")
+    ap.add_argument("--mixed-max-wait", type=int, default=4)
     ap.add_argument("--retrieval-batch", type=int, default=8,
                     help="queries per embedding+search launch (dynamic batching, like the reference's Triton embedder)")
     ap.add_argument("--retrieval-delay-ms", type=float, default=50.0,
@@ -86,7 +89,8 @@ def main():
     ecfg = EngineConfig(model=args.model, max_num_seqs=max(R, 1), max_batched_tokens=args.max_batched_tokens,
                         max_model_len=8192, use_graphs=gpu and not args.no_graphs,
                         graph_batch_sizes=sizes, seed=rank, kv_cache_fraction=0.3,
-                        mixed_prefill_tokens=args.mixed_prefill_tokens)
+                        mixed_prefill_tokens=args.mixed_prefill_tokens,
+                        mixed_min_tokens=args.mixed_min_tokens, mixed_max_wait=args.mixed_max_wait)
     llm = LLMEngine(ecfg, device=dev, pctx=pctx)
     emb = EmbeddingEngine(args.embed_model, device=dev, seed=rank)
     index = FlatIndex(emb.dim, "cosine", dev, capacity=args.index_size)

@@ -128,6 +128,7 @@ struct Seq {
   int status = WAITING;
   int64_t arrival;
   int preemptions = 0;
+  int64_t enq_step = 0;  // scheduler step at which it (re)entered the waiting queue
 };
 
 class Scheduler {
@@ -148,6 +149,7 @@ class Scheduler {
     s.prompt_len = (int)prompt.size();
     s.max_new = max_new;
     s.arrival = clock_++;
+    s.enq_step = step_;
     seqs_.emplace(id, std::move(s));
     waiting_.push_back(id);
   }
@@ -160,6 +162,14 @@ class Scheduler {
   // last prefill chunks (the remainder runs next step): the projection GEMMs then always see
   // M in a small set of tile-aligned sizes, which the per-shape GEMM table covers.
   void set_token_alignment(int a) { align_ = std::max(1, a); }
+  // Accumulate prefill work for mixed steps: while decodes are running, a mixed step is only
+  // formed once at least `min_tokens` prompt tokens are pending or the oldest waiting request
+  // has waited `max_wait_steps` scheduler steps — larger mixed GEMMs run closer to the MFMA
+  // roofline than one small prefill per step, at a bounded cost in time-to-first-token.
+  void set_mixed_min_tokens(int min_tokens, int max_wait_steps) {
+    mixed_min_ = std::max(0, min_tokens);
+    mixed_wait_ = std::max(0, max_wait_steps);
+  }
   int last_num_decode() const { return last_nd_; }
 
   // Fill the step buffers. Returns (kind, num_seqs, num_tokens); kind 0 idle, 1 prefill,
@@ -177,8 +187,16 @@ class Scheduler {
     const int cap_seqs = std::min<int>((int)B.sid.shape(0), max_seqs_);
     last_nd_ = 0;
 
+    ++step_;
     if (mixed_tokens_ > 0) {
       std::vector<int64_t> dec = decode_ready();
+      if (!dec.empty() && !prefill_ready()) {
+        std::vector<int64_t> ok = prepare_decode(dec, cap_seqs);
+        const std::vector<int> ones(ok.size(), 1);
+        B.cq(0) = 0;
+        const int t = fill_rows(B, ok, ones, 0, 0);
+        return py::make_tuple(ok.empty() ? 0 : 2, (int)ok.size(), t);
+      }
       if (!dec.empty()) {
         std::vector<int64_t> ok = prepare_decode(dec, cap_seqs);
         std::vector<int64_t> chosen;
@@ -345,6 +363,28 @@ class Scheduler {
     }
   }
 
+  // Enough prefill work pending (or waited long enough) to form a mixed step.
+  bool prefill_ready() const {
+    if (mixed_min_ <= 0) return true;
+    int64_t pending = 0;
+    int64_t oldest = -1;
+    for (int64_t id : running_) {  // admitted, partially prefilled (chunk cut by the budget)
+      const Seq& s = seqs_.at(id);
+      if (s.computed < s.prompt_len) {
+        pending += (int)s.toks.size() - s.computed;
+        if (oldest < 0 || s.enq_step < oldest) oldest = s.enq_step;
+      }
+    }
+    for (int64_t id : waiting_) {
+      const Seq& s = seqs_.at(id);
+      pending += (int)s.toks.size() - s.computed;
+      if (oldest < 0 || s.enq_step < oldest) oldest = s.enq_step;
+    }
+    if (pending == 0) return false;
+    if (pending >= mixed_min_) return true;
+    return oldest >= 0 && step_ - oldest >= mixed_wait_;
+  }
+
   std::vector<int64_t> decode_ready() {
     std::vector<int64_t> dec;
     for (int64_t id : running_) {
@@ -467,6 +507,7 @@ class Scheduler {
     s.preemptions += 1;
     ++preempt_count_;
     running_.erase(std::find(running_.begin(), running_.end(), id));
+    s.enq_step = step_ - mixed_wait_;  // a preempted sequence is due at once
     waiting_.push_front(id);
   }
 
@@ -485,6 +526,9 @@ class Scheduler {
   int64_t clock_ = 0;
   int64_t preempt_count_ = 0;
   int mixed_tokens_ = 0;
+  int mixed_min_ = 0;
+  int mixed_wait_ = 0;
+  int64_t step_ = 0;
   int align_ = 1;
   int last_nd_ = 0;
 };
@@ -536,6 +580,7 @@ PYBIND11_MODULE(_rt, m) {
       .def("reset_prefix_cache", &Scheduler::reset_prefix_cache)
       .def("set_mixed_prefill_tokens", &Scheduler::set_mixed_prefill_tokens)
       .def("set_token_alignment", &Scheduler::set_token_alignment)
+      .def("set_mixed_min_tokens", &Scheduler::set_mixed_min_tokens)
       .def("last_num_decode", &Scheduler::last_num_decode);
   register_bm25(m);
   register_text(m);

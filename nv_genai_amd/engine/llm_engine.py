@@ -98,6 +98,8 @@ class EngineConfig:
     async_decode: bool = True  # pipeline steps (host work overlaps the GPU)
     mixed_prefill_tokens: int = 2048  # prefill tokens that ride along a decode step (0 = off)
     token_alignment: int = 256   # prefill/mixed steps carry a multiple of this many tokens
+    mixed_min_tokens: int = 0     # accumulate this many prompt tokens before a mixed step ...
+    mixed_max_wait: int = 4       # ... unless the oldest waiting request waited this many steps
     tuned_gemms: bool = True   # load the per-shape hipBLASLt/rocBLAS table (ops/gemm_tuning.py)
 
 
@@ -141,6 +143,7 @@ class LLMEngine:
                                   cfg.enable_prefix_caching)
         self.sched.set_mixed_prefill_tokens(cfg.mixed_prefill_tokens)
         self.sched.set_token_alignment(cfg.token_alignment)
+        self.sched.set_mixed_min_tokens(cfg.mixed_min_tokens, cfg.mixed_max_wait)
         # ---- host step buffers (pinned) filled by the native scheduler
         pin = self.gpu
         T, S = max(cfg.max_batched_tokens, cfg.max_num_seqs), cfg.max_num_seqs

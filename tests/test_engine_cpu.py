@@ -125,8 +125,9 @@ def test_mixed_prefill_decode_steps_exact(model, async_):
     running ones (mixed steps); greedy outputs equal the unmixed engine's."""
     p = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
     outs = []
-    for mixed, align in ((0, 1), (40, 1), (40, 16)):
-        e = _engine(model, mixed_prefill_tokens=mixed, async_decode=async_, token_alignment=align)
+    for mixed, align, mn in ((0, 1, 0), (40, 1, 0), (40, 16, 0), (64, 16, 100)):
+        e = _engine(model, mixed_prefill_tokens=mixed, async_decode=async_, token_alignment=align,
+                    mixed_min_tokens=mn, mixed_max_wait=3)
         reqs = [e.add_request(PROMPTS[0], p)]
         for i, pr in enumerate(PROMPTS[1:] + [[5, 6, 7] * 30]):
             for _ in range(3):
@@ -138,4 +139,4 @@ def test_mixed_prefill_decode_steps_exact(model, async_):
             assert e.stats["mixed_steps"] > 0
         else:
             assert e.stats["mixed_steps"] == 0
-    assert outs[0] == outs[1] == outs[2]
+    assert outs[0] == outs[1] == outs[2] == outs[3]
