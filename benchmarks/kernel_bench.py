@@ -1,0 +1,85 @@
+"""Micro-benchmarks of the hand-written hot kernels at serving shapes (Llama-3-8B):
+prefill attention (paged, causal, GQA 32/8, D=128), decode attention, sampling."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from nv_genai_amd import ops  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters * 1e3  # us
+
+
+def paged_setup(lens, Hkv=8, D=128, dev="cuda", width=None):
+    nb = sum((l + 63) // 64 for l in lens)
+    kc = torch.randn(nb, Hkv, 64, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.randn(nb, Hkv, D, 64, device=dev, dtype=torch.bfloat16)
+    mb = width or max((l + 63) // 64 for l in lens)
+    bt = torch.zeros(len(lens), mb, dtype=torch.int32, device=dev)
+    o = 0
+    for i, l in enumerate(lens):
+        n = (l + 63) // 64
+        bt[i, :n] = torch.arange(o, o + n, dtype=torch.int32)
+        o += n
+    return kc, vc, bt
+
+
+def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="", help="prefill | decode | sample (default: all)")
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    global timeit
+    _t = timeit
+    timeit = lambda fn: _t(fn, args.iters)  # noqa: E731
+    dev = "cuda"
+    Hq, Hkv, D = 32, 8, 128
+    out = {}
+    for name, lens in (("prefill_1x1196", [1196]), ("prefill_27x1200", [1200] * 27)):
+        if args.only and args.only != "prefill":
+            break
+        kc, vc, bt = paged_setup(lens)
+        T = sum(lens)
+        q = torch.randn(T, Hq * D, device=dev, dtype=torch.bfloat16)
+        cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0).tolist()), dtype=torch.int32, device=dev)
+        ctx = torch.tensor(lens, dtype=torch.int32, device=dev)
+        us = timeit(lambda: ops.prefill_attention_paged(q, kc, vc, bt, cu, ctx, Hq, Hkv, D, max(lens), D ** -0.5))
+        flops = sum(2 * 2 * l * (l + 1) / 2 * D * Hq for l in lens)
+        out[name] = {"us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1)}
+    B, L = 256, 1400
+    if args.only == "prefill":
+        print(json.dumps(out))
+        return
+    kc, vc, bt = paged_setup([L] * B, width=8192 // 64)
+    q = torch.randn(B, Hq * D, device=dev, dtype=torch.bfloat16)
+    ctx = torch.full((B,), L, dtype=torch.int32, device=dev)
+    ws = ops.DecodeWorkspace(B, Hq, Hkv, 8192, torch.device(dev))
+    us = timeit(lambda: ops.decode_attention(q, kc, vc, bt, ctx, Hq, Hkv, 8192, D ** -0.5, ws=ws))
+    out["decode_256x1400"] = {"us": round(us, 1), "TBps": round(B * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
+    V = 128256
+    logits = torch.randn(B, V, device=dev) * 3
+    z = lambda v, dt=torch.float32: torch.full((B,), v, dtype=dt, device=dev)  # noqa: E731
+    for nm, (t, k, p) in {"sample_greedy": (0.0, 0, 1.0), "sample_t0.2_p0.7": (0.2, 0, 0.7),
+                          "sample_t1_k50": (1.0, 50, 1.0)}.items():
+        us = timeit(lambda: ops.sample(logits, z(t), z(k, torch.int32), z(p), z(1, torch.int64), z(0, torch.int64)))
+        out[nm] = {"us": round(us, 1)}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

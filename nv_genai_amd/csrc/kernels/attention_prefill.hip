@@ -16,6 +16,8 @@
 //        queries are the last q_len positions of a ctx_len context (chunked prefill and
 //        prefix-cache hits work unchanged).  Otherwise: K and V rows come from packed
 //        [T, H, D] tensors with per-sequence offsets (cu_q), V is transposed while staging.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -23,57 +25,68 @@ namespace nga {
 
 namespace {
 constexpr float LOG2E_P = 1.4426950408889634f;
+constexpr float RESCALE_LOG2 = 8.f;
 
 __device__ __forceinline__ int row_swz(int row) {  // 4-bit key: distinct over a tile's 16 rows
   return (row & 3) | (((row >> 3) & 3) << 2);
 }
 }  // namespace
 
-template <int D, bool PAGED, bool CAUSAL>
+template <int D, bool PAGED, bool CAUSAL, int NCG>
 __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
+  // NCG query column-groups (16 rows each) per wave: the K and V^T fragments read from LDS
+  // for one key tile feed NCG MFMAs each, and the tile's staging + barriers are amortised
+  // over a 64*NCG-row query tile.
   constexpr int KT = 64;          // keys per tile (= KV page size when PAGED)
   constexpr int NCH_K = D / 8;    // 16-B chunks per K row
   constexpr int DS = D / 32;      // d-steps of the QK^T MFMA
   constexpr int DT = D / 16;      // d-tiles of the PV MFMA
   constexpr int K_CHUNKS = KT * NCH_K;   // = V chunks too
   constexpr int PER_T = K_CHUNKS / 256;  // chunks per thread per operand
+  constexpr int QT = 64 * NCG;           // query rows per workgroup
 
   __shared__ __attribute__((aligned(16))) uint16_t k_s[KT * D];
   __shared__ __attribute__((aligned(16))) uint16_t v_s[D * KT];
 
   const int b = blockIdx.z, hq = blockIdx.y, tile = blockIdx.x;
   const int q0 = P.cu_q[b], qlen = P.cu_q[b + 1] - q0;
-  if (tile * 64 >= qlen) return;
+  if (tile * QT >= qlen) return;
   const int ctx = PAGED ? P.ctx_lens[b] : qlen;
   const int G = P.Hq / P.Hkv;
   const int kvh = hq / G;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int col = lane & 15, h = lane >> 4;
   const int tid = threadIdx.x;
 
-  // this lane's query row (column of the MFMA tile)
-  int qr = tile * 64 + w * 16 + col;
-  const bool row_ok = qr < qlen;
-  if (!row_ok) qr = qlen - 1;
-  const int qpos = ctx - qlen + qr;  // absolute key index of this query
-
-  bf16x8 qf[DS];
-  {
-    const uint16_t* qp = P.q + (int64_t)(q0 + qr) * P.q_stride + (int64_t)hq * D;
+  // this lane's query rows (one per column group)
+  int qr[NCG], qpos[NCG];
+  bool row_ok[NCG];
+  bf16x8 qf[NCG][DS];
 #pragma unroll
-    for (int s = 0; s < DS; ++s) qf[s] = as_bf16x8(load8(qp + 32 * s + 8 * h));
+  for (int cg = 0; cg < NCG; ++cg) {
+    int r = tile * QT + w * 16 * NCG + cg * 16 + col;
+    row_ok[cg] = r < qlen;
+    if (!row_ok[cg]) r = qlen - 1;
+    qr[cg] = r;
+    qpos[cg] = ctx - qlen + r;  // absolute key index of this query
+    const uint16_t* qp = P.q + (int64_t)(q0 + r) * P.q_stride + (int64_t)hq * D;
+#pragma unroll
+    for (int s2 = 0; s2 < DS; ++s2) qf[cg][s2] = as_bf16x8(load8(qp + 32 * s2 + 8 * h));
   }
 
+  const int qpos_w0 = ctx - qlen + tile * QT + w * 16 * NCG;  // smallest query position of this wave
   int last_key = ctx - 1;
   if (CAUSAL) {
-    const int qmax = min(qlen - 1, tile * 64 + 63);
+    const int qmax = min(qlen - 1, tile * QT + QT - 1);
     last_key = min(last_key, ctx - qlen + qmax);
   }
   const int n_tiles = last_key / KT + 1;
 
-  // staging registers (one tile ahead)
-  u16x8 kreg[PER_T], vreg[PER_T];
-  auto load_tile = [&](int t) {
+  // staging registers, one tile ahead (a second set, two tiles ahead, measured no faster
+  // and costs 32 VGPRs that the accumulators need)
+  u16x8 kA[PER_T], vA[PER_T];
+  auto load_tile = [&](int t, u16x8 (&kreg)[PER_T], u16x8 (&vreg)[PER_T]) {
     if (PAGED) {
       const int64_t blk = P.block_tables[(int64_t)b * P.max_blocks + t];
       const uint16_t* kp = P.kc + (blk * P.Hkv + kvh) * (int64_t)(KT * D);
@@ -100,7 +113,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
       }
     }
   };
-  auto store_tile = [&]() {
+  auto store_tile = [&](const u16x8 (&kreg)[PER_T], const u16x8 (&vreg)[PER_T]) {
 #pragma unroll
     for (int i = 0; i < PER_T; ++i) {
       const int c = tid + 256 * i;
@@ -125,84 +138,117 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
   };
 
   const float sl2 = P.scale * LOG2E_P;
-  float m = -INFINITY, l = 0.f;
-  f32x4 o[DT];
+  float m[NCG], l[NCG];
+  f32x4 o[NCG][DT];
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x4)(0.f);
+  for (int cg = 0; cg < NCG; ++cg) {
+    m[cg] = -INFINITY;
+    l[cg] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[cg][dt] = (f32x4)(0.f);
+  }
 
-  load_tile(0);
+  auto compute_tile = [&](int t) {
+      f32x4 sacc[NCG][4];
+#pragma unroll
+      for (int tau = 0; tau < 4; ++tau) {
+        const int row = 32 * (tau >> 1) + 8 * (col >> 2) + 4 * (tau & 1) + (col & 3);
+        const int sw = (NCH_K == 16) ? row_swz(row) : (row_swz(row) >> 1);
+#pragma unroll
+        for (int cg = 0; cg < NCG; ++cg) sacc[cg][tau] = (f32x4)(0.f);
+#pragma unroll
+        for (int s2 = 0; s2 < DS; ++s2) {
+          const int ch = 4 * s2 + h;
+          bf16x8 a = as_bf16x8(*reinterpret_cast<const u16x8*>(&k_s[row * D + ((ch ^ sw) * 8)]));
+#pragma unroll
+          for (int cg = 0; cg < NCG; ++cg) sacc[cg][tau] = mfma16(a, qf[cg][s2], sacc[cg][tau]);
+        }
+      }
+      const int kbase = t * KT;
+      // masking is only needed on tiles that cross this wave's causal diagonal (or the end
+      // of the context); the test is wave-uniform
+      const bool need_mask = CAUSAL ? (kbase + KT - 1 > qpos_w0) : (kbase + KT > ctx);
+      bf16x8 pf[NCG][2];
+#pragma unroll
+      for (int cg = 0; cg < NCG; ++cg) {
+        float mloc = -INFINITY;
+#pragma unroll
+        for (int tau = 0; tau < 4; ++tau)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float sv = sacc[cg][tau][r];  // raw score; the scale is folded into the exp
+            if (need_mask) {
+              const int key = kbase + 32 * (tau >> 1) + 8 * h + 4 * (tau & 1) + r;
+              const bool ok = CAUSAL ? (key <= qpos[cg]) : (key < ctx);
+              sv = ok ? sv : -INFINITY;
+            }
+            sacc[cg][tau][r] = sv;
+            mloc = fmaxf(mloc, sv);
+          }
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+        mloc *= sl2;  // scale > 0: max commutes with it
+        // Lazy rescaling: the running max only moves (and O / l are only rescaled) when a
+        // row's tile max exceeds it by more than 2^RESCALE_LOG2; until then P = 2^(s - m)
+        // stays <= 2^8, harmless in fp32 accumulators and bf16 P. Keeps O in the MFMA
+        // accumulators instead of a VALU round trip every tile. m starts at -inf, so the
+        // first tile always rescales (alpha = 2^-inf = 0 on an all-zero O).
+        const bool grow = mloc > m[cg] + RESCALE_LOG2;
+        if (__ballot(grow)) {
+          const float m_new = grow ? mloc : m[cg];
+          const float alpha = __builtin_amdgcn_exp2f(m[cg] - m_new);
+          m[cg] = m_new;
+          l[cg] *= alpha;
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) o[cg][dt] *= alpha;
+        }
+        const float mc = m[cg];
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[cg][2 * g + (j >> 2)][j & 3], sl2, -mc));  // 2^-inf = 0
+            l[cg] += pv;
+            pf[cg][g][j] = (__bf16)pv;
+          }
+      }
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const int ch = 4 * g + h;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int row = 16 * dt + col;
+          bf16x8 a = as_bf16x8(
+              *reinterpret_cast<const u16x8*>(&v_s[row * KT + ((ch ^ ((row >> 1) & 7)) * 8)]));
+#pragma unroll
+          for (int cg = 0; cg < NCG; ++cg) o[cg][dt] = mfma16(a, pf[cg][g], o[cg][dt]);
+        }
+      }
+  };
+
+  load_tile(0, kA, vA);
   for (int t = 0; t < n_tiles; ++t) {
     __syncthreads();  // previous tile's LDS reads are done
-    store_tile();
+    store_tile(kA, vA);
     __syncthreads();
-    if (t + 1 < n_tiles) load_tile(t + 1);
-
-    f32x4 sacc[4];
+    if (t + 1 < n_tiles) load_tile(t + 1, kA, vA);
+    compute_tile(t);
+  }
 #pragma unroll
-    for (int tau = 0; tau < 4; ++tau) {
-      const int row = 32 * (tau >> 1) + 8 * (col >> 2) + 4 * (tau & 1) + (col & 3);
-      const int sw = (NCH_K == 16) ? row_swz(row) : (row_swz(row) >> 1);
-      sacc[tau] = (f32x4)(0.f);
-#pragma unroll
-      for (int s = 0; s < DS; ++s) {
-        const int ch = 4 * s + h;
-        bf16x8 a = as_bf16x8(*reinterpret_cast<const u16x8*>(&k_s[row * D + ((ch ^ sw) * 8)]));
-        sacc[tau] = mfma16(a, qf[s], sacc[tau]);
-      }
-    }
-    const int kbase = t * KT;
-    float mloc = -INFINITY;
-#pragma unroll
-    for (int tau = 0; tau < 4; ++tau)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kbase + 32 * (tau >> 1) + 8 * h + 4 * (tau & 1) + r;
-        float s = sacc[tau][r] * sl2;
-        const bool ok = CAUSAL ? (key <= qpos) : (key < ctx);
-        s = ok ? s : -INFINITY;
-        sacc[tau][r] = s;
-        mloc = fmaxf(mloc, s);
-      }
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    const float m_new = fmaxf(m, mloc);  // finite: tile 0 always holds key 0 <= qpos
-    const float alpha = exp2f(m - m_new);
-    m = m_new;
-    l *= alpha;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
-    bf16x8 pf[2];
-#pragma unroll
-    for (int g = 0; g < 2; ++g)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float pv = exp2f(sacc[2 * g + (j >> 2)][j & 3] - m_new);
-        l += pv;
-        pf[g][j] = (__bf16)pv;
-      }
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      const int ch = 4 * g + h;
+  for (int cg = 0; cg < NCG; ++cg) {
+    float ll = l[cg];
+    ll += __shfl_xor(ll, 16, 64);
+    ll += __shfl_xor(ll, 32, 64);
+    if (row_ok[cg]) {
+      const float inv = 1.f / ll;
+      uint16_t* op = P.out + (int64_t)(q0 + qr[cg]) * P.out_stride + (int64_t)hq * D;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        const int row = 16 * dt + col;
-        bf16x8 a = as_bf16x8(
-            *reinterpret_cast<const u16x8*>(&v_s[row * KT + ((ch ^ ((row >> 1) & 7)) * 8)]));
-        o[dt] = mfma16(a, pf[g], o[dt]);
+        u16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = f2bf(o[cg][dt][r] * inv);
+        *reinterpret_cast<u16x4*>(op + 16 * dt + 4 * h) = v;
       }
-    }
-  }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  if (row_ok) {
-    const float inv = 1.f / l;
-    uint16_t* op = P.out + (int64_t)(q0 + qr) * P.out_stride + (int64_t)hq * D;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      u16x4 v;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[dt][r] * inv);
-      *reinterpret_cast<u16x4*>(op + 16 * dt + 4 * h) = v;
     }
   }
 }
@@ -210,8 +256,20 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
 void launch_prefill_attention(const PrefillParams& p, int num_seqs, int max_q_len, int D,
                               bool paged, bool causal, hipStream_t stream) {
   if (num_seqs == 0 || max_q_len == 0) return;
-  dim3 grid((max_q_len + 63) / 64, p.Hq, num_seqs);
-#define NGA_PF(DD, PG, CS) prefill_attn_kernel<DD, PG, CS><<<grid, 256, 0, stream>>>(p)
+  // 64-row query tiles. The 128-row variant (two column groups per wave) halves the LDS
+  // fragment traffic per MFMA but needs ~300 VGPR+AGPR, i.e. one wave per SIMD, and measured
+  // 1.4-1.5x slower on MI355X (benchmarks/kernel_bench.py); NGA_PREFILL_NCG=2 selects it.
+  static const int forced = [] {
+    const char* e = getenv("NGA_PREFILL_NCG");
+    return e ? atoi(e) : 0;
+  }();
+  const int ncg = forced == 2 ? 2 : 1;
+  dim3 grid((max_q_len + 64 * ncg - 1) / (64 * ncg), p.Hq, num_seqs);
+#define NGA_PF(DD, PG, CS)                                                    \
+  do {                                                                        \
+    if (ncg == 2) prefill_attn_kernel<DD, PG, CS, 2><<<grid, 256, 0, stream>>>(p); \
+    else prefill_attn_kernel<DD, PG, CS, 1><<<grid, 256, 0, stream>>>(p);          \
+  } while (0)
   if (D == 128) {
     if (paged) {
       if (causal) NGA_PF(128, true, true); else NGA_PF(128, true, false);

@@ -70,6 +70,26 @@ __device__ int find_crossing(T* bins, T target, T* above_out, T* scan) {
   return s;
 }
 
+// Visit every element of a row: float4 loads for the body (rows of the [B, V] fp32 logits
+// are 16-B aligned when V % 4 == 0), scalar loads for any tail. f(index, value).
+template <typename F>
+__device__ __forceinline__ void for_row(const float* __restrict__ x, int V, F f) {
+  const int t = threadIdx.x;
+  if ((V & 3) == 0) {
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    const int n4 = V >> 2;
+    for (int j = t; j < n4; j += NT) {
+      const float4 v = x4[j];
+      f(4 * j, v.x);
+      f(4 * j + 1, v.y);
+      f(4 * j + 2, v.z);
+      f(4 * j + 3, v.w);
+    }
+  } else {
+    for (int i = t; i < V; i += NT) f(i, x[i]);
+  }
+}
+
 struct ArgMax {
   float v;
   int i;
@@ -137,15 +157,23 @@ __global__ void __launch_bounds__(NT) sample_kernel(
   const bool greedy = !(temp > 0.f) || k == 1;
   const float inv_t = greedy ? 1.f : 1.f / temp;
 
-  // pass: max (+ argmax for greedy)
+  // one pass: argmax and the partition function (online: per-thread running max + rescaled sum)
   ArgMax am{-INFINITY, 0x7fffffff};
-  for (int i = t; i < V; i += NT) am = am_max(am, ArgMax{x[i] * inv_t, i});
+  float z = 0.f;
+  for_row(x, V, [&](int i, float raw) {
+    const float v = raw * inv_t;
+    if (v > am.v) {
+      z = z * __expf(am.v - v) + 1.f;
+      am = ArgMax{v, i};
+    } else if (v > -INFINITY) {
+      z += __expf(v - am.v);
+      if (v == am.v && i < am.i) am.i = i;
+    }
+  });
+  const float m_thr = am.v;
   am = block_argmax(am, ared);
   const float M = am.v;
-  // pass: partition function
-  float z = 0.f;
-  for (int i = t; i < V; i += NT) z += __expf(x[i] * inv_t - M);
-  const float Z = block_sum(z, red);
+  const float Z = block_sum(m_thr == -INFINITY ? 0.f : z * __expf(m_thr - M), red);
   const float logZ = __logf(Z);
 
   if (greedy) {
@@ -168,10 +196,10 @@ __global__ void __launch_bounds__(NT) sample_kernel(
       __syncthreads();
       const int sh = shifts[lvl];
       const uint32_t bm = (1u << widths[lvl]) - 1u;
-      for (int i = t; i < V; i += NT) {
-        const uint32_t key = fkey(x[i] * inv_t);
+      for_row(x, V, [&](int, float raw) {
+        const uint32_t key = fkey(raw * inv_t);
         if ((key & mask) == prefix) atomicAdd(&hcnt[(key >> sh) & bm], 1u);
-      }
+      });
       __syncthreads();
       uint32_t above;
       const int bin = find_crossing<uint32_t>(hcnt, (uint32_t)remaining, &above, scan_u);
@@ -181,10 +209,10 @@ __global__ void __launch_bounds__(NT) sample_kernel(
     }
     thr = prefix;
     float km = 0.f;
-    for (int i = t; i < V; i += NT) {
-      const float v = x[i] * inv_t;
+    for_row(x, V, [&](int, float raw) {
+      const float v = raw * inv_t;
       if (fkey(v) >= thr) km += __expf(v - M);
-    }
+    });
     kept_mass = block_sum(km, red);
   }
   if (p < 1.f) {
@@ -197,11 +225,11 @@ __global__ void __launch_bounds__(NT) sample_kernel(
       __syncthreads();
       const int sh = shifts[lvl];
       const uint32_t bm = (1u << widths[lvl]) - 1u;
-      for (int i = t; i < V; i += NT) {
-        const float v = x[i] * inv_t;
+      for_row(x, V, [&](int, float raw) {
+        const float v = raw * inv_t;
         const uint32_t key = fkey(v);
         if ((key & mask) == prefix && key >= thr) atomicAdd(&hmass[(key >> sh) & bm], __expf(v - M));
-      }
+      });
       __syncthreads();
       float above;
       const int bin = find_crossing<float>(hmass, remaining, &above, scan_f);
@@ -216,14 +244,14 @@ __global__ void __launch_bounds__(NT) sample_kernel(
   const uint64_t seed = (uint64_t)seeds[row];
   const uint64_t base = (uint64_t)steps[row] * (uint64_t)V;
   ArgMax best{-INFINITY, 0x7fffffff};
-  for (int i = t; i < V; i += NT) {
-    const float v = x[i] * inv_t;
+  for_row(x, V, [&](int i, float raw) {
+    const float v = raw * inv_t;
     if (fkey(v) >= thr) {
       const float u = hash_uniform(seed, base + i);
       const float g = -__logf(-__logf(u));
       best = am_max(best, ArgMax{v + g, i});
     }
-  }
+  });
   best = block_argmax(best, ared);
   if (t == 0) {
     const int tok = best.i == 0x7fffffff ? am.i : best.i;

@@ -275,3 +275,21 @@ def test_sdr_pipeline_gpu_recovers_tone(gpu):
     spec = np.abs(np.fft.rfft(y))
     f = np.fft.rfftfreq(len(y), 1 / (1e6 / 62))
     assert abs(f[spec.argmax()] - 440) < 5
+
+
+def test_sample_odd_vocab_and_masked_logits(gpu):
+    """Scalar-tail path (V % 4 != 0) and -inf (masked) logits in the fused max/partition pass."""
+    torch.manual_seed(9)
+    B, V = 6, 1001
+    logits = torch.randn(B, V, device=gpu) * 2
+    logits[:, ::3] = float("-inf")
+    temp = torch.tensor([0.0, 0.8, 0.8, 1.0, 0.5, 0.0], device=gpu)
+    topk = torch.tensor([0, 0, 20, 0, 5, 1], dtype=torch.int32, device=gpu)
+    topp = torch.tensor([1.0, 0.9, 1.0, 0.6, 1.0, 1.0], device=gpu)
+    seeds = torch.arange(B, dtype=torch.int64, device=gpu)
+    steps = torch.zeros(B, dtype=torch.int64, device=gpu)
+    tok, lp = ops.sample(logits.clone(), temp, topk, topp, seeds, steps)
+    tok_r, lp_r = ref.sample(logits.cpu(), temp.cpu(), topk.cpu(), topp.cpu(), seeds.cpu(), steps.cpu())
+    assert (tok.cpu() % 3 != 0).all()
+    assert tok.cpu()[0] == tok_r[0] and torch.isfinite(lp).all()
+    assert (tok.cpu() == tok_r).float().mean() >= 0.8
