@@ -25,11 +25,12 @@ def main():
     B, L = args.batch, args.ctx
     eng = LLMEngine(EngineConfig(model=args.model, max_num_seqs=B, max_batched_tokens=32768,
                                  max_model_len=8192, use_graphs=not args.no_graphs,
-                                 graph_batch_sizes=(B,), enable_prefix_caching=False))
+                                 graph_batch_sizes=(B,), enable_prefix_caching=False,
+                                 mixed_prefill_tokens=0, token_alignment=1))
     g = torch.Generator().manual_seed(0)
     V = 30000
     prompts = [torch.randint(100, V, (L,), generator=g).tolist() for _ in range(B)]
-    p = SamplingParams(temperature=0.7, top_p=0.9, max_tokens=args.steps + 8, ignore_eos=True)
+    p = SamplingParams(temperature=0.7, top_p=0.9, max_tokens=args.steps + 64, ignore_eos=True)
     reqs = [eng.add_request(x, p) for x in prompts]
     torch.cuda.synchronize()
     t0 = time.perf_counter()

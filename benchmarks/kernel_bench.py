@@ -68,9 +68,13 @@ def main():
     kc, vc, bt = paged_setup([L] * B, width=8192 // 64)
     q = torch.randn(B, Hq * D, device=dev, dtype=torch.bfloat16)
     ctx = torch.full((B,), L, dtype=torch.int32, device=dev)
-    ws = ops.DecodeWorkspace(B, Hq, Hkv, 8192, torch.device(dev))
-    us = timeit(lambda: ops.decode_attention(q, kc, vc, bt, ctx, Hq, Hkv, 8192, D ** -0.5, ws=ws))
-    out["decode_256x1400"] = {"us": round(us, 1), "TBps": round(B * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
+    for ppp in (None, 16, 32):
+        ws = ops.DecodeWorkspace(B, Hq, Hkv, 8192, torch.device(dev), ppp)
+        us = timeit(lambda: ops.decode_attention(q, kc, vc, bt, ctx, Hq, Hkv, 8192, D ** -0.5, ws=ws))
+        out[f"decode_256x1400_ppp{ppp}"] = {"us": round(us, 1), "TBps": round(B * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
+    if args.only == "decode":
+        print(json.dumps(out))
+        return
     V = 128256
     logits = torch.randn(B, V, device=dev) * 3
     z = lambda v, dt=torch.float32: torch.full((B,), v, dtype=dt, device=dev)  # noqa: E731

@@ -201,7 +201,11 @@ class Scheduler {
         std::vector<int64_t> ok = prepare_decode(dec, cap_seqs);
         std::vector<int64_t> chosen;
         std::vector<int> qlen;
-        pick_prefill(std::min(cap_tokens - (int)ok.size(), mixed_tokens_), cap_seqs - (int)ok.size(),
+        // a large prefill backlog (a burst of arrivals) is worked off in full-size chunks:
+        // capping it at mixed_tokens_ would stretch it over many decode-dominated steps
+        const int budget = pending_prefill_tokens() >= 4LL * mixed_tokens_ ? cap_tokens - (int)ok.size()
+                                                                           : mixed_tokens_;
+        pick_prefill(std::min(cap_tokens - (int)ok.size(), budget), cap_seqs - (int)ok.size(),
                      chosen, qlen);
         align_tokens((int)ok.size(), chosen, qlen);
         const std::vector<int> ones(ok.size(), 1);
@@ -361,6 +365,19 @@ class Scheduler {
         qlen.pop_back();
       }
     }
+  }
+
+  int64_t pending_prefill_tokens() const {
+    int64_t pending = 0;
+    for (int64_t id : running_) {
+      const Seq& s = seqs_.at(id);
+      if (s.computed < s.prompt_len) pending += (int)s.toks.size() - s.computed;
+    }
+    for (int64_t id : waiting_) {
+      const Seq& s = seqs_.at(id);
+      pending += (int)s.toks.size() - s.computed;
+    }
+    return pending;
   }
 
   // Enough prefill work pending (or waited long enough) to form a mixed step.

@@ -92,7 +92,7 @@ class EngineConfig:
     enable_prefix_caching: bool = True
     use_graphs: bool = True
     graph_batch_sizes: Sequence[int] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256)
-    decode_pages_per_part: int = 16
+    decode_pages_per_part: Optional[int] = None  # None: adapt the KV split to the batch
     seed: int = 0
     detokenize: bool = True
     async_decode: bool = True  # pipeline steps (host work overlaps the GPU)
