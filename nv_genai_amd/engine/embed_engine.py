@@ -17,6 +17,8 @@ from typing import List, Optional, Sequence
 
 import torch
 
+from ..observability.markers import gpu_range
+
 from ..models.config import EncoderConfig, encoder_config
 from ..models.encoder import EncoderModel
 from ..utils.tokenizer import EmbedTokenizer, embed_tokenizer
@@ -104,10 +106,11 @@ class EmbeddingEngine:
                 tt = None
                 if type_ids is not None:
                     tt = torch.tensor([t for b in batch for t in type_ids[b]], dtype=torch.int32).to(self.device, non_blocking=True)
-                res = self.model.forward(ids.to(self.device, non_blocking=True),
-                                         pos.to(self.device, non_blocking=True),
-                                         cu_t.to(self.device, non_blocking=True),
-                                         max(len(seqs[b]) for b in batch), tt)
+                with gpu_range(f"embed n={len(batch)} tok={tok}"):
+                    res = self.model.forward(ids.to(self.device, non_blocking=True),
+                                             pos.to(self.device, non_blocking=True),
+                                             cu_t.to(self.device, non_blocking=True),
+                                             max(len(seqs[b]) for b in batch), tt)
                 if self.center is not None and not self.cfg.num_labels:
                     res = res - self.center
                     if self.whiten is not None:

@@ -17,6 +17,7 @@ kv_cache_free_gpu_mem_fraction -> ``kv_cache_fraction``, tensor_para_size -> ``t
 """
 from __future__ import annotations
 
+import collections
 import itertools
 import logging
 import random
@@ -29,6 +30,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..observability.markers import gpu_range
 from .._native import rt
 from ..models.config import LlamaConfig, llama_config
 from ..models.llama import AttnMeta, LlamaModel
@@ -194,6 +196,7 @@ class LLMEngine:
         self._pending: Optional[dict] = None
         self._tok_flip = 0
         self._up_ev = None  # marks the last host->device upload of the pinned step buffers
+        self._timeline = collections.deque(maxlen=4096)
         self._tok_host = [(hbuf(S), hbuf(S, dtype=torch.float32)) for _ in range(2)]
         if self.p.tp_size > 1:
             # followers replay from broadcast host buffers; the device-side id gather of the
@@ -317,7 +320,15 @@ class LLMEngine:
                     done.append(r)
             return done
 
+    def timeline(self, last: int = 256) -> List[dict]:
+        """Recent scheduler steps: wall time at launch, kind, rows, tokens, decode rows and
+        the host time spent in ``step()`` (the engine step-timeline of SURVEY.md §5.1)."""
+        return list(self._timeline)[-last:]
+
     def _count(self, kind, n, ntok, nd):
+        self._timeline.append({"t": time.time(), "kind": "decode" if kind == 2 else ("mixed" if nd else "prefill"),
+                               "rows": n, "tokens": ntok, "decode_rows": nd,
+                               "waiting": self.sched.num_waiting(), "running": self.sched.num_running()})
         if kind == 2:
             self.stats["decode_steps"] += 1
             self.stats["decode_tokens"] += n
@@ -337,16 +348,18 @@ class LLMEngine:
         Tokens are copied to pinned host memory right after sampling, so the next step may
         overwrite the device buffers."""
         if kind == 2:
-            self._decode_launch(n, src)
+            with gpu_range(f"decode n={n}"):
+                self._decode_launch(n, src)
         else:
             cu = self._np[3][: n + 1]
             max_q = int((cu[1:] - cu[:-1]).max())
             max_ctx = int(self._np[4][:n].max())
-            self._sync_step(kind, n, ntok, max_q, max_ctx, 0, nd)
-            self._upload(n, ntok)
-            self._gather_ids(src)
-            logits = self._prefill_forward(n, ntok, max_q, max_ctx, nd)
-            self._sample(logits, n)
+            with gpu_range(f"{'mixed' if nd else 'prefill'} n={n} tok={ntok} dec={nd}"):
+                self._sync_step(kind, n, ntok, max_q, max_ctx, 0, nd)
+                self._upload(n, ntok)
+                self._gather_ids(src)
+                logits = self._prefill_forward(n, ntok, max_q, max_ctx, nd)
+                self._sample(logits, n)
         buf = self._tok_host[self._tok_flip]
         self._tok_flip ^= 1
         buf[0][:n].copy_(self.d_tok[:n], non_blocking=self.gpu)

@@ -22,6 +22,7 @@ from typing import Optional, Tuple
 import torch
 
 from .. import ops
+from ..observability.markers import gpu_range
 
 
 class FlatIndex:
@@ -136,6 +137,10 @@ class FlatIndex:
         if self.n == 0:
             nq = q.shape[0]
             return (torch.empty(nq, 0, device=self.device), torch.empty(nq, 0, dtype=torch.int64, device=self.device))
+        with gpu_range(f"search q={q.shape[0]} n={self.n}"):
+            return self._search(q, k)
+
+    def _search(self, q: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
         qb = q.to(self.dtype).contiguous()
         X = self.X[: self.n]
         if self.metric == "l2":

@@ -301,6 +301,12 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
         return JSONResponse({"object": "health-response", "message": "Service is ready." if ok else "not ready"},
                             status_code=200 if ok else 503)
 
+    @app.get("/v1/debug/timeline")
+    def timeline(last: int = 256):
+        """Recent engine steps (kind, rows, tokens, decode rows, queue depths)."""
+        svc = _need(app.state.llm, "LLM")
+        return {"steps": svc.engine.timeline(last)}
+
     @app.get("/metrics")
     def prom():
         g = app.state.llm.metrics() if app.state.llm is not None else {}
