@@ -5,6 +5,7 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
+#include "kernels/custom_ar.h"
 #include "kernels/kernels.h"
 
 namespace {
@@ -331,6 +332,30 @@ void resample_pcm(Tensor x, Tensor h, int64_t down, int64_t pre, double gain, c1
                            (int)pre, (int)nout, (float)gain, fp, ip, cur_stream(x));
 }
 
+// ---- custom all-reduce over IPC peer buffers (TP decode)
+struct CustomAR {
+  std::unique_ptr<nga::CustomAllReduce> impl;
+  CustomAR(int64_t rank, int64_t world, int64_t cap_bytes, double timeout_s)
+      : impl(new nga::CustomAllReduce((int)rank, (int)world, cap_bytes, timeout_s)) {}
+  py::bytes handle() const { return py::bytes(impl->handle()); }
+  void open(const std::vector<std::string>& handles) { impl->open(handles); }
+  // out may alias inp (in-place all-reduce)
+  void all_reduce(Tensor inp, Tensor out, int64_t algo) {
+    CHECK_DEV(inp); CHECK_DEV(out); CHECK_CONTIG(inp); CHECK_CONTIG(out);
+    TORCH_CHECK(inp.scalar_type() == out.scalar_type() && inp.numel() == out.numel(),
+                "custom all-reduce: in/out must match");
+    TORCH_CHECK(inp.scalar_type() == at::kBFloat16 || inp.scalar_type() == at::kFloat,
+                "custom all-reduce: bf16 or fp32");
+    TORCH_CHECK(algo >= 0 && algo <= 2, "custom all-reduce: algo 0 (auto), 1 (one-shot), 2 (two-shot)");
+    const int64_t bytes = inp.numel() * inp.element_size();
+    impl->run(inp.data_ptr(), out.data_ptr(), bytes, inp.scalar_type() == at::kBFloat16, (int)algo,
+              cur_stream(inp));
+  }
+  int64_t error() const { return impl->error(); }
+  int64_t capacity() const { return impl->capacity(); }
+  void set_two_shot_threshold(int64_t b) { impl->set_two_shot_threshold(b); }
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -352,4 +377,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("fir_c64", &fir_c64);
   m.def("fm_demod", &fm_demod);
   m.def("resample_pcm", &resample_pcm);
+  py::class_<CustomAR>(m, "CustomAllReduce")
+      .def(py::init<int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("world"),
+           py::arg("capacity_bytes"), py::arg("timeout_s") = 5.0)
+      .def("handle", &CustomAR::handle)
+      .def("open", &CustomAR::open)
+      .def("all_reduce", &CustomAR::all_reduce, py::arg("inp"), py::arg("out"), py::arg("algo") = 0)
+      .def("error", &CustomAR::error)
+      .def("capacity", &CustomAR::capacity)
+      .def("set_two_shot_threshold", &CustomAR::set_two_shot_threshold);
 }

@@ -1,0 +1,50 @@
+// Host API of the IPC custom all-reduce (custom_ar.hip). No PyTorch types here: the
+// binding layer hands in raw device pointers and the current HIP stream.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace nga {
+
+constexpr int kArMaxRanks = 8;
+constexpr int kArMaxBlocks = 80;
+
+class CustomAllReduce {
+ public:
+  // Allocates this rank's Signal block + 2 staging buffers of `cap_bytes` (uncached HBM).
+  CustomAllReduce(int rank, int world, int64_t cap_bytes, double timeout_s);
+  ~CustomAllReduce();
+  CustomAllReduce(const CustomAllReduce&) = delete;
+  CustomAllReduce& operator=(const CustomAllReduce&) = delete;
+
+  // IPC handle (raw bytes) of this rank's allocation, to be exchanged with the peers.
+  std::string handle() const;
+  // Map every peer's allocation (handles indexed by rank; our own entry is ignored).
+  void open(const std::vector<std::string>& handles);
+  // out = sum over ranks of in (bf16 or fp32, `bytes` a multiple of 16). algo: 0 = pick by
+  // size, 1 = one-shot, 2 = two-shot. Capture-safe: no allocation, no host sync.
+  void run(const void* in, void* out, int64_t bytes, bool is_bf16, int algo, hipStream_t stream);
+  // Sticky barrier-timeout flag (synchronous read; call outside graph capture).
+  int error() const;
+
+  int64_t capacity() const { return cap_; }
+  int world() const { return world_; }
+  int rank() const { return rank_; }
+  void set_two_shot_threshold(int64_t b) { two_shot_threshold_ = b; }
+  static size_t alloc_bytes(int64_t cap);
+
+ private:
+  int grid_for(int64_t nvec, bool two_shot) const;
+  int rank_, world_, device_ = 0;
+  int64_t cap_;
+  int64_t two_shot_threshold_ = 512 * 1024;
+  uint64_t timeout_ticks_ = 0;
+  void* mine_ = nullptr;
+  void* peers_[kArMaxRanks];
+  bool opened_ = false;
+};
+
+}  // namespace nga

@@ -1,0 +1,134 @@
+"""Custom all-reduce for tensor-parallel decode: direct reads of IPC-mapped peer buffers
+over xGMI (``csrc/kernels/custom_ar.hip``), with RCCL for everything it does not cover.
+
+Where the reference gets this: TensorRT-LLM's ``enable_custom_all_reduce`` knob inside NIM
+(experimental/fm-asr-streaming-rag/nim/configs/mistral-7b.yaml:36; SURVEY.md §2.D CC1/CC2,
+§2.F). Llama-3-70B at TP=8 issues 160 all-reduces per generated token, each only
+16 KiB x batch: RCCL's ring pays W-1 serial hops on one xGMI link each; here every rank
+reads all 7 peers at once and a call is one (one-shot) or two (two-shot) cross-GPU flag
+round trips plus the data time.
+
+Construction is collective over the group: every rank allocates its uncached
+Signal+staging block, the IPC handles are exchanged with ``all_gather_object`` and every
+rank maps its peers. A start-up self-test compares the result against the process group's
+own all-reduce (and checks the kernel's barrier-timeout flag) and all ranks agree on the
+outcome; on any failure the object disables itself and callers fall back to RCCL.
+"""
+from __future__ import annotations
+
+import logging
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+log = logging.getLogger(__name__)
+
+ALGO_AUTO, ALGO_ONE_SHOT, ALGO_TWO_SHOT = 0, 1, 2
+
+
+class CustomAllReduce:
+    def __init__(self, group=None, capacity_mb: float = 64.0, timeout_s: float = 5.0,
+                 two_shot_threshold_kb: Optional[float] = None, self_test: bool = True):
+        from ..ops import kernels
+
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        cap = int(capacity_mb * 2 ** 20) // 128 * 128
+        self.capacity = cap
+        self.enabled = False
+        self.impl = None
+        # every stage ends with an agreement among the ranks, so a failure on one rank
+        # never leaves the others waiting in a collective
+        handle, err = b"", None
+        try:
+            self.impl = kernels().CustomAllReduce(self.rank, self.world, cap, float(timeout_s))
+            if two_shot_threshold_kb is not None:
+                self.impl.set_two_shot_threshold(int(two_shot_threshold_kb * 1024))
+            handle = self.impl.handle()
+        except Exception as e:  # noqa: BLE001
+            err = e
+        if not self._agree(err is None):
+            raise RuntimeError(f"custom all-reduce: allocation/export failed on some rank ({err!r})")
+        handles = [None] * self.world
+        dist.all_gather_object(handles, handle, group=group)
+        try:
+            self.impl.open(handles)
+        except Exception as e:  # noqa: BLE001
+            err = e
+        if not self._agree(err is None):
+            raise RuntimeError(f"custom all-reduce: mapping peer buffers failed on some rank ({err!r})")
+        self.enabled = True
+        if self_test:
+            self.enabled = self._self_test()
+
+    # ------------------------------------------------------------------ API
+    def eligible(self, x: torch.Tensor) -> bool:
+        nbytes = x.numel() * x.element_size()
+        return (self.enabled and x.is_cuda and x.is_contiguous()
+                and x.dtype in (torch.bfloat16, torch.float32)
+                and 0 < nbytes <= self.capacity and nbytes % 16 == 0
+                and x.data_ptr() % 16 == 0)
+
+    def all_reduce(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
+                   algo: int = ALGO_AUTO) -> torch.Tensor:
+        """Sum of ``x`` over the group (in place unless ``out`` is given)."""
+        if out is None:
+            out = x
+        self.impl.all_reduce(x, out, algo)
+        return out
+
+    def error(self) -> int:
+        return int(self.impl.error())
+
+    def _agree(self, ok: bool) -> bool:
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        if dist.get_backend(self.group) == "nccl":
+            flag = flag.to(torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(flag.item())
+
+    # ------------------------------------------------------------------ self-test
+    def _reference_sum(self, x: torch.Tensor) -> torch.Tensor:
+        backend = dist.get_backend(self.group)
+        y = x.float().clone() if backend == "nccl" else x.float().cpu()
+        dist.all_reduce(y, group=self.group)
+        return y.to(x.device)
+
+    def _self_test(self) -> bool:
+        ok = True
+        dev = torch.device("cuda", torch.cuda.current_device())
+        try:
+            dist.barrier(group=self.group)
+            for n, algo in ((4096, ALGO_ONE_SHOT), (1 << 20, ALGO_TWO_SHOT), (1 << 20, ALGO_AUTO)):
+                g = torch.Generator(device="cpu").manual_seed(1000 + self.rank)
+                x = torch.randn(n, generator=g).to(dev, torch.bfloat16)
+                ref = self._reference_sum(x)
+                got = self.all_reduce(x.clone(), algo=algo)
+                torch.cuda.synchronize(dev)
+                # no early exit: every rank must issue the same collectives
+                ok = ok and not self.error() and torch.allclose(got.float(), ref, atol=0.05, rtol=0.02)
+        except Exception as e:  # noqa: BLE001 - any failure means "use RCCL"
+            log.warning("custom all-reduce self-test raised: %r", e)
+            ok = False
+        ok = self._agree(ok)
+        if not ok:
+            log.warning("custom all-reduce disabled (self-test failed); TP all-reduces use RCCL")
+        return ok
+
+
+def maybe_create(group, world: int) -> Optional[CustomAllReduce]:
+    """The TP group's custom all-reduce, or None when it does not apply (CPU, world 1 or
+    > 8, ``NGA_CUSTOM_AR=0``). Collective: every rank of ``group`` must call it."""
+    if world <= 1 or world > 8 or not torch.cuda.is_available():
+        return None
+    if os.environ.get("NGA_CUSTOM_AR", "1") == "0":
+        return None
+    try:
+        car = CustomAllReduce(group, capacity_mb=float(os.environ.get("NGA_CUSTOM_AR_MB", "64")))
+    except Exception as e:  # noqa: BLE001
+        log.warning("custom all-reduce unavailable (%r); TP all-reduces use RCCL", e)
+        return None
+    return car if car.enabled else None

@@ -91,6 +91,12 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
                            tp_rank=rank % tp_size, tp_group=tp_group, dp_size=dp,
                            dp_rank=rank // tp_size, dp_group=dp_group,
                            backend=backend if world > 1 else "none", device=dev)
+    if tp_size > 1 and backend == "nccl" and use_gpu:
+        # IPC custom all-reduce for the TP group's small decode messages (RCCL otherwise)
+        from .comm import register_custom_all_reduce
+        from .custom_ar import maybe_create
+
+        register_custom_all_reduce(tp_group, maybe_create(tp_group, tp_size))
     return _CTX
 
 

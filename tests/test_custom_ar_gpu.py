@@ -1,0 +1,135 @@
+"""Custom IPC all-reduce (csrc/kernels/custom_ar.hip) on the GPU box.
+
+The box has ONE MI355X, so the two ranks share cuda:0: each process exports its uncached
+Signal+staging allocation with hipIpcGetMemHandle and maps the other's, exactly as across
+xGMI peers (what this cannot show is cross-GPU cache coherence — the start-up self-test
+against RCCL covers that on a real TP group). Handles and the reference sums go over gloo.
+
+Expected values: each rank's input is a deterministic function of (rank, case), so every
+process recomputes all inputs and the exact fp32 sum in rank order 0..W-1 — the kernel's
+own summation order — and the result must match bit for bit.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+WORLD = 2
+CASES = [  # (numel, dtype, algo)
+    (8, torch.bfloat16, 1),
+    (8192, torch.bfloat16, 0),
+    (8192 * 64, torch.bfloat16, 1),
+    (8192 * 64, torch.bfloat16, 2),
+    (8192 * 256 + 8, torch.bfloat16, 2),   # chunk does not divide evenly
+    (3 * 1024 * 1024, torch.bfloat16, 0),  # auto -> two-shot
+    (4096, torch.float32, 1),
+    (1 << 20, torch.float32, 2),
+]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _inp(rank, ci, n, dtype):
+    g = torch.Generator().manual_seed(7919 * ci + rank)
+    return torch.randn(n, generator=g).to(dtype)
+
+
+def _expect(ci, n, dtype):
+    acc = torch.zeros(n, dtype=torch.float32)
+    for r in range(WORLD):
+        acc = acc + _inp(r, ci, n, dtype).float()
+    return acc.to(dtype)
+
+
+def _worker(rank, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(WORLD), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from nv_genai_amd.parallel.custom_ar import CustomAllReduce
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    res = {"rank": rank}
+    try:
+        car = CustomAllReduce(None, capacity_mb=16, timeout_s=10.0)
+        res["self_test"] = car.enabled
+        bad = []
+        for ci, (n, dt, algo) in enumerate(CASES):
+            x = _inp(rank, ci, n, dt).cuda()
+            out = car.all_reduce(x, out=torch.empty_like(x), algo=algo)
+            inplace = car.all_reduce(x.clone(), algo=algo)
+            torch.cuda.synchronize()
+            exp = _expect(ci, n, dt)
+            if not torch.equal(out.cpu(), exp) or not torch.equal(inplace.cpu(), exp):
+                bad.append((ci, float((out.cpu().float() - exp.float()).abs().max())))
+        res["bad"] = bad
+        # hipGraph: 3 all-reduces captured once, replayed twice with new inputs
+        xs = [torch.empty(8192 * 16, dtype=torch.bfloat16, device="cuda") for _ in range(3)]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for x in xs:
+                car.all_reduce(x)
+            torch.cuda.synchronize()
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, stream=s):
+                for x in xs:
+                    car.all_reduce(x)
+        graph_ok = True
+        for rep in range(2):
+            for i, x in enumerate(xs):
+                x.copy_(_inp(rank, 100 + 10 * rep + i, x.numel(), torch.bfloat16))
+            gr.replay()
+            torch.cuda.synchronize()
+            for i, x in enumerate(xs):
+                graph_ok &= torch.equal(x.cpu(), _expect(100 + 10 * rep + i, x.numel(), torch.bfloat16))
+        res["graph_ok"] = graph_ok
+        # latency of a decode-sized message (same-GPU peers: kernel + flag overhead only)
+        x = torch.randn(8192 * 8, device="cuda").to(torch.bfloat16)
+        for _ in range(20):
+            car.all_reduce(x)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(200):
+            car.all_reduce(x)
+        e1.record()
+        torch.cuda.synchronize()
+        res["us_per_call_128KiB"] = e0.elapsed_time(e1) * 1e3 / 200
+        res["error"] = car.error()
+    except Exception as e:  # noqa: BLE001
+        res["exc"] = repr(e)
+    q.put(res)
+    dist.destroy_process_group()
+
+
+def test_custom_all_reduce_two_ranks_one_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=150) for _ in range(WORLD)]
+    for p in procs:
+        p.join(timeout=60)
+    print(results)
+    for r in results:
+        assert "exc" not in r, r
+        assert r["self_test"], r
+        assert r["bad"] == [], r
+        assert r["graph_ok"], r
+        assert r["error"] == 0, r

@@ -99,3 +99,32 @@ def test_sharded_index_matches_flat():
     assert nlocal == 1500
     assert torch.allclose(vals, rv, atol=1e-5)
     assert torch.equal(ids, ri)
+
+
+def test_all_reduce_routes_to_registered_custom_all_reduce():
+    """comm.all_reduce takes a group's custom all-reduce when the tensor is eligible and
+    falls back to the process group otherwise."""
+    from nv_genai_amd.parallel import comm
+
+    class FakeCAR:
+        def __init__(self):
+            self.calls = 0
+
+        def eligible(self, x):
+            return x.numel() <= 4
+
+        def all_reduce(self, x):
+            self.calls += 1
+            return x.mul_(2)
+
+    group = object()
+    car = FakeCAR()
+    comm.register_custom_all_reduce(group, car)
+    try:
+        assert comm.custom_all_reduce_for(group) is car
+        x = torch.ones(4)
+        comm.all_reduce(x, group)
+        assert car.calls == 1 and torch.equal(x, torch.full((4,), 2.0))
+    finally:
+        comm.register_custom_all_reduce(group, None)
+    assert comm.custom_all_reduce_for(group) is None
