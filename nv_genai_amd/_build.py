@@ -124,15 +124,19 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
     return out
 
 
-def build_runtime(force: bool = False, jobs: int = 8) -> Path:
-    """Compile the host-only native runtime (_rt) with the system C++ compiler."""
-    out = PKG / f"_rt{EXT_SUFFIX}"
-    objdir = BUILD / "runtime"
+def build_runtime(force: bool = False, jobs: int = 8, out_dir: Path | None = None,
+                  extra_flags: list | None = None) -> Path:
+    """Compile the host-only native runtime (_rt) with the system C++ compiler.
+
+    ``out_dir``/``extra_flags`` build a variant elsewhere, e.g. the ASan+UBSan build that
+    tests/test_runtime_sanitizers.py drives."""
+    out = (Path(out_dir) if out_dir else PKG) / f"_rt{EXT_SUFFIX}"
+    objdir = (Path(out_dir) / "obj") if out_dir else BUILD / "runtime"
     objdir.mkdir(parents=True, exist_ok=True)
     srcs = sorted((CSRC / "runtime").glob("*.cpp"))
     cxx = os.environ.get("CXX", "g++")
     flags = ["-O2", "-fPIC", "-std=c++17", "-fvisibility=hidden", *_py_inc(), *_pybind_inc()]
-    extra = os.environ.get("NGA_RT_CXXFLAGS", "").split()
+    extra = os.environ.get("NGA_RT_CXXFLAGS", "").split() + list(extra_flags or [])
     jobs_list, objs = [], []
     for s in srcs:
         o = objdir / (s.stem + ".o")

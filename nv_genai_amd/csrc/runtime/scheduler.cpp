@@ -87,6 +87,7 @@ class BlockManager {
     return b;
   }
   void register_full(int b, uint64_t h) {
+    if (b < 0 || b >= nb_ || ref_[b] <= 0) throw std::runtime_error("register_full of a free block");
     if (!prefix_ || hash_[b] != 0) return;
     if (cached_.count(h)) return;  // identical content already cached in another block
     hash_[b] = h;

@@ -1,0 +1,120 @@
+"""ASan + UBSan build of the native host runtime (_rt: paged-KV block manager, continuous-
+batching scheduler, BM25 index, splitters), driven by a randomized stress workload in a
+child interpreter (the reference has no sanitizer coverage at all).
+
+The instrumented module is built into a temp dir (the in-tree _rt stays uninstrumented) and
+loaded with libasan preloaded ahead of anything already in LD_PRELOAD; any ASan report or
+UBSan "runtime error" fails the test (-fno-sanitize-recover makes UB fatal).
+"""
+import os
+import shutil
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+STRESS = textwrap.dedent(r'''
+    import importlib.util, random, sys
+    import numpy as np
+    spec = importlib.util.spec_from_file_location("_rt", sys.argv[1])
+    rt = importlib.util.module_from_spec(spec); spec.loader.exec_module(rt)
+    rng = random.Random(0)
+
+    # block manager: random alloc / release / prefix register / lookup, incl. error paths
+    bm = rt.BlockManager(64, 16, True)
+    live = []
+    for it in range(20000):
+        op = rng.random()
+        if op < 0.45 and bm.num_free() > 0:
+            b = bm.alloc(); live.append(b)
+            if rng.random() < 0.5:
+                bm.register_full(b, rng.randrange(1 << 60))
+        elif op < 0.85 and live:
+            bm.release(live.pop(rng.randrange(len(live))))
+        else:
+            b = bm.lookup(rng.randrange(1 << 60))
+            if b >= 0: live.append(b)
+    for bad in (-1, 64, 10 ** 6):
+        try:
+            bm.release(bad)
+        except (RuntimeError, ValueError, IndexError):
+            pass
+
+    # scheduler: random arrivals, chunked prefill, mixed steps, finishes, preemption pressure
+    T, S, MB = 512, 16, 64
+    s = rt.Scheduler(48, 16, S, T, 1024, True)
+    s.set_mixed_prefill_tokens(128)
+    bufs = (np.zeros(T, np.int32), np.zeros(T, np.int32), np.zeros(T, np.int32), np.zeros(S + 1, np.int32),
+            np.zeros(S, np.int32), np.zeros((S, MB), np.int32), np.zeros(S, np.int64), np.zeros(S, np.int32))
+    nxt, active = 1, set()
+    for step in range(3000):
+        if rng.random() < 0.3 and len(active) < 40:
+            n = rng.randrange(1, 300)
+            base = rng.randrange(4)  # shared prefixes exercise the prefix cache
+            s.add(nxt, [base * 1000 + (i % 97) for i in range(n)], rng.randrange(1, 40))
+            active.add(nxt); nxt += 1
+        if not s.has_work():
+            continue
+        kind, n, ntok = s.schedule(*bufs)
+        sids = [int(x) for x in bufs[6][:n]]
+        smp = [int(x) for x in bufs[7][:n]]
+        for sid, sm in zip(sids, smp):
+            if sm and sid in active:
+                s.append_token(sid, rng.randrange(50000))
+                if rng.random() < 0.05 or s.num_generated(sid) > 30:
+                    s.finish(sid); active.discard(sid)
+    for sid in list(active):
+        s.finish(sid)
+    assert s.used_blocks() == 0 or not s.has_work()
+
+    # BM25 + splitters
+    idx = rt.BM25Index(1.2, 0.75)
+    words = ["alpha", "beta", "gamma", "delta", "epsilon", "zeta", "eta", "theta", "x" * 300, ""]
+    for d in range(3000):
+        idx.add(d, " ".join(rng.choice(words) for _ in range(rng.randrange(0, 60))))
+    for d in range(0, 3000, 7):
+        idx.remove(d)
+    for _ in range(200):
+        idx.search(" ".join(rng.choice(words) for _ in range(rng.randrange(0, 6))), rng.randrange(1, 50))
+    for n in (0, 1, 5, 510, 10000):
+        rt.token_windows(n, 508, 200)
+    text = "".join(rng.choice(["a", "b", " ", "\n", "\n\n", ". "]) for _ in range(20000))
+    rt.char_split(text, 1000, 100, ["\n\n", "\n", " ", ""])
+    rt.char_split("", 10, 0, ["\n"])
+    print("STRESS_OK")
+''')
+
+
+@pytest.mark.timeout(600)
+def test_runtime_under_asan_ubsan(tmp_path):
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    libasan = subprocess.run(["g++", "-print-file-name=libasan.so"], capture_output=True,
+                             text=True).stdout.strip()
+    if not os.path.isabs(libasan) or not os.path.exists(libasan):
+        pytest.skip("libasan not available")
+    sys.path.insert(0, ROOT)
+    from nv_genai_amd import _build
+
+    san = ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+           "-fno-omit-frame-pointer", "-g"]
+    so = _build.build_runtime(force=True, out_dir=tmp_path, extra_flags=san)
+    script = tmp_path / "stress.py"
+    script.write_text(STRESS)
+    env = dict(os.environ)
+    # libstdc++ right after libasan: python itself does not link it, and ASan's
+    # __cxa_throw interceptor must resolve the real one when _rt throws
+    libstdcxx = subprocess.run(["g++", "-print-file-name=libstdc++.so.6"], capture_output=True,
+                               text=True).stdout.strip()
+    env["LD_PRELOAD"] = " ".join(p for p in (libasan, libstdcxx, os.environ.get("LD_PRELOAD", "")) if p)
+    env["ASAN_OPTIONS"] = "detect_leaks=0:abort_on_error=1"
+    env["UBSAN_OPTIONS"] = "print_stacktrace=1"
+    r = subprocess.run([sys.executable, str(script), str(so)], capture_output=True, text=True,
+                       env=env, timeout=500)
+    report = r.stdout[-3000:] + r.stderr[-6000:]
+    assert r.returncode == 0, report
+    assert "STRESS_OK" in r.stdout, report
+    assert "AddressSanitizer" not in r.stderr and "runtime error:" not in r.stderr, report
