@@ -39,6 +39,9 @@ import time
 import torch
 
 
+REF_EQUIV_QPS_PER_GPU = 4.40   # profiles/r1_refeq/ref_eq.json
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -199,7 +202,9 @@ def main():
         "ms_per_step": round(1000 * t_max / args.steps, 2),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": None,
+        # reference-equivalent stack (HF eager + torch brute-force search) measured on the
+        # same MI355X: 4.40 QPS per GPU (BASELINE.md "Measured on MI355X")
+        "vs_baseline": round(qps / (REF_EQUIV_QPS_PER_GPU * world), 3),
         "dtype": "bf16",
         "data": "synthetic: random-init weights; 1M random unit-vector index + generated ~500-token chunks; generated questions",
         "config": {
