@@ -67,6 +67,8 @@ class LlamaModel:
             self._load(weights)
         self.cos_sin = ops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta,
                                         cfg.rope_scaling).to(self.device)
+        self.split_mixed = False   # mixed steps on two streams (forward_split)
+        self._aux = None
 
     # ------------------------------------------------------------------ weights
     def _random_init(self, seed: int):
@@ -173,54 +175,103 @@ class LlamaModel:
         h = h * ok.unsqueeze(-1).to(h.dtype)
         return tp_all_reduce(h, self.p)
 
+    def _attention(self, q, qkv, li, meta: AttnMeta, T: int):
+        hq, hkv, D = self.hq, self.hkv, self.D
+        qdim = hq * D
+        if meta.kind == "decode":
+            return ops.decode_attention(q, self.k_cache[li], self.v_cache[li],
+                                        meta.block_tables, meta.ctx_lens, hq, hkv,
+                                        meta.max_ctx, self.scale, ws=meta.decode_ws)
+        if meta.kind == "mixed":
+            nd = meta.n_decode
+            attn = torch.empty(T, qdim, dtype=qkv.dtype, device=qkv.device)
+            ops.decode_attention(q[:nd], self.k_cache[li], self.v_cache[li],
+                                 meta.block_tables[:nd], meta.ctx_lens[:nd], hq, hkv,
+                                 meta.max_ctx, self.scale, out=attn[:nd], ws=meta.decode_ws)
+            ops.prefill_attention_paged(q[nd:], self.k_cache[li], self.v_cache[li],
+                                        meta.block_tables[nd:], meta.cu_q_prefill,
+                                        meta.ctx_lens[nd:], hq, hkv, D, meta.max_q_len,
+                                        self.scale, out=attn[nd:])
+            return attn
+        return ops.prefill_attention_paged(q, self.k_cache[li], self.v_cache[li],
+                                           meta.block_tables, meta.cu_q, meta.ctx_lens,
+                                           hq, hkv, D, meta.max_q_len, self.scale)
+
+    def _layer(self, li: int, x, resid, pos, meta: AttnMeta):
+        """One decoder layer on rows (x = rmsnorm(resid)); returns the MLP output d, which
+        the caller folds into resid with the next layer's (or the final) norm."""
+        cfg, L = self.cfg, self.layers[li]
+        qkv = x @ L["wqkv"].t()
+        ops.rope_cache_(qkv, pos, self.cos_sin, meta.slots, self.k_cache[li],
+                        self.v_cache[li], self.hq, self.hkv, self.D)
+        attn = self._attention(qkv[:, :self.hq * self.D], qkv, li, meta, x.shape[0])
+        o = attn @ L["wo"].t()
+        tp_all_reduce(o, self.p)
+        x = ops.add_rmsnorm(resid, o, L["mlp_norm"], cfg.eps)
+        h = ops.silu_mul(x @ L["wgu"].t())
+        d = h @ L["wd"].t()
+        tp_all_reduce(d, self.p)
+        return d
+
+    def _stack(self, resid, pos, meta: AttnMeta, sample_idx: Optional[torch.Tensor]):
+        cfg = self.cfg
+        x = ops.rmsnorm(resid, self.layers[0]["attn_norm"], cfg.eps)
+        n = len(self.layers)
+        for li in range(n):
+            d = self._layer(li, x, resid, pos, meta)
+            if li + 1 < n:
+                x = ops.add_rmsnorm(resid, d, self.layers[li + 1]["attn_norm"], cfg.eps)
+            elif sample_idx is not None:
+                # only rows that sample need the final norm
+                rows = resid.index_select(0, sample_idx) + d.index_select(0, sample_idx)
+                return ops.rmsnorm(rows.contiguous(), self.final_norm, cfg.eps)
+            else:
+                return ops.add_rmsnorm(resid, d, self.final_norm, cfg.eps)
+        raise RuntimeError("model has no layers")
+
     def forward(self, ids: torch.Tensor, pos: torch.Tensor, meta: AttnMeta,
                 sample_idx: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Returns the final-normed hidden rows selected by ``sample_idx`` (all rows if None)."""
-        cfg = self.cfg
-        hq, hkv, D = self.hq, self.hkv, self.D
+        if meta.kind == "mixed" and self.split_mixed and ids.is_cuda and self.p.tp_size == 1:
+            return self.forward_split(ids, pos, meta, sample_idx)
+        return self._stack(self.embed_tokens(ids), pos, meta, sample_idx)
+
+    def forward_split(self, ids: torch.Tensor, pos: torch.Tensor, meta: AttnMeta,
+                      sample_idx: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Mixed step as two independent row groups on two HIP streams: the decode rows
+        (memory-bound: paged-KV attention streams ~1.4 GB per layer at 256 x 1400) on an
+        auxiliary stream, the prefill chunk (compute-bound GEMMs) on the current stream.
+        The groups share no data inside the stack — each writes the KV pages of its own
+        sequences — so the GPU co-schedules them for all layers and the KV stream of the
+        decode rows fills the CUs that the prefill GEMMs' tile grid leaves idle.
+        ``sample_idx`` must list the decode rows first (the engine's layout).
+
+        Measured on MI355X (benchmarks/mixed_step.py, profiles/r1_mixed_split): 256 decode
+        rows x 1330 ctx + a 1170-token chunk takes 31.1 ms split vs 28.5 ms fused (2048-token
+        chunk: 38.9 vs 37.8 ms). hipBLASLt's stream-K GEMMs occupy every CU, so the decode
+        attention gets no idle CUs to run on while the split costs GEMM efficiency (M=256 and
+        M=1170 instead of one M=1426 GEMM). Off by default (``split_mixed``)."""
+        nd = meta.n_decode
+        main = torch.cuda.current_stream(ids.device)
+        if self._aux is None:
+            self._aux = torch.cuda.Stream(ids.device)
+        aux = self._aux
         resid = self.embed_tokens(ids)
-        T = resid.shape[0]
-        x = ops.rmsnorm(resid, self.layers[0]["attn_norm"], cfg.eps)
-        qdim = hq * D
-        for li, L in enumerate(self.layers):
-            qkv = x @ L["wqkv"].t()
-            ops.rope_cache_(qkv, pos, self.cos_sin, meta.slots, self.k_cache[li],
-                            self.v_cache[li], hq, hkv, D)
-            q = qkv[:, :qdim]
-            if meta.kind == "decode":
-                attn = ops.decode_attention(q, self.k_cache[li], self.v_cache[li],
-                                            meta.block_tables, meta.ctx_lens, hq, hkv,
-                                            meta.max_ctx, self.scale, ws=meta.decode_ws)
-            elif meta.kind == "mixed":
-                nd = meta.n_decode
-                attn = torch.empty(T, qdim, dtype=qkv.dtype, device=qkv.device)
-                ops.decode_attention(q[:nd], self.k_cache[li], self.v_cache[li],
-                                     meta.block_tables[:nd], meta.ctx_lens[:nd], hq, hkv,
-                                     meta.max_ctx, self.scale, out=attn[:nd], ws=meta.decode_ws)
-                ops.prefill_attention_paged(q[nd:], self.k_cache[li], self.v_cache[li],
-                                            meta.block_tables[nd:], meta.cu_q_prefill,
-                                            meta.ctx_lens[nd:], hq, hkv, D, meta.max_q_len,
-                                            self.scale, out=attn[nd:])
-            else:
-                attn = ops.prefill_attention_paged(q, self.k_cache[li], self.v_cache[li],
-                                                   meta.block_tables, meta.cu_q, meta.ctx_lens,
-                                                   hq, hkv, D, meta.max_q_len, self.scale)
-            o = attn @ L["wo"].t()
-            tp_all_reduce(o, self.p)
-            x = ops.add_rmsnorm(resid, o, L["mlp_norm"], cfg.eps)
-            h = ops.silu_mul(x @ L["wgu"].t())
-            d = h @ L["wd"].t()
-            tp_all_reduce(d, self.p)
-            nxt = self.layers[li + 1]["attn_norm"] if li + 1 < len(self.layers) else None
-            if nxt is not None:
-                x = ops.add_rmsnorm(resid, d, nxt, cfg.eps)
-            else:
-                # only rows that sample need the final norm
-                if sample_idx is not None:
-                    rows = resid.index_select(0, sample_idx) + d.index_select(0, sample_idx)
-                    return ops.rmsnorm(rows.contiguous(), self.final_norm, cfg.eps)
-                return ops.add_rmsnorm(resid, d, self.final_norm, cfg.eps)
-        raise RuntimeError("unreachable")
+        md = AttnMeta(kind="decode", slots=meta.slots[:nd], cu_q=meta.cu_q[:nd + 1],
+                      ctx_lens=meta.ctx_lens[:nd], block_tables=meta.block_tables[:nd],
+                      max_q_len=1, max_ctx=meta.max_ctx, decode_ws=meta.decode_ws)
+        mp = AttnMeta(kind="prefill", slots=meta.slots[nd:], cu_q=meta.cu_q_prefill,
+                      ctx_lens=meta.ctx_lens[nd:], block_tables=meta.block_tables[nd:],
+                      max_q_len=meta.max_q_len, max_ctx=meta.max_ctx)
+        aux.wait_stream(main)
+        with torch.cuda.stream(aux):
+            hd = self._stack(resid[:nd], pos[:nd], md, None)
+        sp = None if sample_idx is None else sample_idx[nd:] - nd
+        hp = self._stack(resid[nd:], pos[nd:], mp, sp)
+        main.wait_stream(aux)
+        hd.record_stream(main)
+        resid.record_stream(aux)
+        return torch.cat([hd, hp])
 
     def logits(self, h: torch.Tensor) -> torch.Tensor:
         """fp32 logits over the full vocabulary (vocab-parallel head + all-gather)."""
