@@ -198,10 +198,14 @@ class LLMEngine:
         self._up_ev = None  # marks the last host->device upload of the pinned step buffers
         self._timeline = collections.deque(maxlen=4096)
         self._tok_host = [(hbuf(S), hbuf(S, dtype=torch.float32)) for _ in range(2)]
-        if self.p.tp_size > 1:
+        if self.p.mp_size > 1:
             # followers replay from broadcast host buffers; the device-side id gather of the
-            # pipelined path is not replicated, so TP steps run synchronously
-            self.cfg = cfg = type(cfg)(**{**cfg.__dict__, "async_decode": False})
+            # pipelined path is not replicated, so TP/PP steps run synchronously; pipeline
+            # stages exchange activations with p2p sends, which stay out of hipGraphs
+            over = {"async_decode": False}
+            if self.p.pp_size > 1:
+                over["use_graphs"] = False
+            self.cfg = cfg = type(cfg)(**{**cfg.__dict__, **over})
         if self.gpu and cfg.use_graphs:
             self._capture_graphs()
 
@@ -438,29 +442,30 @@ class LLMEngine:
             pend, self._pending = self._pending, None
             return self._finalize(pend)
 
-    # ------------------------------------------------------------------ tensor parallel
-    # Rank 0 of a TP group drives: it schedules, then broadcasts the step layout (one int32
-    # payload over RCCL) so every rank runs the same forward; the collectives inside the
-    # model (row-parallel all-reduces, vocab all-gather) then line up. Followers loop in
+    # ------------------------------------------------------------------ model parallel
+    # The replica's driver (pipeline stage 0, TP rank 0) schedules, then broadcasts the step
+    # layout (one int32 payload over RCCL) to every rank of the replica (tp x pp) so they
+    # all run the same forward; the collectives inside the model (row-parallel all-reduces,
+    # vocab all-gather, stage-to-stage sends) then line up. Followers loop in
     # run_follower() until the driver broadcasts a stop header.
     @property
     def is_driver(self) -> bool:
-        return self.p.tp_size == 1 or self.p.tp_rank == 0
+        return self.p.mp_size == 1 or (self.p.tp_rank == 0 and self.p.pp_rank == 0)
 
     def _tp_src(self) -> int:
-        return self.p.rank - self.p.tp_rank
+        return self.p.mp_src
 
     def _bcast(self, t: torch.Tensor) -> torch.Tensor:
         import torch.distributed as dist
 
         dev = self.device if self.p.backend == "nccl" else torch.device("cpu")
         x = t.to(dev)
-        dist.broadcast(x, src=self._tp_src(), group=self.p.tp_group)
+        dist.broadcast(x, src=self._tp_src(), group=self.p.mp_group)
         return x
 
     def _sync_step(self, kind: int, n: int, ntok: int, max_q: int, max_ctx: int, bs: int, nd: int = 0) -> None:
-        """Driver: publish the step (header + packed int buffers) to the TP group."""
-        if self.p.tp_size == 1:
+        """Driver: publish the step (header + packed int buffers) to the replica's ranks."""
+        if self.p.mp_size == 1:
             return
         hdr = torch.tensor([kind, n, ntok, max_q, max_ctx, bs, nd, 0], dtype=torch.int64)
         self._bcast(hdr)
@@ -506,7 +511,7 @@ class LLMEngine:
                 self._decode_eager(n)
 
     def stop_followers(self) -> None:
-        if self.p.tp_size > 1 and self.is_driver:
+        if self.p.mp_size > 1 and self.is_driver:
             self._sync_step(-1, 0, 0, 0, 0, 0, 0)
 
     def _emit(self, r: Request, tok: int, lp: float, now: float, appended: bool = False) -> bool:
@@ -616,7 +621,7 @@ class LLMEngine:
         meta = self._meta("prefill", n, ntok, max_q, max_ctx, nd)
         sample_idx = (self.d_cu[1: n + 1] - 1).long()
         h = self.model.forward(self.d_ids[:ntok], self.d_pos[:ntok], meta, sample_idx)
-        return self.model.logits(h)
+        return None if h is None else self.model.logits(h)   # None: a later pipeline stage
 
     def _decode(self, n):
         if self.graphs and not self._needs_penalty(n):
@@ -636,7 +641,7 @@ class LLMEngine:
         self._upload(n, n)
         meta = self._meta("decode", n, n, 1, self.cfg.max_model_len)
         h = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta)
-        return self.model.logits(h)
+        return None if h is None else self.model.logits(h)
 
     def _decode_body(self, bs):
         meta = self._meta("decode", bs, bs, 1, self.cfg.max_model_len)

@@ -61,6 +61,15 @@ class LlamaModel:
         self.ffn = cfg.ffn // tp
         self.vocab_local = cfg.vocab_size // tp
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        # pipeline stage: a contiguous slice of layers; stage 0 also holds the embedding and
+        # the LM head (it samples), the last stage applies the final norm
+        pp, s = self.p.pp_size, self.p.pp_rank
+        if cfg.layers < pp:
+            raise ValueError(f"{cfg.name}: {cfg.layers} layers cannot fill {pp} pipeline stages")
+        self.layer_lo = s * cfg.layers // pp
+        self.layer_hi = (s + 1) * cfg.layers // pp
+        self.first_stage = s == 0
+        self.last_stage = s == pp - 1
         if weights is None:
             self._random_init(seed)
         else:
@@ -74,8 +83,11 @@ class LlamaModel:
     def _random_init(self, seed: int):
         cfg, dev, dt = self.cfg, self.device, self.dtype
         g = torch.Generator(device=dev)
-        g.manual_seed(seed * 1000 + self.p.tp_rank)
         H = cfg.hidden
+
+        def reseed(part: int):
+            # per-part seeds: a layer's weights do not depend on which stage builds it
+            g.manual_seed(seed * 1_000_003 + self.p.tp_rank * 10_007 + part)
 
         def rnd(*shape, std=0.02):
             t = torch.empty(*shape, device=dev, dtype=dt)
@@ -83,9 +95,11 @@ class LlamaModel:
             return t
 
         out_std = 0.02 / math.sqrt(2 * cfg.layers)
-        self.embed = rnd(self.vocab_local, H)
+        reseed(0)
+        self.embed = rnd(self.vocab_local, H) if self.first_stage else None
         self.layers: List[Dict[str, torch.Tensor]] = []
-        for _ in range(cfg.layers):
+        for i in range(self.layer_lo, self.layer_hi):
+            reseed(i + 2)
             self.layers.append({
                 "attn_norm": torch.ones(H, device=dev, dtype=dt),
                 "wqkv": rnd((self.hq + 2 * self.hkv) * self.D, H),
@@ -95,7 +109,8 @@ class LlamaModel:
                 "wd": rnd(H, self.ffn, std=out_std),
             })
         self.final_norm = torch.ones(H, device=dev, dtype=dt)
-        self.lm_head = rnd(self.vocab_local, H)
+        reseed(1)
+        self.lm_head = rnd(self.vocab_local, H) if self.first_stage else None
 
     def _load(self, w: Dict[str, torch.Tensor]):
         """Load HF-named Llama weights (model.layers.N.self_attn.q_proj.weight, ...),
@@ -114,9 +129,9 @@ class LlamaModel:
         def get(name):
             return w[name].to(dev, dt)
 
-        self.embed = rows(get("model.embed_tokens.weight"), 0).contiguous()
+        self.embed = rows(get("model.embed_tokens.weight"), 0).contiguous() if self.first_stage else None
         self.layers = []
-        for i in range(cfg.layers):
+        for i in range(self.layer_lo, self.layer_hi):
             p = f"model.layers.{i}."
             q, k, v = get(p + "self_attn.q_proj.weight"), get(p + "self_attn.k_proj.weight"), get(p + "self_attn.v_proj.weight")
             gt, up = get(p + "mlp.gate_proj.weight"), get(p + "mlp.up_proj.weight")
@@ -129,15 +144,20 @@ class LlamaModel:
                 "wd": cols(get(p + "mlp.down_proj.weight")).contiguous(),
             })
         self.final_norm = get("model.norm.weight")
-        head = w.get("lm_head.weight", w["model.embed_tokens.weight"]).to(dev, dt)
-        self.lm_head = rows(head, 0).contiguous()
+        self.lm_head = None
+        if self.first_stage:
+            head = w.get("lm_head.weight", w["model.embed_tokens.weight"]).to(dev, dt)
+            self.lm_head = rows(head, 0).contiguous()
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
-        """HF-named weights of this rank (unfused; TP shards are local slices)."""
-        out = {"model.embed_tokens.weight": self.embed, "model.norm.weight": self.final_norm,
-               "lm_head.weight": self.lm_head}
+        """HF-named weights of this rank (unfused; TP shards are local slices; a pipeline
+        stage holds only its layers, plus embedding and LM head on stage 0)."""
+        out = {"model.norm.weight": self.final_norm}
+        if self.first_stage:
+            out["model.embed_tokens.weight"] = self.embed
+            out["lm_head.weight"] = self.lm_head
         qd, kd = self.hq * self.D, self.hkv * self.D
-        for i, L in enumerate(self.layers):
+        for i, L in enumerate(self.layers, start=self.layer_lo):
             p = f"model.layers.{i}."
             out[p + "input_layernorm.weight"] = L["attn_norm"]
             out[p + "self_attn.q_proj.weight"] = L["wqkv"][:qd]
@@ -154,15 +174,15 @@ class LlamaModel:
     def allocate_kv_cache(self, num_blocks: int, block_size: int = 64):
         if block_size != 64:
             raise ValueError("the gfx950 attention kernels use 64-token KV pages")
-        shape_k = (self.cfg.layers, num_blocks, self.hkv, block_size, self.D)
-        shape_v = (self.cfg.layers, num_blocks, self.hkv, self.D, block_size)
+        shape_k = (len(self.layers), num_blocks, self.hkv, block_size, self.D)
+        shape_v = (len(self.layers), num_blocks, self.hkv, self.D, block_size)
         # zero-filled: masked keys of a partially filled page must stay finite
         self.k_cache = torch.zeros(shape_k, device=self.device, dtype=self.dtype)
         self.v_cache = torch.zeros(shape_v, device=self.device, dtype=self.dtype)
         return self.k_cache, self.v_cache
 
     def kv_block_bytes(self, block_size: int = 64) -> int:
-        return 2 * self.cfg.layers * self.hkv * self.D * block_size * torch.finfo(self.dtype).bits // 8
+        return 2 * len(self.layers) * self.hkv * self.D * block_size * torch.finfo(self.dtype).bits // 8
 
     # ------------------------------------------------------------------ forward
     def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
@@ -231,10 +251,53 @@ class LlamaModel:
 
     def forward(self, ids: torch.Tensor, pos: torch.Tensor, meta: AttnMeta,
                 sample_idx: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Returns the final-normed hidden rows selected by ``sample_idx`` (all rows if None)."""
+        """Returns the final-normed hidden rows selected by ``sample_idx`` (all rows if None).
+        With pipeline stages only stage 0 gets them (other stages return None)."""
+        if self.p.pp_size > 1:
+            return self._forward_pp(ids, pos, meta, sample_idx)
         if meta.kind == "mixed" and self.split_mixed and ids.is_cuda and self.p.tp_size == 1:
             return self.forward_split(ids, pos, meta, sample_idx)
         return self._stack(self.embed_tokens(ids), pos, meta, sample_idx)
+
+    def _forward_pp(self, ids, pos, meta: AttnMeta, sample_idx):
+        """Layer-split pipeline (SURVEY.md §2.E "PP", CC6): stage s receives the residual
+        stream from stage s-1, runs its layers and sends it on (RCCL p2p over xGMI); the
+        last stage applies the final norm to the sampling rows and returns them to stage 0,
+        which owns the LM head and samples. One step flows through the stages in turn — the
+        reference's HF ``device_map="auto"`` layer placement (examples/multimodal_rag/llm/
+        llm.py:42-47), for models that outgrow one GPU's HBM without a TP group."""
+        import torch.distributed as dist
+
+        cfg, p = self.cfg, self.p
+        T = ids.shape[0]
+        if self.first_stage:
+            resid = self.embed_tokens(ids)
+        else:
+            resid = torch.empty(T, cfg.hidden, dtype=self.dtype, device=self.device)
+            dist.recv(resid, src=p.pp_prev)
+        x = ops.rmsnorm(resid, self.layers[0]["attn_norm"], cfg.eps)
+        n = len(self.layers)
+        for li in range(n):
+            d = self._layer(li, x, resid, pos, meta)
+            if li + 1 < n:
+                x = ops.add_rmsnorm(resid, d, self.layers[li + 1]["attn_norm"], cfg.eps)
+        rows = T if sample_idx is None else int(sample_idx.shape[0])
+        if not self.last_stage:
+            resid.add_(d)
+            dist.send(resid, dst=p.pp_next)
+            h = None
+        else:
+            if sample_idx is not None:
+                r = resid.index_select(0, sample_idx) + d.index_select(0, sample_idx)
+                h = ops.rmsnorm(r.contiguous(), self.final_norm, cfg.eps)
+            else:
+                h = ops.add_rmsnorm(resid, d, self.final_norm, cfg.eps)
+            dist.send(h.contiguous(), dst=p.pp_first_rank)
+            h = None
+        if self.first_stage:
+            h = torch.empty(rows, cfg.hidden, dtype=self.dtype, device=self.device)
+            dist.recv(h, src=p.pp_last_rank)
+        return h
 
     def forward_split(self, ids: torch.Tensor, pos: torch.Tensor, meta: AttnMeta,
                       sample_idx: Optional[torch.Tensor] = None) -> torch.Tensor:

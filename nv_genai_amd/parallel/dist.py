@@ -29,12 +29,41 @@ class ParallelContext:
     dp_size: int = 1
     dp_rank: int = 0
     dp_group: Optional[object] = None
+    pp_size: int = 1
+    pp_rank: int = 0
+    mp_group: Optional[object] = None   # every rank of one model replica (tp x pp)
     backend: str = "none"
     device: torch.device = torch.device("cpu")
 
     @property
     def is_distributed(self) -> bool:
         return self.world_size > 1
+
+    @property
+    def mp_size(self) -> int:
+        return self.tp_size * self.pp_size
+
+    @property
+    def mp_src(self) -> int:
+        """Global rank of the replica's driver (pp stage 0, tp rank 0)."""
+        return self.rank - self.pp_rank * self.tp_size - self.tp_rank
+
+    @property
+    def pp_prev(self) -> int:
+        return self.rank - self.tp_size
+
+    @property
+    def pp_next(self) -> int:
+        return self.rank + self.tp_size
+
+    @property
+    def pp_first_rank(self) -> int:
+        """Global rank of this tp rank's peer on pipeline stage 0."""
+        return self.rank - self.pp_rank * self.tp_size
+
+    @property
+    def pp_last_rank(self) -> int:
+        return self.pp_first_rank + (self.pp_size - 1) * self.tp_size
 
 
 _CTX = ParallelContext()
@@ -50,11 +79,14 @@ def env_world() -> tuple:
 
 
 def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
-                     device: Optional[str] = None, timeout_s: int = 600) -> ParallelContext:
-    """Initialise the default group from torchrun env vars and build TP/DP subgroups.
+                     device: Optional[str] = None, timeout_s: int = 600,
+                     pp_size: int = 1) -> ParallelContext:
+    """Initialise the default group from torchrun env vars and build TP/PP/DP subgroups.
 
-    Ranks are laid out TP-major inside a node: ranks [0..tp) form TP group 0, etc., so a TP
-    group's all-reduces stay on directly-linked xGMI peers.
+    Ranks are laid out TP-major, then pipeline stage, then replica:
+    ``rank = dp_rank * (tp * pp) + pp_rank * tp + tp_rank``. A TP group's all-reduces stay
+    on directly-linked xGMI peers; pipeline stage s sends activations to the same tp rank of
+    stage s + 1 (``rank + tp``); a replica's tp x pp ranks form its model-parallel group.
     """
     global _CTX
     world, rank, local = env_world()
@@ -72,24 +104,33 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
             kw["device_id"] = dev
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
-    if world % tp_size != 0:
-        raise ValueError(f"world size {world} not divisible by tp {tp_size}")
-    dp = world // tp_size
-    tp_group = dp_group = None
+    mp = tp_size * pp_size
+    if world % mp != 0:
+        raise ValueError(f"world size {world} not divisible by tp {tp_size} x pp {pp_size}")
+    dp = world // mp
+    tp_group = dp_group = mp_group = None
     if world > 1:
+        # new_group is collective over the default group: every rank creates every group
         for d in range(dp):
-            ranks = list(range(d * tp_size, (d + 1) * tp_size))
-            g = dist.new_group(ranks) if tp_size > 1 else None
+            for s_ in range(pp_size):
+                ranks = [d * mp + s_ * tp_size + t for t in range(tp_size)]
+                g = dist.new_group(ranks) if tp_size > 1 else None
+                if rank in ranks:
+                    tp_group = g
+        for d in range(dp):
+            ranks = list(range(d * mp, (d + 1) * mp))
+            g = dist.new_group(ranks) if mp > 1 else None
             if rank in ranks:
-                tp_group = g
-        for t in range(tp_size):
-            ranks = list(range(t, world, tp_size))
+                mp_group = g
+        for j in range(mp):
+            ranks = list(range(j, world, mp))
             g = dist.new_group(ranks) if dp > 1 else None
             if rank in ranks:
                 dp_group = g
     _CTX = ParallelContext(world_size=world, rank=rank, local_rank=local, tp_size=tp_size,
                            tp_rank=rank % tp_size, tp_group=tp_group, dp_size=dp,
-                           dp_rank=rank // tp_size, dp_group=dp_group,
+                           dp_rank=rank // mp, dp_group=dp_group, pp_size=pp_size,
+                           pp_rank=(rank % mp) // tp_size, mp_group=mp_group,
                            backend=backend if world > 1 else "none", device=dev)
     if tp_size > 1 and backend == "nccl" and use_gpu:
         # IPC custom all-reduce for the TP group's small decode messages (RCCL otherwise)

@@ -1,4 +1,4 @@
-"""Tensor-parallel model server (Llama-3-70B on 8 x MI355X; SURVEY.md §2.E "TP", §7.2 step 7).
+"""Model-parallel model server (Llama-3-70B on 8 x MI355X; SURVEY.md §2.E "TP"/"PP", §7.2 step 7).
 
 Launched with one process per GPU::
 
@@ -11,6 +11,10 @@ of each TP group runs the HTTP front end and the scheduler and broadcasts each s
 the other ranks execute the same forward in :meth:`LLMEngine.run_follower`, and the
 row-parallel all-reduces / vocab all-gather run over RCCL on xGMI. With ``world > tp`` the
 TP groups are data-parallel replicas, each serving on ``port + replica``.
+
+``--pp`` splits the layers into pipeline stages (each stage optionally TP inside): stage 0
+holds the embedding + LM head and drives, activations flow stage to stage over RCCL p2p —
+for models that do not fit one TP group's HBM, e.g. ``--tp 4 --pp 2``.
 """
 from __future__ import annotations
 
@@ -23,6 +27,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--llm", default="llama3-70b")
     ap.add_argument("--tp", type=int, default=8)
+    ap.add_argument("--pp", type=int, default=1, help="pipeline stages (layer split)")
     ap.add_argument("--embed", default="", help="encoder preset served by rank 0 of each replica")
     ap.add_argument("--weights", default="")
     ap.add_argument("--host", default="0.0.0.0")
@@ -36,7 +41,7 @@ def main(argv=None):
     from ..engine.llm_engine import EngineConfig, LLMEngine
     from ..parallel import dist as pd
 
-    pctx = pd.init_distributed(tp_size=args.tp)
+    pctx = pd.init_distributed(tp_size=args.tp, pp_size=args.pp)
     weights = None
     if args.weights:
         from ..utils.checkpoint import load_weights

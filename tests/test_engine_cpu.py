@@ -59,9 +59,11 @@ def test_stop_token_and_length(model):
     e = _engine(model)
     p = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True)
     out = e.generate([PROMPTS[2]], p)[0]
-    tok = out.output_ids[2]
+    # stop on the first token that did not already occur earlier in the greedy output
+    k = next(i for i in range(1, 10) if out.output_ids[i] not in out.output_ids[:i])
+    tok = out.output_ids[k]
     r = e.generate([PROMPTS[2]], SamplingParams(temperature=0.0, max_tokens=10, stop_token_ids=[tok]))[0]
-    assert r.finish_reason == "stop" and r.output_ids[-1] == tok and len(r.output_ids) == 3
+    assert r.finish_reason == "stop" and r.output_ids[-1] == tok and len(r.output_ids) == k + 1
     assert out.finish_reason == "length" and len(out.output_ids) == 10
 
 
