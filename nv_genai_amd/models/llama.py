@@ -84,16 +84,21 @@ class LlamaModel:
         cfg, dev, dt = self.cfg, self.device, self.dtype
         g = torch.Generator(device=dev)
         H = cfg.hidden
+        staged = self.p.pp_size > 1
 
         def reseed(part: int):
-            # per-part seeds: a layer's weights do not depend on which stage builds it
-            g.manual_seed(seed * 1_000_003 + self.p.tp_rank * 10_007 + part)
+            # pipeline stages: per-part seeds, so a layer's weights do not depend on which
+            # stage builds it. One stage: one sequential stream (the weights every earlier
+            # measurement in profiles/ used)
+            if staged:
+                g.manual_seed(seed * 1_000_003 + self.p.tp_rank * 10_007 + part)
 
         def rnd(*shape, std=0.02):
             t = torch.empty(*shape, device=dev, dtype=dt)
             t.normal_(0.0, std, generator=g)
             return t
 
+        g.manual_seed(seed * 1000 + self.p.tp_rank)
         out_std = 0.02 / math.sqrt(2 * cfg.layers)
         reseed(0)
         self.embed = rnd(self.vocab_local, H) if self.first_stage else None

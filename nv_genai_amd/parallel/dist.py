@@ -132,7 +132,7 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
                            dp_rank=rank // mp, dp_group=dp_group, pp_size=pp_size,
                            pp_rank=(rank % mp) // tp_size, mp_group=mp_group,
                            backend=backend if world > 1 else "none", device=dev)
-    if tp_size > 1 and backend == "nccl" and use_gpu:
+    if tp_size > 1 and use_gpu:
         # IPC custom all-reduce for the TP group's small decode messages (RCCL otherwise)
         from .comm import register_custom_all_reduce
         from .custom_ar import maybe_create
@@ -159,9 +159,12 @@ def tp_all_gather(x: torch.Tensor, dim: int = -1, ctx: Optional[ParallelContext]
     ctx = ctx or _CTX
     if ctx.tp_size == 1:
         return x
-    parts = [torch.empty_like(x) for _ in range(ctx.tp_size)]
-    dist.all_gather(parts, x.contiguous(), group=ctx.tp_group)
-    return torch.cat(parts, dim=dim)
+    y = x.contiguous()
+    if ctx.backend == "gloo" and y.is_cuda:   # gloo gathers host tensors
+        y = y.cpu()
+    parts = [torch.empty_like(y) for _ in range(ctx.tp_size)]
+    dist.all_gather(parts, y, group=ctx.tp_group)
+    return torch.cat(parts, dim=dim).to(x.device)
 
 
 def barrier():

@@ -1,0 +1,101 @@
+"""Tensor-parallel Llama on the GPU box: two TP ranks share the box's one MI355X, their
+row-parallel all-reduces go through the IPC custom all-reduce (csrc/kernels/custom_ar.hip),
+and step broadcasts / the vocab all-gather go over gloo (RCCL refuses two ranks on one
+device). The TP=2 prefill logits must match a single-process model with the same weights,
+and the TP engine must generate through the custom all-reduce without falling back."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    res = {"rank": rank}
+    try:
+        from nv_genai_amd.engine.llm_engine import EngineConfig, LLMEngine, SamplingParams
+        from nv_genai_amd.models.config import llama_config
+        from nv_genai_amd.models.llama import AttnMeta, LlamaModel
+        from nv_genai_amd.parallel import comm
+        from nv_genai_amd.parallel import dist as pd
+
+        cfg = llama_config("llama-small")
+        full = LlamaModel(cfg, "cpu", dtype=torch.bfloat16, pctx=pd.ParallelContext(), seed=5).state_dict()
+        full["lm_head.weight"] = full["lm_head.weight"] * 40.0  # peaky logits (as test_engine_gpu)
+        pctx = pd.init_distributed(tp_size=2, backend="gloo", device="cuda")
+        car = comm.custom_all_reduce_for(pctx.tp_group)
+        res["custom_ar"] = car is not None and car.enabled
+        dev = torch.device("cuda", 0)
+        ecfg = EngineConfig(model="llama-small", max_num_seqs=4, max_batched_tokens=1024, max_model_len=1024,
+                            kv_cache_blocks=64, use_graphs=False)
+        eng = LLMEngine(ecfg, device="cuda", pctx=pctx, weights=full)
+        # 1) prefill logits of one 200-token prompt through the TP model (every rank runs it)
+        T = 200
+        ids = torch.arange(10, 10 + T, dtype=torch.int32, device=dev)
+        pos = torch.arange(T, dtype=torch.int32, device=dev)
+        bt = torch.arange(4, dtype=torch.int32, device=dev).view(1, 4)
+        meta = AttnMeta(kind="prefill", slots=torch.arange(T, dtype=torch.int32, device=dev),
+                        cu_q=torch.tensor([0, T], dtype=torch.int32, device=dev),
+                        ctx_lens=torch.tensor([T], dtype=torch.int32, device=dev), block_tables=bt,
+                        max_q_len=T, max_ctx=T)
+        lg = eng.model.logits(eng.model.forward(ids, pos, meta)).float()
+        if rank == 0:
+            single = LlamaModel(cfg, dev, pctx=pd.ParallelContext(), weights=full)
+            single.allocate_kv_cache(8)
+            ref = single.logits(single.forward(ids, pos, meta)).float()
+            res["max_abs_diff"] = float((lg - ref).abs().max())
+            res["ref_abs_max"] = float(ref.abs().max())
+            res["argmax_agree"] = float((lg.argmax(-1) == ref.argmax(-1)).float().mean())
+            del single
+        # 2) the TP engine generates (driver + follower) through the custom all-reduce
+        if eng.is_driver:
+            out = eng.generate([[5, 6, 7, 8] * 30, [9, 10, 11] * 20],
+                               SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True))
+            eng.stop_followers()
+            res["gen_lens"] = [len(r.output_ids) for r in out]
+        else:
+            eng.run_follower()
+        torch.cuda.synchronize()
+        res["ar_error"] = car.error() if car is not None else -1
+        pd.destroy()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        res["exc"] = traceback.format_exc()[-3000:]
+    q.put(res)
+
+
+def test_tp2_on_one_gpu_with_custom_all_reduce():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = sorted([q.get(timeout=200) for _ in range(2)], key=lambda r: r["rank"])
+    for p in procs:
+        p.join(timeout=60)
+    print(results)
+    for r in results:
+        assert "exc" not in r, r["exc"]
+        assert r["custom_ar"], r
+        assert r["ar_error"] == 0, r
+    r0 = results[0]
+    assert r0["gen_lens"] == [8, 8]
+    assert r0["max_abs_diff"] <= 0.05 * r0["ref_abs_max"] + 0.05, r0
+    assert r0["argmax_agree"] >= 0.9, r0
