@@ -1,5 +1,6 @@
 """Micro-benchmarks of the hand-written hot kernels at serving shapes (Llama-3-8B):
-prefill attention (paged, causal, GQA 32/8, D=128), decode attention, sampling."""
+prefill attention (paged, causal, GQA 32/8, D=128), decode attention, sampling, and the
+1M x 1024 flat-index search (MFMA scoring + radix top-k)."""
 import json
 import os
 import sys
@@ -41,7 +42,7 @@ def main():
     import argparse
 
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="", help="prefill | decode | sample (default: all)")
+    ap.add_argument("--only", default="", help="prefill | decode | sample | search (default: all)")
     ap.add_argument("--iters", type=int, default=20)
     args = ap.parse_args()
     global timeit
@@ -50,6 +51,19 @@ def main():
     dev = "cuda"
     Hq, Hkv, D = 32, 8, 128
     out = {}
+    if args.only in ("", "search"):
+        N, Dx = 1_000_000, 1024
+        X = torch.nn.functional.normalize(torch.randn(N, Dx, device=dev), dim=1).to(torch.bfloat16)
+        for nq in (1, 8, 64):
+            Q = torch.nn.functional.normalize(torch.randn(nq, Dx, device=dev), dim=1).to(torch.bfloat16)
+            us = timeit(lambda: ops.score(Q, X, None, 1.0))
+            us_all = timeit(lambda: ops.topk(ops.score(Q, X, None, 1.0), 4))
+            out[f"search_1Mx1024_q{nq}"] = {"score_us": round(us, 1), "score_TBps": round(N * Dx * 2 / us / 1e6, 2),
+                                             "score_topk_us": round(us_all, 1)}
+        del X
+        if args.only == "search":
+            print(json.dumps(out))
+            return
     for name, lens in (("prefill_1x1196", [1196]), ("prefill_27x1200", [1200] * 27)):
         if args.only and args.only != "prefill":
             break

@@ -29,7 +29,10 @@ __global__ void __launch_bounds__(256) score_kernel(const uint16_t* __restrict__
                                                     int D, const float* __restrict__ row_bias,
                                                     float q_bias_scale, float* __restrict__ S,
                                                     float dot_scale) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t q_s[];  // [SC_QT][D], swizzled chunks
+  // [16 * ngrp][D] query rows, swizzled 16-B chunks; sized by the launch to the queries
+  // actually present (a 1024-d batch of 8 queries stages 32 KB, not 64 x 2 KB), so several
+  // blocks share a CU and keep enough X loads in flight to stream HBM
+  extern __shared__ __attribute__((aligned(16))) uint16_t q_s[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int col = lane & 15, h = lane >> 4;
   const int q0 = blockIdx.y * SC_QT;
@@ -37,7 +40,7 @@ __global__ void __launch_bounds__(256) score_kernel(const uint16_t* __restrict__
   const int ngrp = (nql + 15) / 16;
   const int nch = D / 8;
 
-  for (int c = tid; c < SC_QT * nch; c += 256) {
+  for (int c = tid; c < 16 * ngrp * nch; c += 256) {
     const int r = c / nch, ch = c % nch;
     u16x8 v = (u16x8)(0);
     if (r < nql) v = load8(Q + (int64_t)(q0 + r) * D + ch * 8);
@@ -45,7 +48,11 @@ __global__ void __launch_bounds__(256) score_kernel(const uint16_t* __restrict__
   }
   __syncthreads();
 
-  const int64_t row_base = (int64_t)blockIdx.x * SC_ROWS + w * 32;
+  // blocks stride over 128-row tiles of X, so the query staging above is paid once per
+  // block rather than once per tile
+  const int64_t ntiles = (N + SC_ROWS - 1) / SC_ROWS;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  const int64_t row_base = tile * SC_ROWS + w * 32;
   int64_t r0 = row_base + col, r1 = row_base + 16 + col;
   if (r0 >= N) r0 = N - 1;
   if (r1 >= N) r1 = N - 1;
@@ -126,6 +133,7 @@ __global__ void __launch_bounds__(256) score_kernel(const uint16_t* __restrict__
       }
     }
   }
+  }  // tile loop
 }
 
 // ---------------------------------------------------------------- top-k selection
@@ -275,8 +283,12 @@ __global__ void __launch_bounds__(TK_NT) topk_select_kernel(
 void launch_score(const uint16_t* Q, int nq, const uint16_t* X, int64_t N, int D,
                   const float* row_bias, float* S, float dot_scale, hipStream_t stream) {
   if (nq == 0 || N == 0) return;
-  dim3 grid((unsigned)((N + SC_ROWS - 1) / SC_ROWS), (nq + SC_QT - 1) / SC_QT);
-  const size_t lds = (size_t)SC_QT * D * sizeof(uint16_t);
+  const int64_t ntiles = (N + SC_ROWS - 1) / SC_ROWS;
+  // ~4 resident blocks per CU on 256 CUs; each strides over ntiles / grid tiles
+  const int64_t gx = ntiles < 1024 ? ntiles : 1024;
+  dim3 grid((unsigned)gx, (nq + SC_QT - 1) / SC_QT);
+  const int qrows = nq >= SC_QT ? SC_QT : ((nq + 15) / 16) * 16;
+  const size_t lds = (size_t)qrows * D * sizeof(uint16_t);
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)score_kernel,
