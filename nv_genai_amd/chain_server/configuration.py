@@ -115,6 +115,8 @@ class EngineConfigSection(ConfigWizard):
                                    help_txt="Directory of safetensors weights ('' = random init)")
     tp_size: int = configfield("tp_size", default=1, help_txt="Tensor-parallel degree of the LLM")
     pp_size: int = configfield("pp_size", default=1, help_txt="Pipeline stages of the LLM (layer split)")
+    sequence_parallel: bool = configfield("sequence_parallel", default=False,
+                                          help_txt="Sequence-parallel TP prefill (reduce-scatter/all-gather)")
     kv_cache_fraction: float = configfield("kv_cache_fraction", default=0.3,
                                            help_txt="Fraction of free HBM given to the paged KV cache")
     max_num_seqs: int = configfield("max_num_seqs", default=256, help_txt="Max concurrent sequences")

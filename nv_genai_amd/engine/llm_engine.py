@@ -103,6 +103,8 @@ class EngineConfig:
     mixed_min_tokens: int = 0     # accumulate this many prompt tokens before a mixed step ...
     mixed_max_wait: int = 4       # ... unless the oldest waiting request waited this many steps
     tuned_gemms: bool = True   # load the per-shape hipBLASLt/rocBLAS table (ops/gemm_tuning.py)
+    sequence_parallel: bool = False  # TP prefill >= sp_min_tokens: reduce-scatter/all-gather
+    sp_min_tokens: int = 512
 
 
 _INERT = Request(id=-1, prompt_ids=[0], params=SamplingParams(temperature=0.0))
@@ -122,6 +124,8 @@ class LLMEngine:
         self.mcfg = model_cfg or llama_config(cfg.model, max_position=max(cfg.max_model_len, 256))
         self.model = model or LlamaModel(self.mcfg, self.device, pctx=self.p, seed=cfg.seed,
                                          weights=weights)
+        self.model.sequence_parallel = cfg.sequence_parallel
+        self.model.sp_min_tokens = cfg.sp_min_tokens
         self.tok = tokenizer or llm_tokenizer()
         self.stop_ids = set(self.tok.stop_ids) | set(self.mcfg.eos_ids)
         self.gpu = self.device.type == "cuda"

@@ -24,7 +24,8 @@ from typing import Dict, List, Optional
 import torch
 
 from .. import ops
-from ..parallel.dist import ParallelContext, get_context, tp_all_gather, tp_all_reduce
+from ..parallel.dist import (ParallelContext, get_context, tp_all_gather, tp_all_gather_rows,
+                             tp_all_reduce, tp_reduce_scatter_rows)
 from .config import LlamaConfig
 
 
@@ -78,6 +79,11 @@ class LlamaModel:
                                         cfg.rope_scaling).to(self.device)
         self.split_mixed = False   # mixed steps on two streams (forward_split)
         self._aux = None
+        # sequence parallelism for TP prefill: norms and residual on T / tp rows, reduce-
+        # scatter + all-gather instead of all-reduce (SURVEY.md §2.E "SP", §5.7)
+        self.sequence_parallel = False
+        self.sp_min_tokens = 512
+        self.sp_steps = 0
 
     # ------------------------------------------------------------------ weights
     def _random_init(self, seed: int):
@@ -260,9 +266,58 @@ class LlamaModel:
         With pipeline stages only stage 0 gets them (other stages return None)."""
         if self.p.pp_size > 1:
             return self._forward_pp(ids, pos, meta, sample_idx)
+        if (self.sequence_parallel and self.p.tp_size > 1 and meta.kind == "prefill"
+                and ids.shape[0] >= self.sp_min_tokens):
+            return self._forward_sp(ids, pos, meta, sample_idx)
         if meta.kind == "mixed" and self.split_mixed and ids.is_cuda and self.p.tp_size == 1:
             return self.forward_split(ids, pos, meta, sample_idx)
         return self._stack(self.embed_tokens(ids), pos, meta, sample_idx)
+
+    def _forward_sp(self, ids, pos, meta: AttnMeta, sample_idx):
+        """Megatron-style sequence parallelism inside the TP group for long prefills: the
+        residual stream and both RMSNorms live on this rank's T / tp rows; each column-
+        parallel GEMM is preceded by an all-gather of the normed rows and each row-parallel
+        GEMM followed by a reduce-scatter, which together move the bytes of the all-reduce
+        they replace while the norm/residual work and activation memory drop by tp x.
+        Rows are padded to a multiple of tp (padding rows write no KV: slot -1)."""
+        cfg, p = self.cfg, self.p
+        tp, r = p.tp_size, p.tp_rank
+        self.sp_steps += 1
+        T = ids.shape[0]
+        Tp = -(-T // tp) * tp
+        if Tp != T:
+            pad = Tp - T
+            ids = torch.cat([ids, ids.new_zeros(pad)])
+            pos = torch.cat([pos, pos.new_zeros(pad)])
+            slots = torch.cat([meta.slots, meta.slots.new_full((pad,), -1)])
+            meta = AttnMeta(kind=meta.kind, slots=slots, cu_q=meta.cu_q, ctx_lens=meta.ctx_lens,
+                            block_tables=meta.block_tables, max_q_len=meta.max_q_len,
+                            max_ctx=meta.max_ctx, decode_ws=meta.decode_ws)
+        rows = Tp // tp
+        # vocab-parallel embedding: partial rows, reduce-scattered straight into the shard
+        lo = r * self.vocab_local
+        local = ids.long() - lo
+        ok = (local >= 0) & (local < self.vocab_local)
+        h = torch.nn.functional.embedding(local.clamp(0, self.vocab_local - 1), self.embed)
+        resid = tp_reduce_scatter_rows(h * ok.unsqueeze(-1).to(h.dtype), p).contiguous()
+        x = ops.rmsnorm(resid, self.layers[0]["attn_norm"], cfg.eps)
+        n = len(self.layers)
+        d = None
+        for li in range(n):
+            L = self.layers[li]
+            xf = tp_all_gather_rows(x, p)
+            qkv = xf @ L["wqkv"].t()
+            ops.rope_cache_(qkv, pos, self.cos_sin, meta.slots, self.k_cache[li],
+                            self.v_cache[li], self.hq, self.hkv, self.D)
+            attn = self._attention(qkv[:, :self.hq * self.D], qkv, li, meta, Tp)
+            o = tp_reduce_scatter_rows(attn @ L["wo"].t(), p).contiguous()
+            x = ops.add_rmsnorm(resid, o, L["mlp_norm"], cfg.eps)
+            hmid = ops.silu_mul(tp_all_gather_rows(x, p) @ L["wgu"].t())
+            d = tp_reduce_scatter_rows(hmid @ L["wd"].t(), p).contiguous()
+            if li + 1 < n:
+                x = ops.add_rmsnorm(resid, d, self.layers[li + 1]["attn_norm"], cfg.eps)
+        out = tp_all_gather_rows(ops.add_rmsnorm(resid, d, self.final_norm, cfg.eps), p)[:T]
+        return out if sample_idx is None else out.index_select(0, sample_idx)
 
     def _forward_pp(self, ids, pos, meta: AttnMeta, sample_idx):
         """Layer-split pipeline (SURVEY.md §2.E "PP", CC6): stage s receives the residual

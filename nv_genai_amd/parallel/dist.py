@@ -167,6 +167,37 @@ def tp_all_gather(x: torch.Tensor, dim: int = -1, ctx: Optional[ParallelContext]
     return torch.cat(parts, dim=dim).to(x.device)
 
 
+def tp_reduce_scatter_rows(x: torch.Tensor, ctx: Optional[ParallelContext] = None) -> torch.Tensor:
+    """Sum of ``x`` [T, H] over the TP group, keeping only this rank's T / tp rows
+    (sequence parallelism: replaces the all-reduce after a row-parallel GEMM)."""
+    ctx = ctx or _CTX
+    tp = ctx.tp_size
+    if tp == 1:
+        return x
+    rows = x.shape[0] // tp
+    if ctx.backend == "nccl":
+        out = torch.empty(rows, *x.shape[1:], dtype=x.dtype, device=x.device)
+        dist.reduce_scatter_tensor(out, x.contiguous(), group=ctx.tp_group)
+        return out
+    # gloo has no reduce-scatter: all-reduce on the host, keep our slice
+    y = x.contiguous().cpu() if x.is_cuda else x.contiguous().clone()
+    dist.all_reduce(y, group=ctx.tp_group)
+    return y[ctx.tp_rank * rows:(ctx.tp_rank + 1) * rows].to(x.device)
+
+
+def tp_all_gather_rows(x: torch.Tensor, ctx: Optional[ParallelContext] = None) -> torch.Tensor:
+    """Concatenate every TP rank's row shard [T / tp, H] into [T, H] (rank order)."""
+    ctx = ctx or _CTX
+    tp = ctx.tp_size
+    if tp == 1:
+        return x
+    if ctx.backend == "nccl":
+        out = torch.empty(x.shape[0] * tp, *x.shape[1:], dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, x.contiguous(), group=ctx.tp_group)
+        return out
+    return tp_all_gather(x, dim=0, ctx=ctx)
+
+
 def barrier():
     if dist.is_initialized():
         if _CTX.backend == "nccl":

@@ -28,6 +28,7 @@ def main(argv=None):
     ap.add_argument("--llm", default="llama3-70b")
     ap.add_argument("--tp", type=int, default=8)
     ap.add_argument("--pp", type=int, default=1, help="pipeline stages (layer split)")
+    ap.add_argument("--sequence-parallel", action="store_true", help="SP for long TP prefills")
     ap.add_argument("--embed", default="", help="encoder preset served by rank 0 of each replica")
     ap.add_argument("--weights", default="")
     ap.add_argument("--host", default="0.0.0.0")
@@ -48,7 +49,8 @@ def main(argv=None):
 
         weights = load_weights(args.weights)
     eng = LLMEngine(EngineConfig(model=args.llm, max_num_seqs=args.max_num_seqs, max_model_len=args.max_model_len,
-                                 kv_cache_fraction=args.kv_cache_fraction), pctx=pctx, weights=weights)
+                                 kv_cache_fraction=args.kv_cache_fraction,
+                                 sequence_parallel=args.sequence_parallel), pctx=pctx, weights=weights)
     if not eng.is_driver:
         eng.run_follower()
         pd.destroy()

@@ -16,7 +16,7 @@ def _free_port():
     return p
 
 
-def _tp_worker(rank, world, port, q, tp=2, pp=1):
+def _tp_worker(rank, world, port, q, tp=2, pp=1, sp=False):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
@@ -29,7 +29,7 @@ def _tp_worker(rank, world, port, q, tp=2, pp=1):
     cfg = llama_config("llama-tiny")
     full = LlamaModel(cfg, "cpu", pctx=single, seed=7).state_dict()
     ecfg = EngineConfig(model="llama-tiny", max_num_seqs=4, max_batched_tokens=256, max_model_len=512,
-                        kv_cache_blocks=32)
+                        kv_cache_blocks=32, sequence_parallel=sp, sp_min_tokens=16)
     prompts = [[5, 6, 7, 8] * 20, [9, 10, 11] * 11]
     params = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
     # fp32: a TP shard sums its partial products in a different order than one device, and
@@ -45,7 +45,7 @@ def _tp_worker(rank, world, port, q, tp=2, pp=1):
     if eng.is_driver:
         out = [r.output_ids for r in eng.generate(prompts, params)]
         eng.stop_followers()
-        q.put((out, ref, eng.model.layer_lo, eng.model.layer_hi))
+        q.put((out, ref, eng.model.layer_lo, eng.model.layer_hi, eng.model.sp_steps))
     else:
         eng.run_follower()
     pd.destroy()
@@ -58,10 +58,26 @@ def test_tensor_parallel_matches_single():
     procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out, ref, _, _ = q.get(timeout=300)
+    out, ref, _, _, _ = q.get(timeout=300)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    assert out == ref
+
+
+def test_sequence_parallel_tp_matches_single():
+    """TP=2 with sequence-parallel prefill (odd token counts exercise the row padding)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q, 2, 1, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out, ref, _, _, sp_steps = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sp_steps >= 1
     assert out == ref
 
 
@@ -75,7 +91,7 @@ def test_pipeline_parallel_matches_single(tp, pp):
     procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q, tp, pp)) for r in range(world)]
     for p in procs:
         p.start()
-    out, ref, lo, hi = q.get(timeout=300)
+    out, ref, lo, hi, _ = q.get(timeout=300)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
