@@ -145,3 +145,31 @@ def test_tracing_traceparent_propagation():
     assert names["POST /generate"].trace_id == names["predict"].trace_id
     assert names["POST /generate"].parent_id == names["predict"].span_id
     assert names["retriever"].parent_id == names["POST /generate"].span_id
+
+
+def test_reference_style_vector_clients():
+    """MilvusVectorClient / QdrantVectorClient contract (experimental/multimodal_assistant/
+    retriever/vector.py) over the in-HBM indices."""
+    import torch
+
+    from nv_genai_amd.index.clients import MilvusStyleClient, QdrantStyleClient, drop_collection
+    from nv_genai_amd.index.vectorstore import Document
+
+    g = torch.Generator().manual_seed(0)
+    docs = [Document(f"content {i}", {"source": f"file{i}.pdf", "page_num": i}) for i in range(300)]
+    emb = torch.randn(300, 32, generator=g)
+    for cls, first in ((MilvusStyleClient, 0), (QdrantStyleClient, 1)):
+        name = f"test_{cls.__name__}"
+        drop_collection(name)
+        c = cls(collection_name=name, embedding_size=32, device="cpu")
+        c.update(docs, emb.tolist(), name)
+        text, sources = c.search(emb[17].tolist(), limit=3)
+        assert text.startswith(f"[[DOCUMENT {first}]]\n\ncontent 17\n\n")
+        assert "file17.pdf" in sources and sources["file17.pdf"]["doc_metadata"]["page_num"] == 17
+        assert len(sources) == 3
+    q = QdrantStyleClient(collection_name="test_QdrantStyleClient", embedding_size=32, device="cpu")
+    q.update(docs[:10], emb[:10].tolist(), "test_QdrantStyleClient")  # upsert: same ids replaced
+    assert len(q._col().index) == 300
+    m = MilvusStyleClient(collection_name="test_MilvusStyleClient", embedding_size=32, device="cpu")
+    m.update(docs[:10], emb[:10].tolist(), "test_MilvusStyleClient")  # insert: appended
+    assert len(m._col().payloads) == 310
