@@ -351,6 +351,16 @@ struct CustomAR {
     impl->run(inp.data_ptr(), out.data_ptr(), bytes, inp.scalar_type() == at::kBFloat16, (int)algo,
               cur_stream(inp));
   }
+  // resid += all_reduce(inp); out = rmsnorm(resid) * w   (bf16 [rows, H])
+  void all_reduce_add_rmsnorm(Tensor inp, Tensor resid, Tensor w, Tensor out, double eps) {
+    CHECK_BF16(inp); CHECK_BF16(resid); CHECK_BF16(w); CHECK_BF16(out);
+    CHECK_CONTIG(inp); CHECK_CONTIG(resid); CHECK_CONTIG(w); CHECK_CONTIG(out);
+    TORCH_CHECK(inp.dim() == 2 && resid.sizes() == inp.sizes() && out.sizes() == inp.sizes(),
+                "all_reduce_add_rmsnorm: inp/resid/out must be the same [rows, H]");
+    TORCH_CHECK(w.numel() == inp.size(1), "all_reduce_add_rmsnorm: weight must have H entries");
+    impl->run_add_rmsnorm(inp.data_ptr(), bfp(resid), bfp(w), bfp(out), (int)inp.size(0), (int)inp.size(1),
+                          (float)eps, cur_stream(inp));
+  }
   int64_t error() const { return impl->error(); }
   int64_t capacity() const { return impl->capacity(); }
   void set_two_shot_threshold(int64_t b) { impl->set_two_shot_threshold(b); }
@@ -383,6 +393,7 @@ PYBIND11_MODULE(_C, m) {
       .def("handle", &CustomAR::handle)
       .def("open", &CustomAR::open)
       .def("all_reduce", &CustomAR::all_reduce, py::arg("inp"), py::arg("out"), py::arg("algo") = 0)
+      .def("all_reduce_add_rmsnorm", &CustomAR::all_reduce_add_rmsnorm)
       .def("error", &CustomAR::error)
       .def("capacity", &CustomAR::capacity)
       .def("set_two_shot_threshold", &CustomAR::set_two_shot_threshold);

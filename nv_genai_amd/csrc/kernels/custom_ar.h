@@ -27,6 +27,9 @@ class CustomAllReduce {
   // out = sum over ranks of in (bf16 or fp32, `bytes` a multiple of 16). algo: 0 = pick by
   // size, 1 = one-shot, 2 = two-shot. Capture-safe: no allocation, no host sync.
   void run(const void* in, void* out, int64_t bytes, bool is_bf16, int algo, hipStream_t stream);
+  // resid += sum over ranks of in; out = rmsnorm(resid) * w (bf16 [rows, H], one-shot).
+  void run_add_rmsnorm(const void* in, uint16_t* resid, const uint16_t* w, uint16_t* out, int rows, int H,
+                       float eps, hipStream_t stream);
   // Sticky barrier-timeout flag (synchronous read; call outside graph capture).
   int error() const;
 

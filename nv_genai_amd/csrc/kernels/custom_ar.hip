@@ -220,6 +220,69 @@ __global__ __launch_bounds__(kThreads) void ar_two_shot(ArArgs a) {
   end_call(a, flag, ok);
 }
 
+// Fused TP epilogue: resid += all_reduce(in); out = rmsnorm(resid) * w  (one-shot, bf16).
+// The row-parallel GEMM output is summed over the ranks, added to the residual stream and
+// normalised for the next GEMM in one pass: the sum never round-trips through HBM and the
+// separate add+RMSNorm launch disappears. Rounding matches the unfused path (sum -> bf16,
+// resid + sum -> bf16, norm of the stored residual). Block b owns rows b, b + G, ...
+constexpr int kNormMaxVec = 4;  // packets per thread: H <= 4 * 512 * 8 = 16384
+
+__global__ __launch_bounds__(kThreads) void ar_add_rmsnorm(ArArgs a, uint16_t* __restrict__ resid,
+                                                           const uint16_t* __restrict__ w,
+                                                           uint16_t* __restrict__ out, int rows, int H,
+                                                           float eps) {
+  uint32_t flag;
+  if (!begin_call(a, flag)) return;
+  const uint32_t par = flag & 1u;
+  const int hv = H / 8;
+  const uint4* in = reinterpret_cast<const uint4*>(a.in);
+  uint4* mine = stage_of(a, a.rank, par);
+  for (int row = blockIdx.x; row < rows; row += gridDim.x)
+    for (int p = threadIdx.x; p < hv; p += kThreads) mine[(int64_t)row * hv + p] = in[(int64_t)row * hv + p];
+  bool ok = block_barrier(a, offsetof(Signal, start), flag);
+  __shared__ float red[kThreads / 64];
+  if (ok) {
+    for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+      float x[kNormMaxVec][8];
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < kNormMaxVec; ++j) {
+        const int p = threadIdx.x + j * kThreads;
+        if (p < hv) {
+          const int64_t e = (int64_t)row * hv + p;
+          float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          for (int r = 0; r < a.world; ++r) acc_packet(acc, stage_of(a, r, par)[e], 1);
+          u16x8 rv = load8(resid + e * 8);
+          u16x8 sv;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float o = bf2f(f2bf(acc[i]));          // the all-reduced value, as bf16
+            sv[i] = f2bf(bf2f(rv[i]) + o);
+            x[j][i] = bf2f(sv[i]);
+            ss += x[j][i] * x[j][i];
+          }
+          store8(resid + e * 8, sv);
+        }
+      }
+      ss = block_sum(ss, red);
+      const float rs = rsqrtf(ss / (float)H + eps);
+#pragma unroll
+      for (int j = 0; j < kNormMaxVec; ++j) {
+        const int p = threadIdx.x + j * kThreads;
+        if (p < hv) {
+          u16x8 wv = load8(w + p * 8);
+          u16x8 ov;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) ov[i] = f2bf(x[j][i] * rs * bf2f(wv[i]));
+          store8(out + ((int64_t)row * hv + p) * 8, ov);
+        }
+      }
+      __syncthreads();  // red[] is reused by the next row
+    }
+  }
+  end_call(a, flag, ok);
+}
+
 void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -302,6 +365,29 @@ void CustomAllReduce::run(const void* in, void* out, int64_t bytes, bool is_bf16
     hipLaunchKernelGGL(ar_two_shot, dim3(g), dim3(kThreads), 0, stream, a);
   else
     hipLaunchKernelGGL(ar_one_shot, dim3(g), dim3(kThreads), 0, stream, a);
+}
+
+void CustomAllReduce::run_add_rmsnorm(const void* in, uint16_t* resid, const uint16_t* w, uint16_t* out,
+                                      int rows, int H, float eps, hipStream_t stream) {
+  if (!opened_) throw std::runtime_error("custom all-reduce: open() the peer handles first");
+  const int64_t bytes = (int64_t)rows * H * 2;
+  if (rows <= 0 || H % 8 != 0 || H > kNormMaxVec * kThreads * 8 || bytes > cap_)
+    throw std::runtime_error("custom all-reduce + rmsnorm: rows > 0, H % 8 == 0, H <= 16384, within capacity");
+  if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(resid) | reinterpret_cast<uintptr_t>(w) |
+       reinterpret_cast<uintptr_t>(out)) & 15)
+    throw std::runtime_error("custom all-reduce + rmsnorm: buffers must be 16-B aligned");
+  ArArgs a;
+  for (int r = 0; r < kArMaxRanks; ++r) a.base[r] = static_cast<const uint8_t*>(r < world_ ? peers_[r] : nullptr);
+  a.in = in;
+  a.out = out;
+  a.nvec = bytes / 16;
+  a.cap = cap_;
+  a.timeout = timeout_ticks_;
+  a.rank = rank_;
+  a.world = world_;
+  a.is_bf16 = 1;
+  const int g = rows < kArMaxBlocks ? rows : kArMaxBlocks;
+  hipLaunchKernelGGL(ar_add_rmsnorm, dim3(g), dim3(kThreads), 0, stream, a, resid, w, out, rows, H, eps);
 }
 
 int CustomAllReduce::error() const {

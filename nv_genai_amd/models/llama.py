@@ -24,6 +24,7 @@ from typing import Dict, List, Optional
 import torch
 
 from .. import ops
+from ..parallel.comm import custom_all_reduce_for
 from ..parallel.dist import (ParallelContext, get_context, tp_all_gather, tp_all_gather_rows,
                              tp_all_reduce, tp_reduce_scatter_rows)
 from .config import LlamaConfig
@@ -228,21 +229,30 @@ class LlamaModel:
                                            meta.block_tables, meta.cu_q, meta.ctx_lens,
                                            hq, hkv, D, meta.max_q_len, self.scale)
 
+    def _reduce_add_norm(self, partial, resid, w):
+        """resid += all_reduce_TP(partial); returns rmsnorm(resid) * w. A small TP message
+        goes through the custom all-reduce's fused epilogue kernel (one launch, the sum never
+        round-trips through HBM); otherwise all-reduce, then the add+RMSNorm kernel."""
+        if self.p.tp_size > 1:
+            car = custom_all_reduce_for(self.p.tp_group)
+            if car is not None and car.fused_norm_eligible(partial):
+                return car.all_reduce_add_rmsnorm(partial, resid, w, self.cfg.eps)
+            tp_all_reduce(partial, self.p)
+        return ops.add_rmsnorm(resid, partial, w, self.cfg.eps)
+
     def _layer(self, li: int, x, resid, pos, meta: AttnMeta):
-        """One decoder layer on rows (x = rmsnorm(resid)); returns the MLP output d, which
-        the caller folds into resid with the next layer's (or the final) norm."""
-        cfg, L = self.cfg, self.layers[li]
+        """One decoder layer on rows (x = rmsnorm(resid)); returns the MLP output d — still
+        a TP partial sum — which the caller reduces into resid with the next layer's (or
+        the final) norm."""
+        L = self.layers[li]
         qkv = x @ L["wqkv"].t()
         ops.rope_cache_(qkv, pos, self.cos_sin, meta.slots, self.k_cache[li],
                         self.v_cache[li], self.hq, self.hkv, self.D)
         attn = self._attention(qkv[:, :self.hq * self.D], qkv, li, meta, x.shape[0])
         o = attn @ L["wo"].t()
-        tp_all_reduce(o, self.p)
-        x = ops.add_rmsnorm(resid, o, L["mlp_norm"], cfg.eps)
+        x = self._reduce_add_norm(o, resid, L["mlp_norm"])
         h = ops.silu_mul(x @ L["wgu"].t())
-        d = h @ L["wd"].t()
-        tp_all_reduce(d, self.p)
-        return d
+        return h @ L["wd"].t()
 
     def _stack(self, resid, pos, meta: AttnMeta, sample_idx: Optional[torch.Tensor]):
         cfg = self.cfg
@@ -251,8 +261,10 @@ class LlamaModel:
         for li in range(n):
             d = self._layer(li, x, resid, pos, meta)
             if li + 1 < n:
-                x = ops.add_rmsnorm(resid, d, self.layers[li + 1]["attn_norm"], cfg.eps)
-            elif sample_idx is not None:
+                x = self._reduce_add_norm(d, resid, self.layers[li + 1]["attn_norm"])
+                continue
+            tp_all_reduce(d, self.p)
+            if sample_idx is not None:
                 # only rows that sample need the final norm
                 rows = resid.index_select(0, sample_idx) + d.index_select(0, sample_idx)
                 return ops.rmsnorm(rows.contiguous(), self.final_norm, cfg.eps)
@@ -340,7 +352,8 @@ class LlamaModel:
         for li in range(n):
             d = self._layer(li, x, resid, pos, meta)
             if li + 1 < n:
-                x = ops.add_rmsnorm(resid, d, self.layers[li + 1]["attn_norm"], cfg.eps)
+                x = self._reduce_add_norm(d, resid, self.layers[li + 1]["attn_norm"])
+        tp_all_reduce(d, self.p)
         rows = T if sample_idx is None else int(sample_idx.shape[0])
         if not self.last_stage:
             resid.add_(d)

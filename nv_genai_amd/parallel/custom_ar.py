@@ -38,6 +38,7 @@ class CustomAllReduce:
         self.rank = dist.get_rank(group)
         cap = int(capacity_mb * 2 ** 20) // 128 * 128
         self.capacity = cap
+        self.fused_norm_max_bytes = 1 << 20
         self.enabled = False
         self.impl = None
         # every stage ends with an agreement among the ranks, so a failure on one rank
@@ -78,6 +79,22 @@ class CustomAllReduce:
         if out is None:
             out = x
         self.impl.all_reduce(x, out, algo)
+        return out
+
+    def fused_norm_eligible(self, x: torch.Tensor) -> bool:
+        """The one-shot all-reduce + residual add + RMSNorm kernel takes bf16 [rows, H]
+        messages up to ``fused_norm_max_bytes`` (above that the two-shot all-reduce plus a
+        separate add+norm moves fewer bytes over xGMI)."""
+        return (self.eligible(x) and x.dtype == torch.bfloat16 and x.dim() == 2
+                and x.shape[1] % 8 == 0 and x.shape[1] <= 16384
+                and x.numel() * 2 <= self.fused_norm_max_bytes)
+
+    def all_reduce_add_rmsnorm(self, x: torch.Tensor, resid: torch.Tensor, w: torch.Tensor,
+                               eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """resid += all_reduce(x) (in place); returns rmsnorm(resid) * w."""
+        if out is None:
+            out = torch.empty_like(resid)
+        self.impl.all_reduce_add_rmsnorm(x, resid, w, out, float(eps))
         return out
 
     def error(self) -> int:

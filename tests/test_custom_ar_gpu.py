@@ -74,6 +74,22 @@ def _worker(rank, port, q):
             if not torch.equal(out.cpu(), exp) or not torch.equal(inplace.cpu(), exp):
                 bad.append((ci, float((out.cpu().float() - exp.float()).abs().max())))
         res["bad"] = bad
+        # fused epilogue: resid += all_reduce(x); out = rmsnorm(resid) * w
+        fused_bad = []
+        for ci, (rows, H) in enumerate(((1, 4096), (7, 4096), (64, 8192), (200, 1024))):
+            x = _inp(rank, 50 + ci, rows * H, torch.bfloat16).view(rows, H).cuda()
+            resid0 = _inp(99, 60 + ci, rows * H, torch.bfloat16).view(rows, H)
+            w = (_inp(98, 70 + ci, H, torch.bfloat16).float().abs() + 0.5).to(torch.bfloat16)
+            resid = resid0.clone().cuda()
+            out = car.all_reduce_add_rmsnorm(x, resid, w.cuda(), 1e-5)
+            torch.cuda.synchronize()
+            s_ = _expect(50 + ci, rows * H, torch.bfloat16).view(rows, H)
+            r_exp = (resid0.float() + s_.float()).to(torch.bfloat16)
+            xf = r_exp.float()
+            o_exp = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float())
+            if not torch.equal(resid.cpu(), r_exp) or (out.cpu().float() - o_exp).abs().max() > 0.02 * o_exp.abs().max():
+                fused_bad.append(ci)
+        res["fused_bad"] = fused_bad
         # hipGraph: 3 all-reduces captured once, replayed twice with new inputs
         xs = [torch.empty(8192 * 16, dtype=torch.bfloat16, device="cuda") for _ in range(3)]
         s = torch.cuda.Stream()
@@ -131,5 +147,6 @@ def test_custom_all_reduce_two_ranks_one_gpu():
         assert "exc" not in r, r
         assert r["self_test"], r
         assert r["bad"] == [], r
+        assert r["fused_bad"] == [], r
         assert r["graph_ok"], r
         assert r["error"] == 0, r
