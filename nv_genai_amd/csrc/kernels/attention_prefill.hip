@@ -48,7 +48,17 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
   __shared__ __attribute__((aligned(16))) uint16_t k_s[KT * D];
   __shared__ __attribute__((aligned(16))) uint16_t v_s[D * KT];
 
-  const int b = blockIdx.z, hq = blockIdx.y, tile = blockIdx.x;
+  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so physical block p
+  // runs on XCD p % 8. Logical work item L = (p % 8) * per_xcd + p / 8 gives every XCD one
+  // contiguous range of the (sequence, kv head, q head, tile) order: the G query heads that
+  // share a KV head — and every query tile of them — read their K/V pages through the same
+  // 4 MB L2. Within a (sequence, head) the longest causal tiles go first.
+  const int pblk = blockIdx.x;
+  const int L = (pblk & 7) * P.per_xcd + (pblk >> 3);
+  if (L >= P.total) return;
+  const int tile = P.ntiles - 1 - L % P.ntiles;
+  const int hq = (L / P.ntiles) % P.Hq;
+  const int b = L / (P.ntiles * P.Hq);
   const int q0 = P.cu_q[b], qlen = P.cu_q[b + 1] - q0;
   if (tile * QT >= qlen) return;
   const int ctx = PAGED ? P.ctx_lens[b] : qlen;
@@ -264,11 +274,17 @@ void launch_prefill_attention(const PrefillParams& p, int num_seqs, int max_q_le
     return e ? atoi(e) : 0;
   }();
   const int ncg = forced == 2 ? 2 : 1;
-  dim3 grid((max_q_len + 64 * ncg - 1) / (64 * ncg), p.Hq, num_seqs);
+  PrefillParams pp = p;
+  pp.ntiles = (max_q_len + 64 * ncg - 1) / (64 * ncg);
+  const int64_t total = (int64_t)pp.ntiles * p.Hq * num_seqs;
+  pp.total = (int)total;
+  pp.per_xcd = (int)((total + 7) / 8);
+  // 1-D grid of 8 * per_xcd workgroups (see the XCD mapping in the kernel)
+  dim3 grid(8 * pp.per_xcd);
 #define NGA_PF(DD, PG, CS)                                                    \
   do {                                                                        \
-    if (ncg == 2) prefill_attn_kernel<DD, PG, CS, 2><<<grid, 256, 0, stream>>>(p); \
-    else prefill_attn_kernel<DD, PG, CS, 1><<<grid, 256, 0, stream>>>(p);          \
+    if (ncg == 2) prefill_attn_kernel<DD, PG, CS, 2><<<grid, 256, 0, stream>>>(pp); \
+    else prefill_attn_kernel<DD, PG, CS, 1><<<grid, 256, 0, stream>>>(pp);          \
   } while (0)
   if (D == 128) {
     if (paged) {

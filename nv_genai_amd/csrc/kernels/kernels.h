@@ -49,6 +49,9 @@ struct PrefillParams {
   int Hq;
   int Hkv;
   float scale;
+  int ntiles;  // query tiles per (sequence, head) — set by the launcher
+  int per_xcd; // workgroups per XCD slice of the 1-D grid — set by the launcher
+  int total;   // ntiles * Hq * num_seqs — set by the launcher
 };
 void launch_prefill_attention(const PrefillParams& p, int num_seqs, int max_q_len, int D,
                               bool paged, bool causal, hipStream_t stream);
