@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--mixed-max-wait", type=int, default=4)
     ap.add_argument("--retrieval-batch", type=int, default=8,
                     help="queries per embedding+search launch (dynamic batching, like the reference's Triton embedder)")
+    ap.add_argument("--no-quiet-gc", action="store_true",
+                    help="keep CPython's default GC (multi-ms host pauses stall the GPU)")
     ap.add_argument("--retrieval-delay-ms", type=float, default=50.0,
                     help="max time a query waits for its retrieval batch to fill (Triton max_queue_delay)")
     return ap.parse_args()
@@ -116,6 +118,7 @@ def main():
         return rag.run(qs, params)
 
     active = {}                     # request id -> RAGResult of the closed-loop clients
+    hostprof = {"poll": [], "submit": [], "work": []}
     ramp = max(1, -(-R // max(1, args.max_tokens)))  # new clients per engine step while ramping
 
     pending = []                    # retrievals in flight on the retrieval stream
@@ -124,19 +127,19 @@ def main():
 
     def closed_loop(n_done: int, ramping: bool):
         """Serve until ``n_done`` requests complete; a completed client re-submits at once.
-        Each iteration launches the next engine step first, then does the host work for
-        retrieval (non-blocking) while that step runs on the GPU."""
+        The client/retrieval host work (prompts for finished retrievals, the next retrieval
+        batch on the retrieval stream) runs inside ``llm.step`` between launching the next
+        engine step and waiting for the previous one, i.e. while the GPU is busy."""
         out = []
-        while len(out) < n_done:
-            for req in llm.step():
-                res = active.pop(req.id, None)
-                if res is not None:
-                    out.append(res)
-                    clients[0] -= 1
-            for res in rag.poll(pending, block=not llm.has_work()):
+        st = {"ramping": ramping}
+
+        def host_work(block: bool = False):
+            hw0 = time.perf_counter()
+            for res in rag.poll(pending, block=block):
                 active[res.request.id] = res
+            hw1 = time.perf_counter()
             need = R - clients[0]
-            if ramping:
+            if st["ramping"]:
                 need = min(need, ramp)
             if need > 0:
                 now = time.perf_counter()
@@ -144,11 +147,24 @@ def main():
                 clients[0] += need
             if queued and (len(queued) >= args.retrieval_batch or not llm.has_work()
                            or time.perf_counter() - queued[0][1] >= args.retrieval_delay_ms / 1e3):
+                hs0 = time.perf_counter()
                 pr = rag.submit_async([q for q, _ in queued], params)
                 pr.t0 = [t for _, t in queued]        # latency counts the batching wait
                 pending.append(pr)
                 queued.clear()
-            ramping = ramping and clients[0] < R
+                hostprof["submit"].append(time.perf_counter() - hs0)
+            hostprof["poll"].append(hw1 - hw0)
+            hostprof["work"].append(time.perf_counter() - hw0)
+            st["ramping"] = st["ramping"] and clients[0] < R
+
+        while len(out) < n_done:
+            for req in llm.step(between=host_work):
+                res = active.pop(req.id, None)
+                if res is not None:
+                    out.append(res)
+                    clients[0] -= 1
+            if not llm.has_work():
+                host_work(block=True)
         return out
 
     if args.mode == "wave":
@@ -156,6 +172,10 @@ def main():
             one_step()
     else:
         closed_loop(max(1, args.warmup) * R, ramping=True)
+    if not args.no_quiet_gc:
+        from nv_genai_amd.utils.runtime import quiet_gc
+
+        quiet_gc()
     pd.barrier()
     if gpu:
         torch.cuda.synchronize()
@@ -166,6 +186,8 @@ def main():
         prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA])
         prof.__enter__()
     llm.stats.update({k: 0 if isinstance(v, int) else 0.0 for k, v in llm.stats.items()})
+    for v in hostprof.values():
+        v.clear()
     t0 = time.perf_counter()
     results = []
     if args.mode == "wave":
@@ -228,6 +250,11 @@ def main():
         "decode_s": round(llm.stats["decode_time"], 3),
         "steps_prefill_decode_mixed": [llm.stats["prefill_steps"] - llm.stats["mixed_steps"],
                                        llm.stats["decode_steps"], llm.stats["mixed_steps"]],
+        "unpipelined_steps": llm.stats["unpipelined_steps"],
+        "host_work_ms": {k: [len(v), round(1e3 * sum(v), 1), round(1e3 * max(v), 2) if v else 0.0,
+                             sum(1 for x in v if x > 4e-3)] for k, v in hostprof.items()},
+        "host_s": {k[5:-2]: round(llm.stats[k], 3) for k in ("host_sched_s", "host_launch_s", "host_between_s",
+                                                             "host_wait_s", "host_finalize_s")},
         "setup_s": round(setup_s, 1),
         "prefix_cache_hit_blocks": int(llm.sched.prefix_hits()),
         "distinct_docs_retrieved": len({d for r in results for d in r.doc_ids}),

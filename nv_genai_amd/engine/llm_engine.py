@@ -195,7 +195,9 @@ class LLMEngine:
         self._rng = random.Random(cfg.seed)
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.stats = {"prefill_steps": 0, "decode_steps": 0, "mixed_steps": 0, "prefill_tokens": 0,
-                      "decode_tokens": 0, "prefill_time": 0.0, "decode_time": 0.0}
+                      "decode_tokens": 0, "prefill_time": 0.0, "decode_time": 0.0, "unpipelined_steps": 0,
+                      "host_sched_s": 0.0, "host_launch_s": 0.0, "host_between_s": 0.0,
+                      "host_wait_s": 0.0, "host_finalize_s": 0.0}
         self.lock = threading.RLock()
         self._pending: Optional[dict] = None
         self._tok_flip = 0
@@ -259,8 +261,14 @@ class LLMEngine:
         self.n_step[:n] = [len(r.output_ids) + (r.id in pending_ids) for r in reqs]
         self.n_pen[:n] = [r.params.repetition_penalty for r in reqs]
 
-    def step(self) -> List[Request]:
+    def step(self, between: Optional[Callable[[], None]] = None) -> List[Request]:
         """Run one scheduler step; returns requests that finished in it.
+
+        ``between`` (optional) runs after the next step has been launched and before the
+        host blocks on the previous step's tokens — the window where the GPU is busy and the
+        host would otherwise wait. A serving loop puts its own host work there (building
+        prompts for finished retrievals, launching the next retrieval batch), so that work
+        never delays the launch of the following step.
 
         Steps are pipelined when possible: step k+1 is scheduled and launched before step k's
         tokens are read back (input ids that step k is still producing are gathered on the
@@ -269,6 +277,11 @@ class LLMEngine:
         (``mixed_prefill_tokens``) a step carries the decode rows of every running sequence
         plus a prefill chunk, so decode rows ride on the prefill GEMMs."""
         with self.lock:
+            done = self._step(between)
+        return done
+
+    def _step(self, between) -> List[Request]:
+        if True:
             pend = self._pending
             done: List[Request] = []
             if pend is not None:
@@ -280,6 +293,7 @@ class LLMEngine:
                 # the in-flight step's upload may still be queued behind the GPU's previous
                 # step: the pinned buffers must not be rewritten before the DMA has read them
                 self._up_ev.synchronize()
+            t_sched = time.perf_counter()
             kind, n, ntok = self.sched.schedule(ids, pos, sl, cu, ctx, bt, sid, smp)
             nd = n if kind == 2 else (self.sched.last_num_decode() if kind == 3 else 0)
             src = None
@@ -292,6 +306,7 @@ class LLMEngine:
                     src = (ph, [rows[int(sid[i])] for i in ph.tolist()])
                 else:
                     # cannot pipeline: settle the in-flight step, then run this one normally
+                    self.stats["unpipelined_steps"] += 1
                     done += self._finalize(pend)
                     pend = self._pending = None
                     for i in ph.tolist():
@@ -301,6 +316,8 @@ class LLMEngine:
                         except (IndexError, KeyError):  # finished meanwhile: row is inert
                             ids[i] = 0
             if kind == 0:
+                if between is not None:
+                    between()
                 return done
             t0 = time.perf_counter()
             reqs = [self.requests.get(int(s)) for s in sid[:n].tolist()]
@@ -309,9 +326,22 @@ class LLMEngine:
             key = "decode_time" if kind == 2 else "prefill_time"
             self._count(kind, n, ntok, nd)
             if self.cfg.async_decode and not self._needs_penalty(n):
+                h0 = time.perf_counter()
                 nxt = self._launch(kind, n, ntok, nd, src)
+                h1 = time.perf_counter()
+                if between is not None:
+                    between()
+                h2 = time.perf_counter()
                 if pend is not None:
+                    if pend["ev"] is not None:
+                        pend["ev"].synchronize()
+                    h3 = time.perf_counter()
                     done += self._finalize(pend)
+                    self.stats["host_wait_s"] += h3 - h2
+                    self.stats["host_finalize_s"] += time.perf_counter() - h3
+                self.stats["host_launch_s"] += h1 - h0
+                self.stats["host_between_s"] += h2 - h1
+                self.stats["host_sched_s"] += h0 - t_sched
                 self._pending = nxt
                 self.stats[key] += time.perf_counter() - t0
                 return done
@@ -326,6 +356,8 @@ class LLMEngine:
             for i, (r, s) in enumerate(zip(reqs, smp[:n].tolist())):
                 if s and r is not None and not r.finished and self._emit(r, toks[i], lps[i], now):
                     done.append(r)
+            if between is not None:
+                between()
             return done
 
     def timeline(self, last: int = 256) -> List[dict]:

@@ -112,7 +112,12 @@ class StreamHandle:
 
 
 class EngineService:
-    def __init__(self, engine: LLMEngine, watchdog_s: float = 300.0, name: str = "llm"):
+    def __init__(self, engine: LLMEngine, watchdog_s: float = 300.0, name: str = "llm",
+                 quiet_gc: bool = True):
+        if quiet_gc:   # no multi-ms GC pauses on the thread that launches GPU steps
+            from ..utils.runtime import quiet_gc as _quiet
+
+            _quiet()
         self.engine = engine
         self.watchdog_s = watchdog_s
         self.name = name
