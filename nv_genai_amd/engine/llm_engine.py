@@ -281,84 +281,83 @@ class LLMEngine:
         return done
 
     def _step(self, between) -> List[Request]:
-        if True:
-            pend = self._pending
-            done: List[Request] = []
-            if pend is not None:
-                cont = [r.id for r, s in zip(pend["reqs"], pend["smp"]) if s and r is not None
-                        and len(r.output_ids) + 1 < r.params.max_tokens and r.id in self.requests]
-                self.sched.append_placeholders(cont)
-            ids, pos, sl, cu, ctx, bt, sid, smp = self._np
-            if self._up_ev is not None:
-                # the in-flight step's upload may still be queued behind the GPU's previous
-                # step: the pinned buffers must not be rewritten before the DMA has read them
-                self._up_ev.synchronize()
-            t_sched = time.perf_counter()
-            kind, n, ntok = self.sched.schedule(ids, pos, sl, cu, ctx, bt, sid, smp)
-            nd = n if kind == 2 else (self.sched.last_num_decode() if kind == 3 else 0)
-            src = None
-            if pend is not None:
-                ph = np.flatnonzero(ids[:ntok] < 0) if kind else np.empty(0, dtype=np.int64)
-                rows = pend["rows"]
-                ok = (kind != 0 and self.cfg.async_decode and not self._needs_penalty_reqs(pend["reqs"])
-                      and all(i < nd and int(sid[i]) in rows for i in ph.tolist()))
-                if ok:
-                    src = (ph, [rows[int(sid[i])] for i in ph.tolist()])
-                else:
-                    # cannot pipeline: settle the in-flight step, then run this one normally
-                    self.stats["unpipelined_steps"] += 1
-                    done += self._finalize(pend)
-                    pend = self._pending = None
-                    for i in ph.tolist():
-                        r = int(np.searchsorted(cu[1:n + 1], i, side="right"))
-                        try:
-                            ids[i] = self.sched.tokens(int(sid[r]))[pos[i]]
-                        except (IndexError, KeyError):  # finished meanwhile: row is inert
-                            ids[i] = 0
-            if kind == 0:
-                if between is not None:
-                    between()
-                return done
-            t0 = time.perf_counter()
-            reqs = [self.requests.get(int(s)) for s in sid[:n].tolist()]
-            pending_ids = pend["sampled"] if pend is not None else ()
-            self._fill_params(reqs, pending_ids=pending_ids)
-            key = "decode_time" if kind == 2 else "prefill_time"
-            self._count(kind, n, ntok, nd)
-            if self.cfg.async_decode and not self._needs_penalty(n):
-                h0 = time.perf_counter()
-                nxt = self._launch(kind, n, ntok, nd, src)
-                h1 = time.perf_counter()
-                if between is not None:
-                    between()
-                h2 = time.perf_counter()
-                if pend is not None:
-                    if pend["ev"] is not None:
-                        pend["ev"].synchronize()
-                    h3 = time.perf_counter()
-                    done += self._finalize(pend)
-                    self.stats["host_wait_s"] += h3 - h2
-                    self.stats["host_finalize_s"] += time.perf_counter() - h3
-                self.stats["host_launch_s"] += h1 - h0
-                self.stats["host_between_s"] += h2 - h1
-                self.stats["host_sched_s"] += h0 - t_sched
-                self._pending = nxt
-                self.stats[key] += time.perf_counter() - t0
-                return done
-            if kind == 2:
-                toks, lps = self._decode(n)
+        pend = self._pending
+        done: List[Request] = []
+        if pend is not None:
+            cont = [r.id for r, s in zip(pend["reqs"], pend["smp"]) if s and r is not None
+                    and len(r.output_ids) + 1 < r.params.max_tokens and r.id in self.requests]
+            self.sched.append_placeholders(cont)
+        ids, pos, sl, cu, ctx, bt, sid, smp = self._np
+        if self._up_ev is not None:
+            # the in-flight step's upload may still be queued behind the GPU's previous
+            # step: the pinned buffers must not be rewritten before the DMA has read them
+            self._up_ev.synchronize()
+        t_sched = time.perf_counter()
+        kind, n, ntok = self.sched.schedule(ids, pos, sl, cu, ctx, bt, sid, smp)
+        nd = n if kind == 2 else (self.sched.last_num_decode() if kind == 3 else 0)
+        src = None
+        if pend is not None:
+            ph = np.flatnonzero(ids[:ntok] < 0) if kind else np.empty(0, dtype=np.int64)
+            rows = pend["rows"]
+            ok = (kind != 0 and self.cfg.async_decode and not self._needs_penalty_reqs(pend["reqs"])
+                  and all(i < nd and int(sid[i]) in rows for i in ph.tolist()))
+            if ok:
+                src = (ph, [rows[int(sid[i])] for i in ph.tolist()])
             else:
-                toks, lps = self._prefill(n, ntok, nd)
-            toks = toks.tolist()
-            lps = lps.tolist()
-            self.stats[key] += time.perf_counter() - t0
-            now = time.perf_counter()
-            for i, (r, s) in enumerate(zip(reqs, smp[:n].tolist())):
-                if s and r is not None and not r.finished and self._emit(r, toks[i], lps[i], now):
-                    done.append(r)
+                # cannot pipeline: settle the in-flight step, then run this one normally
+                self.stats["unpipelined_steps"] += 1
+                done += self._finalize(pend)
+                pend = self._pending = None
+                for i in ph.tolist():
+                    r = int(np.searchsorted(cu[1:n + 1], i, side="right"))
+                    try:
+                        ids[i] = self.sched.tokens(int(sid[r]))[pos[i]]
+                    except (IndexError, KeyError):  # finished meanwhile: row is inert
+                        ids[i] = 0
+        if kind == 0:
             if between is not None:
                 between()
             return done
+        t0 = time.perf_counter()
+        reqs = [self.requests.get(int(s)) for s in sid[:n].tolist()]
+        pending_ids = pend["sampled"] if pend is not None else ()
+        self._fill_params(reqs, pending_ids=pending_ids)
+        key = "decode_time" if kind == 2 else "prefill_time"
+        self._count(kind, n, ntok, nd)
+        if self.cfg.async_decode and not self._needs_penalty(n):
+            h0 = time.perf_counter()
+            nxt = self._launch(kind, n, ntok, nd, src)
+            h1 = time.perf_counter()
+            if between is not None:
+                between()
+            h2 = time.perf_counter()
+            if pend is not None:
+                if pend["ev"] is not None:
+                    pend["ev"].synchronize()
+                h3 = time.perf_counter()
+                done += self._finalize(pend)
+                self.stats["host_wait_s"] += h3 - h2
+                self.stats["host_finalize_s"] += time.perf_counter() - h3
+            self.stats["host_launch_s"] += h1 - h0
+            self.stats["host_between_s"] += h2 - h1
+            self.stats["host_sched_s"] += h0 - t_sched
+            self._pending = nxt
+            self.stats[key] += time.perf_counter() - t0
+            return done
+        if kind == 2:
+            toks, lps = self._decode(n)
+        else:
+            toks, lps = self._prefill(n, ntok, nd)
+        toks = toks.tolist()
+        lps = lps.tolist()
+        self.stats[key] += time.perf_counter() - t0
+        now = time.perf_counter()
+        for i, (r, s) in enumerate(zip(reqs, smp[:n].tolist())):
+            if s and r is not None and not r.finished and self._emit(r, toks[i], lps[i], now):
+                done.append(r)
+        if between is not None:
+            between()
+        return done
 
     def timeline(self, last: int = 256) -> List[dict]:
         """Recent scheduler steps: wall time at launch, kind, rows, tokens, decode rows and
