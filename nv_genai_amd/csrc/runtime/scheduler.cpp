@@ -75,6 +75,11 @@ class BlockManager {
       }
     }
   }
+  // Add a reference to a block another sequence already holds (copy-on-fork sharing).
+  void share(int b) {
+    if (b < 0 || b >= nb_ || ref_[b] <= 0) throw std::runtime_error("share of a free block");
+    ref_[b] += 1;
+  }
   // Look up a full block by content hash; on hit the block is referenced.
   int lookup(uint64_t h) {
     if (!prefix_) return -1;
@@ -279,6 +284,47 @@ class Scheduler {
       s.toks.pop_back();
       if (s.computed > (int)s.toks.size()) s.computed = (int)s.toks.size();
     }
+  }
+
+  // Beam search: clone a sequence. The child shares every full KV block of the parent
+  // (reference-counted) and gets a fresh block for the partially filled last one; the caller
+  // copies that block's KV on the GPU (returned as (src, dst), or (-1, -1) when the parent's
+  // computed length is block-aligned). With no free block the child re-enters the waiting
+  // queue and recomputes (prefix-cached blocks still hit), like a preempted sequence.
+  py::tuple fork(int64_t pid, int64_t cid) {
+    if (seqs_.count(cid)) throw std::runtime_error("duplicate sequence id");
+    const Seq& p = seqs_.at(pid);
+    Seq c;
+    c.id = cid;
+    c.toks = p.toks;
+    c.prompt_len = p.prompt_len;
+    c.max_new = p.max_new;
+    c.arrival = p.arrival;
+    c.enq_step = step_;
+    int src = -1, dst = -1;
+    const int full = p.computed / bs_;
+    const bool partial = p.computed % bs_ != 0;
+    if (p.status == RUNNING && (!partial || bm_.num_free() > 0)) {
+      for (int i = 0; i < full; ++i) {
+        bm_.share(p.blocks[i]);
+        c.blocks.push_back(p.blocks[i]);
+      }
+      if (partial) {
+        src = p.blocks[full];
+        dst = bm_.alloc();
+        c.blocks.push_back(dst);
+      }
+      c.hashes.assign(p.hashes.begin(), p.hashes.begin() + std::min<size_t>(full, p.hashes.size()));
+      c.computed = p.computed;
+      c.cached_prefix = p.cached_prefix;
+      c.status = RUNNING;
+      running_.push_back(cid);
+    } else {
+      c.status = WAITING;
+      waiting_.push_front(cid);
+    }
+    seqs_.emplace(cid, std::move(c));
+    return py::make_tuple(src, dst);
   }
 
   void finish(int64_t id) {
@@ -584,6 +630,7 @@ PYBIND11_MODULE(_rt, m) {
       .def("has_placeholder", &Scheduler::has_placeholder)
       .def("drop_placeholder", &Scheduler::drop_placeholder)
       .def("finish", &Scheduler::finish)
+      .def("fork", &Scheduler::fork)
       .def("num_generated", &Scheduler::num_generated)
       .def("tokens", &Scheduler::tokens)
       .def("cached_prefix", &Scheduler::cached_prefix)

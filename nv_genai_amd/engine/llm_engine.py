@@ -36,6 +36,7 @@ from ..models.config import LlamaConfig, llama_config
 from ..models.llama import AttnMeta, LlamaModel
 from ..parallel.dist import ParallelContext, get_context
 from ..utils.tokenizer import IncrementalDetokenizer, LLMTokenizer, llm_tokenizer
+from .beam import BeamGroup, advance
 
 log = logging.getLogger(__name__)
 
@@ -53,6 +54,10 @@ class SamplingParams:
     repetition_penalty: float = 1.0
     logprobs: bool = False
     min_tokens: int = 0
+    frequency_penalty: float = 0.0  # OpenAI semantics over generated tokens:
+    presence_penalty: float = 0.0   #   logit -= freq * count + presence * (count > 0)
+    beam_width: int = 1             # > 1: beam search (engine/beam.py); sampling knobs ignored
+    length_penalty: float = 1.0     # beam hypotheses score sum_logprob / len ** length_penalty
 
 
 @dataclass
@@ -72,6 +77,7 @@ class Request:
     on_token: Optional[Callable[["Request", str], None]] = None
     detok: Optional[IncrementalDetokenizer] = None
     cached_prefix: int = 0
+    beams: List[tuple] = field(default_factory=list)   # beam search: (score, token ids, text)
 
     @property
     def ttft(self) -> Optional[float]:
@@ -204,6 +210,10 @@ class LLMEngine:
         self._up_ev = None  # marks the last host->device upload of the pinned step buffers
         self._timeline = collections.deque(maxlen=4096)
         self._tok_host = [(hbuf(S), hbuf(S, dtype=torch.float32)) for _ in range(2)]
+        self._step_reqs: List[Request] = []
+        self._beam_of: Dict[int, BeamGroup] = {}   # live beam seq id -> its group
+        self._beam_rows: List[tuple] = []         # (row, seq id) of beam rows in this step
+        self._beam_out = None
         if self.p.mp_size > 1:
             # followers replay from broadcast host buffers; the device-side id gather of the
             # pipelined path is not replicated, so TP/PP steps run synchronously; pipeline
@@ -233,13 +243,25 @@ class LLMEngine:
             req.detok = IncrementalDetokenizer(self.tok)
         with self.lock:
             self.sched.add(rid, req.prompt_ids, max_new)
-            self.requests[rid] = req
+            if params.beam_width > 1:
+                g = BeamGroup(req, int(params.beam_width), float(params.length_penalty))
+                g.beams[rid] = 0.0
+                self._beam_of[rid] = g
+            else:
+                self.requests[rid] = req
         return req
 
     def abort(self, rid: int):
         with self.lock:
             req = self.requests.pop(rid, None)
             self.sched.finish(rid)
+            g = next((g for g in set(self._beam_of.values()) if g.req.id == rid), None)
+            if g is not None:
+                req = g.req
+                for sid in g.beams:
+                    self.sched.finish(sid)
+                    self._beam_of.pop(sid, None)
+                g.beams = {}
             if req is not None and not req.finished:
                 req.finished, req.finish_reason = True, "abort"
                 req.finish_time = time.perf_counter()
@@ -260,6 +282,7 @@ class LLMEngine:
         self.n_seed[:n] = [r.seed for r in reqs]
         self.n_step[:n] = [len(r.output_ids) + (r.id in pending_ids) for r in reqs]
         self.n_pen[:n] = [r.params.repetition_penalty for r in reqs]
+        self._step_reqs = reqs
 
     def step(self, between: Optional[Callable[[], None]] = None) -> List[Request]:
         """Run one scheduler step; returns requests that finished in it.
@@ -296,10 +319,16 @@ class LLMEngine:
         kind, n, ntok = self.sched.schedule(ids, pos, sl, cu, ctx, bt, sid, smp)
         nd = n if kind == 2 else (self.sched.last_num_decode() if kind == 3 else 0)
         src = None
+        sids = sid[:n].tolist()
+        # rows that need the host between steps (penalty history, beam candidates) run the
+        # step synchronously
+        sync_rows = (self._needs_penalty_reqs([self.requests.get(int(s)) for s in sids])
+                     or (bool(self._beam_of) and any(int(s) in self._beam_of for s in sids)))
         if pend is not None:
             ph = np.flatnonzero(ids[:ntok] < 0) if kind else np.empty(0, dtype=np.int64)
             rows = pend["rows"]
             ok = (kind != 0 and self.cfg.async_decode and not self._needs_penalty_reqs(pend["reqs"])
+                  and not sync_rows
                   and all(i < nd and int(sid[i]) in rows for i in ph.tolist()))
             if ok:
                 src = (ph, [rows[int(sid[i])] for i in ph.tolist()])
@@ -324,7 +353,9 @@ class LLMEngine:
         self._fill_params(reqs, pending_ids=pending_ids)
         key = "decode_time" if kind == 2 else "prefill_time"
         self._count(kind, n, ntok, nd)
-        if self.cfg.async_decode and not self._needs_penalty(n):
+        self._beam_rows = ([(i, int(s)) for i, s in enumerate(sids) if int(s) in self._beam_of]
+                           if self._beam_of else [])
+        if self.cfg.async_decode and not sync_rows and not self._needs_penalty(n):
             h0 = time.perf_counter()
             nxt = self._launch(kind, n, ntok, nd, src)
             h1 = time.perf_counter()
@@ -355,6 +386,8 @@ class LLMEngine:
         for i, (r, s) in enumerate(zip(reqs, smp[:n].tolist())):
             if s and r is not None and not r.finished and self._emit(r, toks[i], lps[i], now):
                 done.append(r)
+        if self._beam_rows:
+            done += self._beam_step(smp[:n].tolist(), now)
         if between is not None:
             between()
         return done
@@ -379,7 +412,8 @@ class LLMEngine:
                 self.stats["decode_tokens"] += nd
 
     def _needs_penalty_reqs(self, reqs) -> bool:
-        return any(r is not None and r.params.repetition_penalty != 1.0 for r in reqs)
+        return any(r is not None and (r.params.repetition_penalty != 1.0 or r.params.frequency_penalty
+                                      or r.params.presence_penalty) for r in reqs)
 
     def _launch(self, kind: int, n: int, ntok: int, nd: int, src) -> dict:
         """Launch a step without waiting for it. ``src = (token_idx, prev_rows)`` gathers the
@@ -516,7 +550,7 @@ class LLMEngine:
         hdr = self._bcast(torch.zeros(8, dtype=torch.int64)).cpu().tolist()
         kind, n, ntok, max_q, max_ctx, bs, nd = hdr[:7]
         if kind < 0:
-            return kind, 0, 0, 0, 0, 0, 0
+            return kind, n, 0, 0, 0, 0, 0
         rows, toks = max(n, bs), max(ntok, bs)
         size = 3 * toks + (rows + 1) + rows + rows * self.max_blocks
         payload = self._bcast(torch.zeros(size, dtype=torch.int32)).cpu()
@@ -534,6 +568,10 @@ class LLMEngine:
         """Non-driver TP ranks: execute every step the driver publishes."""
         while True:
             kind, n, ntok, max_q, max_ctx, bs, nd = self._recv_step()
+            if kind == -2:   # copy-on-fork pages (beam search), n pairs
+                pairs = self._bcast(torch.zeros(2 * n, dtype=torch.int32)).cpu().view(2, n)
+                self.model.copy_kv_blocks(pairs[0], pairs[1])
+                continue
             if kind < 0:
                 return
             if kind in (1, 3):
@@ -548,6 +586,73 @@ class LLMEngine:
     def stop_followers(self) -> None:
         if self.p.mp_size > 1 and self.is_driver:
             self._sync_step(-1, 0, 0, 0, 0, 0, 0)
+
+    # ------------------------------------------------------------------ beam search
+    def _beam_step(self, smp: List[int], now: float) -> List[Request]:
+        """Record this step's top-2·width candidates of every beam row; advance each group
+        whose live beams have all reported (engine/beam.py)."""
+        vals, idxs = self._beam_out
+        self._beam_out = None
+        touched = []
+        for k, (row, sid) in enumerate(self._beam_rows):
+            g = self._beam_of.get(sid)
+            if g is None or not smp[row]:
+                continue
+            w2 = 2 * g.width
+            g.reported[sid] = (vals[k][:w2], idxs[k][:w2])
+            if g not in touched:
+                touched.append(g)
+        self._beam_rows = []
+        done, copies = [], []
+        for g in touched:
+            if set(g.reported) != set(g.beams):
+                continue
+            r = g.req
+            if r.first_token_time is None:
+                r.first_token_time = now
+            old = list(g.beams)
+            finished, cp, forked = advance(
+                g, self.sched, len(r.prompt_ids),
+                lambda t, r=r: (t in self.stop_ids and not r.params.ignore_eos) or t in r.params.stop_token_ids,
+                r.params.min_tokens, r.params.max_tokens)
+            copies += cp
+            for sid in old:
+                if sid not in g.beams:
+                    self._beam_of.pop(sid, None)
+            for sid in forked:
+                self._beam_of[sid] = g
+            if finished:
+                self._beam_finish(g, now)
+                done.append(r)
+        if copies:
+            src = torch.tensor([c[0] for c in copies], dtype=torch.int32)
+            dst = torch.tensor([c[1] for c in copies], dtype=torch.int32)
+            if self.p.mp_size > 1:
+                hdr = torch.tensor([-2, len(copies), 0, 0, 0, 0, 0, 0], dtype=torch.int64)
+                self._bcast(hdr)
+                self._bcast(torch.cat([src, dst]))
+            self.model.copy_kv_blocks(src, dst)
+        return done
+
+    def _beam_finish(self, g: BeamGroup, now: float) -> None:
+        r = g.req
+        for score, toks, eos in g.hyps:
+            text = self.tok.decode([t for t in toks if t not in self.stop_ids]) if self.cfg.detokenize else ""
+            for s in r.params.stop:
+                if s and s in text:
+                    text = text[: text.index(s)]
+            r.beams.append((score, toks, text))
+        score, toks, eos = g.hyps[0] if g.hyps else (0.0, [], False)
+        r.output_ids = list(toks)
+        r.text = r.beams[0][2] if r.beams else ""
+        r.finished, r.finish_reason, r.finish_time = True, ("stop" if eos else "length"), now
+        if r.on_token is not None:
+            try:
+                if r.text:
+                    r.on_token(r, r.text)
+                r.on_token(r, "")
+            except Exception:  # noqa: BLE001
+                log.exception("on_token callback failed")
 
     def _emit(self, r: Request, tok: int, lp: float, now: float, appended: bool = False) -> bool:
         if r.first_token_time is None:
@@ -620,6 +725,13 @@ class LLMEngine:
             self._up_ev.record()
 
     def _sample(self, logits, n):
+        if self._beam_rows and logits is not None:
+            rows = torch.tensor([i for i, _ in self._beam_rows], device=logits.device)
+            k = max(2 * self._beam_of[s].width for _, s in self._beam_rows)
+            lp = torch.log_softmax(logits.index_select(0, rows).float(), dim=-1)
+            v, ix = lp.topk(min(k, lp.shape[-1]), dim=-1)
+            self._beam_out = (v.cpu().tolist(), ix.cpu().tolist())
+        self._apply_count_penalties(logits, n)
         rep = self.d_pen[:n] if self._needs_penalty(n) else None
         hist = self._history(n) if rep is not None else None
         tok, lp = ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n],
@@ -631,7 +743,21 @@ class LLMEngine:
         return self.d_tok[:n], self.d_lp[:n]
 
     def _needs_penalty(self, n) -> bool:
-        return bool((self.h_pen[:n] != 1.0).any())
+        return bool((self.h_pen[:n] != 1.0).any()) or any(
+            r.params.frequency_penalty or r.params.presence_penalty for r in self._step_reqs[:n])
+
+    def _apply_count_penalties(self, logits, n) -> None:
+        """frequency/presence penalties (OpenAI /v1/completions semantics) on the rows that
+        ask for them: a bincount of the row's generated tokens, subtracted in place."""
+        if logits is None:
+            return
+        for i, r in enumerate(self._step_reqs[:n]):
+            if not (r.params.frequency_penalty or r.params.presence_penalty) or not r.output_ids:
+                continue
+            cnt = torch.bincount(torch.tensor(r.output_ids, dtype=torch.int64),
+                                 minlength=logits.shape[1])[: logits.shape[1]].to(logits.device)
+            logits[i] -= (r.params.frequency_penalty * cnt
+                          + r.params.presence_penalty * (cnt > 0)).to(logits.dtype)
 
     def _history(self, n):
         rows = [self.sched.tokens(int(self.h_sid[i])) for i in range(n)]
@@ -659,7 +785,7 @@ class LLMEngine:
         return None if h is None else self.model.logits(h)   # None: a later pipeline stage
 
     def _decode(self, n):
-        if self.graphs and not self._needs_penalty(n):
+        if self.graphs and not self._needs_penalty(n) and not self._beam_rows:
             bs = next((b for b in sorted(self.graphs) if b >= n), None)
             if bs is not None:
                 self._pad_rows(n, bs)

@@ -193,6 +193,13 @@ class LlamaModel:
         self.v_cache = torch.zeros(shape_v, device=self.device, dtype=self.dtype)
         return self.k_cache, self.v_cache
 
+    def copy_kv_blocks(self, src: torch.Tensor, dst: torch.Tensor) -> None:
+        """Copy-on-fork (beam search): page ``dst[i]`` of every layer takes the K and Vᵀ of
+        page ``src[i]`` — one gather/scatter per cache over the [layers, blocks] dims."""
+        src, dst = src.to(self.device).long(), dst.to(self.device).long()
+        self.k_cache.index_copy_(1, dst, self.k_cache.index_select(1, src))
+        self.v_cache.index_copy_(1, dst, self.v_cache.index_select(1, src))
+
     def kv_block_bytes(self, block_size: int = 64) -> int:
         return 2 * len(self.layers) * self.hkv * self.D * block_size * torch.finfo(self.dtype).bits // 8
 

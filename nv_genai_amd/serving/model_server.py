@@ -55,6 +55,10 @@ class ChatRequest(BaseModel):
     repetition_penalty: float = Field(1.0, gt=0.0)
     ignore_eos: bool = False
     logprobs: bool = False
+    frequency_penalty: float = Field(0.0, ge=-2.0, le=2.0)
+    presence_penalty: float = Field(0.0, ge=-2.0, le=2.0)
+    beam_width: int = Field(1, ge=1, le=16)
+    length_penalty: float = 1.0
 
 
 class CompletionRequest(BaseModel):
@@ -69,6 +73,10 @@ class CompletionRequest(BaseModel):
     stream: bool = False
     repetition_penalty: float = Field(1.0, gt=0.0)
     ignore_eos: bool = False
+    frequency_penalty: float = Field(0.0, ge=-2.0, le=2.0)
+    presence_penalty: float = Field(0.0, ge=-2.0, le=2.0)
+    beam_width: int = Field(1, ge=1, le=16)
+    length_penalty: float = 1.0
 
 
 class EmbeddingRequest(BaseModel):
@@ -94,7 +102,9 @@ def _params(r) -> SamplingParams:
     stop = [r.stop] if isinstance(r.stop, str) else list(r.stop or [])
     return SamplingParams(temperature=r.temperature, top_p=r.top_p, top_k=r.top_k, max_tokens=r.max_tokens,
                           stop=stop, seed=r.seed, repetition_penalty=r.repetition_penalty,
-                          ignore_eos=r.ignore_eos, logprobs=getattr(r, "logprobs", False))
+                          ignore_eos=r.ignore_eos, logprobs=getattr(r, "logprobs", False),
+                          frequency_penalty=r.frequency_penalty, presence_penalty=r.presence_penalty,
+                          beam_width=r.beam_width, length_penalty=r.length_penalty)
 
 
 def _content_text(c) -> str:
@@ -241,14 +251,16 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
     # Triton "generate" extension (the TRT-LLM ensemble contract of
     # experimental/AzureML/trt_llm_azureml.py:282-320): text_input + sampling knobs.
     def _triton_params(b: dict) -> SamplingParams:
-        if int(b.get("beam_width", 1)) != 1:
-            raise ValueError("beam_width > 1 is not supported; use sampling")
+        if not 1 <= int(b.get("beam_width", 1)) <= 16:
+            raise ValueError("beam_width must be in [1, 16]")
         stop = b.get("stop_words") or []
         return SamplingParams(temperature=float(b.get("temperature", 1.0)), top_p=float(b.get("top_p", 1.0)),
                               top_k=int(b.get("top_k", 0)), max_tokens=int(b.get("max_tokens", 64)),
                               repetition_penalty=float(b.get("repetition_penalty", 1.0)),
                               seed=b.get("random_seed"), stop=[stop] if isinstance(stop, str) else list(stop),
-                              ignore_eos=bool(b.get("ignore_eos", False)))
+                              ignore_eos=bool(b.get("ignore_eos", False)),
+                              beam_width=int(b.get("beam_width", 1)),
+                              length_penalty=float(b.get("length_penalty", 1.0)))
 
     @app.post("/v2/models/{model}/generate")
     async def triton_generate(model: str, request: Request):

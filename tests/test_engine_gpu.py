@@ -155,3 +155,17 @@ def test_mixed_step_logits_match_separate_steps(gpu, weights):
             cos = torch.nn.functional.cosine_similarity(x, y, dim=0)
             assert cos > 0.999, cos
     assert seen[0][2][:3] == seen[2048][2][:3] and seen[0][3][:2] == seen[2048][3][:2]
+
+
+def test_beam_search_gpu_matches_cpu(gpu, weights):
+    """Beam search through the HIP kernels (copy-on-fork KV pages on the GPU, eager decode
+    for beam rows) picks the same best beam as the CPU reference engine."""
+    from nv_genai_amd.engine.llm_engine import SamplingParams
+
+    p = SamplingParams(beam_width=4, max_tokens=10, ignore_eos=True)
+    eg = _engine(weights, "cuda")
+    g = eg.generate([PROMPTS[1]], p)[0]
+    c = _engine(weights, "cpu", use_graphs=False).generate([PROMPTS[1]], p)[0]
+    assert g.output_ids == c.output_ids and len(g.beams) == 4
+    assert abs(g.beams[0][0] - c.beams[0][0]) < 0.05 * abs(c.beams[0][0]) + 0.05
+    assert not eg._beam_of and not eg.has_work()

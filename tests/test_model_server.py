@@ -155,3 +155,18 @@ def test_router_proxies_and_balances(http_url):
         assert s.rstrip().endswith("data: [DONE]")
         st = c.get("/router/status").json()
         assert all(v == 0 for v in st["inflight"].values())
+
+
+def test_beam_search_and_count_penalties(client):
+    body = {"prompt": "beam me up", "max_tokens": 5, "ignore_eos": True, "beam_width": 3}
+    a = client.post("/v1/completions", json=body).json()
+    b = client.post("/v1/completions", json=body).json()
+    assert a["choices"][0]["text"] == b["choices"][0]["text"]
+    assert client.post("/v1/completions", json={**body, "beam_width": 99}).status_code == 422
+    g = {"prompt": "x x x", "max_tokens": 12, "ignore_eos": True, "temperature": 0.0}
+    plain = client.post("/v1/completions", json=g).json()["choices"][0]["text"]
+    pen = client.post("/v1/completions", json={**g, "frequency_penalty": 2.0,
+                                               "presence_penalty": 2.0}).json()["choices"][0]["text"]
+    assert isinstance(pen, str) and client.post(
+        "/v1/completions", json={**g, "presence_penalty": 3.0}).status_code == 422
+    assert plain != pen or len(set(plain.split())) == len(plain.split())
