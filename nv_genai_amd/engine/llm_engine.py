@@ -35,6 +35,7 @@ from .._native import rt
 from ..models.config import LlamaConfig, llama_config
 from ..models.llama import AttnMeta, LlamaModel
 from ..parallel.dist import ParallelContext, get_context
+from ..utils.faults import FaultInjector
 from ..utils.tokenizer import IncrementalDetokenizer, LLMTokenizer, llm_tokenizer
 from .beam import BeamGroup, advance
 
@@ -211,6 +212,8 @@ class LLMEngine:
         self._timeline = collections.deque(maxlen=4096)
         self._tok_host = [(hbuf(S), hbuf(S, dtype=torch.float32)) for _ in range(2)]
         self._step_reqs: List[Request] = []
+        self._faults = FaultInjector(rank=self.p.rank)   # NGA_FAULT (utils/faults.py)
+        self._nstep = 0
         self._beam_of: Dict[int, BeamGroup] = {}   # live beam seq id -> its group
         self._beam_rows: List[tuple] = []         # (row, seq id) of beam rows in this step
         self._beam_out = None
@@ -300,6 +303,9 @@ class LLMEngine:
         (``mixed_prefill_tokens``) a step carries the decode rows of every running sequence
         plus a prefill chunk, so decode rows ride on the prefill GEMMs."""
         with self.lock:
+            self._nstep += 1
+            if self._faults:
+                self._faults.check(self._nstep, "driver")
             done = self._step(between)
         return done
 
@@ -568,6 +574,9 @@ class LLMEngine:
         """Non-driver TP ranks: execute every step the driver publishes."""
         while True:
             kind, n, ntok, max_q, max_ctx, bs, nd = self._recv_step()
+            self._nstep += 1
+            if self._faults:
+                self._faults.check(self._nstep, "follower")
             if kind == -2:   # copy-on-fork pages (beam search), n pairs
                 pairs = self._bcast(torch.zeros(2 * n, dtype=torch.int32)).cpu().view(2, n)
                 self.model.copy_kv_blocks(pairs[0], pairs[1])

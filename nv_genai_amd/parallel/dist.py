@@ -102,8 +102,14 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
         kw = {}
         if backend == "nccl":
             kw["device_id"] = dev
-        dist.init_process_group(backend=backend, rank=rank, world_size=world,
-                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        # one key namespace per elastic incarnation: after a group restart (torchrun
+        # --max-restarts) the rendezvous store still holds the dead ranks' gloo/RCCL
+        # addresses, and a fresh rank must not connect to those
+        td = datetime.timedelta(seconds=timeout_s)
+        store, _, _ = next(dist.rendezvous("env://", rank, world, timeout=td))
+        store = dist.PrefixStore(f"nga{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}/", store)
+        dist.init_process_group(backend=backend, store=store, rank=rank, world_size=world,
+                                timeout=td, **kw)
     mp = tp_size * pp_size
     if world % mp != 0:
         raise ValueError(f"world size {world} not divisible by tp {tp_size} x pp {pp_size}")

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import os
 import queue
 import threading
 import time
@@ -113,7 +114,7 @@ class StreamHandle:
 
 class EngineService:
     def __init__(self, engine: LLMEngine, watchdog_s: float = 300.0, name: str = "llm",
-                 quiet_gc: bool = True):
+                 quiet_gc: bool = True, fail_fast: bool = False):
         if quiet_gc:   # no multi-ms GC pauses on the thread that launches GPU steps
             from ..utils.runtime import quiet_gc as _quiet
 
@@ -127,8 +128,24 @@ class EngineService:
         self.step_started: Optional[float] = None
         self.last_error: Optional[str] = None
         self.steps = 0
+        self.fail_fast = fail_fast
         self.thread = threading.Thread(target=self._loop, name=f"{name}-engine", daemon=True)
         self.thread.start()
+        if fail_fast:
+            threading.Thread(target=self._watchdog, name=f"{name}-watchdog", daemon=True).start()
+
+    def _watchdog(self):
+        """Model-parallel replicas: a step stuck past ``watchdog_s`` is a stuck collective (a
+        peer rank died or wedged); it cannot be cancelled in-process, so exit and let the
+        elastic agent (torchrun --max-restarts) restart the whole TP/PP group with fresh
+        RCCL communicators."""
+        while self.running:
+            time.sleep(min(1.0, self.watchdog_s / 4))
+            st = self.step_started
+            if st is not None and time.monotonic() - st > self.watchdog_s:
+                log.error("engine step stuck for %.0f s: exiting for a group restart", self.watchdog_s)
+                logging.shutdown()
+                os._exit(70)
 
     def submit(self, prompt_ids: List[int], params: SamplingParams) -> StreamHandle:
         h = StreamHandle(self)
@@ -166,6 +183,12 @@ class EngineService:
                         pass
                     h._fail(e)
                 self.handles.clear()
+                if self.fail_fast:
+                    # model-parallel: the followers' state after a failed step is unknown
+                    # (a peer may be dead) -> restart the group rather than limp on
+                    log.error("step failed in a model-parallel replica: exiting for a group restart")
+                    logging.shutdown()
+                    os._exit(70)
             finally:
                 self.step_started = None
 

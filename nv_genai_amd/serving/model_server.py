@@ -118,6 +118,14 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
                batch_delay_s: float = 0.002) -> FastAPI:
     app = FastAPI(title="nv_genai_amd model server")
     metrics = Registry()
+
+    from .engine_service import EngineError
+
+    @app.exception_handler(EngineError)
+    async def _engine_error(request: Request, exc: EngineError):
+        # a failed engine step (non-streaming request): 503 + the OpenAI error object
+        metrics.inc("engine_errors_total")
+        return JSONResponse({"error": {"message": str(exc), "type": "engine_error"}}, status_code=503)
     tracer = get_tracer("model-server")
     batcher = None
     if embed_engine is not None:

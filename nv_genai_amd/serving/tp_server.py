@@ -12,6 +12,11 @@ the other ranks execute the same forward in :meth:`LLMEngine.run_follower`, and 
 row-parallel all-reduces / vocab all-gather run over RCCL on xGMI. With ``world > tp`` the
 TP groups are data-parallel replicas, each serving on ``port + replica``.
 
+Recovery: run under ``torchrun --max-restarts N``. A rank that dies (or a driver step stuck
+past ``--watchdog-s``, which the driver turns into an exit) makes the elastic agent stop the
+group and start it again — fresh RCCL communicators, KV caches and weights — and the server
+comes back on the same port; ``NGA_FAULT`` (utils/faults.py) injects such failures.
+
 ``--pp`` splits the layers into pipeline stages (each stage optionally TP inside): stage 0
 holds the embedding + LM head and drives, activations flow stage to stage over RCCL p2p —
 for models that do not fit one TP group's HBM, e.g. ``--tp 4 --pp 2``.
@@ -36,6 +41,8 @@ def main(argv=None):
     ap.add_argument("--max-num-seqs", type=int, default=128)
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--kv-cache-fraction", type=float, default=0.5)
+    ap.add_argument("--watchdog-s", type=float, default=120.0,
+                    help="a step stuck this long exits the driver so torchrun restarts the group")
     args = ap.parse_args(argv)
     logging.basicConfig(level=os.environ.get("LOGLEVEL", "INFO").upper())
 
@@ -65,7 +72,9 @@ def main(argv=None):
         from ..engine.embed_engine import EmbeddingEngine
 
         emb = EmbeddingEngine(args.embed)
-    svc = EngineService(eng)
+    # fail fast: a stuck collective (dead / wedged peer) ends the process, and torchrun's
+    # elastic agent (--max-restarts) restarts the whole group with fresh communicators
+    svc = EngineService(eng, watchdog_s=args.watchdog_s, fail_fast=pctx.mp_size > 1)
     app = create_app(svc, emb, llm_name=f"meta/{args.llm}-instruct")
     try:
         uvicorn.run(app, host=args.host, port=args.port + pctx.dp_rank)
