@@ -77,6 +77,10 @@ LLAMA_PRESETS = {
     "llama3-8b": LlamaConfig(),
     "llama3-70b": LlamaConfig(name="llama3-70b", hidden=8192, layers=80, heads=64, kv_heads=8,
                               ffn=28672),
+    # small language model (models/NeMo/slm/slm_pretraining_sft.ipynb#cell 18: 12 layers,
+    # hidden 768) in this architecture, for training/pretrain.py
+    "slm-125m": LlamaConfig(name="slm-125m", hidden=768, layers=12, heads=12, kv_heads=12,
+                            head_dim=64, ffn=2048, rope_theta=10000.0, max_position=2048),
     # small configs with the same structure for CPU tests / smoke runs
     "llama-tiny": LlamaConfig(name="llama-tiny", vocab_size=32768, hidden=256, layers=2, heads=4,
                               kv_heads=2, head_dim=64, ffn=512, max_position=2048,

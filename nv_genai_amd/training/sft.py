@@ -91,7 +91,7 @@ class Trainer:
     """Generic loop: ``loss_fn(micro_batch) -> scalar``, trainable tensors ``named``."""
 
     def __init__(self, named: Dict[str, torch.Tensor], loss_fn, batches: Sequence, cfg: TrainConfig,
-                 group=None, ckpt_dir: Optional[str] = None, on_save=None):
+                 group=None, ckpt_dir: Optional[str] = None, on_save=None, fused: bool = False):
         import torch.distributed as dist
 
         from ..parallel.grad_sync import GradBucketer, broadcast_params
@@ -105,7 +105,8 @@ class Trainer:
         decay = [p for n, p in named.items() if p.ndim >= 2]
         nodecay = [p for n, p in named.items() if p.ndim < 2]
         self.opt = torch.optim.AdamW([{"params": decay, "weight_decay": cfg.weight_decay},
-                                      {"params": nodecay, "weight_decay": 0.0}], lr=cfg.lr, betas=cfg.betas)
+                                      {"params": nodecay, "weight_decay": 0.0}], lr=cfg.lr, betas=cfg.betas,
+                                     **({"fused": True} if fused else {}))
         self.step = 0
         self.cursor = 0
         self.ckpt_dir = ckpt_dir

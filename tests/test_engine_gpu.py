@@ -169,3 +169,21 @@ def test_beam_search_gpu_matches_cpu(gpu, weights):
     assert g.output_ids == c.output_ids and len(g.beams) == 4
     assert abs(g.beams[0][0] - c.beams[0][0]) < 0.05 * abs(c.beams[0][0]) + 0.05
     assert not eg._beam_of and not eg.has_work()
+
+
+def test_pretrain_steps_gpu_fused_adam(gpu):
+    """SLM pretraining on the GPU: bf16 autocast forward/backward, fused AdamW."""
+    from nv_genai_amd.models.config import llama_config
+    from nv_genai_amd.models.llama import LlamaModel
+    from nv_genai_amd.parallel.dist import ParallelContext
+    from nv_genai_amd.training.pretrain import init_slm, pack, pretrain_trainer
+    from nv_genai_amd.training.sft import TrainConfig
+
+    m = LlamaModel(llama_config("llama-tiny"), "cuda", pctx=ParallelContext(), seed=1)
+    init_slm(m, seed=1)
+    docs = [[(17 * i + j) % 300 + 3 for j in range(50)] for i in range(40)]
+    tr, _ = pretrain_trainer(m, pack(docs, 64, 2), TrainConfig(lr=3e-3, warmup_steps=2, max_steps=12,
+                                                               micro_batch=8, global_batch=8, log_every=0))
+    assert type(tr.opt).__name__ == "AdamW" and tr.opt.defaults.get("fused")
+    hist = tr.fit()
+    assert all(h == h for h in hist) and hist[-1] < hist[0]

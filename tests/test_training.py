@@ -223,3 +223,34 @@ def test_embedding_finetune_improves_recall():
     Fn.write_back(eng.model, params, "encoder")
     after = recall()
     assert hist[-1] < hist[0] and after > before, (before, after, hist[0], hist[-1])
+
+
+def test_pretrain_packing_loss_and_serving_handoff(tmp_path):
+    """SLM pretraining (training/pretrain.py): packed windows, loss falls from a from-scratch
+    init, the weights written back are served by the engine, and the SFT trainer takes over."""
+    from nv_genai_amd.engine.llm_engine import EngineConfig, LLMEngine, SamplingParams
+    from nv_genai_amd.training import functional as Fn
+    from nv_genai_amd.training.pretrain import init_slm, pack, pretrain_trainer
+    from nv_genai_amd.training.sft import TrainConfig, sft_trainer
+
+    w = pack([[5, 6, 7], [8, 9], [10]], 3, eos=2)
+    assert w.tolist() == [[5, 6, 7, 2], [8, 9, 2, 10]]
+    m = _llama()
+    init_slm(m, seed=0)
+    tok = CharTok()
+    docs = [tok.encode(f"the cat sat on mat number {i % 7}. ") * 3 for i in range(64)]
+    win = pack(docs, 32, 2)
+    cfg = TrainConfig(lr=3e-3, warmup_steps=4, max_steps=60, micro_batch=8, global_batch=8, log_every=0,
+                      betas=(0.9, 0.95), weight_decay=0.1)
+    tr, params = pretrain_trainer(m, win, cfg, ckpt_dir=str(tmp_path / "ck"))
+    hist = tr.fit()
+    assert min(hist[-3:]) < 0.6 * hist[0], hist
+    Fn.write_back(m, params, "llama")
+    eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=2, max_batched_tokens=256, max_model_len=256,
+                                 kv_cache_blocks=8, use_graphs=False), device="cpu", model=m, model_cfg=m.cfg)
+    prompt = tok.encode("the cat sat on mat number 3. the cat sat on ")
+    out = eng.generate([prompt], SamplingParams(temperature=0.0, max_tokens=3, ignore_eos=True))[0].output_ids
+    assert out == tok.encode("mat")                      # the pretrained model learned the corpus
+    st, _ = sft_trainer(m, tok, DATA, TrainConfig(lr=1e-3, warmup_steps=1, max_steps=2, micro_batch=4,
+                                                  global_batch=4, max_seq_len=64, log_every=0))
+    assert len(st.fit()) == 2
