@@ -51,8 +51,10 @@ class LocalChatModel:
         d = dict(self.defaults)
         for k, v in kw.items():
             if v is not None and k in ("temperature", "top_p", "max_tokens", "stop", "seed", "top_k",
-                                       "repetition_penalty", "ignore_eos", "stop_token_ids"):
-                d[k] = v
+                                       "repetition_penalty", "ignore_eos", "stop_token_ids",
+                                       "frequency_penalty", "presence_penalty", "beam_width",
+                                       "length_penalty", "response_format"):
+                d[k] = v.get("type") if k == "response_format" and isinstance(v, dict) else v
         return SamplingParams(**d)
 
     def _submit(self, messages: Messages, **kw) -> StreamHandle:

@@ -601,6 +601,7 @@ class Scheduler {
 
 void register_bm25(py::module_& m);
 void register_text(py::module_& m);
+void register_json(py::module_& m);
 
 PYBIND11_MODULE(_rt, m) {
   m.doc() = "nv_genai_amd native host runtime";
@@ -649,4 +650,5 @@ PYBIND11_MODULE(_rt, m) {
       .def("last_num_decode", &Scheduler::last_num_decode);
   register_bm25(m);
   register_text(m);
+  register_json(m);
 }

@@ -57,6 +57,7 @@ class SamplingParams:
     min_tokens: int = 0
     frequency_penalty: float = 0.0  # OpenAI semantics over generated tokens:
     presence_penalty: float = 0.0   #   logit -= freq * count + presence * (count > 0)
+    response_format: Optional[str] = None   # "json_object": grammar-constrained JSON output
     beam_width: int = 1             # > 1: beam search (engine/beam.py); sampling knobs ignored
     length_penalty: float = 1.0     # beam hypotheses score sum_logprob / len ** length_penalty
 
@@ -79,6 +80,7 @@ class Request:
     detok: Optional[IncrementalDetokenizer] = None
     cached_prefix: int = 0
     beams: List[tuple] = field(default_factory=list)   # beam search: (score, token ids, text)
+    json_state: Optional[object] = None    # _rt.JsonState of a response_format=json_object request
 
     @property
     def ttft(self) -> Optional[float]:
@@ -244,6 +246,11 @@ class LLMEngine:
         req.params = SamplingParams(**{**params.__dict__, "max_tokens": max_new})
         if self.cfg.detokenize:
             req.detok = IncrementalDetokenizer(self.tok)
+        if params.response_format == "json_object":
+            self._grammar()
+            req.json_state = rt.JsonState(True)
+        elif params.response_format not in (None, "text"):
+            raise ValueError(f"unsupported response_format {params.response_format!r}")
         with self.lock:
             self.sched.add(rid, req.prompt_ids, max_new)
             if params.beam_width > 1:
@@ -418,8 +425,10 @@ class LLMEngine:
                 self.stats["decode_tokens"] += nd
 
     def _needs_penalty_reqs(self, reqs) -> bool:
+        """Rows whose sampling needs host state (penalty history, JSON grammar)."""
         return any(r is not None and (r.params.repetition_penalty != 1.0 or r.params.frequency_penalty
-                                      or r.params.presence_penalty) for r in reqs)
+                                      or r.params.presence_penalty or r.json_state is not None)
+                   for r in reqs)
 
     def _launch(self, kind: int, n: int, ntok: int, nd: int, src) -> dict:
         """Launch a step without waiting for it. ``src = (token_idx, prev_rows)`` gathers the
@@ -668,6 +677,8 @@ class LLMEngine:
             r.first_token_time = now
             r.cached_prefix = self.sched.cached_prefix(r.id)
         r.output_ids.append(tok)
+        if r.json_state is not None:
+            self._json_grammar.advance(r.json_state, tok)
         if r.params.logprobs:
             r.logprobs.append(lp)
         if not appended:
@@ -741,6 +752,7 @@ class LLMEngine:
             v, ix = lp.topk(min(k, lp.shape[-1]), dim=-1)
             self._beam_out = (v.cpu().tolist(), ix.cpu().tolist())
         self._apply_count_penalties(logits, n)
+        self._apply_json_masks(logits, n)
         rep = self.d_pen[:n] if self._needs_penalty(n) else None
         hist = self._history(n) if rep is not None else None
         tok, lp = ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n],
@@ -753,7 +765,32 @@ class LLMEngine:
 
     def _needs_penalty(self, n) -> bool:
         return bool((self.h_pen[:n] != 1.0).any()) or any(
-            r.params.frequency_penalty or r.params.presence_penalty for r in self._step_reqs[:n])
+            r.params.frequency_penalty or r.params.presence_penalty or r.json_state is not None
+            for r in self._step_reqs[:n])
+
+    def _grammar(self):
+        g = getattr(self, "_json_grammar", None)
+        if g is None:
+            from ..utils.tokenizer import token_bytes_table
+
+            g = self._json_grammar = rt.JsonGrammar(token_bytes_table(self.tok), sorted(self.stop_ids))
+        return g
+
+    def _apply_json_masks(self, logits, n) -> None:
+        """response_format=json_object rows: logits of tokens the JSON grammar rejects from
+        the row's state become -inf before the sampling kernel (json_grammar.cpp)."""
+        if logits is None:
+            return
+        rows = [i for i, r in enumerate(self._step_reqs[:n]) if r.json_state is not None]
+        if not rows:
+            return
+        V = logits.shape[1]
+        m = np.zeros((len(rows), V), dtype=np.uint8)
+        for k, i in enumerate(rows):
+            self._json_grammar.fill_mask(self._step_reqs[i].json_state, m[k])
+        idx = torch.tensor(rows, device=logits.device)
+        bad = torch.from_numpy(m).to(logits.device) == 0
+        logits.index_copy_(0, idx, logits.index_select(0, idx).masked_fill(bad, float("-inf")))
 
     def _apply_count_penalties(self, logits, n) -> None:
         """frequency/presence penalties (OpenAI /v1/completions semantics) on the rows that

@@ -59,6 +59,7 @@ class ChatRequest(BaseModel):
     presence_penalty: float = Field(0.0, ge=-2.0, le=2.0)
     beam_width: int = Field(1, ge=1, le=16)
     length_penalty: float = 1.0
+    response_format: Optional[Dict[str, Any]] = None   # {"type": "json_object"} constrains to JSON
 
 
 class CompletionRequest(BaseModel):
@@ -77,6 +78,7 @@ class CompletionRequest(BaseModel):
     presence_penalty: float = Field(0.0, ge=-2.0, le=2.0)
     beam_width: int = Field(1, ge=1, le=16)
     length_penalty: float = 1.0
+    response_format: Optional[Dict[str, Any]] = None   # {"type": "json_object"} constrains to JSON
 
 
 class EmbeddingRequest(BaseModel):
@@ -104,7 +106,8 @@ def _params(r) -> SamplingParams:
                           stop=stop, seed=r.seed, repetition_penalty=r.repetition_penalty,
                           ignore_eos=r.ignore_eos, logprobs=getattr(r, "logprobs", False),
                           frequency_penalty=r.frequency_penalty, presence_penalty=r.presence_penalty,
-                          beam_width=r.beam_width, length_penalty=r.length_penalty)
+                          beam_width=r.beam_width, length_penalty=r.length_penalty,
+                          response_format=(r.response_format or {}).get("type"))
 
 
 def _content_text(c) -> str:

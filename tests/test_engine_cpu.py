@@ -142,3 +142,44 @@ def test_mixed_prefill_decode_steps_exact(model, async_):
         else:
             assert e.stats["mixed_steps"] == 0
     assert outs[0] == outs[1] == outs[2] == outs[3]
+
+
+@pytest.mark.parametrize("temp", [0.0, 1.0])
+def test_json_object_output_is_valid_json(model, temp):
+    """response_format=json_object: the grammar mask (csrc/runtime/json_grammar.cpp) makes
+    even a random-weight model emit one syntactically valid JSON object, then stop."""
+    import json
+
+    e = _engine(model)
+    p = SamplingParams(temperature=temp, max_tokens=120, response_format="json_object", seed=11)
+    outs = e.generate([PROMPTS[0], PROMPTS[1]], p)
+    for r in outs:
+        if r.finish_reason == "stop":
+            obj = json.loads(r.text)
+            assert isinstance(obj, dict)
+        else:   # cut by max_tokens: still a valid JSON prefix
+            from nv_genai_amd._native import rt
+
+            assert r.finish_reason == "length" and rt.JsonState(True).feed(r.text)
+    assert not e.has_work()
+
+
+def test_json_grammar_mask_semantics():
+    from nv_genai_amd._native import rt
+
+    toks = [b"{", b"}", b'"a"', b":", b" 1", b"x", b"", b'{"', b"[1]"]
+    g = rt.JsonGrammar(toks, [100])
+    import numpy as np
+
+    m = np.zeros(101, dtype=np.uint8)
+    s = rt.JsonState(True)
+    g.fill_mask(s, m)
+    # ids past the tokenizer fold onto it (i % 9), as the detokenizer does
+    assert [i for i in range(9) if m[i]] == [0, 7] and m[100] == 0   # object start only
+    for t in (0, 2, 3, 4):
+        assert g.advance(s, t)
+    g.fill_mask(s, m)
+    assert m[1] == 1 and m[5] == 0 and m[100] == 0
+    assert g.advance(s, 1) and s.done
+    g.fill_mask(s, m)
+    assert [i for i in range(101) if m[i]] == [100]         # complete: only the stop token

@@ -187,3 +187,19 @@ def test_pretrain_steps_gpu_fused_adam(gpu):
     assert type(tr.opt).__name__ == "AdamW" and tr.opt.defaults.get("fused")
     hist = tr.fit()
     assert all(h == h for h in hist) and hist[-1] < hist[0]
+
+
+def test_json_object_decoding_gpu(gpu, weights):
+    """Grammar-masked logits through the HIP sampling kernel: valid JSON object or prefix."""
+    import json
+
+    from nv_genai_amd._native import rt
+    from nv_genai_amd.engine.llm_engine import SamplingParams
+
+    e = _engine(weights, "cuda")
+    outs = e.generate(PROMPTS[:3], SamplingParams(temperature=0.8, max_tokens=96, response_format="json_object",
+                                                  seed=5))
+    for r in outs:
+        assert rt.JsonState(True).feed(r.text)
+        if r.finish_reason == "stop":
+            assert isinstance(json.loads(r.text), dict)

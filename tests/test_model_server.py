@@ -170,3 +170,16 @@ def test_beam_search_and_count_penalties(client):
     assert isinstance(pen, str) and client.post(
         "/v1/completions", json={**g, "presence_penalty": 3.0}).status_code == 422
     assert plain != pen or len(set(plain.split())) == len(plain.split())
+
+
+def test_response_format_json_object(client):
+    import json as _json
+
+    body = {"messages": [{"role": "user", "content": "give me json"}], "max_tokens": 60,
+            "response_format": {"type": "json_object"}, "seed": 1}
+    r = client.post("/v1/chat/completions", json=body).json()
+    txt = r["choices"][0]["message"]["content"]
+    if r["choices"][0]["finish_reason"] == "stop":
+        assert isinstance(_json.loads(txt), dict)
+    else:
+        assert txt.lstrip().startswith("{")
