@@ -3,6 +3,9 @@
 // and launch grid assume before launching (a malformed launch on the GPU box can fault the
 // device), and launches on PyTorch's current HIP stream so calls are hipGraph-capturable.
 #include <torch/extension.h>
+
+#include <cstdlib>
+#include <functional>
 #include <c10/hip/HIPStream.h>
 
 #include "kernels/custom_ar.h"
@@ -366,27 +369,61 @@ struct CustomAR {
   void set_two_shot_threshold(int64_t b) { impl->set_two_shot_threshold(b); }
 };
 
+// ---- debug launch checking (SURVEY.md §5.2 "stream-ordering asserts in debug builds"):
+// NGA_DEBUG_SYNC=1 checks every kernel launch and synchronises its stream right after it, so
+// an asynchronous fault is reported by the op that caused it (the HIP_LAUNCH_BLOCKING-style
+// localisation the box's no-debugger policy calls for). Streams under hipGraph capture are
+// only launch-checked. Off by default: no cost on the serving path.
+bool debug_sync() {
+  static const bool on = [] {
+    const char* e = std::getenv("NGA_DEBUG_SYNC");
+    return e != nullptr && e[0] != '\0' && e[0] != '0';
+  }();
+  return on;
+}
+
+void post_launch(const char* name) {
+  if (!debug_sync()) return;
+  hipError_t e = hipGetLastError();
+  TORCH_CHECK(e == hipSuccess, name, ": kernel launch failed: ", hipGetErrorString(e));
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+    e = hipStreamSynchronize(st);
+    TORCH_CHECK(e == hipSuccess, name, ": kernel failed on the GPU: ", hipGetErrorString(e));
+  }
+}
+
+template <typename... A>
+std::function<void(A...)> checked(const char* name, void (*f)(A...)) {
+  return [name, f](A... a) {
+    f(std::forward<A>(a)...);
+    post_launch(name);
+  };
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "nv_genai_amd gfx950 HIP kernels";
-  m.def("rmsnorm", &rmsnorm);
-  m.def("add_rmsnorm", &add_rmsnorm);
-  m.def("layernorm", &layernorm);
-  m.def("silu_mul", &silu_mul);
-  m.def("bias_gelu", &bias_gelu);
-  m.def("rope_cache", &rope_cache);
+  m.def("debug_sync", &debug_sync);
+  m.def("rmsnorm", checked("rmsnorm", &rmsnorm));
+  m.def("add_rmsnorm", checked("add_rmsnorm", &add_rmsnorm));
+  m.def("layernorm", checked("layernorm", &layernorm));
+  m.def("silu_mul", checked("silu_mul", &silu_mul));
+  m.def("bias_gelu", checked("bias_gelu", &bias_gelu));
+  m.def("rope_cache", checked("rope_cache", &rope_cache));
   m.def("decode_pages_per_part", &decode_pages_per_part);
-  m.def("decode_attention", &decode_attention);
-  m.def("prefill_attention", &prefill_attention);
-  m.def("sample", &sample);
-  m.def("score", &score);
-  m.def("topk", &topk);
-  m.def("pool_l2norm", &pool_l2norm);
-  m.def("row_sqnorm", &row_sqnorm);
-  m.def("fir_c64", &fir_c64);
-  m.def("fm_demod", &fm_demod);
-  m.def("resample_pcm", &resample_pcm);
+  m.def("decode_attention", checked("decode_attention", &decode_attention));
+  m.def("prefill_attention", checked("prefill_attention", &prefill_attention));
+  m.def("sample", checked("sample", &sample));
+  m.def("score", checked("score", &score));
+  m.def("topk", checked("topk", &topk));
+  m.def("pool_l2norm", checked("pool_l2norm", &pool_l2norm));
+  m.def("row_sqnorm", checked("row_sqnorm", &row_sqnorm));
+  m.def("fir_c64", checked("fir_c64", &fir_c64));
+  m.def("fm_demod", checked("fm_demod", &fm_demod));
+  m.def("resample_pcm", checked("resample_pcm", &resample_pcm));
   py::class_<CustomAR>(m, "CustomAllReduce")
       .def(py::init<int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("world"),
            py::arg("capacity_bytes"), py::arg("timeout_s") = 5.0)

@@ -293,3 +293,20 @@ def test_sample_odd_vocab_and_masked_logits(gpu):
     assert (tok.cpu() % 3 != 0).all()
     assert tok.cpu()[0] == tok_r[0] and torch.isfinite(lp).all()
     assert (tok.cpu() == tok_r).float().mean() >= 0.8
+
+
+def test_debug_sync_mode_checks_launches(gpu):
+    """NGA_DEBUG_SYNC=1: every kernel binding checks its launch and synchronises its stream
+    (fault localisation without a debugger); results are unchanged."""
+    import os
+    import subprocess
+    import sys
+
+    code = ("import torch; from nv_genai_amd import ops; from nv_genai_amd import _C;"
+            "x = torch.randn(64, 4096, device='cuda').bfloat16(); w = torch.ones(4096, device='cuda').bfloat16();"
+            "y = ops.rmsnorm(x, w, 1e-5); torch.cuda.synchronize();"
+            "print(_C.debug_sync(), bool(torch.isfinite(y.float()).all()))")
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, NGA_DEBUG_SYNC="1"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().endswith("True True")
