@@ -4,7 +4,7 @@ and on the GPU the top-k kernel's exactness with ties and the sampling kernel's 
 import numpy as np
 import pytest
 import torch
-from hypothesis import HealthCheck, given, settings
+from hypothesis import HealthCheck, example, given, settings
 from hypothesis import strategies as st
 
 from nv_genai_amd._native import rt
@@ -130,7 +130,8 @@ def test_topk_kernel_exact_with_ties(gpu, rows, n, k, levels):
 
 
 @pytest.mark.gpu
-@settings(max_examples=6, deadline=None)
+@settings(max_examples=10, deadline=None)
+@example(temp=1.0, top_k=5, top_p=0.8, seed=0)   # top-p inside top-k: renormalised
 @given(temp=st.sampled_from([0.5, 1.0, 1.5]), top_k=st.sampled_from([0, 5, 20]),
        top_p=st.sampled_from([1.0, 0.8, 0.5]), seed=st.integers(0, 10000))
 def test_sampling_kernel_distribution(gpu, temp, top_k, top_p, seed):
@@ -150,11 +151,13 @@ def test_sampling_kernel_distribution(gpu, temp, top_k, top_p, seed):
                         torch.zeros(B, dtype=torch.int64, device=gpu))
     p = torch.softmax(base / temp, 0).double()
     order = torch.argsort(p, descending=True)
+    # TensorRT-LLM / HF semantics: top-k first, then top-p on the renormalised top-k mass
     keep = torch.zeros(V, dtype=torch.bool)
     kmax = top_k if top_k > 0 else V
+    mass = float(p[order[:kmax]].sum())
     cum = 0.0
-    for j, t in enumerate(order.tolist()):
-        if j >= kmax or (j > 0 and cum >= top_p):
+    for j, t in enumerate(order.tolist()[:kmax]):
+        if j > 0 and cum >= top_p * mass:
             break
         keep[t] = True
         cum += float(p[t])
