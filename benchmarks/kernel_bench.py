@@ -86,6 +86,15 @@ def main():
         ws = ops.DecodeWorkspace(B, Hq, Hkv, 8192, torch.device(dev), ppp)
         us = timeit(lambda: ops.decode_attention(q, kc, vc, bt, ctx, Hq, Hkv, 8192, D ** -0.5, ws=ws))
         out[f"decode_256x1400_ppp{ppp}"] = {"us": round(us, 1), "TBps": round(B * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
+    # adaptive split at other batch sizes (max_ctx 8192 as in the captured decode graphs)
+    for Bs in (250, 64, 16, 4):
+        kc2, vc2, bt2 = paged_setup([L] * Bs, width=8192 // 64)
+        q2 = torch.randn(Bs, Hq * D, device=dev, dtype=torch.bfloat16)
+        ctx2 = torch.full((Bs,), L, dtype=torch.int32, device=dev)
+        ws = ops.DecodeWorkspace(Bs, Hq, Hkv, 8192, torch.device(dev))
+        us = timeit(lambda: ops.decode_attention(q2, kc2, vc2, bt2, ctx2, Hq, Hkv, 8192, D ** -0.5, ws=ws))
+        out[f"decode_{Bs}x1400_auto"] = {"us": round(us, 1), "parts": ws.nparts(Bs),
+                                         "TBps": round(Bs * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
     if args.only == "decode":
         print(json.dumps(out))
         return

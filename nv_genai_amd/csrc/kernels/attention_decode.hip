@@ -16,7 +16,9 @@
 //
 // Work split: grid = (seqs, kv_heads, partitions); 4 waves per workgroup stride over the
 // partition's pages; waves combine through LDS; partitions (flash-decoding split-K, used
-// when seqs*kv_heads is too small to fill 256 CUs) combine in a second small kernel.
+// when seqs*kv_heads is too small to fill 256 CUs) combine in a second small kernel. A
+// sequence's pages are divided evenly over the partitions at run time (pages_per_part only
+// sizes the grid), so the split adapts to each sequence's real context length.
 #include "common.h"
 #include "kernels.h"
 
@@ -41,8 +43,11 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   const int col = lane & 15, h = lane >> 4;
   const int ctx = ctx_lens[b];
   const int n_pages = (ctx + BS - 1) / BS;
-  const int p_begin = part * pages_per_part;
-  const int p_end = min(n_pages, p_begin + pages_per_part);
+  // each sequence's own pages split evenly over the grid's partitions, so a split sized for
+  // the batch (hipGraph-captured with the worst-case context) still divides short contexts
+  const int ppp = (n_pages + nparts - 1) / nparts;
+  const int p_begin = part * ppp;
+  const int p_end = min(n_pages, p_begin + ppp);
 
   __shared__ float o_s[NW][16][D + 4];
   __shared__ float m_s[NW][16], l_s[NW][16];

@@ -104,13 +104,17 @@ def rope_cache_(qkv, pos, cos_sin, slots, kc, vc, Hq: int, Hkv: int, D: int):
 class DecodeWorkspace:
     """Split-K partition buffers for decode attention, sized for (max_seqs, Hq, max_ctx).
 
-    The number of key partitions per (sequence, kv head) adapts to the batch: enough
-    workgroups to fill the chip (~2048 (seq, kv-head, partition) triples), but no split at
-    all once the batch alone provides them — at 256 x 1400-token sequences one partition
-    reads the KV stream 9 % faster than 16-page partitions and needs no combine kernel
-    (benchmarks/kernel_bench.py). ``pages_per_part`` fixes the split instead."""
+    The number of key partitions per (sequence, kv head) adapts to the batch: none once the
+    batch alone gives >= 4 workgroups per CU (at 256 x 1400-token sequences one partition
+    reads the KV stream 9 % faster than 16-page partitions and needs no combine kernel,
+    benchmarks/kernel_bench.py), otherwise enough to reach ~2048 workgroups. The kernel
+    divides each sequence's own pages evenly over the partitions, so the split also works
+    for hipGraphs captured with the worst-case context. ``pages_per_part`` fixes the split
+    (partitions = pages(max_ctx) / pages_per_part) instead."""
 
     TARGET_WGS = 2048
+    FILL_WGS = 1024
+    MAX_PARTS = 16
 
     def __init__(self, max_seqs: int, Hq: int, Hkv: int, max_ctx: int, device,
                  pages_per_part: Optional[int] = None):
@@ -122,14 +126,18 @@ class DecodeWorkspace:
         self.ml = torch.empty(need * Hq * 2, dtype=torch.float32, device=device)
         self.o = torch.empty(need * Hq * 128, dtype=torch.float32, device=device)
 
-    def pages_per_part(self, B: int) -> int:
-        if self.fixed:
-            return max(1, self.fixed)
-        parts = max(1, min(-(-self.TARGET_WGS // (B * self.Hkv)), max(1, self.pages // 4)))
-        return -(-self.pages // parts)
-
     def nparts(self, B: int) -> int:
-        return -(-self.pages // self.pages_per_part(B))
+        if self.fixed:
+            return -(-self.pages // max(1, self.fixed))
+        items = B * self.Hkv
+        if items >= self.FILL_WGS:
+            return 1
+        return max(1, min(-(-self.TARGET_WGS // items), self.MAX_PARTS, max(1, self.pages // 4)))
+
+    def pages_per_part(self, B: int, max_ctx: Optional[int] = None) -> int:
+        """Grid sizing for the launcher: ceil(pages(max_ctx) / nparts)."""
+        pages = (int(max_ctx if max_ctx is not None else self.max_ctx) + 63) // 64
+        return max(1, -(-pages // self.nparts(B)))
 
 
 def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, max_ctx, scale,
@@ -147,7 +155,7 @@ def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, max_ctx, scale,
         ws = DecodeWorkspace(B, Hq, Hkv, max_ctx, q.device)
     assert max_ctx <= ws.max_ctx
     kernels().decode_attention(out, q, kc, vc, block_tables, ctx_lens, Hq, Hkv, int(max_ctx),
-                               float(scale), ws.pages_per_part(B), ws.ml, ws.o)
+                               float(scale), ws.pages_per_part(B, max_ctx), ws.ml, ws.o)
     return out
 
 
