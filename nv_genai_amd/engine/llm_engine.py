@@ -518,6 +518,24 @@ class LLMEngine:
                 done.append(r)
         return done
 
+    def drain_and_run(self, fn):
+        """Run ``fn()`` with no step in flight (the pipelined step is settled first; requests
+        it finishes still get their callbacks)."""
+        with self.lock:
+            if self._pending is not None:
+                pend, self._pending = self._pending, None
+                self._finalize(pend)
+            return fn()
+
+    def broadcast_command(self, kind: int, n: int = 0) -> None:
+        """Driver of a model-parallel replica: announce a non-step command (kind <= -3) to
+        the followers, which run the hook registered for it in :meth:`run_follower` —
+        the same ordered channel as the step layouts, so collectives line up."""
+        if kind > -3:
+            raise ValueError("command kinds are <= -3 (-1 stop, -2 copy-on-fork are reserved)")
+        if self.p.mp_size > 1:
+            self._sync_step(kind, n, 0, 0, 0, 0, 0)
+
     def drain(self) -> List[Request]:
         """Settle the in-flight pipelined step (if any)."""
         with self.lock:
@@ -579,13 +597,19 @@ class LLMEngine:
         self.h_bt[:rows] = payload[o:o + rows * self.max_blocks].view(rows, self.max_blocks)
         return kind, n, ntok, max_q, max_ctx, bs, nd
 
-    def run_follower(self) -> None:
-        """Non-driver TP ranks: execute every step the driver publishes."""
+    def run_follower(self, hooks: Optional[Dict[int, Callable[[int], None]]] = None) -> None:
+        """Non-driver TP ranks: execute every step the driver publishes, and the hook for
+        each command kind (<= -3) it broadcasts (``broadcast_command``)."""
         while True:
             kind, n, ntok, max_q, max_ctx, bs, nd = self._recv_step()
             self._nstep += 1
             if self._faults:
                 self._faults.check(self._nstep, "follower")
+            if kind <= -3:
+                if not hooks or kind not in hooks:
+                    raise RuntimeError(f"follower has no hook for command {kind}")
+                hooks[kind](n)
+                continue
             if kind == -2:   # copy-on-fork pages (beam search), n pairs
                 pairs = self._bcast(torch.zeros(2 * n, dtype=torch.int32)).cpu().view(2, n)
                 self.model.copy_kv_blocks(pairs[0], pairs[1])

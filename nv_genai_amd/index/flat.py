@@ -83,11 +83,13 @@ class FlatIndex:
         self.n += m
         return ids
 
-    def add_random(self, n: int, seed: int = 0, chunk: int = 1 << 18) -> None:
-        """Fill with n random unit vectors (synthetic corpus embeddings for benchmarks)."""
+    def add_random(self, n: int, seed: int = 0, chunk: int = 1 << 18, first_id: Optional[int] = None,
+                   id_stride: int = 1) -> None:
+        """Fill with n random unit vectors (synthetic corpus embeddings for benchmarks); ids
+        are ``first_id + id_stride * i`` (a sharded index strides its global ids)."""
         g = torch.Generator(device=self.device)
         g.manual_seed(seed)
-        start = max(self._id2row.keys(), default=-1) + 1
+        start = max(self._id2row.keys(), default=-1) + 1 if first_id is None else first_id
         if self.n + n > self.capacity:
             self._alloc(self.n + n)
         for c in range(0, n, chunk):
@@ -97,10 +99,10 @@ class FlatIndex:
             r0 = self.n
             self.X[r0:r0 + m] = v.to(self.dtype)
             self.bias[r0:r0 + m] = (-ops.row_sqnorm(self.X[r0:r0 + m])) if self.metric == "l2" else 0.0
-            self.ids[r0:r0 + m] = torch.arange(start + c, start + c + m, device=self.device)
+            self.ids[r0:r0 + m] = start + id_stride * torch.arange(c, c + m, device=self.device)
             self.n += m
         base = self.n - n
-        self._id2row.update(zip(range(start, start + n), range(base, base + n)))
+        self._id2row.update(zip(range(start, start + id_stride * n, id_stride), range(base, base + n)))
 
     def _delete_row(self, r: int):
         if self.bias[r].item() != float("-inf"):

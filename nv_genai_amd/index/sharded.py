@@ -42,9 +42,10 @@ class ShardedIndex:
         self.local.add(vecs[sel], ids[sel])
 
     def add_random(self, n_total: int, seed: int = 0) -> None:
-        """Each rank generates only its own stripe of a synthetic index."""
+        """Each rank generates only its own stripe of a synthetic index; global ids are
+        striped like ``add`` (row i of rank r is id ``i * world + r``)."""
         n_local = n_total // self.world + (1 if self.rank < n_total % self.world else 0)
-        self.local.add_random(n_local, seed=seed * 1009 + self.rank)
+        self.local.add_random(n_local, seed=seed * 1009 + self.rank, first_id=self.rank, id_stride=self.world)
 
     def remove(self, ids) -> int:
         return self.local.remove(ids)

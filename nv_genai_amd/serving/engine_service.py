@@ -128,6 +128,7 @@ class EngineService:
         self.step_started: Optional[float] = None
         self.last_error: Optional[str] = None
         self.steps = 0
+        self.tasks: "queue.Queue" = queue.Queue()   # callables run on the engine thread
         self.fail_fast = fail_fast
         self.thread = threading.Thread(target=self._loop, name=f"{name}-engine", daemon=True)
         self.thread.start()
@@ -156,6 +157,32 @@ class EngineService:
             self.cv.notify()
         return h
 
+    def call(self, fn):
+        """Run ``fn()`` on the engine thread between two steps and return a Future of its
+        result. Model-parallel replicas use this for collectives that must interleave with the
+        step broadcasts in the same order on every rank (e.g. a sharded-index search, whose
+        command the followers receive through the step channel)."""
+        import concurrent.futures as cf
+
+        fut = cf.Future()
+        with self.cv:
+            self.tasks.put((fn, fut))
+            self.cv.notify()
+        return fut
+
+    def _run_tasks(self):
+        while True:
+            try:
+                fn, fut = self.tasks.get_nowait()
+            except queue.Empty:
+                return
+            if not fut.set_running_or_notify_cancel():
+                continue
+            try:
+                fut.set_result(fn())
+            except BaseException as e:  # noqa: BLE001 - delivered to the caller
+                fut.set_exception(e)
+
     def abort(self, rid: int):
         self.engine.abort(rid)
         self.handles.pop(rid, None)
@@ -163,10 +190,14 @@ class EngineService:
     def _loop(self):
         while self.running:
             with self.cv:
-                while self.running and not self.engine.has_work():
+                while self.running and not self.engine.has_work() and self.tasks.empty():
                     self.cv.wait(timeout=0.5)
             if not self.running:
                 break
+            if not self.tasks.empty():
+                self.engine.drain_and_run(self._run_tasks)
+                if not self.engine.has_work():
+                    continue
             try:
                 self.step_started = time.monotonic()
                 done = self.engine.step()

@@ -166,3 +166,54 @@ def test_all_reduce_routes_to_registered_custom_all_reduce():
     finally:
         comm.register_custom_all_reduce(group, None)
     assert comm.custom_all_reduce_for(group) is None
+
+
+def test_agent_benchmark_tp2_sharded_index(tmp_path):
+    """benchmarks/agent_tp.py on CPU (gloo): one TP=2 replica whose sharded-index searches
+    travel the engine's step channel (broadcast_command + EngineService.call) between LLM
+    steps; every scripted agent finishes and the JSON line reports it."""
+    import json
+    import subprocess
+    import sys
+
+    port = _free_port()
+    out = tmp_path / "agent.json"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", "benchmarks/agent_tp.py",
+           "--model", "llama-tiny", "--embed-model", "encoder-tiny", "--index-size", "5000",
+           "--queries", "6", "--warmup", "1", "--concurrency", "3", "--plan-tokens", "4",
+           "--extract-tokens", "4", "--answer-tokens", "6", "--max-num-seqs", "8", "--out", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=os.getcwd()))
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    res = json.loads(out.read_text())
+    assert res["parallelism"] == "tp2" and res["queries"] == 6 and res["value"] > 0
+    assert res["searches_per_s"] > 0 and res["llm_calls_per_s"] > 0
+
+
+def _sharded_ids_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from nv_genai_amd.index.sharded import ShardedIndex
+    from nv_genai_amd.parallel import dist as pd
+
+    pd.init_distributed()
+    idx = ShardedIndex(16, "cosine", "cpu")
+    idx.add_random(101, seed=3)
+    ids = idx.local.ids[: idx.local.n].tolist()
+    q.put((rank, ids, len(idx)))
+    pd.destroy()
+
+
+def test_sharded_random_ids_are_global():
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_sharded_ids_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(60)
+    all_ids = sorted(i for _, ids, _ in got for i in ids)
+    assert all_ids == list(range(101)) and all(n == 101 for _, _, n in got)
