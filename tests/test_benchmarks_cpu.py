@@ -1,0 +1,20 @@
+"""Benchmark harnesses run end to end on CPU with tiny models (their GPU numbers are in
+BASELINE.md / profiles/)."""
+import json
+import os
+import subprocess
+import sys
+
+
+def test_multi_turn_benchmark_cpu(tmp_path):
+    out = tmp_path / "mt.json"
+    r = subprocess.run([sys.executable, "benchmarks/multi_turn.py", "--model", "llama-tiny", "--embed-model",
+                        "encoder-tiny", "--index-size", "3000", "--sessions", "3", "--turns", "3",
+                        "--warmup-sessions", "1", "--max-tokens", "5", "--out", str(out)],
+                       capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=os.getcwd()))
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    # every turn wrote two memory entries; later turns retrieve history
+    assert res["memory_entries"] == 2 * (1 * 3 + 3 * 3) and res["history_hits_per_turn"] > 0
+    assert res["value"] > 0 and res["turns"] == 3
