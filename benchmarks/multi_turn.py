@@ -11,8 +11,9 @@ reference chain:
 5. write "User previously responded with ..." and "Agent previously responded with ..." back
    into ``conv_store``: embed both passages and insert them into the index and the docstore.
 
-The memory index therefore grows while the benchmark runs. Searches and inserts share one
-lock; the LLM engine steps on its own thread (``EngineService``). Rank 0 prints one JSON line
+The memory index therefore grows while the benchmark runs. One retrieval worker owns the
+encoder and both indexes and serves queued queries and memory writes in batches on its own
+HIP stream; the LLM engine steps on its own thread (``EngineService``). Rank 0 prints one JSON line
 with turns/s and the p50/p95 turn latency.
 """
 from __future__ import annotations
@@ -27,6 +28,14 @@ import time
 from concurrent.futures import ThreadPoolExecutor
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def parse(argv=None):
@@ -79,15 +88,69 @@ def main(argv=None):
     stats = {"prompt_tokens": 0, "output_tokens": 0, "history_hits": 0}
     ttft = []
 
+    # One retrieval worker owns the encoder and both indexes: it drains queued memory writes
+    # and queries in batches on its own HIP stream, so retrieval neither queues behind the
+    # engine's in-flight step nor serialises the sessions one GPU round-trip at a time.
+    import concurrent.futures as cf
+    import queue as _queue
+
+    work: "_queue.Queue" = _queue.Queue()
+    rstream = torch.cuda.Stream(device=dev) if gpu else None
+
+    def retrieval_worker():
+        while True:
+            items = [work.get()]
+            if items[0] is None:
+                return
+            time.sleep(0.002)                      # let a batch form
+            while True:
+                try:
+                    items.append(work.get_nowait())
+                except _queue.Empty:
+                    break
+            stop = any(it is None for it in items)
+            items = [it for it in items if it is not None]
+            writes = [it for it in items if it[0] == "write"]
+            reads = [it for it in items if it[0] == "read"]
+            try:
+                serve(writes, reads)
+            except BaseException as e:  # noqa: BLE001 - fail the waiting turns, never hang them
+                for it in writes + reads:
+                    if not it[2].done():
+                        it[2].set_exception(e)
+            if stop:
+                return
+
+    def serve(writes, reads):
+            ctxmgr = torch.cuda.stream(rstream) if gpu else _nullctx()
+            with ctxmgr:
+                if writes:
+                    texts = [t for w in writes for t in w[1]]
+                    v = emb.embed(texts, input_type="passage")
+                    new = conv_docs.new_ids(len(texts))
+                    conv_docs.add(new, texts)
+                    conv_index.add(v, torch.tensor(new))
+                    for w in writes:
+                        w[2].set_result(None)
+                if reads:
+                    q = emb.embed([r[1] for r in reads], input_type="query")
+                    _, di = docs_index.search(q, args.top_k)
+                    hi = conv_index.search(q, args.top_k)[1] if len(conv_index) else None
+                    di = di.cpu().tolist()
+                    hi = None if hi is None else hi.cpu().tolist()
+                    for j, r in enumerate(reads):
+                        ctx = "".join(docs.get(int(i)) + "\n\n" for i in di[j] if int(i) >= 0)
+                        hist = "" if hi is None else "".join(conv_docs.get(int(i)) + "\n\n" for i in hi[j] if int(i) >= 0)
+                        r[2].set_result((ctx, hist, 0 if hi is None else sum(int(i) >= 0 for i in hi[j])))
+
+    worker = threading.Thread(target=retrieval_worker, daemon=True)
+    worker.start()
+
     def turn(question: str) -> float:
         t = time.perf_counter()
-        with lock:
-            q = emb.embed([question], input_type="query")
-            _, di = docs_index.search(q, args.top_k)
-            hv, hi = conv_index.search(q, args.top_k) if len(conv_index) else (None, None)
-            ctx = "".join(docs.get(int(i)) + "\n\n" for i in di[0].tolist() if int(i) >= 0)
-            hist = "" if hi is None else "".join(conv_docs.get(int(i)) + "\n\n" for i in hi[0].tolist()
-                                                  if int(i) >= 0)
+        fut = cf.Future()
+        work.put(("read", question, fut))
+        ctx, hist, nh = fut.result()
         prompt = (template.replace("{input}", question).replace("{history}", hist)
                   .replace("{context}", ctx)) + "User Query: " + question
         ids = tok.apply_chat_template([{"role": "user", "content": prompt}])
@@ -95,14 +158,13 @@ def main(argv=None):
         answer = h.text()
         r = h.request
         mem = [f"User previously responded with {question}", f"Agent previously responded with {answer}"]
+        wf = cf.Future()
+        work.put(("write", mem, wf))
+        wf.result()                                # the next turn sees this turn's memory
         with lock:
-            v = emb.embed(mem, input_type="passage")
-            new = conv_docs.new_ids(2)
-            conv_docs.add(new, mem)
-            conv_index.add(v, torch.tensor(new))
             stats["prompt_tokens"] += len(ids)
             stats["output_tokens"] += len(r.output_ids)
-            stats["history_hits"] += 0 if hi is None else int((hi >= 0).sum())
+            stats["history_hits"] += nh
             if r.ttft is not None:
                 ttft.append(r.ttft)
         return time.perf_counter() - t
@@ -126,6 +188,8 @@ def main(argv=None):
     elapsed = time.perf_counter() - t1
     t_max = pd.all_reduce_max(elapsed)
     svc.shutdown()
+    work.put(None)
+    worker.join(timeout=30)
     n_turns = args.sessions * args.turns * pctx.world_size
     lat.sort()
     res = {"metric": "multi-turn RAG turns/s + p50 latency (conversation-memory retriever)",
