@@ -42,7 +42,7 @@ def main():
     import argparse
 
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="", help="prefill | decode | sample | search (default: all)")
+    ap.add_argument("--only", default="", help="rope | prefill | decode | sample | search (default: all)")
     ap.add_argument("--iters", type=int, default=20)
     args = ap.parse_args()
     global timeit
@@ -51,6 +51,24 @@ def main():
     dev = "cuda"
     Hq, Hkv, D = 32, 8, 128
     out = {}
+    if args.only in ("", "rope"):
+        cs = ops.rope_cos_sin(8192, D).to(dev)
+        nb = 4096
+        kc = torch.zeros(nb, Hkv, 64, D, device=dev, dtype=torch.bfloat16)
+        vc = torch.zeros(nb, Hkv, D, 64, device=dev, dtype=torch.bfloat16)
+        for T, contiguous in ((1536, True), (256, False)):
+            qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
+            pos = torch.arange(T, dtype=torch.int32, device=dev) % 4096
+            slots = (torch.arange(T, device=dev) if contiguous
+                     else torch.randperm(nb, device=dev)[:T] * 64 + 17).to(torch.int32)
+            us = timeit(lambda: ops.rope_cache_(qkv, pos, cs, slots, kc, vc, Hq, Hkv, D))
+            moved = T * (Hq + 2 * Hkv) * D * 2 + T * (Hq + Hkv) * D * 2 + 2 * T * Hkv * D * 2
+            out[f"rope_cache_T{T}_{'prefill' if contiguous else 'decode'}"] = {
+                "us": round(us, 1), "TBps": round(moved / us / 1e6, 2)}
+        del kc, vc
+        if args.only == "rope":
+            print(json.dumps(out))
+            return
     if args.only in ("", "search"):
         N, Dx = 1_000_000, 1024
         X = torch.nn.functional.normalize(torch.randn(N, Dx, device=dev), dim=1).to(torch.bfloat16)

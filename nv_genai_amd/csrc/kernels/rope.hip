@@ -64,10 +64,89 @@ __global__ void rope_cache_kernel(uint16_t* __restrict__ qkv, const int32_t* __r
   }
 }
 
+// Tiled form for multi-token steps: grid = (token tiles of 64, Hq + 2*Hkv heads). A q/k head
+// block rotates its 64 tokens with 16-B loads/stores (8-element chunks of each half, cos/sin
+// as two float4 pairs) and writes k heads to the K cache; a v head block stages the 64 tokens
+// x D tile in LDS and writes the transposed page rows with lanes = tokens, so the consecutive
+// slots of a prefill chunk become one 128-B store per d row instead of 64 scattered 2-B ones
+// per token (the per-token kernel above wrote Vt at ~2 TB/s effective).
+constexpr int RT = 64;  // tokens per tile
+
+template <int D>
+__global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
+    uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos, const float* __restrict__ cos_sin,
+    const int32_t* __restrict__ slots, uint16_t* __restrict__ kc, uint16_t* __restrict__ vc,
+    int64_t T, int Hq, int Hkv, int BS) {
+  constexpr int HALF = D / 2;
+  constexpr int CH = HALF / 8;       // 8-element chunks per half
+  constexpr int LDP = D + 2;         // padded LDS row (bank-conflict-free column reads)
+  __shared__ uint16_t tile[RT * LDP];
+  const int64_t t0 = (int64_t)blockIdx.x * RT;
+  const int h = blockIdx.y;
+  const int64_t row = (int64_t)(Hq + 2 * Hkv) * D;
+  if (h < Hq + Hkv) {
+    for (int i = threadIdx.x; i < RT * CH; i += blockDim.x) {
+      const int64_t t = t0 + i / CH;
+      if (t >= T) break;
+      const int i0 = (i % CH) * 8;
+      uint16_t* x = qkv + t * row + (int64_t)h * D;
+      const float* cs = cos_sin + (int64_t)pos[t] * D;
+      const u16x8 a = load8(x + i0), b = load8(x + HALF + i0);
+      const float4 c0 = *reinterpret_cast<const float4*>(cs + i0);
+      const float4 c1 = *reinterpret_cast<const float4*>(cs + i0 + 4);
+      const float4 s0 = *reinterpret_cast<const float4*>(cs + HALF + i0);
+      const float4 s1 = *reinterpret_cast<const float4*>(cs + HALF + i0 + 4);
+      const float c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      u16x8 oa, ob;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x1 = bf2f(a[j]), x2 = bf2f(b[j]);
+        oa[j] = f2bf(x1 * c[j] - x2 * sn[j]);
+        ob[j] = f2bf(x2 * c[j] + x1 * sn[j]);
+      }
+      store8(x + i0, oa);
+      store8(x + HALF + i0, ob);
+      const int slot = (slots && h >= Hq) ? slots[t] : -1;
+      if (slot >= 0) {
+        uint16_t* dst = kc + (((int64_t)(slot / BS) * Hkv + (h - Hq)) * BS + slot % BS) * D;
+        store8(dst + i0, oa);
+        store8(dst + HALF + i0, ob);
+      }
+    }
+    return;
+  }
+  if (slots == nullptr) return;
+  const int vh = h - Hq - Hkv;
+  // stage V[t0:t0+64, vh, :] (4-byte pairs; padded rows keep 4-B alignment)
+  for (int i = threadIdx.x; i < RT * (D / 2); i += blockDim.x) {
+    const int r = i / (D / 2), c2 = i % (D / 2);
+    const int64_t t = t0 + r;
+    uint32_t v = 0;
+    if (t < T) v = *reinterpret_cast<const uint32_t*>(qkv + t * row + (int64_t)(Hq + Hkv + vh) * D + 2 * c2);
+    *reinterpret_cast<uint32_t*>(tile + r * LDP + 2 * c2) = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int64_t t = t0 + lane;
+  const int slot = t < T ? slots[t] : -1;
+  if (slot < 0) return;
+  uint16_t* dst = vc + ((int64_t)(slot / BS) * Hkv + vh) * D * BS + slot % BS;
+  for (int d = w; d < D; d += nw) dst[(int64_t)d * BS] = tile[lane * LDP + d];
+}
+
 void launch_rope_cache(uint16_t* qkv, const int32_t* pos, const float* cos_sin,
                        const int32_t* slots, uint16_t* kc, uint16_t* vc, int64_t T, int Hq,
                        int Hkv, int D, int BS, hipStream_t stream) {
   if (T == 0) return;
+  if (T >= RT) {
+    dim3 grid((unsigned)((T + RT - 1) / RT), (unsigned)(Hq + 2 * Hkv)), block(256);
+    if (D == 128)
+      rope_cache_tiled_kernel<128><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS);
+    else if (D == 64)
+      rope_cache_tiled_kernel<64><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS);
+    return;
+  }
   dim3 grid((unsigned)T), block(256);
   if (D == 128)
     rope_cache_kernel<128><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, BS);

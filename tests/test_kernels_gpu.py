@@ -54,13 +54,15 @@ def _make_cache(nb, Hkv, D, dev):
     return kc, vc
 
 
-def test_rope_cache(gpu):
+@pytest.mark.parametrize("Hq,Hkv,D,T", [(32, 8, 128, 70), (32, 8, 128, 7), (32, 8, 128, 300), (4, 2, 64, 130)])
+def test_rope_cache(gpu, Hq, Hkv, D, T):
+    """per-token kernel (T < 64) and tiled kernel (T >= 64: LDS-transposed Vt page rows),
+    random slots with a padding row (-1)."""
     torch.manual_seed(2)
-    Hq, Hkv, D, T = 32, 8, 128, 70
     qkv = _bf(T, (Hq + 2 * Hkv) * D, dev=gpu)
     pos = torch.randint(0, 4000, (T,), dtype=torch.int32, device=gpu)
     cs = ops.rope_cos_sin(4096, D).to(gpu)
-    nb = 8
+    nb = (T + 63) // 64 + 4
     kc, vc = _make_cache(nb, Hkv, D, gpu)
     slots = torch.randperm(nb * 64, device=gpu)[:T].to(torch.int32)
     slots[5] = -1
