@@ -66,27 +66,30 @@ def main():
     ids, pos = ids.to(dev), pos.to(dev)
     sample_idx = (cu[1:] - 1).long().to(dev)
 
-    def run(split):
-        m.split_mixed = split
+    modes = {"fused": (False, False), "fused_concurrent_attn": (False, True), "split": (True, False)}
+
+    def run(mode):
+        m.split_mixed, m.concurrent_attention = modes[mode]
         return m.forward(ids, pos, meta, sample_idx)
 
     out = {}
-    ref = run(False).float()
-    got = run(True).float()
-    torch.cuda.synchronize()
-    out["max_abs_diff"] = float((ref - got).abs().max())
+    ref = run("fused").float()
+    for mode in ("fused_concurrent_attn", "split"):
+        got = run(mode).float()
+        torch.cuda.synchronize()
+        out[f"max_abs_diff_{mode}"] = float((ref - got).abs().max())
     out["ref_abs_max"] = float(ref.abs().max())
-    for split in (False, True, False, True):
+    for mode in list(modes) * 2:
         for _ in range(2):
-            run(split)
+            run(mode)
         torch.cuda.synchronize()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         for _ in range(args.iters):
-            run(split)
+            run(mode)
         b.record()
         torch.cuda.synchronize()
-        out[f"{'split' if split else 'fused'}_ms"] = round(a.elapsed_time(b) / args.iters, 3)
+        out[f"{mode}_ms"] = round(a.elapsed_time(b) / args.iters, 3)
     out.update(decode=B, ctx=L, prefill=pre, tokens=T)
     print(json.dumps(out), flush=True)
 

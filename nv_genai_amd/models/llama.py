@@ -18,6 +18,7 @@ row) go through the final norm and the vocab-parallel LM head (+ all-gather, CC4
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -79,6 +80,10 @@ class LlamaModel:
         self.cos_sin = ops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta,
                                         cfg.rope_scaling).to(self.device)
         self.split_mixed = False   # mixed steps on two streams (forward_split)
+        # mixed steps: prefill attention on a side stream, concurrent with the decode
+        # attention (HBM-bound, spare MFMA issue slots) on the main stream
+        self.concurrent_attention = os.environ.get("NGA_CONCURRENT_ATTN", "1") != "0"
+        self._attn_stream = None
         self._aux = None
         # sequence parallelism for TP prefill: norms and residual on T / tp rows, reduce-
         # scatter + all-gather instead of all-reduce (SURVEY.md §2.E "SP", §5.7)
@@ -224,13 +229,29 @@ class LlamaModel:
         if meta.kind == "mixed":
             nd = meta.n_decode
             attn = torch.empty(T, qdim, dtype=qkv.dtype, device=qkv.device)
+
+            def prefill():
+                ops.prefill_attention_paged(q[nd:], self.k_cache[li], self.v_cache[li],
+                                            meta.block_tables[nd:], meta.cu_q_prefill,
+                                            meta.ctx_lens[nd:], hq, hkv, D, meta.max_q_len,
+                                            self.scale, out=attn[nd:])
+
+            side = None
+            if self.concurrent_attention and qkv.is_cuda and not torch.cuda.is_current_stream_capturing():
+                if self._attn_stream is None:
+                    self._attn_stream = torch.cuda.Stream(qkv.device)
+                side = self._attn_stream
+                main = torch.cuda.current_stream(qkv.device)
+                side.wait_stream(main)           # q / K / V pages written on main
+                with torch.cuda.stream(side):
+                    prefill()
             ops.decode_attention(q[:nd], self.k_cache[li], self.v_cache[li],
                                  meta.block_tables[:nd], meta.ctx_lens[:nd], hq, hkv,
                                  meta.max_ctx, self.scale, out=attn[:nd], ws=meta.decode_ws)
-            ops.prefill_attention_paged(q[nd:], self.k_cache[li], self.v_cache[li],
-                                        meta.block_tables[nd:], meta.cu_q_prefill,
-                                        meta.ctx_lens[nd:], hq, hkv, D, meta.max_q_len,
-                                        self.scale, out=attn[nd:])
+            if side is not None:
+                main.wait_stream(side)           # attn (allocated on main) complete
+            else:
+                prefill()
             return attn
         return ops.prefill_attention_paged(q, self.k_cache[li], self.v_cache[li],
                                            meta.block_tables, meta.cu_q, meta.ctx_lens,
