@@ -335,6 +335,24 @@ void resample_pcm(Tensor x, Tensor h, int64_t down, int64_t pre, double gain, c1
                            (int)pre, (int)nout, (float)gain, fp, ip, cur_stream(x));
 }
 
+// ---- FP8 W8A8: row-wise activation quantisation (mode 0: x; mode 1: silu(gate) * up)
+void quant_fp8_rows(Tensor x, int64_t mode, Tensor y, Tensor scale) {
+  CHECK_BF16(x);
+  CHECK_DEV(y); CHECK_CONTIG(y); CHECK_DEV(scale); CHECK_CONTIG(scale);
+  TORCH_CHECK(y.scalar_type() == at::kFloat8_e4m3fn, "quant_fp8_rows: y must be float8_e4m3fn");
+  CHECK_DT(scale, at::kFloat);
+  TORCH_CHECK(mode == 0 || mode == 1, "quant_fp8_rows: mode 0 (x) or 1 (silu(gate) * up)");
+  TORCH_CHECK(x.dim() == 2 && y.dim() == 2 && x.stride(1) == 1, "quant_fp8_rows: 2-D, unit column stride");
+  const int64_t rows = x.size(0);
+  const int64_t H = mode == 0 ? x.size(1) : x.size(1) / 2;
+  TORCH_CHECK(mode == 0 || x.size(1) % 2 == 0, "quant_fp8_rows: SwiGLU input must be [rows, 2F]");
+  TORCH_CHECK(H % 8 == 0 && x.stride(0) % 8 == 0, "quant_fp8_rows: H and the row stride must be multiples of 8");
+  TORCH_CHECK(y.size(0) >= rows && y.size(1) == H, "quant_fp8_rows: y must be [>= rows, H]");
+  TORCH_CHECK(scale.numel() >= rows, "quant_fp8_rows: scale must hold one value per row");
+  nga::launch_quant_fp8_rows(bfp(x), x.stride(0), rows, (int)H, (int)mode,
+                             reinterpret_cast<uint8_t*>(y.data_ptr()), scale.data_ptr<float>(), cur_stream(x));
+}
+
 // ---- custom all-reduce over IPC peer buffers (TP decode)
 struct CustomAR {
   std::unique_ptr<nga::CustomAllReduce> impl;
@@ -424,6 +442,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("fir_c64", checked("fir_c64", &fir_c64));
   m.def("fm_demod", checked("fm_demod", &fm_demod));
   m.def("resample_pcm", checked("resample_pcm", &resample_pcm));
+  m.def("quant_fp8_rows", checked("quant_fp8_rows", &quant_fp8_rows));
   py::class_<CustomAR>(m, "CustomAllReduce")
       .def(py::init<int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("world"),
            py::arg("capacity_bytes"), py::arg("timeout_s") = 5.0)

@@ -81,5 +81,7 @@ void launch_fm_demod(const float* x, int n, float prev_re, float prev_im, int ha
                      hipStream_t stream);
 void launch_resample_pcm(const float* x, int n, const float* h, int nh, int down, int pre, int nout,
                          float gain, float* yf, int16_t* yi, hipStream_t stream);
+void launch_quant_fp8_rows(const uint16_t* x, int64_t ldx, int64_t rows, int H, int mode, uint8_t* y,
+                           float* scale, hipStream_t stream);
 
 }  // namespace nga

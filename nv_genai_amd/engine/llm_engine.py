@@ -113,6 +113,7 @@ class EngineConfig:
     mixed_max_wait: int = 4       # ... unless the oldest waiting request waited this many steps
     tuned_gemms: bool = True   # load the per-shape hipBLASLt/rocBLAS table (ops/gemm_tuning.py)
     sequence_parallel: bool = False  # TP prefill >= sp_min_tokens: reduce-scatter/all-gather
+    fp8: bool = False   # W8A8 FP8 projections (LlamaModel.quantize_fp8); KV cache stays bf16
     sp_min_tokens: int = 512
 
 
@@ -132,7 +133,9 @@ class LLMEngine:
         self.device = torch.device(device)
         self.mcfg = model_cfg or llama_config(cfg.model, max_position=max(cfg.max_model_len, 256))
         self.model = model or LlamaModel(self.mcfg, self.device, pctx=self.p, seed=cfg.seed,
-                                         weights=weights)
+                                         weights=weights, fp8=cfg.fp8)
+        if cfg.fp8 and not self.model.fp8:
+            self.model.quantize_fp8()
         self.model.sequence_parallel = cfg.sequence_parallel
         self.model.sp_min_tokens = cfg.sp_min_tokens
         self.tok = tokenizer or llm_tokenizer()

@@ -50,7 +50,7 @@ class AttnMeta:
 class LlamaModel:
     def __init__(self, cfg: LlamaConfig, device="cuda", dtype=torch.bfloat16,
                  pctx: Optional[ParallelContext] = None, seed: int = 0,
-                 weights: Optional[Dict[str, torch.Tensor]] = None):
+                 weights: Optional[Dict[str, torch.Tensor]] = None, fp8: bool = False):
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
@@ -90,6 +90,36 @@ class LlamaModel:
         self.sequence_parallel = False
         self.sp_min_tokens = 512
         self.sp_steps = 0
+        self.fp8 = False
+        if fp8:
+            self.quantize_fp8()
+
+    # ------------------------------------------------------------------ FP8 (W8A8)
+    _LINEARS = ("wqkv", "wo", "wgu", "wd")
+
+    def quantize_fp8(self) -> None:
+        """W8A8 serving mode (the engine's int8/fp8 precision knob, TRT-LLM
+        ``mistral-7b.yaml:34-35``; here OCP e4m3fn, gfx950's native FP8): the four projection
+        weights of every layer become FP8 with one scale per output channel and the bf16 copies
+        are freed; activations are quantised per token row by ``ops.quant_fp8_rows`` and the
+        GEMMs run as row-scaled hipBLASLt FP8 GEMMs. Embedding, LM head, norms, attention and
+        the KV cache stay bf16."""
+        if self.fp8:
+            return
+        for L in self.layers:
+            for n in self._LINEARS:
+                L[n + "8"], L[n + "_s"] = ops.quantize_weight_fp8(L.pop(n))
+        self.fp8 = True
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
+
+    def _lin(self, x: torch.Tensor, L: dict, name: str, swiglu: bool = False) -> torch.Tensor:
+        """x @ W^T for projection ``name`` (bf16, or FP8 W8A8 when quantised); ``swiglu``:
+        x is the [M, 2F] gate|up output and the projection consumes silu(gate) * up."""
+        if not self.fp8:
+            return (ops.silu_mul(x) if swiglu else x) @ L[name].t()
+        x8, sx = ops.quant_fp8_rows(x, mode=1 if swiglu else 0)
+        return ops.fp8_linear(x8, sx, L[name + "8"], L[name + "_s"], x.shape[0])
 
     # ------------------------------------------------------------------ weights
     def _random_init(self, seed: int):
@@ -169,6 +199,8 @@ class LlamaModel:
     def state_dict(self) -> Dict[str, torch.Tensor]:
         """HF-named weights of this rank (unfused; TP shards are local slices; a pipeline
         stage holds only its layers, plus embedding and LM head on stage 0)."""
+        if self.fp8:
+            raise RuntimeError("state_dict of an FP8-quantised model: export the bf16 model before quantize_fp8()")
         out = {"model.norm.weight": self.final_norm}
         if self.first_stage:
             out["model.embed_tokens.weight"] = self.embed
@@ -273,14 +305,13 @@ class LlamaModel:
         a TP partial sum — which the caller reduces into resid with the next layer's (or
         the final) norm."""
         L = self.layers[li]
-        qkv = x @ L["wqkv"].t()
+        qkv = self._lin(x, L, "wqkv")
         ops.rope_cache_(qkv, pos, self.cos_sin, meta.slots, self.k_cache[li],
                         self.v_cache[li], self.hq, self.hkv, self.D)
         attn = self._attention(qkv[:, :self.hq * self.D], qkv, li, meta, x.shape[0])
-        o = attn @ L["wo"].t()
+        o = self._lin(attn, L, "wo")
         x = self._reduce_add_norm(o, resid, L["mlp_norm"])
-        h = ops.silu_mul(x @ L["wgu"].t())
-        return h @ L["wd"].t()
+        return self._lin(self._lin(x, L, "wgu"), L, "wd", swiglu=True)
 
     def _stack(self, resid, pos, meta: AttnMeta, sample_idx: Optional[torch.Tensor]):
         cfg = self.cfg
@@ -346,14 +377,14 @@ class LlamaModel:
         for li in range(n):
             L = self.layers[li]
             xf = tp_all_gather_rows(x, p)
-            qkv = xf @ L["wqkv"].t()
+            qkv = self._lin(xf, L, "wqkv")
             ops.rope_cache_(qkv, pos, self.cos_sin, meta.slots, self.k_cache[li],
                             self.v_cache[li], self.hq, self.hkv, self.D)
             attn = self._attention(qkv[:, :self.hq * self.D], qkv, li, meta, Tp)
-            o = tp_reduce_scatter_rows(attn @ L["wo"].t(), p).contiguous()
+            o = tp_reduce_scatter_rows(self._lin(attn, L, "wo"), p).contiguous()
             x = ops.add_rmsnorm(resid, o, L["mlp_norm"], cfg.eps)
-            hmid = ops.silu_mul(tp_all_gather_rows(x, p) @ L["wgu"].t())
-            d = tp_reduce_scatter_rows(hmid @ L["wd"].t(), p).contiguous()
+            gu = self._lin(tp_all_gather_rows(x, p), L, "wgu")
+            d = tp_reduce_scatter_rows(self._lin(gu, L, "wd", swiglu=True), p).contiguous()
             if li + 1 < n:
                 x = ops.add_rmsnorm(resid, d, self.layers[li + 1]["attn_norm"], cfg.eps)
         out = tp_all_gather_rows(ops.add_rmsnorm(resid, d, self.final_norm, cfg.eps), p)[:T]

@@ -202,6 +202,46 @@ def sample(logits, temperature, top_k, top_p, seeds, steps, rep_penalty=None, hi
     return out_tok, out_lp
 
 
+# ------------------------------------------------------------------------- FP8 W8A8
+FP8 = torch.float8_e4m3fn
+FP8_MAX = 448.0
+
+
+def quant_fp8_rows(x: torch.Tensor, mode: int = 0, pad_to: int = 16):
+    """Row-wise FP8 quantisation of a GEMM input: mode 0 quantises x [M, H]; mode 1 the
+    SwiGLU of x [M, 2F] = [gate | up]. Returns (y [Mp, H] e4m3fn, scale [Mp, 1] fp32) with M
+    padded to ``pad_to`` rows (zero rows, scale 1) for the FP8 GEMM's tile constraints."""
+    M = x.shape[0]
+    H = x.shape[1] if mode == 0 else x.shape[1] // 2
+    Mp = -(-max(M, 1) // pad_to) * pad_to
+    if not _gpu(x):
+        return ref.quant_fp8_rows(x, mode, Mp)
+    y = torch.empty(Mp, H, dtype=FP8, device=x.device)
+    s = torch.empty(Mp, 1, dtype=torch.float32, device=x.device)
+    if Mp > M:
+        y[M:].view(torch.uint8).zero_()
+        s[M:].fill_(1.0)
+    kernels().quant_fp8_rows(x, int(mode), y, s)
+    return y, s
+
+
+def quantize_weight_fp8(w: torch.Tensor):
+    """[N, K] -> (e4m3fn [N, K], per-output-channel scale [1, N] fp32)."""
+    wf = w.float()
+    s = wf.abs().amax(1, keepdim=True).clamp_min(1e-12) / FP8_MAX
+    w8 = (wf / s).clamp(-FP8_MAX, FP8_MAX).to(FP8)
+    return w8.contiguous(), s.t().contiguous()
+
+
+def fp8_linear(x8: torch.Tensor, sx: torch.Tensor, w8: torch.Tensor, sw: torch.Tensor, M: int) -> torch.Tensor:
+    """bf16 [M, N] = (x8 * sx) @ (w8 * sw^T)^T: a row-scaled hipBLASLt FP8 GEMM on the GPU."""
+    if x8.is_cuda:
+        y = torch._scaled_mm(x8, w8.t(), scale_a=sx, scale_b=sw, out_dtype=torch.bfloat16)
+    else:
+        y = ((x8.float() * sx) @ (w8.float() * sw.t()).t()).to(torch.bfloat16)
+    return y[:M]
+
+
 # ------------------------------------------------------------------------- vector search
 def score(Q, X, row_bias=None, dot_scale: float = 1.0, out=None):
     if not _gpu(X):

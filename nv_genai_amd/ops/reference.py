@@ -289,3 +289,19 @@ def resample_pcm(x, h, down, pre, nout, gain):
     y = (gain * y).float()
     pcm = (y * 32768.0).clamp(-32768.0, 32767.0).to(torch.int16)
     return y, pcm
+
+
+def quant_fp8_rows(x, mode: int, Mp: int):
+    """fp32 reference of the row-wise FP8 quantiser (kernels/quant.hip)."""
+    xf = x.float()
+    if mode == 1:
+        F = xf.shape[1] // 2
+        g, u = xf[:, :F], xf[:, F:]
+        xf = g / (1.0 + torch.exp(-g)) * u
+    M, H = xf.shape
+    s = xf.abs().amax(1, keepdim=True).clamp_min(1e-12) / 448.0
+    y = torch.zeros(Mp, H, dtype=torch.float8_e4m3fn)
+    y[:M] = (xf / s).clamp(-448.0, 448.0).to(torch.float8_e4m3fn)
+    sp = torch.ones(Mp, 1)
+    sp[:M] = s
+    return y, sp

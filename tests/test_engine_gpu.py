@@ -203,3 +203,27 @@ def test_json_object_decoding_gpu(gpu, weights):
         assert rt.JsonState(True).feed(r.text)
         if r.finish_reason == "stop":
             assert isinstance(json.loads(r.text), dict)
+
+
+def test_fp8_engine_gpu(gpu, weights):
+    """W8A8 FP8 engine: prefill logits close to the bf16 engine, hipGraph decode == eager."""
+    from nv_genai_amd.engine.llm_engine import SamplingParams
+
+    def first_logits(e):
+        cap = {}
+        orig = e._sample
+
+        def sample(logits, n):
+            cap.setdefault("lg", logits[:n].float().cpu())
+            return orig(logits, n)
+        e._sample = sample
+        e.generate([PROMPTS[0]], SamplingParams(temperature=0.0, max_tokens=1, ignore_eos=True))
+        return cap["lg"]
+
+    a = first_logits(_engine(weights, "cuda", use_graphs=False))
+    b = first_logits(_engine(weights, "cuda", use_graphs=False, fp8=True))
+    assert float((a - b).norm() / a.norm()) < 0.1
+    p = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
+    g = [r.output_ids for r in _engine(weights, "cuda", fp8=True).generate(PROMPTS[:3], p)]
+    e = [r.output_ids for r in _engine(weights, "cuda", fp8=True, use_graphs=False).generate(PROMPTS[:3], p)]
+    assert g == e

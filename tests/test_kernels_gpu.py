@@ -312,3 +312,33 @@ def test_debug_sync_mode_checks_launches(gpu):
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().endswith("True True")
+
+
+@pytest.mark.parametrize("mode,M,H", [(0, 37, 4096), (1, 19, 14336), (0, 16, 1024)])
+def test_quant_fp8_rows(gpu, mode, M, H):
+    """Row-wise e4m3fn quantiser (quant.hip) vs the fp32 reference: same scales, the same FP8
+    codes except rare rounding ties, padded rows zero with scale 1."""
+    torch.manual_seed(9)
+    x = _bf(M, H * (2 if mode else 1), dev=gpu, scale=3.0)
+    y, s = ops.quant_fp8_rows(x, mode)
+    yr, sr = ref.quant_fp8_rows(x.cpu(), mode, y.shape[0])
+    assert y.shape == yr.shape and y.dtype == torch.float8_e4m3fn
+    _close(s, sr, 0.0, 1e-5)
+    codes, codes_r = y.cpu().view(torch.uint8), yr.view(torch.uint8)
+    assert (codes != codes_r).float().mean().item() < 1e-3
+    deq = (y.float() * s)[:M].cpu()
+    xv = x.float().cpu() if mode == 0 else torch.nn.functional.silu(x.float().cpu()[:, :H]) * x.float().cpu()[:, H:]
+    assert float((deq - xv).norm() / xv.norm()) < 0.04
+
+
+def test_fp8_linear_matches_dequantised_matmul(gpu):
+    torch.manual_seed(10)
+    x = _bf(50, 4096, dev=gpu)
+    w = _bf(6144, 4096, dev=gpu, scale=0.02)
+    x8, sx = ops.quant_fp8_rows(x)
+    w8, sw = ops.quantize_weight_fp8(w)
+    y = ops.fp8_linear(x8, sx, w8, sw, 50)
+    y_ref = (x8.float() * sx)[:50] @ (w8.float() * sw.t()).t()
+    _close(y, y_ref, 0.05, 0.01)
+    exact = x.float() @ w.float().t()
+    assert float((y.float() - exact).norm() / exact.norm()) < 0.06
