@@ -222,7 +222,9 @@ def test_fp8_engine_gpu(gpu, weights):
 
     a = first_logits(_engine(weights, "cuda", use_graphs=False))
     b = first_logits(_engine(weights, "cuda", use_graphs=False, fp8=True))
-    assert float((a - b).norm() / a.norm()) < 0.1
+    # e4m3 keeps 3 mantissa bits: ~3-4 % error per GEMM, compounding over the layers
+    assert float((a - b).norm() / a.norm()) < 0.2
+    assert torch.topk(b[-1], 5).indices.tolist().count(int(a[-1].argmax())) == 1
     p = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
     g = [r.output_ids for r in _engine(weights, "cuda", fp8=True).generate(PROMPTS[:3], p)]
     e = [r.output_ids for r in _engine(weights, "cuda", fp8=True, use_graphs=False).generate(PROMPTS[:3], p)]
