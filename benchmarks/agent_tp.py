@@ -59,6 +59,7 @@ def parse(argv=None):
     ap.add_argument("--max-num-seqs", type=int, default=128)
     ap.add_argument("--kv-cache-fraction", type=float, default=0.5)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--fp8", action="store_true", help="W8A8 FP8 projections (70B: 70 GB of weights)")
     ap.add_argument("--out", default=None)
     return ap.parse_args(argv)
 
@@ -76,7 +77,8 @@ def main(argv=None):
     t0 = time.time()
     eng = LLMEngine(EngineConfig(model=args.model, max_num_seqs=args.max_num_seqs, max_batched_tokens=16384,
                                  max_model_len=8192, kv_cache_fraction=args.kv_cache_fraction,
-                                 use_graphs=gpu and not args.no_graphs, kv_cache_blocks=None if gpu else 512),
+                                 use_graphs=gpu and not args.no_graphs, kv_cache_blocks=None if gpu else 512,
+                                 fp8=args.fp8),
                     device=dev, pctx=pctx)
     from nv_genai_amd.models.config import encoder_config
 
@@ -176,7 +178,8 @@ def main(argv=None):
            "searches_per_s": round(stats["searches"] / elapsed, 2),
            "mean_prompt_tokens": round(stats["prompt_tokens"] / max(1, stats["llm_calls"]), 1),
            "output_tokens_per_s": round(stats["output_tokens"] / elapsed, 1),
-           "dtype": "bf16", "data": "synthetic: random-init weights, random unit-vector index, generated questions",
+           "dtype": "fp8-w8a8" if args.fp8 else "bf16",
+           "data": "synthetic: random-init weights, random unit-vector index, generated questions",
            "setup_s": round(setup_s, 1)}
     line = json.dumps(res)
     print(line, flush=True)
