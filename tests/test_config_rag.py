@@ -173,3 +173,36 @@ def test_reference_style_vector_clients():
     m = MilvusStyleClient(collection_name="test_MilvusStyleClient", embedding_size=32, device="cpu")
     m.update(docs[:10], emb[:10].tolist(), "test_MilvusStyleClient")  # insert: appended
     assert len(m._col().payloads) == 310
+
+
+def test_tracing_callback_spans_first_token_and_retry():
+    """TracingCallback (the reference's OpenTelemetryCallbackHandler, C19/C20): nested spans
+    by run id, first-token latency, token counts, retriever documents, tool spans, retries,
+    process metrics at span end."""
+    import time as _t
+
+    from nv_genai_amd.observability.tracing import InMemoryExporter, Tracer, TracingCallback
+
+    exp = InMemoryExporter()
+    cb = TracingCallback(Tracer("chain-server", exp, enabled=True), token_events=True)
+    cb.on_chain_start("c1", "rag_chain", inputs={"q": "capital?"})
+    cb.on_retriever_start("r1", "capital?", parent_run_id="c1")
+    cb.on_retriever_end("r1", [("Quartz City doc", 0.9)])
+    cb.on_llm_start("l1", ["prompt"], parent_run_id="c1", temperature=0.2)
+    _t.sleep(0.002)
+    for tok in ("Quartz", " City"):
+        cb.on_llm_new_token("l1", tok)
+    cb.on_retry("l1", 1, "timeout")
+    cb.on_llm_end("l1", "Quartz City", prompt_tokens=12)
+    cb.on_tool_start("t1", "Math", "2+2", parent_run_id="c1")
+    cb.on_tool_end("t1", "4")
+    cb.on_chain_end("c1", outputs="Quartz City")
+    by = {s.name: s for s in exp.spans}
+    assert set(by) == {"rag_chain", "retriever", "llm", "tool:Math"}
+    for n in ("retriever", "llm", "tool:Math"):
+        assert by[n].parent_id == by["rag_chain"].span_id and by[n].trace_id == by["rag_chain"].trace_id
+    llm = by["llm"].attributes
+    assert llm["completion_tokens"] == 2 and llm["prompt_tokens"] == 12 and llm["first_token_time_ms"] >= 1.0
+    assert by["retriever"].attributes["documents.0.score"] == 0.9
+    names = [e["name"] for e in by["llm"].events]
+    assert names.count("new_token") == 2 and "retry" in names
