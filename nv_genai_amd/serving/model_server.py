@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import dataclasses
 import base64
 import json
 import logging
@@ -60,6 +61,7 @@ class ChatRequest(BaseModel):
     beam_width: int = Field(1, ge=1, le=16)
     length_penalty: float = 1.0
     response_format: Optional[Dict[str, Any]] = None   # {"type": "json_object"} constrains to JSON
+    n: int = Field(1, ge=1, le=16)   # choices per prompt (parallel sampling, or the top-n beams)
 
 
 class CompletionRequest(BaseModel):
@@ -79,6 +81,7 @@ class CompletionRequest(BaseModel):
     beam_width: int = Field(1, ge=1, le=16)
     length_penalty: float = 1.0
     response_format: Optional[Dict[str, Any]] = None   # {"type": "json_object"} constrains to JSON
+    n: int = Field(1, ge=1, le=16)   # choices per prompt (parallel sampling, or the top-n beams)
 
 
 class EmbeddingRequest(BaseModel):
@@ -178,27 +181,58 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
         metrics.observe("request_seconds", time.perf_counter() - t0)
         return "".join(out)
 
+    def _submit_n(svc, ids, req):
+        """``n`` choices: one beam-search request returns its top-n beams; otherwise n
+        sampled sequences over the shared prompt (prefix-cached KV), seeds seed + i."""
+        params = _params(req)
+        if req.n == 1 or params.beam_width > 1:
+            return [svc.submit(ids, params)]
+        out = []
+        for i in range(req.n):
+            seed = None if params.seed is None else params.seed + i
+            out.append(svc.submit(ids, dataclasses.replace(params, seed=seed)))
+        return out
+
+    def _usage(handles):
+        u = {"prompt_tokens": sum(h.usage.get("prompt_tokens", 0) for h in handles),
+             "completion_tokens": sum(h.usage.get("completion_tokens", 0) for h in handles)}
+        u["total_tokens"] = u["prompt_tokens"] + u["completion_tokens"]
+        return u
+
+    def _texts(handle, text, n):
+        """The choice texts of one request: its beams (beam search) or its one output."""
+        r = handle.request
+        if r is not None and r.beams and n > 1:
+            return [b[2] for b in r.beams[:n]]
+        return [text]
+
     @app.post("/v1/chat/completions")
     async def chat(req: ChatRequest, request: Request):
         svc = _need(app.state.llm, "LLM")
         t0 = time.perf_counter()
         metrics.inc("chat_requests_total")
         msgs = [{"role": m.role, "content": _content_text(m.content)} for m in req.messages]
+        if req.stream and req.n > 1:
+            return JSONResponse({"error": "stream supports n = 1"}, status_code=400)
         with tracer.span("chat.completions", {"model": req.model}, request.headers.get("traceparent")):
             ids = svc.engine.tok.apply_chat_template(msgs)
-            handle = svc.submit(ids, _params(req))
+            handles = _submit_n(svc, ids, req)
         rid = f"chatcmpl-{uuid.uuid4().hex}"
         model = req.model or llm_name
         if req.stream:
-            return StreamingResponse(_run_stream(handle, rid, model, "chat.completion.chunk", True, t0),
+            return StreamingResponse(_run_stream(handles[0], rid, model, "chat.completion.chunk", True, t0),
                                      media_type="text/event-stream")
-        text = await _complete(handle, t0)
-        choice = {"index": 0, "message": {"role": "assistant", "content": text},
-                  "finish_reason": handle.finish_reason}
-        if req.logprobs and handle.request is not None:
-            choice["logprobs"] = {"content": [{"logprob": lp} for lp in handle.request.logprobs]}
+        choices = []
+        for h in handles:
+            text = await _complete(h, t0)
+            for t in _texts(h, text, req.n):
+                choice = {"index": len(choices), "message": {"role": "assistant", "content": t},
+                          "finish_reason": h.finish_reason}
+                if req.logprobs and h.request is not None:
+                    choice["logprobs"] = {"content": [{"logprob": lp} for lp in h.request.logprobs]}
+                choices.append(choice)
         return {"id": rid, "object": "chat.completion", "created": int(time.time()), "model": model,
-                "choices": [choice], "usage": handle.usage}
+                "choices": choices, "usage": _usage(handles)}
 
     @app.post("/v1/completions")
     async def completions(req: CompletionRequest, request: Request):
@@ -209,19 +243,19 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
         tok = svc.engine.tok
         model = req.model or llm_name
         rid = f"cmpl-{uuid.uuid4().hex}"
-        handles = [svc.submit([tok.bos_id] + tok.encode(p), _params(req)) for p in prompts]
+        if req.stream and (len(prompts) != 1 or req.n > 1):
+            return JSONResponse({"error": "stream supports a single prompt and n = 1"}, status_code=400)
+        handles = [h for p in prompts for h in _submit_n(svc, [tok.bos_id] + tok.encode(p), req)]
         if req.stream:
-            if len(handles) != 1:
-                return JSONResponse({"error": "stream supports a single prompt"}, status_code=400)
             return StreamingResponse(_run_stream(handles[0], rid, model, "text_completion", False, t0),
                                      media_type="text/event-stream")
-        texts = [await _complete(h, t0) for h in handles]
-        usage = {"prompt_tokens": sum(h.usage.get("prompt_tokens", 0) for h in handles),
-                 "completion_tokens": sum(h.usage.get("completion_tokens", 0) for h in handles)}
-        usage["total_tokens"] = usage["prompt_tokens"] + usage["completion_tokens"]
+        choices = []
+        for h in handles:
+            text = await _complete(h, t0)
+            for t in _texts(h, text, req.n):
+                choices.append({"index": len(choices), "text": t, "finish_reason": h.finish_reason})
         return {"id": rid, "object": "text_completion", "created": int(time.time()), "model": model,
-                "choices": [{"index": i, "text": t, "finish_reason": h.finish_reason}
-                            for i, (t, h) in enumerate(zip(texts, handles))], "usage": usage}
+                "choices": choices, "usage": _usage(handles)}
 
     @app.post("/v1/embeddings")
     async def embeddings(req: EmbeddingRequest):

@@ -183,3 +183,18 @@ def test_response_format_json_object(client):
         assert isinstance(_json.loads(txt), dict)
     else:
         assert txt.lstrip().startswith("{")
+
+
+def test_n_choices_sampling_and_beams(client):
+    body = {"messages": [{"role": "user", "content": "give me options"}], "max_tokens": 6, "ignore_eos": True,
+            "n": 3, "temperature": 1.0, "seed": 7}
+    r = client.post("/v1/chat/completions", json=body).json()
+    assert [c["index"] for c in r["choices"]] == [0, 1, 2]
+    texts = [c["message"]["content"] for c in r["choices"]]
+    assert len(set(texts)) > 1 and r["usage"]["completion_tokens"] == 18
+    again = client.post("/v1/chat/completions", json=body).json()
+    assert [c["message"]["content"] for c in again["choices"]] == texts    # seeded per choice
+    b = client.post("/v1/completions", json={"prompt": "beams", "max_tokens": 4, "ignore_eos": True,
+                                             "beam_width": 3, "n": 2}).json()
+    assert len(b["choices"]) == 2
+    assert client.post("/v1/chat/completions", json={**body, "stream": True}).status_code == 400
