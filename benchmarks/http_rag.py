@@ -1,0 +1,173 @@
+"""End-to-end RAG QPS through the REST API: the headline workload of bench.py, but every request
+is a real ``POST /generate`` (``use_knowledge_base: true``, SSE stream) to the chain server.
+
+The chain server (``developer_rag`` example, uvicorn) runs in its own process with in-process
+engines on the GPU. It uses ``APP_LLM_MODELENGINE=local`` and
+``APP_EMBEDDINGS_MODELENGINE=local``, and a synthetic 1M-chunk collection
+(``APP_INDEX_SYNTHETICDOCS``). Concurrent requests' searches are coalesced by the vector store's
+query batcher on its own HIP stream. Generation goes through the continuous-batching engine.
+
+The load generator is a separate CPU-only asyncio process. It runs a closed loop: each of
+``--concurrency`` clients posts a generated question, reads the SSE stream to ``[DONE]`` and posts
+the next. After ``--warmup`` requests, ``--requests`` more are timed. The script prints one
+JSON line with QPS and the p50/p95 latency and TTFT of the timed requests.
+
+Each request follows the reference's path, not bench.py's. The chain server forwards only
+temperature, top_p and max_tokens (utils.py:271-286 quirk), so generation may stop early at an
+EOS token. Output tokens are therefore counted from the streamed text and reported.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import socket
+import statistics
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--llm", default="llama3-8b")
+    ap.add_argument("--embed", default="arctic-embed-l")
+    ap.add_argument("--index-size", type=int, default=1_000_000)
+    ap.add_argument("--concurrency", type=int, default=256)
+    ap.add_argument("--requests", type=int, default=512)
+    ap.add_argument("--warmup", type=int, default=256)
+    ap.add_argument("--max-tokens", type=int, default=256)
+    ap.add_argument("--example", default="developer_rag")
+    ap.add_argument("--device", default="", help="engine device for the server ('' = cuda if available)")
+    ap.add_argument("--startup-timeout", type=float, default=600.0)
+    ap.add_argument("--out", default=None)
+    return ap.parse_args(argv)
+
+
+async def _one(client, url, question, max_tokens):
+    t0 = time.perf_counter()
+    ttft = None
+    chars = 0
+    body = {"messages": [{"role": "user", "content": question}], "use_knowledge_base": True,
+            "temperature": 0.2, "top_p": 0.7, "max_tokens": max_tokens}
+    async with client.stream("POST", url, json=body) as r:
+        if r.status_code != 200:
+            raise RuntimeError(f"/generate returned {r.status_code}")
+        async for line in r.aiter_lines():
+            if not line.startswith("data: "):
+                continue
+            frame = json.loads(line[6:])
+            ch = frame["choices"][0]
+            text = ch["message"]["content"]
+            if text and ttft is None:
+                ttft = time.perf_counter() - t0
+            chars += len(text)
+            if ch.get("finish_reason") == "[DONE]":
+                break
+    return time.perf_counter() - t0, ttft, chars
+
+
+async def _load(url, args, questions):
+    import httpx
+
+    limits = httpx.Limits(max_connections=args.concurrency + 8, max_keepalive_connections=args.concurrency + 8)
+    results = []
+    timed_start = [None]
+    total = args.warmup + args.requests
+    issued = [0]
+
+    async def client_loop(client):
+        while issued[0] < total:
+            i = issued[0]
+            issued[0] += 1
+            if i == args.warmup:
+                timed_start[0] = time.perf_counter()
+            lat, ttft, chars = await _one(client, url, questions[i % len(questions)], args.max_tokens)
+            if i >= args.warmup:
+                results.append((lat, ttft, chars, time.perf_counter()))
+
+    async with httpx.AsyncClient(timeout=httpx.Timeout(600.0), limits=limits) as client:
+        await asyncio.gather(*(client_loop(client) for _ in range(args.concurrency)))
+    return results, timed_start[0]
+
+
+def main(argv=None):
+    args = parse(argv)
+    from nv_genai_amd.utils.synthetic import TextGen
+
+    port = _free_port()
+    env = dict(os.environ, EXAMPLE_NAME=args.example, APP_LLM_MODELENGINE="local",
+               APP_EMBEDDINGS_MODELENGINE="local", APP_ENGINE_LLMPRESET=args.llm, APP_ENGINE_EMBEDPRESET=args.embed,
+               APP_INDEX_SYNTHETICDOCS=str(args.index_size), APP_ENGINE_MAXNUMSEQS=str(max(args.concurrency, 1)),
+               APP_ENGINE_DEVICE=args.device, PYTHONPATH=ROOT, LOGLEVEL=os.environ.get("LOGLEVEL", "WARNING"))
+    log_path = os.environ.get("NGA_HTTP_BENCH_LOG", os.path.join(ROOT, "gpurun_out", "http_rag_server.log"))
+    os.makedirs(os.path.dirname(log_path), exist_ok=True)
+    log = open(log_path, "w")
+    server = subprocess.Popen([sys.executable, "-m", "uvicorn", "nv_genai_amd.chain_server.server:app",
+                               "--host", "127.0.0.1", "--port", str(port), "--log-level", "warning"],
+                              env=env, stdout=log, stderr=subprocess.STDOUT)
+    try:
+        import httpx
+
+        base = f"http://127.0.0.1:{port}"
+        t0 = time.time()
+        while True:
+            if server.poll() is not None:
+                raise RuntimeError(f"chain server exited ({server.returncode}); see {log_path}")
+            try:
+                if httpx.get(base + "/health", timeout=5).status_code == 200:
+                    break
+            except Exception:  # noqa: BLE001 - not up yet
+                pass
+            if time.time() - t0 > args.startup_timeout:
+                raise RuntimeError("chain server did not come up")
+            time.sleep(1.0)
+        # first search builds the engines and fills the synthetic collection
+        httpx.post(base + "/search", json={"query": "warm up", "top_k": 4}, timeout=args.startup_timeout)
+        setup_s = time.time() - t0
+        gen = TextGen(seed=100)
+        questions = [gen.question() for _ in range(4096)]
+        results, t_start = asyncio.run(_load(base + "/generate", args, questions))
+        t_end = max(r[3] for r in results)
+        elapsed = t_end - t_start
+        lat = sorted(r[0] for r in results)
+        ttft = sorted(r[1] for r in results if r[1] is not None)
+        res = {"metric": "end-to-end RAG QPS + p50 latency through the chain-server REST API (POST /generate, SSE)",
+               "value": round(len(results) / elapsed, 4), "unit": "requests/s", "n_gpus": 1,
+               "requests": len(results), "concurrency": args.concurrency, "elapsed_s": round(elapsed, 3),
+               "p50_latency_ms": round(1e3 * statistics.median(lat), 1),
+               "p95_latency_ms": round(1e3 * lat[min(len(lat) - 1, int(0.95 * len(lat)))], 1),
+               "p50_ttft_ms": round(1e3 * statistics.median(ttft), 1) if ttft else None,
+               "mean_output_chars": round(sum(r[2] for r in results) / len(results), 1),
+               "config": {"model": f"{args.llm} + {args.embed}", "index_size": args.index_size,
+                          "example": args.example, "max_tokens": args.max_tokens},
+               "dtype": "bf16", "data": "synthetic: random-init weights, 1M random unit-vector index, generated questions",
+               "setup_s": round(setup_s, 1)}
+        line = json.dumps(res)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(line + "\n")
+    finally:
+        server.terminate()
+        try:
+            server.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            server.kill()
+            server.wait()
+
+
+if __name__ == "__main__":
+    main()

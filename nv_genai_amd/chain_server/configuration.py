@@ -134,6 +134,9 @@ class IndexConfig(ConfigWizard):
                                    help_txt="Directory for index snapshots ('' = in-memory only)")
     shards: int = configfield("shards", default=1,
                               help_txt="Shard the index across this many ranks (RCCL merge)")
+    synthetic_docs: int = configfield("synthetic_docs", default=0,
+                                      help_txt="Fill the default collection with this many synthetic chunks and "
+                                               "random unit vectors (benchmarks; 0 = off)")
 
 
 @configclass

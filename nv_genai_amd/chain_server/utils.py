@@ -184,10 +184,30 @@ def get_vectorstore(collection: Optional[str] = None):
         if cfg.vector_store.name == "milvus" and itype == "flat" and os.environ.get("APP_INDEX_TYPE") is None:
             itype = "flat"  # GPU brute force beats IVF at these sizes; set APP_INDEX_TYPE=ivf_flat for IVF
         dev = _device(cfg) if cfg.embeddings.model_engine not in ("hash", "fake") else "cpu"
-        return VectorStore(emb, dim, itype, cfg.index.metric, dev, cfg.vector_store.nlist,
-                           cfg.vector_store.nprobe, name=n, persist_dir=persist)
+        vs = VectorStore(emb, dim, itype, cfg.index.metric, dev, cfg.vector_store.nlist,
+                         cfg.vector_store.nprobe, name=n, persist_dir=persist)
+        if cfg.index.synthetic_docs and n == collection_name() and len(vs) == 0:
+            _fill_synthetic(vs, cfg)
+        return vs
 
     return get_store(name, make)
+
+
+def _fill_synthetic(vs, cfg) -> None:
+    """Benchmark corpus for the REST path (the same synthetic data as bench.py): random unit
+    vectors + generated ~500-token chunks, and a whitened query encoder so concurrent
+    questions retrieve different chunks (a random-init encoder's outputs are nearly collinear)."""
+    from ..index.docstore import SyntheticDocStore
+    from ..utils.synthetic import TextGen
+
+    n = int(cfg.index.synthetic_docs)
+    vs.index.add_random(n, seed=1234)
+    vs.docs = SyntheticDocStore(n)
+    vs._mark_write()
+    if cfg.embeddings.model_engine in ("local", "huggingface"):
+        cal = TextGen(seed=999)
+        get_embedding_engine().calibrate_whitening([cal.question() for _ in range(4096)])
+    log.info("filled collection %s with %d synthetic chunks", vs.name, n)
 
 
 create_vectorstore_langchain = get_vectorstore

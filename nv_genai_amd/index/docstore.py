@@ -47,6 +47,9 @@ class DocStore:
     def get(self, i: int) -> str:
         return self.texts[int(i)]
 
+    def contains(self, i: int) -> bool:
+        return int(i) in self.texts
+
     def metadata(self, i: int) -> dict:
         return self.meta.get(int(i), {})
 
@@ -123,6 +126,10 @@ class SyntheticDocStore(DocStore):
 
     def __len__(self):
         return self.n_docs + len(self.texts)
+
+    def contains(self, i: int) -> bool:
+        i = int(i)
+        return 0 <= i < self.n_docs or i in self.texts
 
     def get(self, i: int) -> str:
         i = int(i)

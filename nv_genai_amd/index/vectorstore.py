@@ -42,10 +42,72 @@ def _embed_queries(embedder, texts: Sequence[str]) -> torch.Tensor:
     return torch.tensor([embedder.embed_query(t) for t in texts], dtype=torch.float32)
 
 
+class _QueryBatcher:
+    """Coalesces concurrent similarity searches (one per chain-server request thread) into one
+    query-encoder forward and one index scan, on a dedicated HIP stream. A search therefore
+    never queues behind the LLM step running on the default stream; the batch waits only on
+    the store's last index write (``VectorStore._mark_write``). Requests arriving within
+    ``wait_s`` of the first share a batch (up to ``max_batch``)."""
+
+    def __init__(self, store: "VectorStore", device: torch.device, max_batch: int = 64, wait_s: float = 0.002):
+        import queue as _queue
+
+        self.store, self.max_batch, self.wait_s = store, max_batch, wait_s
+        self.q: "_queue.Queue" = _queue.Queue()
+        self._empty = _queue.Empty
+        self.stream = torch.cuda.Stream(device) if device.type == "cuda" else None
+        self.batches = 0
+        self.queries = 0
+        self.thread = threading.Thread(target=self._loop, name=f"query-batcher-{store.name}", daemon=True)
+        self.thread.start()
+
+    def submit(self, query: str, k: int):
+        import concurrent.futures as cf
+
+        fut = cf.Future()
+        self.q.put((query, k, fut))
+        return fut
+
+    def _loop(self):
+        import time as _time
+
+        while True:
+            batch = [self.q.get()]
+            deadline = _time.monotonic() + self.wait_s
+            while len(batch) < self.max_batch:
+                left = deadline - _time.monotonic()
+                if left <= 0:
+                    break
+                try:
+                    batch.append(self.q.get(timeout=left))
+                except self._empty:
+                    break
+            try:
+                if self.stream is not None:
+                    ev = self.store._write_ev
+                    if ev is not None:
+                        self.stream.wait_event(ev)
+                    with torch.cuda.stream(self.stream):
+                        res = self.store.similarity_search_with_score_batch([b[0] for b in batch],
+                                                                            max(b[1] for b in batch))
+                else:
+                    res = self.store.similarity_search_with_score_batch([b[0] for b in batch],
+                                                                        max(b[1] for b in batch))
+                for (_, k, fut), r in zip(batch, res):
+                    fut.set_result(r[:k])
+                self.batches += 1
+                self.queries += len(batch)
+            except BaseException as e:  # noqa: BLE001 - delivered to every waiting request
+                for _, _, fut in batch:
+                    if not fut.done():
+                        fut.set_exception(e)
+
+
 class VectorStore:
     def __init__(self, embedder, dim: int, index_type: str = "flat", metric: str = "cosine",
                  device: Optional[str] = None, nlist: int = 64, nprobe: int = 16,
-                 name: str = "default", persist_dir: Optional[str] = None):
+                 name: str = "default", persist_dir: Optional[str] = None,
+                 batch_queries: Optional[bool] = None):
         self.embedder = embedder
         self.dim = dim
         self.name = name
@@ -57,6 +119,13 @@ class VectorStore:
             self.index = FlatIndex(dim, metric, device)
         self.docs = DocStore()
         self.lock = threading.RLock()
+        self._write_ev = None
+        self._batcher = None
+        dev = torch.device(device) if device is not None else self.index_device()
+        use = batch_queries if batch_queries is not None else (
+            dev.type == "cuda" and os.environ.get("NGA_BATCH_QUERIES", "1") != "0")
+        if use:
+            self._batcher = _QueryBatcher(self, dev)
         self.persist_dir = persist_dir
         if persist_dir and (Path(persist_dir) / "index.json").exists():
             self.load(persist_dir)
@@ -75,6 +144,7 @@ class VectorStore:
             ids = self.docs.new_ids(len(texts))
             self.index.add(vecs, torch.tensor(ids, dtype=torch.int64))
             self.docs.add(ids, texts, metadatas)
+            self._mark_write()
         if self.persist_dir:
             self.save(self.persist_dir)
         return ids
@@ -87,6 +157,7 @@ class VectorStore:
         with self.lock:
             n = self.index.remove(ids)
             self.docs.remove(ids)
+            self._mark_write()
         if self.persist_dir:
             self.save(self.persist_dir)
         return n
@@ -122,14 +193,27 @@ class VectorStore:
             for vs, ds in zip(vals, ids):
                 row = []
                 for v, d in zip(vs, ds):
-                    if d < 0 or d not in self.docs.texts:
+                    if d < 0 or not self.docs.contains(d):
                         continue
                     row.append((Document(self.docs.get(d), dict(self.docs.metadata(d), doc_id=d)), float(v)))
                 out.append(row)
         return out
 
     def similarity_search_with_score(self, query: str, k: int = 4) -> List[Tuple[Document, float]]:
+        if self._batcher is not None:
+            return self._batcher.submit(query, k).result()
         return self.similarity_search_with_score_batch([query], k)[0]
+
+    def _mark_write(self):
+        """Event after an index mutation: the query batcher's stream waits on it (and on
+        nothing else, so searches never queue behind an LLM step on the default stream)."""
+        if self._batcher is not None and torch.cuda.is_available() and self.index_device().type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+            self._write_ev = ev
+
+    def index_device(self) -> torch.device:
+        return torch.device(getattr(self.index, "device", "cpu"))
 
     def similarity_search(self, query: str, k: int = 4) -> List[Document]:
         return [d for d, _ in self.similarity_search_with_score(query, k)]

@@ -18,3 +18,18 @@ def test_multi_turn_benchmark_cpu(tmp_path):
     # every turn wrote two memory entries; later turns retrieve history
     assert res["memory_entries"] == 2 * (1 * 3 + 3 * 3) and res["history_hits_per_turn"] > 0
     assert res["value"] > 0 and res["turns"] == 3
+
+
+def test_http_rag_benchmark_cpu(tmp_path):
+    """benchmarks/http_rag.py: chain-server process (developer_rag, in-process engines, synthetic
+    collection, batched vector-store queries) driven over REST + SSE by the async load generator."""
+    out = tmp_path / "http.json"
+    r = subprocess.run([sys.executable, "benchmarks/http_rag.py", "--llm", "llama-tiny", "--embed", "encoder-tiny",
+                        "--index-size", "3000", "--concurrency", "4", "--requests", "8", "--warmup", "2",
+                        "--max-tokens", "6", "--device", "cpu", "--out", str(out)],
+                       capture_output=True, text=True, timeout=400,
+                       env=dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=os.getcwd(),
+                                NGA_HTTP_BENCH_LOG=str(tmp_path / "server.log")))
+    assert r.returncode == 0, (r.stderr[-3000:], (tmp_path / "server.log").read_text()[-3000:])
+    res = json.loads(out.read_text())
+    assert res["requests"] == 8 and res["value"] > 0 and res["p50_ttft_ms"] is not None
