@@ -158,6 +158,11 @@ def load_example():
 
 @app.on_event("startup")
 def import_example() -> None:
+    # every open /generate stream parks a worker thread on its token queue between chunks
+    # (sync example generators): size the pool for the serving concurrency, not anyio's 40
+    import anyio.to_thread
+
+    anyio.to_thread.current_default_thread_limiter().total_tokens = int(os.environ.get("APP_THREADPOOL", "2048"))
     if getattr(app, "example", None) is None:
         app.example = load_example()
 
@@ -250,10 +255,12 @@ async def generate_answer(request: Request, prompt: Prompt) -> StreamingResponse
     METRICS.inc("generate_requests_total")
     try:
         example = app.example()
-        if prompt.use_knowledge_base:
-            generator = example.rag_chain(query=last_user_message, chat_history=chat_history, **llm_settings)
-        else:
-            generator = example.llm_chain(query=last_user_message, chat_history=chat_history, **llm_settings)
+        # the chain's synchronous part (retrieval, prompt assembly) runs on a worker thread:
+        # on the event loop it would serialise every request's retrieval and stall all streams,
+        # and concurrent requests' searches could never share a batch (VectorStore batcher)
+        chain = example.rag_chain if prompt.use_knowledge_base else example.llm_chain
+        generator = await asyncio.to_thread(chain, query=last_user_message, chat_history=chat_history,
+                                            **llm_settings)
     except Exception as e:  # noqa: BLE001
         logger.error("Error from /generate endpoint. Error details: %s", e)
         METRICS.inc("generate_errors_total")
