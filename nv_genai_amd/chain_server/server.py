@@ -165,6 +165,12 @@ def import_example() -> None:
     anyio.to_thread.current_default_thread_limiter().total_tokens = int(os.environ.get("APP_THREADPOOL", "2048"))
     if getattr(app, "example", None) is None:
         app.example = load_example()
+    # in-process engines are built (weights, KV cache, decode hipGraphs) before traffic arrives
+    from . import utils
+
+    cfg = utils.get_config()
+    if cfg.llm.model_engine == "local" and os.environ.get("APP_LAZY_ENGINES", "0") != "1":
+        utils.get_llm_service()
 
 
 @app.exception_handler(RequestValidationError)

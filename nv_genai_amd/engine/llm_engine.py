@@ -900,7 +900,9 @@ class LLMEngine:
                 for _ in range(2):
                     self._decode_body(bs)
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool, stream=stream):
+                # thread_local: other threads of a serving process (retrieval, embeddings, other
+                # engines) keep launching on their own streams while this one captures
+                with torch.cuda.graph(g, pool=pool, stream=stream, capture_error_mode="thread_local"):
                     self._decode_body(bs)
                 pool = g.pool()
                 self.graphs[bs] = g
