@@ -301,6 +301,34 @@ async def generate_answer(request: Request, prompt: Prompt) -> StreamingResponse
             METRICS.observe("generate_seconds", time.perf_counter() - t_start)
             tracer.end(span)
 
+    async def response_agen():
+        """Same frames, fed from the engine's asyncio queue (LLMStream over a local engine)."""
+        resp_id = str(uuid4())
+        first = True
+        try:
+            async for chunk in generator:
+                if first:
+                    METRICS.observe("ttft_seconds", time.perf_counter() - t_start)
+                    first = False
+                r = ChainResponse(id=resp_id, choices=[ChainResponseChoices(
+                    index=0, message=Message(role="assistant", content=chunk))])
+                yield "data: " + r.model_dump_json() + "\n\n"
+            r = ChainResponse(id=resp_id, choices=[ChainResponseChoices(finish_reason="[DONE]")])
+            yield "data: " + r.model_dump_json() + "\n\n"
+        except Exception as e:  # noqa: BLE001
+            logger.error("Error while streaming /generate: %s", e)
+            METRICS.inc("generate_errors_total")
+            r = ChainResponse(id=resp_id, choices=[ChainResponseChoices(
+                index=0, message=Message(role="assistant",
+                                         content="Error from chain server. Please check chain-server logs for more details."),
+                finish_reason="[DONE]")])
+            yield "data: " + r.model_dump_json() + "\n\n"
+        finally:
+            METRICS.observe("generate_seconds", time.perf_counter() - t_start)
+            tracer.end(span)
+
+    if generator is not None and getattr(generator, "supports_async", False):
+        return StreamingResponse(response_agen(), media_type="text/event-stream")
     return StreamingResponse(response_generator(), media_type="text/event-stream")
 
 

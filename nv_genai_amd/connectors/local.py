@@ -71,6 +71,17 @@ class LocalChatModel:
             if not h.done.is_set():
                 h.cancel()
 
+    async def astream(self, messages: Messages, coalesce: bool = False, **kw):
+        """Async token stream straight from the engine's asyncio queue (no worker thread);
+        ``coalesce`` joins the deltas that are already queued into one chunk."""
+        h = self._submit(messages, **kw)
+        try:
+            async for d in h.aiter(coalesce=coalesce):
+                yield d
+        finally:
+            if not h.done.is_set():
+                h.cancel()
+
     def invoke(self, messages: Messages, **kw) -> str:
         return self._submit(messages, **kw).text()
 

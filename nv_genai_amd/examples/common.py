@@ -16,6 +16,50 @@ NO_CONTEXT = "No response generated from LLM, make sure your query is relavent t
 NO_DOCS = "No response generated from LLM, make sure you have ingested document from the Knowledge Base Tab."
 
 
+class LLMStream:
+    """A traced LLM answer stream. Iterating it synchronously is the reference behaviour (a
+    generator of text chunks). With an in-process engine it also iterates asynchronously:
+    the chain server then forwards tokens from the engine's asyncio queue with no thread per
+    stream, coalescing the tokens that arrived since the last frame."""
+
+    def __init__(self, cb, llm, messages, kwargs):
+        self.cb, self.llm, self.messages, self.kwargs = cb, llm, messages, kwargs
+        self.rid = uuid.uuid4().hex
+
+    def _start(self):
+        self.cb.on_llm_start(self.rid, self.messages, **{k: v for k, v in self.kwargs.items() if v is not None})
+
+    def __iter__(self) -> Iterator[str]:
+        self._start()
+        out: List[str] = []
+        try:
+            for chunk in self.llm.stream(self.messages):
+                self.cb.on_llm_new_token(self.rid, chunk)
+                out.append(chunk)
+                yield chunk
+        except Exception as e:
+            self.cb.on_llm_error(self.rid, e)
+            raise
+        self.cb.on_llm_end(self.rid, "".join(out))
+
+    @property
+    def supports_async(self) -> bool:
+        return hasattr(self.llm, "astream")
+
+    async def __aiter__(self):
+        self._start()
+        out: List[str] = []
+        try:
+            async for chunk in self.llm.astream(self.messages, coalesce=True):
+                self.cb.on_llm_new_token(self.rid, chunk)
+                out.append(chunk)
+                yield chunk
+        except Exception as e:
+            self.cb.on_llm_error(self.rid, e)
+            raise
+        self.cb.on_llm_end(self.rid, "".join(out))
+
+
 class TracedExample:
     """Gives every example a callback handler (the reference's
     ``langchain_instrumentation_class_wrapper`` sets ``self.cb_handler``)."""
@@ -23,20 +67,8 @@ class TracedExample:
     def __init__(self):
         self.cb_handler = TracingCallback(get_tracer("chain-server"))
 
-    def stream_llm(self, messages, **kwargs) -> Iterator[str]:
-        llm = utils.get_llm(**kwargs)
-        rid = uuid.uuid4().hex
-        self.cb_handler.on_llm_start(rid, messages, **{k: v for k, v in kwargs.items() if v is not None})
-        out: List[str] = []
-        try:
-            for chunk in llm.stream(messages):
-                self.cb_handler.on_llm_new_token(rid, chunk)
-                out.append(chunk)
-                yield chunk
-        except Exception as e:
-            self.cb_handler.on_llm_error(rid, e)
-            raise
-        self.cb_handler.on_llm_end(rid, "".join(out))
+    def stream_llm(self, messages, **kwargs) -> "LLMStream":
+        return LLMStream(self.cb_handler, utils.get_llm(**kwargs), messages, kwargs)
 
     def invoke_llm(self, messages, **kwargs) -> str:
         return "".join(self.stream_llm(messages, **kwargs))

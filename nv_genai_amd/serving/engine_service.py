@@ -74,7 +74,7 @@ class StreamHandle:
                 return
             yield item
 
-    async def aiter(self) -> AsyncIterator[str]:
+    async def aiter(self, coalesce: bool = False) -> AsyncIterator[str]:
         with self._lock:
             self._loop = asyncio.get_running_loop()
             self._aq = asyncio.Queue()
@@ -89,6 +89,20 @@ class StreamHandle:
                 if self.error is not None:
                     raise EngineError(str(self.error))
                 return
+            if coalesce:
+                parts, end = [item], False
+                while not self._aq.empty():
+                    nxt = self._aq.get_nowait()
+                    if nxt is _END:
+                        end = True
+                        break
+                    parts.append(nxt)
+                yield "".join(parts)
+                if end:
+                    if self.error is not None:
+                        raise EngineError(str(self.error))
+                    return
+                continue
             yield item
 
     def text(self) -> str:
