@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import asyncio
 import importlib
+import json
 import importlib.util
 import logging
 import os
@@ -239,6 +240,17 @@ async def upload_document(request: Request) -> JSONResponse:
             return JSONResponse(content={"message": str(e)}, status_code=500)
 
 
+_MARK = "\u2063SPLICE\u2063"
+
+
+def _frame_parts(resp_id: str):
+    """SSE frame of one ChainResponse chunk split around its content field."""
+    r = ChainResponse(id=resp_id, choices=[ChainResponseChoices(
+        index=0, message=Message(role="assistant", content=_MARK))])
+    head, tail = ("data: " + r.model_dump_json() + "\n\n").split(_MARK)
+    return head, tail
+
+
 def _error_stream(msg: str) -> StreamingResponse:
     resp = ChainResponse(choices=[ChainResponseChoices(index=0, message=Message(role="assistant", content=msg),
                                                        finish_reason="[DONE]")])
@@ -302,17 +314,18 @@ async def generate_answer(request: Request, prompt: Prompt) -> StreamingResponse
             tracer.end(span)
 
     async def response_agen():
-        """Same frames, fed from the engine's asyncio queue (LLMStream over a local engine)."""
+        """Same frames, fed from the engine's asyncio queue (LLMStream over a local engine).
+        Frames are the ChainResponse JSON with the sanitised chunk spliced in (byte-identical
+        to model_dump_json, without a pydantic round trip per token)."""
         resp_id = str(uuid4())
+        head, tail = _frame_parts(resp_id)
         first = True
         try:
             async for chunk in generator:
                 if first:
                     METRICS.observe("ttft_seconds", time.perf_counter() - t_start)
                     first = False
-                r = ChainResponse(id=resp_id, choices=[ChainResponseChoices(
-                    index=0, message=Message(role="assistant", content=chunk))])
-                yield "data: " + r.model_dump_json() + "\n\n"
+                yield head + json.dumps(clean(chunk), ensure_ascii=False)[1:-1] + tail
             r = ChainResponse(id=resp_id, choices=[ChainResponseChoices(finish_reason="[DONE]")])
             yield "data: " + r.model_dump_json() + "\n\n"
         except Exception as e:  # noqa: BLE001

@@ -196,3 +196,19 @@ def test_every_example_serves_the_contract(example, tmp_path, monkeypatch):
             assert c.delete("/documents", params={"filename": listed}).status_code == 200
     utils.reset()
     server.app.example = None
+
+
+def test_fast_sse_frames_are_byte_identical():
+    """The async token path splices sanitised chunks into a pre-rendered ChainResponse frame;
+    it must match model_dump_json byte for byte (golden-format contract)."""
+    import json as _json
+
+    from nv_genai_amd.chain_server.server import ChainResponse, ChainResponseChoices, Message, _frame_parts, clean
+
+    head, tail = _frame_parts("rid")
+    for chunk in ["plain", "quote \" and \\ backslash", "<script>x</script> & <b>b</b>", "é 😀 中文",
+                  "new\nline\ttab\r", "\x01\x1f control", "   separators", ""]:
+        fast = head + _json.dumps(clean(chunk), ensure_ascii=False)[1:-1] + tail
+        ref = "data: " + ChainResponse(id="rid", choices=[ChainResponseChoices(
+            index=0, message=Message(role="assistant", content=chunk))]).model_dump_json() + "\n\n"
+        assert fast == ref, (chunk, fast, ref)
