@@ -9,8 +9,9 @@ query batcher on its own HIP stream. Generation goes through the continuous-batc
 
 The load generator is a separate CPU-only asyncio process. It runs a closed loop: each of
 ``--concurrency`` clients posts a generated question, reads the SSE stream to ``[DONE]`` and posts
-the next. After ``--warmup`` requests, ``--requests`` more are timed. The script prints one
-JSON line with QPS and the p50/p95 latency and TTFT of the timed requests.
+the next. Once ``--warmup`` requests have completed, the next ``--requests`` completions are
+timed, with every client still busy (no drain inside the window, as in bench.py). The script
+prints one JSON line with QPS and the p50/p95 latency and TTFT of the timed requests.
 
 Each request follows the reference's path, not bench.py's. The chain server forwards only
 temperature, top_p and max_tokens (utils.py:271-286 quirk), so generation may stop early at an
@@ -80,27 +81,32 @@ async def _one(client, url, question, max_tokens):
 
 
 async def _load(url, args, questions):
+    """Closed loop without a drain in the timed window (like bench.py): every client keeps a
+    request in flight; completions are counted from the moment ``--warmup`` requests have
+    completed until ``--requests`` more have, while every client is still busy."""
     import httpx
 
     limits = httpx.Limits(max_connections=args.concurrency + 8, max_keepalive_connections=args.concurrency + 8)
     results = []
-    timed_start = [None]
-    total = args.warmup + args.requests
-    issued = [0]
+    state = {"done": 0, "t_start": None, "stop": False, "issued": 0}
 
     async def client_loop(client):
-        while issued[0] < total:
-            i = issued[0]
-            issued[0] += 1
-            if i == args.warmup:
-                timed_start[0] = time.perf_counter()
+        while not state["stop"]:
+            i = state["issued"]
+            state["issued"] += 1
             lat, ttft, chars = await _one(client, url, questions[i % len(questions)], args.max_tokens)
-            if i >= args.warmup:
-                results.append((lat, ttft, chars, time.perf_counter()))
+            now = time.perf_counter()
+            state["done"] += 1
+            if state["done"] == args.warmup:
+                state["t_start"] = now
+            elif state["t_start"] is not None and not state["stop"]:
+                results.append((lat, ttft, chars, now))
+                if len(results) >= args.requests:
+                    state["stop"] = True
 
     async with httpx.AsyncClient(timeout=httpx.Timeout(600.0), limits=limits) as client:
         await asyncio.gather(*(client_loop(client) for _ in range(args.concurrency)))
-    return results, timed_start[0]
+    return results, state["t_start"]
 
 
 def main(argv=None):
