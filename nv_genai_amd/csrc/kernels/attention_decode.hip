@@ -29,6 +29,7 @@ constexpr int D = 128;
 constexpr int BS = 64;
 constexpr int NW = 4;
 constexpr float LOG2E = 1.4426950408889634f;
+constexpr float RESCALE_LOG2 = 8.f;
 }  // namespace
 
 __global__ void __launch_bounds__(256) decode_attn_kernel(
@@ -112,33 +113,47 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 #pragma unroll
       for (int s = 0; s < 4; ++s) sacc[tau] = mfma16(as_bf16x8(kf[tau][s]), qf[s], sacc[tau]);
     }
-    // scale + mask; lane's keys: 32g + 8h + 4t1 + r for tile tau = 2g + t1, reg r
+    // mask (only the sequence's last, partial page); lane's keys: 32g + 8h + 4t1 + r for
+    // tile tau = 2g + t1, reg r. Raw scores: the softmax scale is folded into the exp2 FMA.
     const int kbase = p * BS;
     float mloc = -INFINITY;
+    if (kbase + BS <= ctx) {
 #pragma unroll
-    for (int tau = 0; tau < 4; ++tau)
+      for (int tau = 0; tau < 4; ++tau)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kbase + 32 * (tau >> 1) + 8 * h + 4 * (tau & 1) + r;
-        float s = sacc[tau][r] * sl2;
-        s = key < ctx ? s : -INFINITY;
-        sacc[tau][r] = s;
-        mloc = fmaxf(mloc, s);
-      }
+        for (int r = 0; r < 4; ++r) mloc = fmaxf(mloc, sacc[tau][r]);
+    } else {
+#pragma unroll
+      for (int tau = 0; tau < 4; ++tau)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kbase + 32 * (tau >> 1) + 8 * h + 4 * (tau & 1) + r;
+          const float sv = key < ctx ? sacc[tau][r] : -INFINITY;
+          sacc[tau][r] = sv;
+          mloc = fmaxf(mloc, sv);
+        }
+    }
     mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    const float m_new = fmaxf(m, mloc);
-    const float alpha = exp2f(m - m_new);  // m_new finite: every page has >= 1 valid key
-    m = m_new;
-    l *= alpha;
+    mloc *= sl2;  // scale > 0: max commutes with it
+    // Lazy rescaling (as in the prefill kernel): the running max only moves, and O / l are
+    // only rescaled, when a page's max exceeds it by more than 2^RESCALE_LOG2; until then
+    // P = 2^(s - m) <= 2^8 stays harmless in fp32 l / O and bf16 P. m starts at -inf, so the
+    // first page always rescales (alpha = 2^-inf = 0 on the all-zero O). Every page has at
+    // least one valid key, so m is finite from then on.
+    if (mloc > m + RESCALE_LOG2) {
+      const float alpha = __builtin_amdgcn_exp2f(m - mloc);
+      m = mloc;
+      l *= alpha;
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+      for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+    }
     bf16x8 pf[2];
 #pragma unroll
     for (int g = 0; g < 2; ++g)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float pv = exp2f(sacc[2 * g + (j >> 2)][j & 3] - m_new);
+        const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[2 * g + (j >> 2)][j & 3], sl2, -m));  // 2^-inf = 0
         l += pv;
         pf[g][j] = (__bf16)pv;
       }
