@@ -373,9 +373,9 @@ class IngestPipeline:
         wr = threading.Thread(target=self._writer, daemon=True)
         for t in srcs + chunkers + [emb, wr]:
             t.start()
-        t_end = time.time() + (timeout or 1e18)
+        t_end = None if timeout is None else time.time() + timeout
         for t in srcs:
-            t.join(max(0.0, t_end - time.time()))
+            t.join(None if t_end is None else max(0.0, t_end - time.time()))
         self.stop.set()
         for _ in chunkers:
             self.q_src.put(_END)

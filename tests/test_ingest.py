@@ -93,3 +93,20 @@ def test_kafka_source_refuses_without_client():
     p = IngestPipeline(cfg, Emb(), _factory({}))
     p.run(timeout=10)
     assert p.errors and "kafka" in p.errors[0]
+
+
+def test_pipeline_without_timeout_and_rate_benchmark(tmp_path):
+    """run(timeout=None) waits for finite sources (the CLI default); the ingest-rate benchmark
+    indexes every chunk it produced."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    out = tmp_path / "ing.json"
+    r = subprocess.run([sys.executable, "benchmarks/ingest_rate.py", "--docs", "30", "--embed-model", "encoder-tiny",
+                        "--threads", "2", "--out", str(out)], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=os.getcwd()))
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    assert res["chunks"] > 30 and res["indexed"] == res["chunks"] and res["value"] > 0
