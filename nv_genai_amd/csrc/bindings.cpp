@@ -162,7 +162,8 @@ void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optio
                        int64_t max_q_len, double scale, bool causal) {
   CHECK_BF16(out); CHECK_BF16(q);
   CHECK_DEV(cu_q); CHECK_DT(cu_q, at::kInt); CHECK_CONTIG(cu_q);
-  TORCH_CHECK(D == 64 || D == 128);
+  TORCH_CHECK(D == 64 || D == 128 || (D == 32 && !kc.has_value()),
+              "prefill_attention: head_dim must be 64 or 128 (or 32 without a paged cache)");
   TORCH_CHECK(Hq % Hkv == 0);
   TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1 && q.size(1) >= Hq * D && q.stride(0) % 8 == 0);
   TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) >= Hq * D && out.size(0) == q.size(0));

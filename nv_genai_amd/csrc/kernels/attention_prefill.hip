@@ -16,6 +16,7 @@
 //        queries are the last q_len positions of a ctx_len context (chunked prefill and
 //        prefix-cache hits work unchanged).  Otherwise: K and V rows come from packed
 //        [T, H, D] tensors with per-sequence offsets (cu_q), V is transposed while staging.
+// D is 64 or 128 (either mode) or 32 (packed mode only: the all-MiniLM-L6-v2 encoder).
 #include <cstdlib>
 
 #include "common.h"
@@ -129,7 +130,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
       const int c = tid + 256 * i;
       {  // K: row = key, chunk = d/8
         const int row = c / NCH_K, ch = c % NCH_K;
-        const int sw = (NCH_K == 16) ? row_swz(row) : (row_swz(row) >> 1);
+        const int sw = row_swz(row) >> (NCH_K == 16 ? 0 : NCH_K == 8 ? 1 : 2);
         *reinterpret_cast<u16x8*>(&k_s[row * D + ((ch ^ sw) * 8)]) = kreg[i];
       }
       if (PAGED) {  // Vt page is already [d][key]: row = d, chunk = key/8
@@ -163,7 +164,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
 #pragma unroll
       for (int tau = 0; tau < 4; ++tau) {
         const int row = 32 * (tau >> 1) + 8 * (col >> 2) + 4 * (tau & 1) + (col & 3);
-        const int sw = (NCH_K == 16) ? row_swz(row) : (row_swz(row) >> 1);
+        const int sw = row_swz(row) >> (NCH_K == 16 ? 0 : NCH_K == 8 ? 1 : 2);
 #pragma unroll
         for (int cg = 0; cg < NCG; ++cg) sacc[cg][tau] = (f32x4)(0.f);
 #pragma unroll
@@ -298,6 +299,8 @@ void launch_prefill_attention(const PrefillParams& p, int num_seqs, int max_q_le
     } else {
       if (causal) NGA_PF(64, false, true); else NGA_PF(64, false, false);
     }
+  } else if (D == 32 && !paged) {  // small encoders (MiniLM: 12 heads x 32); one MFMA d-step
+    if (causal) NGA_PF(32, false, true); else NGA_PF(32, false, false);
   }
 #undef NGA_PF
 }

@@ -137,7 +137,7 @@ def test_prefill_attention_paged(gpu):
     _close(out, o_ref, 0.02)
 
 
-@pytest.mark.parametrize("D,H,causal", [(64, 16, False), (128, 8, True)])
+@pytest.mark.parametrize("D,H,causal", [(64, 16, False), (128, 8, True), (32, 12, False)])
 def test_varlen_attention(gpu, D, H, causal):
     torch.manual_seed(4)
     lens = [5, 64, 130, 512, 1]
