@@ -33,3 +33,29 @@ def test_http_rag_benchmark_cpu(tmp_path):
     assert r.returncode == 0, (r.stderr[-3000:], (tmp_path / "server.log").read_text()[-3000:])
     res = json.loads(out.read_text())
     assert res["requests"] == 8 and res["value"] > 0 and res["p50_ttft_ms"] is not None
+
+
+def test_headline_bench_two_ranks_gloo():
+    """bench.py under torch.distributed.run with 2 ranks (gloo on CPU, the driver's N>1 launch):
+    exactly one JSON line, from rank 0, with the whole-job value over both replicas."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr=127.0.0.1", f"--master-port={port}", "bench.py", "--gpus", "2",
+                        "--steps", "1", "--warmup", "1", "--model", "llama-tiny", "--embed-model", "encoder-tiny",
+                        "--index-size", "2000", "--concurrency", "3", "--max-tokens", "4"],
+                       capture_output=True, text=True, timeout=400,
+                       env=dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=os.getcwd()))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2"
+    assert res["config"]["global_batch"] == 6 and res["steps"] == 1 and res["warmup"] == 1
+    # value is the aggregate over ranks: 2 x 3 requests in the max-over-ranks time
+    assert abs(res["value"] - 6 / (res["ms_per_step"] / 1000)) / res["value"] < 0.01
+    for k in ("metric", "unit", "higher_is_better", "scaling", "vs_baseline", "dtype", "data"):
+        assert k in res
