@@ -139,6 +139,64 @@ def test_sharded_index_matches_flat():
     assert torch.equal(ids, ri)
 
 
+def _shard_snapshot_worker(rank, world, port, path, mode, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    from nv_genai_amd.index.sharded import ShardedIndex
+    from nv_genai_amd.parallel import dist as pd
+
+    pctx = pd.init_distributed(tp_size=1, backend="gloo", device="cpu")
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(1001, 32, generator=g)
+    Q = torch.randn(4, 32, generator=g)
+    if mode == "save":
+        sh = ShardedIndex(32, "l2", "cpu", pctx=pctx)
+        sh.add(X, torch.arange(1001) * 5)
+        sh.remove([0, 5, 10])
+        sh.save(path)
+        sh.save(path)  # a second generation replaces the first; the old one is pruned
+    else:
+        sh = ShardedIndex.load(path, "cpu", pctx=pctx)
+    vals, ids = sh.search(Q if rank == 0 else torch.zeros(4, 32), 6)
+    n = len(sh)
+    if rank == 0:
+        q.put((vals, ids, n))
+    pd.destroy()
+
+
+def _run_world(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, *args, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
+
+
+def test_sharded_index_snapshot_restore_and_restripe(tmp_path):
+    """Sharded snapshot: per-rank safetensors shards + an atomically published
+    manifest; restoring on the same world size and on a different one gives the same search."""
+    import json
+
+    path = str(tmp_path / "idx")
+    v0, i0, n0 = _run_world(_shard_snapshot_worker, 2, path, "save")
+    man = json.loads((tmp_path / "idx" / "manifest.json").read_text())
+    assert man["world"] == 2 and man["total"] == n0 == 998
+    gens = [d.name for d in (tmp_path / "idx").iterdir() if d.name.startswith("gen-")]
+    assert len(gens) == 2 and man["generation"] in gens  # new + one kept
+    v1, i1, n1 = _run_world(_shard_snapshot_worker, 2, path, "load")
+    assert n1 == 998 and torch.equal(i0, i1) and torch.allclose(v0, v1, atol=1e-5)
+    v3, i3, n3 = _run_world(_shard_snapshot_worker, 3, path, "load")  # re-striped to 3 ranks
+    assert n3 == 998 and torch.equal(i0, i3) and torch.allclose(v0, v3, atol=1e-4)
+    assert not bool((i0 == 0).any() | (i0 == 5).any() | (i0 == 10).any())
+
+
 def test_all_reduce_routes_to_registered_custom_all_reduce():
     """comm.all_reduce takes a group's custom all-reduce when the tensor is eligible and
     falls back to the process group otherwise."""
