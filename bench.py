@@ -87,6 +87,11 @@ def main():
     world, rank = pctx.world_size, pctx.rank
     dev = str(pctx.device)
     gpu = pctx.device.type == "cuda"
+    if world > 1:
+        # one rank per GPU on a shared host: split the intra-op CPU pool instead of letting
+        # every rank spin up a full-width one (the host work is a single Python loop per rank)
+        ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+        torch.set_num_threads(max(1, min(torch.get_num_threads(), (ncpu or 1) // world)))
     t_setup = time.time()
     R = args.concurrency
     # graphs for the padded decode batch sizes this run can see
