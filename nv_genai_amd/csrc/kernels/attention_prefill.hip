@@ -159,6 +159,10 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
     for (int dt = 0; dt < DT; ++dt) o[cg][dt] = (f32x4)(0.f);
   }
 
+  // (Tried: separate masked/unmasked instantiations of this body behind a wave-uniform
+  // branch to drop the ~60 if-converted mask selects per tile. 39.3 -> 34.5 us at 1 x 1,196
+  // but 658 -> 672 us at 27 x 1,200: the two bodies need 252 VGPRs, 3 -> 2 waves/SIMD, and
+  // forcing 3 waves spills.)
   auto compute_tile = [&](int t) {
       f32x4 sacc[NCG][4];
 #pragma unroll
@@ -213,15 +217,25 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
 #pragma unroll
           for (int dt = 0; dt < DT; ++dt) o[cg][dt] *= alpha;
         }
-        const float mc = m[cg];
+        // exponent argument and row-sum in packed fp32 (v_pk_fma_f32 / v_pk_add_f32: two
+        // scores per VALU op, two independent add chains instead of one 16-long chain).
+        // Loop VALU 141 -> 128 instructions per tile at the same 148 VGPRs; kernel time within
+        // run-to-run noise (633 us at 27 x 1,200, profiles/r1_prefill_valu).
+        const f32x2 sl2v = {sl2, sl2}, nmc = {-m[cg], -m[cg]};
+        f32x2 lsum = {0.f, 0.f};
 #pragma unroll
         for (int g = 0; g < 2; ++g)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[cg][2 * g + (j >> 2)][j & 3], sl2, -mc));  // 2^-inf = 0
-            l[cg] += pv;
-            pf[cg][g][j] = (__bf16)pv;
+          for (int j = 0; j < 8; j += 2) {
+            const f32x4& sv = sacc[cg][2 * g + (j >> 2)];
+            f32x2 e = __builtin_elementwise_fma((f32x2){sv[j & 3], sv[(j & 3) + 1]}, sl2v, nmc);
+            e[0] = __builtin_amdgcn_exp2f(e[0]);  // 2^-inf = 0
+            e[1] = __builtin_amdgcn_exp2f(e[1]);
+            lsum += e;
+            pf[cg][g][j] = (__bf16)e[0];
+            pf[cg][g][j + 1] = (__bf16)e[1];
           }
+        l[cg] += lsum[0] + lsum[1];
       }
 #pragma unroll
       for (int g = 0; g < 2; ++g) {

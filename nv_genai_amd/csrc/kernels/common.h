@@ -17,6 +17,7 @@ namespace nga {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 
