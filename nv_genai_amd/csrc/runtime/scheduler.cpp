@@ -304,7 +304,11 @@ class Scheduler {
     int src = -1, dst = -1;
     const int full = p.computed / bs_;
     const bool partial = p.computed % bs_ != 0;
-    if (p.status == RUNNING && (!partial || bm_.num_free() > 0)) {
+    // the child gets as many blocks as the parent holds: the full ones shared, a copy of the
+    // partial one, and fresh blocks for the rest (a parent still prefilling already holds
+    // the blocks of its whole prompt, and fill_rows indexes them)
+    const int fresh = (int)p.blocks.size() - full;
+    if (p.status == RUNNING && fresh <= bm_.num_free()) {
       for (int i = 0; i < full; ++i) {
         bm_.share(p.blocks[i]);
         c.blocks.push_back(p.blocks[i]);
@@ -314,6 +318,7 @@ class Scheduler {
         dst = bm_.alloc();
         c.blocks.push_back(dst);
       }
+      while (c.blocks.size() < p.blocks.size()) c.blocks.push_back(bm_.alloc());
       c.hashes.assign(p.hashes.begin(), p.hashes.begin() + std::min<size_t>(full, p.hashes.size()));
       c.computed = p.computed;
       c.cached_prefix = p.cached_prefix;
@@ -499,6 +504,8 @@ class Scheduler {
     for (size_t i = 0; i < ids.size(); ++i) {
       Seq& s = seqs_.at(ids[i]);
       const int n = qlen[i];
+      if ((s.computed + n + bs_ - 1) / bs_ > (int)s.blocks.size())
+        throw std::runtime_error("scheduled tokens outside the sequence's KV blocks");
       for (int j = 0; j < n; ++j) {
         const int p = s.computed + j;
         B.ids(t) = s.toks[p];
