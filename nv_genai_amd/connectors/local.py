@@ -58,7 +58,7 @@ class LocalChatModel:
         return SamplingParams(**d)
 
     def _submit(self, messages: Messages, **kw) -> StreamHandle:
-        ids = self.tok.apply_chat_template(normalize_messages(messages))
+        ids = self.service.engine.apply_chat_template(normalize_messages(messages))
         h = self.service.submit(ids, self._params(**kw))
         self.last_handle = h
         return h

@@ -69,6 +69,24 @@ void layernorm(Tensor out, Tensor x, c10::optional<Tensor> resid, Tensor g, Tens
                         cur_stream(x));
 }
 
+// resid += delta; out = LayerNorm(resid) * g + b
+void add_layernorm(Tensor out, Tensor resid, Tensor delta, Tensor g, Tensor b, double eps) {
+  CHECK_BF16(out); CHECK_BF16(resid); CHECK_BF16(delta); CHECK_BF16(g); CHECK_BF16(b);
+  CHECK_CONTIG(out); CHECK_CONTIG(resid); CHECK_CONTIG(delta);
+  TORCH_CHECK(resid.dim() == 2 && resid.sizes() == delta.sizes() && resid.sizes() == out.sizes());
+  const int H = (int)resid.size(1);
+  TORCH_CHECK(H % 8 == 0 && H <= 8192 && g.numel() == H && b.numel() == H);
+  nga::launch_add_layernorm(bfp(out), bfp(resid), bfp(delta), bfp(g), bfp(b), (float)eps,
+                            resid.size(0), H, cur_stream(resid));
+}
+
+void gelu_tanh_mul(Tensor out, Tensor x) {
+  CHECK_BF16(out); CHECK_BF16(x); CHECK_CONTIG(out); CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.size(1) == 2 * out.size(1) && x.size(0) == out.size(0));
+  TORCH_CHECK(out.size(1) % 8 == 0);
+  nga::launch_gelu_tanh_mul(bfp(out), bfp(x), x.size(0), (int)out.size(1), cur_stream(x));
+}
+
 void silu_mul(Tensor out, Tensor x) {
   CHECK_BF16(out); CHECK_BF16(x); CHECK_CONTIG(out); CHECK_CONTIG(x);
   TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.size(1) == 2 * out.size(1) && x.size(0) == out.size(0));
@@ -76,14 +94,14 @@ void silu_mul(Tensor out, Tensor x) {
   nga::launch_silu_mul(bfp(out), bfp(x), x.size(0), (int)out.size(1), cur_stream(x));
 }
 
-void bias_gelu(Tensor x, c10::optional<Tensor> bias) {
+void bias_gelu(Tensor x, c10::optional<Tensor> bias, bool tanh_form) {
   CHECK_BF16(x); CHECK_CONTIG(x);
   TORCH_CHECK(x.dim() == 2 && x.size(1) % 8 == 0);
   if (bias.has_value()) {
     CHECK_BF16(*bias);
     TORCH_CHECK(bias->numel() == x.size(1));
   }
-  nga::launch_bias_gelu(bfp(x), cbfp(bias), x.size(0), (int)x.size(1), cur_stream(x));
+  nga::launch_bias_gelu(bfp(x), cbfp(bias), x.size(0), (int)x.size(1), tanh_form, cur_stream(x));
 }
 
 // ------------------------------------------------------------------ rope + kv cache
@@ -93,7 +111,7 @@ void rope_cache(Tensor qkv, Tensor pos, Tensor cos_sin, c10::optional<Tensor> sl
   CHECK_BF16(qkv); CHECK_CONTIG(qkv);
   CHECK_DEV(pos); CHECK_DT(pos, at::kInt);
   CHECK_DEV(cos_sin); CHECK_DT(cos_sin, at::kFloat); CHECK_CONTIG(cos_sin);
-  TORCH_CHECK(D == 128 || D == 64, "rope_cache: head_dim must be 64 or 128");
+  TORCH_CHECK(D == 128 || D == 64 || D == 256, "rope_cache: head_dim must be 64, 128 or 256");
   TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == (Hq + 2 * Hkv) * D, "rope_cache: qkv must be [T, (Hq+2Hkv)*D]");
   TORCH_CHECK(pos.numel() == qkv.size(0));
   TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D);
@@ -117,6 +135,92 @@ void rope_cache(Tensor qkv, Tensor pos, Tensor cos_sin, c10::optional<Tensor> sl
                          qkv.size(0), (int)Hq, (int)Hkv, (int)D, BS, cur_stream(qkv));
 }
 
+// ------------------------------------------------------------------ MoE
+void moe_route(Tensor logits, int64_t k, Tensor ids, Tensor w) {
+  CHECK_BF16(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "moe_route: logits must be [T, E]");
+  const int64_t T = logits.size(0), E = logits.size(1);
+  TORCH_CHECK(E >= 1 && E <= 64 && k >= 1 && k <= 8 && k <= E, "moe_route: 1 <= k <= min(8, E), E <= 64");
+  CHECK_DEV(ids); CHECK_DT(ids, at::kInt); CHECK_DEV(w); CHECK_DT(w, at::kFloat);
+  TORCH_CHECK(ids.numel() >= T * k && w.numel() >= T * k);
+  nga::launch_moe_route(bfp(logits), logits.stride(0), (int)T, (int)E, (int)k,
+                        ids.data_ptr<int32_t>(), w.data_ptr<float>(), cur_stream(logits));
+}
+
+void moe_align(Tensor ids, Tensor w, int64_t T, int64_t k, int64_t e0, int64_t E, int64_t bm,
+               Tensor sorted_tok, Tensor sorted_w, Tensor inv, Tensor tiles, int64_t mt_cap) {
+  const int64_t M = T * k;
+  CHECK_DEV(ids); CHECK_DT(ids, at::kInt);
+  CHECK_DEV(w); CHECK_DT(w, at::kFloat);
+  CHECK_DEV(sorted_tok); CHECK_DT(sorted_tok, at::kInt);
+  CHECK_DEV(sorted_w); CHECK_DT(sorted_w, at::kFloat);
+  CHECK_DEV(inv); CHECK_DT(inv, at::kInt);
+  CHECK_DEV(tiles); CHECK_DT(tiles, at::kInt);
+  TORCH_CHECK(E >= 1 && E <= 64 && (bm == 64 || bm == 128) && e0 >= 0);
+  TORCH_CHECK(ids.numel() >= M && w.numel() >= M && sorted_tok.numel() >= M &&
+              sorted_w.numel() >= M && inv.numel() >= M && tiles.numel() >= 3 * mt_cap);
+  // every expert's rows fit the table: sum_e ceil(cnt_e / bm) <= M / bm + E
+  TORCH_CHECK(mt_cap >= (M + bm - 1) / bm + E, "moe_align: M-tile table too small");
+  TORCH_CHECK(k >= 1 && k <= 8);
+  nga::launch_moe_align(ids.data_ptr<int32_t>(), w.data_ptr<float>(), (int)M, (int)k, (int)e0, (int)E,
+                        (int)bm, sorted_tok.data_ptr<int32_t>(), sorted_w.data_ptr<float>(),
+                        inv.data_ptr<int32_t>(), tiles.data_ptr<int32_t>(), (int)mt_cap,
+                        cur_stream(ids));
+}
+
+// mode 0: out [M, F] = act(A[sorted_tok] @ W_e[:F]^T) * (A[sorted_tok] @ W_e[F:]^T)
+// mode 1: out [M, N] = (A @ W_e^T) * sorted_w
+void moe_gemm(Tensor A, Tensor W, Tensor sorted_tok, Tensor sorted_w, Tensor tiles, int64_t mt,
+              int64_t bm, Tensor out, int64_t mode, int64_t act) {
+  CHECK_BF16(A); CHECK_BF16(W); CHECK_BF16(out);
+  CHECK_CONTIG(W); CHECK_CONTIG(out);
+  CHECK_DEV(sorted_tok); CHECK_DT(sorted_tok, at::kInt);
+  CHECK_DEV(sorted_w); CHECK_DT(sorted_w, at::kFloat);
+  CHECK_DEV(tiles); CHECK_DT(tiles, at::kInt);
+  TORCH_CHECK(mode == 0 || mode == 1);
+  TORCH_CHECK(bm == 64 || bm == 128);
+  TORCH_CHECK(W.dim() == 3 && A.dim() == 2 && out.dim() == 2 && A.stride(1) == 1);
+  const int64_t K = W.size(2);
+  TORCH_CHECK(A.size(1) == K && K % 64 == 0 && A.stride(0) % 8 == 0, "moe_gemm: K must match and be a multiple of 64");
+  TORCH_CHECK(tiles.numel() >= 3 * mt);
+  nga::MoeGemmParams p{};
+  p.A = bfp(A);
+  p.lda = A.stride(0);
+  p.W = bfp(W);
+  p.w_rows = W.size(1);
+  p.K = (int)K;
+  p.mt = (int)mt;
+  if (mode == 0) {
+    TORCH_CHECK(W.size(1) % 128 == 0, "moe_gemm: 2F must be a multiple of 128");
+    p.F = (int)(W.size(1) / 2);
+    TORCH_CHECK(out.size(1) == p.F, "moe_gemm: out must be [M, F]");
+    p.nt = p.F / 64;
+  } else {
+    TORCH_CHECK(W.size(1) % 128 == 0 && out.size(1) == W.size(1), "moe_gemm: out must be [M, N], N % 128 == 0");
+    p.F = 0;
+    p.nt = (int)(W.size(1) / 128);
+  }
+  TORCH_CHECK(sorted_tok.numel() >= out.size(0) && sorted_w.numel() >= out.size(0));
+  TORCH_CHECK(mode == 1 || A.size(0) >= 1);
+  // rows addressed by the table are < out.size(0) (moe_align writes positions < M = out rows)
+  p.sorted_tok = sorted_tok.data_ptr<int32_t>();
+  p.sorted_w = sorted_w.data_ptr<float>();
+  p.tiles = tiles.data_ptr<int32_t>();
+  p.out = bfp(out);
+  p.ldo = out.stride(0);
+  p.act = (int)act;
+  nga::launch_moe_gemm(p, (int)bm, (int)mode, cur_stream(out));
+}
+
+void moe_combine(Tensor y, Tensor inv, int64_t T, int64_t k, Tensor out) {
+  CHECK_BF16(y); CHECK_BF16(out); CHECK_CONTIG(y); CHECK_CONTIG(out);
+  CHECK_DEV(inv); CHECK_DT(inv, at::kInt);
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == T && y.dim() == 2 && y.size(1) == out.size(1));
+  TORCH_CHECK(out.size(1) % 8 == 0 && inv.numel() >= T * k && y.size(0) >= T * k);
+  nga::launch_moe_combine(bfp(y), inv.data_ptr<int32_t>(), (int)T, (int)k, (int)out.size(1),
+                          bfp(out), cur_stream(y));
+}
+
 // ------------------------------------------------------------------ attention
 int64_t decode_pages_per_part(int64_t num_seqs, int64_t Hkv, int64_t max_ctx) {
   return nga::decode_attn_pages_per_part((int)num_seqs, (int)Hkv, (int)max_ctx);
@@ -124,18 +228,21 @@ int64_t decode_pages_per_part(int64_t num_seqs, int64_t Hkv, int64_t max_ctx) {
 
 void decode_attention(Tensor out, Tensor q, Tensor kc, Tensor vc, Tensor block_tables,
                       Tensor ctx_lens, int64_t Hq, int64_t Hkv, int64_t max_ctx, double scale,
-                      int64_t pages_per_part, Tensor part_ml, Tensor part_o) {
+                      int64_t pages_per_part, Tensor part_ml, Tensor part_o, int64_t window) {
   CHECK_BF16(out); CHECK_BF16(q); CHECK_BF16(kc); CHECK_BF16(vc);
   CHECK_CONTIG(kc); CHECK_CONTIG(vc);
   CHECK_DEV(block_tables); CHECK_DT(block_tables, at::kInt); CHECK_CONTIG(block_tables);
   CHECK_DEV(ctx_lens); CHECK_DT(ctx_lens, at::kInt);
   const int64_t B = ctx_lens.numel();
-  TORCH_CHECK(q.dim() == 2 && q.size(0) >= B && q.stride(1) == 1 && q.size(1) >= Hq * 128,
-              "decode_attention: q must be [B, >=Hq*128] with unit inner stride");
-  TORCH_CHECK(out.dim() == 2 && out.size(0) >= B && out.stride(1) == 1 && out.size(1) >= Hq * 128);
-  TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(2) == 64 && kc.size(3) == 128,
-              "decode_attention: k cache must be [nb, Hkv, 64, 128]");
-  TORCH_CHECK(vc.sizes() == at::IntArrayRef({kc.size(0), Hkv, 128, 64}), "v cache must be [nb, Hkv, 128, 64]");
+  TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(2) == 64 &&
+              (kc.size(3) == 128 || kc.size(3) == 256),
+              "decode_attention: k cache must be [nb, Hkv, 64, 128|256]");
+  const int64_t D = kc.size(3);
+  TORCH_CHECK(q.dim() == 2 && q.size(0) >= B && q.stride(1) == 1 && q.size(1) >= Hq * D,
+              "decode_attention: q must be [B, >=Hq*D] with unit inner stride");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) >= B && out.stride(1) == 1 && out.size(1) >= Hq * D);
+  TORCH_CHECK(vc.sizes() == at::IntArrayRef({kc.size(0), Hkv, D, 64}), "v cache must be [nb, Hkv, D, 64]");
+  TORCH_CHECK(window >= 0);
   TORCH_CHECK(Hq % Hkv == 0 && Hq / Hkv <= 16, "decode_attention: G = Hq/Hkv must be <= 16");
   TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B);
   TORCH_CHECK(block_tables.size(1) * 64 >= max_ctx, "block table too narrow for max_ctx");
@@ -144,26 +251,28 @@ void decode_attention(Tensor out, Tensor q, Tensor kc, Tensor vc, Tensor block_t
   const int64_t nparts = (pages + pages_per_part - 1) / pages_per_part;
   if (nparts > 1) {
     CHECK_DEV(part_ml); CHECK_DEV(part_o);
-    TORCH_CHECK(part_ml.numel() >= B * Hq * nparts * 2 && part_o.numel() >= B * Hq * nparts * 128,
+    TORCH_CHECK(part_ml.numel() >= B * Hq * nparts * 2 && part_o.numel() >= B * Hq * nparts * D,
                 "decode_attention: partition workspace too small");
   }
   nga::launch_decode_attention(bfp(out), out.stride(0), bfp(q), q.stride(0), bfp(kc), bfp(vc),
                                block_tables.data_ptr<int32_t>(), (int)block_tables.size(1),
-                               ctx_lens.data_ptr<int32_t>(), (int)B, (int)Hq, (int)Hkv,
+                               ctx_lens.data_ptr<int32_t>(), (int)B, (int)Hq, (int)Hkv, (int)D,
                                (int)max_ctx, (float)scale, (int)pages_per_part,
                                nparts > 1 ? part_ml.data_ptr<float>() : nullptr,
-                               nparts > 1 ? part_o.data_ptr<float>() : nullptr, cur_stream(q));
+                               nparts > 1 ? part_o.data_ptr<float>() : nullptr, (int)window,
+                               cur_stream(q));
 }
 
 void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optional<Tensor> v,
                        c10::optional<Tensor> kc, c10::optional<Tensor> vc,
                        c10::optional<Tensor> block_tables, Tensor cu_q,
                        c10::optional<Tensor> ctx_lens, int64_t Hq, int64_t Hkv, int64_t D,
-                       int64_t max_q_len, double scale, bool causal) {
+                       int64_t max_q_len, double scale, bool causal, int64_t window) {
   CHECK_BF16(out); CHECK_BF16(q);
   CHECK_DEV(cu_q); CHECK_DT(cu_q, at::kInt); CHECK_CONTIG(cu_q);
-  TORCH_CHECK(D == 64 || D == 128 || (D == 32 && !kc.has_value()),
-              "prefill_attention: head_dim must be 64 or 128 (or 32 without a paged cache)");
+  TORCH_CHECK(D == 64 || D == 128 || (D == 32 && !kc.has_value()) || (D == 256 && kc.has_value()),
+              "prefill_attention: head_dim must be 64 or 128 (32: packed only, 256: paged only)");
+  TORCH_CHECK(window >= 0 && (window == 0 || causal), "prefill_attention: a window needs causal attention");
   TORCH_CHECK(Hq % Hkv == 0);
   TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1 && q.size(1) >= Hq * D && q.stride(0) % 8 == 0);
   TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) >= Hq * D && out.size(0) == q.size(0));
@@ -177,6 +286,7 @@ void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optio
   p.Hq = (int)Hq;
   p.Hkv = (int)Hkv;
   p.scale = (float)scale;
+  p.window = (int)window;
   const bool paged = kc.has_value();
   if (paged) {
     TORCH_CHECK(vc.has_value() && block_tables.has_value() && ctx_lens.has_value());
@@ -429,12 +539,18 @@ PYBIND11_MODULE(_C, m) {
   m.def("rmsnorm", checked("rmsnorm", &rmsnorm));
   m.def("add_rmsnorm", checked("add_rmsnorm", &add_rmsnorm));
   m.def("layernorm", checked("layernorm", &layernorm));
+  m.def("add_layernorm", checked("add_layernorm", &add_layernorm));
+  m.def("gelu_tanh_mul", checked("gelu_tanh_mul", &gelu_tanh_mul));
   m.def("silu_mul", checked("silu_mul", &silu_mul));
   m.def("bias_gelu", checked("bias_gelu", &bias_gelu));
   m.def("rope_cache", checked("rope_cache", &rope_cache));
   m.def("decode_pages_per_part", &decode_pages_per_part);
   m.def("decode_attention", checked("decode_attention", &decode_attention));
   m.def("prefill_attention", checked("prefill_attention", &prefill_attention));
+  m.def("moe_route", checked("moe_route", &moe_route));
+  m.def("moe_align", checked("moe_align", &moe_align));
+  m.def("moe_gemm", checked("moe_gemm", &moe_gemm));
+  m.def("moe_combine", checked("moe_combine", &moe_combine));
   m.def("sample", checked("sample", &sample));
   m.def("score", checked("score", &score));
   m.def("topk", checked("topk", &topk));

@@ -1,4 +1,4 @@
-// Elementwise activations (K5 SwiGLU, K11 bias+GELU). Memory-bound, 16-B vectors,
+// Elementwise activations (K5 SwiGLU / GeGLU, K11 bias+GELU). Memory-bound, 16-B vectors,
 // grid-stride with a capped grid (Guideline 11).
 #include "common.h"
 #include "kernels.h"
@@ -27,7 +27,33 @@ __global__ void silu_mul_kernel(uint16_t* __restrict__ out, const uint16_t* __re
   }
 }
 
-// x: [T, F] inout; x = gelu_erf(x + bias)
+// tanh-form GELU, 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3))), with tanh(u) written
+// as 1 - 2 / (1 + e^{2u}) so it costs one exp and one reciprocal
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return x - x / (1.f + __expf(2.f * u));
+}
+
+// in: [T, 2F] = [gate | up]; out: [T, F] = gelu_tanh(gate) * up   (Gemma GeGLU)
+__global__ void gelu_tanh_mul_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ in,
+                                     int64_t T, int F) {
+  const int64_t vec_per_row = F / 8;
+  const int64_t total = T * vec_per_row;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = i / vec_per_row;
+    const int64_t c = (i - t * vec_per_row) * 8;
+    u16x8 g = load8(in + t * 2 * F + c);
+    u16x8 u = load8(in + t * 2 * F + F + c);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(gelu_tanh(bf2f(g[j])) * bf2f(u[j]));
+    store8(out + t * F + c, o);
+  }
+}
+
+// x: [T, F] inout; x = gelu(x + bias), erf form or (TANH) the tanh approximation
+template <bool TANH>
 __global__ void bias_gelu_kernel(uint16_t* __restrict__ x, const uint16_t* __restrict__ bias,
                                  int64_t T, int F) {
   const int64_t vec_per_row = F / 8;
@@ -43,7 +69,7 @@ __global__ void bias_gelu_kernel(uint16_t* __restrict__ x, const uint16_t* __res
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float f = bf2f(v[j]) + (bias ? bf2f(b[j]) : 0.f);
-      o[j] = f2bf(0.5f * f * (1.f + erff(f * 0.70710678118654752f)));
+      o[j] = f2bf(TANH ? gelu_tanh(f) : 0.5f * f * (1.f + erff(f * 0.70710678118654752f)));
     }
     store8(x + t * F + c, o);
   }
@@ -61,9 +87,18 @@ void launch_silu_mul(uint16_t* out, const uint16_t* in, int64_t T, int F, hipStr
   silu_mul_kernel<<<ew_grid(T * F / 8), 256, 0, stream>>>(out, in, T, F);
 }
 
-void launch_bias_gelu(uint16_t* x, const uint16_t* bias, int64_t T, int F, hipStream_t stream) {
+void launch_gelu_tanh_mul(uint16_t* out, const uint16_t* in, int64_t T, int F, hipStream_t stream) {
   if (T == 0) return;
-  bias_gelu_kernel<<<ew_grid(T * F / 8), 256, 0, stream>>>(x, bias, T, F);
+  gelu_tanh_mul_kernel<<<ew_grid(T * F / 8), 256, 0, stream>>>(out, in, T, F);
+}
+
+void launch_bias_gelu(uint16_t* x, const uint16_t* bias, int64_t T, int F, bool tanh_form,
+                      hipStream_t stream) {
+  if (T == 0) return;
+  if (tanh_form)
+    bias_gelu_kernel<true><<<ew_grid(T * F / 8), 256, 0, stream>>>(x, bias, T, F);
+  else
+    bias_gelu_kernel<false><<<ew_grid(T * F / 8), 256, 0, stream>>>(x, bias, T, F);
 }
 
 }  // namespace nga

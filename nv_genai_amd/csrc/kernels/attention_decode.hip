@@ -1,4 +1,5 @@
-// Paged decode attention with GQA on MFMA (K2 in SURVEY.md §2.C).
+// Paged decode attention with GQA on MFMA (K2 in SURVEY.md §2.C), head_dim 128 / 256,
+// optional sliding window.
 //
 // One query token per sequence. For a (sequence, kv-head) pair the G = Hq/Hkv query rows
 // that share the kv head form the 16 columns of an MFMA tile (padded with zero rows), so
@@ -25,29 +26,41 @@
 namespace nga {
 
 namespace {
-constexpr int D = 128;
 constexpr int BS = 64;
 constexpr int NW = 4;
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float RESCALE_LOG2 = 8.f;
 }  // namespace
 
+// D = head_dim (128 or 256). For D = 128 a page's 64 keys are loaded and softmaxed in one
+// pass (KH = 2 key groups of 32); for D = 256 the K / Vt fragments of a whole page would need
+// 256 VGPRs, so the page is processed as two 32-key passes with their own online-softmax
+// update (KH = 1). WINDOW > 0 (sliding-window attention): the query at position ctx - 1 sees
+// keys (ctx - 1 - window, ctx - 1]; pages wholly before the window are never read.
+template <int D>
 __global__ void __launch_bounds__(256) decode_attn_kernel(
     uint16_t* __restrict__ out, int64_t out_stride, const uint16_t* __restrict__ q,
     int64_t q_stride, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int max_blocks,
     const int32_t* __restrict__ ctx_lens, int Hq, int Hkv, float scale, int pages_per_part,
-    float* __restrict__ part_ml, float* __restrict__ part_o) {
+    float* __restrict__ part_ml, float* __restrict__ part_o, int window) {
+  constexpr int DS = D / 32;   // d-steps of the QK^T MFMA
+  constexpr int DT = D / 16;   // d-tiles of the PV MFMA
+  constexpr int KH = D <= 128 ? 2 : 1;  // 32-key groups per softmax pass
+  constexpr int NPASS = 2 / KH;
   const int b = blockIdx.x, kvh = blockIdx.y, part = blockIdx.z, nparts = gridDim.z;
   const int G = Hq / Hkv;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = lane & 15, h = lane >> 4;
   const int ctx = ctx_lens[b];
   const int n_pages = (ctx + BS - 1) / BS;
-  // each sequence's own pages split evenly over the grid's partitions, so a split sized for
-  // the batch (hipGraph-captured with the worst-case context) still divides short contexts
-  const int ppp = (n_pages + nparts - 1) / nparts;
-  const int p_begin = part * ppp;
+  const int key_lo = window > 0 ? max(0, ctx - window) : 0;   // first visible key
+  const int p_lo = key_lo / BS;
+  // each sequence's own (visible) pages split evenly over the grid's partitions, so a split
+  // sized for the batch (hipGraph-captured with the worst-case context) still divides short
+  // contexts
+  const int ppp = (n_pages - p_lo + nparts - 1) / nparts;
+  const int p_begin = p_lo + part * ppp;
   const int p_end = min(n_pages, p_begin + ppp);
 
   __shared__ float o_s[NW][16][D + 4];
@@ -69,12 +82,12 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   }
 
   // Q^T as the B operand: lane holds Q[q=col][d = 32s + 8h + j]
-  bf16x8 qf[4];
+  bf16x8 qf[DS];
   {
     const bool qv = col < G;
     const uint16_t* qp = q + (int64_t)b * q_stride + (int64_t)(kvh * G + (qv ? col : 0)) * D;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < DS; ++s) {
       u16x8 v = load8(qp + 32 * s + 8 * h);
       if (!qv) v = (u16x8)(0);
       qf[s] = as_bf16x8(v);
@@ -83,91 +96,102 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 
   const float sl2 = scale * LOG2E;
   float m = -INFINITY, l = 0.f;
-  f32x4 o[8];
+  f32x4 o[DT];
 #pragma unroll
-  for (int dt = 0; dt < 8; ++dt) o[dt] = (f32x4)(0.f);
+  for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x4)(0.f);
 
   const int32_t* bt = block_tables + (int64_t)b * max_blocks;
   for (int p = p_begin + w; p < p_end; p += NW) {
     const int64_t blk = bt[p];
     const uint16_t* kp = kc + (blk * Hkv + kvh) * (int64_t)(BS * D);
     const uint16_t* vp = vc + (blk * Hkv + kvh) * (int64_t)(D * BS);
-    // K operand loads: tile tau (g = tau>>1, t1 = tau&1), row = col
-    u16x8 kf[4][4];
-#pragma unroll
-    for (int tau = 0; tau < 4; ++tau) {
-      const int key = 32 * (tau >> 1) + 8 * (col >> 2) + 4 * (tau & 1) + (col & 3);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) kf[tau][s] = load8(kp + key * D + 32 * s + 8 * h);
-    }
-    u16x8 vf[2][8];
-#pragma unroll
-    for (int g = 0; g < 2; ++g)
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) vf[g][dt] = load8(vp + (16 * dt + col) * BS + 32 * g + 8 * h);
-
-    f32x4 sacc[4];
-#pragma unroll
-    for (int tau = 0; tau < 4; ++tau) {
-      sacc[tau] = (f32x4)(0.f);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) sacc[tau] = mfma16(as_bf16x8(kf[tau][s]), qf[s], sacc[tau]);
-    }
-    // mask (only the sequence's last, partial page); lane's keys: 32g + 8h + 4t1 + r for
-    // tile tau = 2g + t1, reg r. Raw scores: the softmax scale is folded into the exp2 FMA.
     const int kbase = p * BS;
-    float mloc = -INFINITY;
-    if (kbase + BS <= ctx) {
+    const bool full = kbase + BS <= ctx && kbase >= key_lo;
 #pragma unroll
-      for (int tau = 0; tau < 4; ++tau)
+    for (int pass = 0; pass < NPASS; ++pass) {
+      // K operand loads: tile tau (g = tau>>1, t1 = tau&1), row = col
+      u16x8 kf[2 * KH][DS];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) mloc = fmaxf(mloc, sacc[tau][r]);
-    } else {
+      for (int ti = 0; ti < 2 * KH; ++ti) {
+        const int tau = 2 * KH * pass + ti;
+        const int key = 32 * (tau >> 1) + 8 * (col >> 2) + 4 * (tau & 1) + (col & 3);
 #pragma unroll
-      for (int tau = 0; tau < 4; ++tau)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kbase + 32 * (tau >> 1) + 8 * h + 4 * (tau & 1) + r;
-          const float sv = key < ctx ? sacc[tau][r] : -INFINITY;
-          sacc[tau][r] = sv;
-          mloc = fmaxf(mloc, sv);
-        }
-    }
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    mloc *= sl2;  // scale > 0: max commutes with it
-    // Lazy rescaling (as in the prefill kernel): the running max only moves, and O / l are
-    // only rescaled, when a page's max exceeds it by more than 2^RESCALE_LOG2; until then
-    // P = 2^(s - m) <= 2^8 stays harmless in fp32 l / O and bf16 P. m starts at -inf, so the
-    // first page always rescales (alpha = 2^-inf = 0 on the all-zero O). Every page has at
-    // least one valid key, so m is finite from then on.
-    if (mloc > m + RESCALE_LOG2) {
-      const float alpha = __builtin_amdgcn_exp2f(m - mloc);
-      m = mloc;
-      l *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
-    }
-    bf16x8 pf[2];
-#pragma unroll
-    for (int g = 0; g < 2; ++g)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[2 * g + (j >> 2)][j & 3], sl2, -m));  // 2^-inf = 0
-        l += pv;
-        pf[g][j] = (__bf16)pv;
+        for (int s = 0; s < DS; ++s) kf[ti][s] = load8(kp + key * D + 32 * s + 8 * h);
       }
+      u16x8 vf[KH][DT];
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+      for (int gi = 0; gi < KH; ++gi) {
+        const int g = KH * pass + gi;
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt) o[dt] = mfma16(as_bf16x8(vf[g][dt]), pf[g], o[dt]);
+        for (int dt = 0; dt < DT; ++dt) vf[gi][dt] = load8(vp + (16 * dt + col) * BS + 32 * g + 8 * h);
+      }
+
+      f32x4 sacc[2 * KH];
+#pragma unroll
+      for (int ti = 0; ti < 2 * KH; ++ti) {
+        sacc[ti] = (f32x4)(0.f);
+#pragma unroll
+        for (int s = 0; s < DS; ++s) sacc[ti] = mfma16(as_bf16x8(kf[ti][s]), qf[s], sacc[ti]);
+      }
+      // mask (the sequence's last, partial page; the window's first page); lane's keys:
+      // 32g + 8h + 4t1 + r for tile tau = 2g + t1, reg r. Raw scores: the softmax scale is
+      // folded into the exp2 FMA.
+      float mloc = -INFINITY;
+      if (full) {
+#pragma unroll
+        for (int ti = 0; ti < 2 * KH; ++ti)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mloc = fmaxf(mloc, sacc[ti][r]);
+      } else {
+#pragma unroll
+        for (int ti = 0; ti < 2 * KH; ++ti)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int tau = 2 * KH * pass + ti;
+            const int key = kbase + 32 * (tau >> 1) + 8 * h + 4 * (tau & 1) + r;
+            const float sv = (key < ctx && key >= key_lo) ? sacc[ti][r] : -INFINITY;
+            sacc[ti][r] = sv;
+            mloc = fmaxf(mloc, sv);
+          }
+      }
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      mloc *= sl2;  // scale > 0: max commutes with it
+      // Lazy rescaling (as in the prefill kernel): the running max only moves, and O / l are
+      // only rescaled, when a pass's max exceeds it by more than 2^RESCALE_LOG2; until then
+      // P = 2^(s - m) <= 2^8 stays harmless in fp32 l / O and bf16 P. m starts at -inf, so
+      // the first pass with a visible key rescales (alpha = 2^-inf = 0 on the all-zero O). A
+      // pass can be fully masked (D = 256 halves, window edges): m may still be -inf then, so
+      // the exponent offset uses 0 instead (2^-inf = 0 either way).
+      if (mloc > m + RESCALE_LOG2) {
+        const float alpha = __builtin_amdgcn_exp2f(m - mloc);
+        m = mloc;
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      }
+      const float mo = m == -INFINITY ? 0.f : -m;
+      bf16x8 pf[KH];
+#pragma unroll
+      for (int gi = 0; gi < KH; ++gi)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[2 * gi + (j >> 2)][j & 3], sl2, mo));  // 2^-inf = 0
+          l += pv;
+          pf[gi][j] = (__bf16)pv;
+        }
+#pragma unroll
+      for (int gi = 0; gi < KH; ++gi)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16(as_bf16x8(vf[gi][dt]), pf[gi], o[dt]);
+    }
   }
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
 
   // wave partials -> LDS. O^T layout: lane holds O[q=col][d = 16dt + 4h + r]
 #pragma unroll
-  for (int dt = 0; dt < 8; ++dt)
+  for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) o_s[w][col][16 * dt + 4 * h + r] = o[dt][r];
   if (h == 0) {
@@ -190,7 +214,7 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     }
     const int hq = kvh * G + qi;
     if (nparts == 1) {
-      out[(int64_t)b * out_stride + (int64_t)hq * D + d] = f2bf(acc / L);
+      out[(int64_t)b * out_stride + (int64_t)hq * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
     } else {
       const int64_t idx = ((int64_t)b * Hq + hq) * nparts + part;
       part_o[idx * D + d] = acc;
@@ -202,22 +226,25 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   }
 }
 
+template <int D>
 __global__ void decode_attn_reduce_kernel(uint16_t* __restrict__ out, int64_t out_stride,
                                           const float* __restrict__ part_ml,
                                           const float* __restrict__ part_o, int Hq, int nparts) {
-  const int b = blockIdx.x, hq = blockIdx.y, d = threadIdx.x;
+  const int b = blockIdx.x, hq = blockIdx.y;
   const int64_t base = ((int64_t)b * Hq + hq) * nparts;
   float M = -INFINITY;
   for (int p = 0; p < nparts; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
-  float L = 0.f, acc = 0.f;
-  for (int p = 0; p < nparts; ++p) {
-    const float mp = part_ml[2 * (base + p)];
-    if (mp == -INFINITY) continue;
-    const float f = exp2f(mp - M);
-    L += f * part_ml[2 * (base + p) + 1];
-    acc += f * part_o[(base + p) * D + d];
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float L = 0.f, acc = 0.f;
+    for (int p = 0; p < nparts; ++p) {
+      const float mp = part_ml[2 * (base + p)];
+      if (mp == -INFINITY) continue;
+      const float f = exp2f(mp - M);
+      L += f * part_ml[2 * (base + p) + 1];
+      acc += f * part_o[(base + p) * D + d];
+    }
+    out[(int64_t)b * out_stride + (int64_t)hq * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
   }
-  out[(int64_t)b * out_stride + (int64_t)hq * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
 }
 
 int decode_attn_pages_per_part(int num_seqs, int Hkv, int max_ctx) {
@@ -234,19 +261,27 @@ int decode_attn_pages_per_part(int num_seqs, int Hkv, int max_ctx) {
 void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* q,
                              int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
                              const int32_t* block_tables, int max_blocks, const int32_t* ctx_lens,
-                             int num_seqs, int Hq, int Hkv, int max_ctx, float scale,
-                             int pages_per_part, float* part_ml, float* part_o,
+                             int num_seqs, int Hq, int Hkv, int D, int max_ctx, float scale,
+                             int pages_per_part, float* part_ml, float* part_o, int window,
                              hipStream_t stream) {
   if (num_seqs == 0) return;
-  const int pages = (max_ctx + BS - 1) / BS;
+  int pages = (max_ctx + BS - 1) / BS;
+  if (window > 0) pages = min(pages, (window + BS - 1) / BS + 1);  // visible pages at most
   const int nparts = (pages + pages_per_part - 1) / pages_per_part;
   dim3 grid(num_seqs, Hkv, nparts);
-  decode_attn_kernel<<<grid, 256, 0, stream>>>(out, out_stride, q, q_stride, kc, vc, block_tables,
-                                               max_blocks, ctx_lens, Hq, Hkv, scale,
-                                               pages_per_part, part_ml, part_o);
-  if (nparts > 1) {
-    dim3 g2(num_seqs, Hq);
-    decode_attn_reduce_kernel<<<g2, D, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts);
+  dim3 g2(num_seqs, Hq);
+  if (D == 256) {
+    decode_attn_kernel<256><<<grid, 256, 0, stream>>>(out, out_stride, q, q_stride, kc, vc,
+                                                      block_tables, max_blocks, ctx_lens, Hq, Hkv,
+                                                      scale, pages_per_part, part_ml, part_o, window);
+    if (nparts > 1)
+      decode_attn_reduce_kernel<256><<<g2, 256, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts);
+  } else {
+    decode_attn_kernel<128><<<grid, 256, 0, stream>>>(out, out_stride, q, q_stride, kc, vc,
+                                                      block_tables, max_blocks, ctx_lens, Hq, Hkv,
+                                                      scale, pages_per_part, part_ml, part_o, window);
+    if (nparts > 1)
+      decode_attn_reduce_kernel<128><<<g2, 128, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts);
   }
 }
 

@@ -16,7 +16,9 @@
 //        queries are the last q_len positions of a ctx_len context (chunked prefill and
 //        prefix-cache hits work unchanged).  Otherwise: K and V rows come from packed
 //        [T, H, D] tensors with per-sequence offsets (cu_q), V is transposed while staging.
-// D is 64 or 128 (either mode) or 32 (packed mode only: the all-MiniLM-L6-v2 encoder).
+// D is 64 or 128 (either mode), 256 (paged: Gemma) or 32 (packed mode only: the
+// all-MiniLM-L6-v2 encoder). P.window > 0: sliding-window causal attention (query i sees keys
+// (i - window, i]); key tiles wholly before every query's window are skipped.
 #include <cstdlib>
 
 #include "common.h"
@@ -54,6 +56,9 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
   // contiguous range of the (sequence, kv head, q head, tile) order: the G query heads that
   // share a KV head — and every query tile of them — read their K/V pages through the same
   // 4 MB L2. Within a (sequence, head) the longest causal tiles go first.
+  // K-row swizzle: XOR the 16-B chunk index with up to 4 bits of the row (fewer for short
+  // rows: the XOR value must stay below the chunk count)
+  constexpr int SWS = NCH_K >= 16 ? 0 : NCH_K == 8 ? 1 : 2;
   const int pblk = blockIdx.x;
   const int L = (pblk & 7) * P.per_xcd + (pblk >> 3);
   if (L >= P.total) return;
@@ -87,12 +92,16 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
   }
 
   const int qpos_w0 = ctx - qlen + tile * QT + w * 16 * NCG;  // smallest query position of this wave
+  const int qpos_w1 = qpos_w0 + 16 * NCG - 1;                  // largest (may exceed ctx: masked rows)
+  const int W = CAUSAL ? P.window : 0;
   int last_key = ctx - 1;
   if (CAUSAL) {
     const int qmax = min(qlen - 1, tile * QT + QT - 1);
     last_key = min(last_key, ctx - qlen + qmax);
   }
   const int n_tiles = last_key / KT + 1;
+  // sliding window: the workgroup's oldest visible key belongs to its first query row
+  const int t_first = W > 0 ? max(0, ctx - qlen + tile * QT - W + 1) / KT : 0;
 
   // staging registers, one tile ahead (a second set, two tiles ahead, measured no faster
   // and costs 32 VGPRs that the accumulators need)
@@ -130,7 +139,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
       const int c = tid + 256 * i;
       {  // K: row = key, chunk = d/8
         const int row = c / NCH_K, ch = c % NCH_K;
-        const int sw = row_swz(row) >> (NCH_K == 16 ? 0 : NCH_K == 8 ? 1 : 2);
+        const int sw = row_swz(row) >> SWS;
         *reinterpret_cast<u16x8*>(&k_s[row * D + ((ch ^ sw) * 8)]) = kreg[i];
       }
       if (PAGED) {  // Vt page is already [d][key]: row = d, chunk = key/8
@@ -168,7 +177,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
 #pragma unroll
       for (int tau = 0; tau < 4; ++tau) {
         const int row = 32 * (tau >> 1) + 8 * (col >> 2) + 4 * (tau & 1) + (col & 3);
-        const int sw = row_swz(row) >> (NCH_K == 16 ? 0 : NCH_K == 8 ? 1 : 2);
+        const int sw = row_swz(row) >> SWS;
 #pragma unroll
         for (int cg = 0; cg < NCG; ++cg) sacc[cg][tau] = (f32x4)(0.f);
 #pragma unroll
@@ -182,7 +191,8 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
       const int kbase = t * KT;
       // masking is only needed on tiles that cross this wave's causal diagonal (or the end
       // of the context); the test is wave-uniform
-      const bool need_mask = CAUSAL ? (kbase + KT - 1 > qpos_w0) : (kbase + KT > ctx);
+      const bool need_mask = CAUSAL ? (kbase + KT - 1 > qpos_w0 || (W > 0 && kbase <= qpos_w1 - W))
+                                    : (kbase + KT > ctx);
       bf16x8 pf[NCG][2];
 #pragma unroll
       for (int cg = 0; cg < NCG; ++cg) {
@@ -194,7 +204,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
             float sv = sacc[cg][tau][r];  // raw score; the scale is folded into the exp
             if (need_mask) {
               const int key = kbase + 32 * (tau >> 1) + 8 * h + 4 * (tau & 1) + r;
-              const bool ok = CAUSAL ? (key <= qpos[cg]) : (key < ctx);
+              const bool ok = CAUSAL ? (key <= qpos[cg] && (W == 0 || key > qpos[cg] - W)) : (key < ctx);
               sv = ok ? sv : -INFINITY;
             }
             sacc[cg][tau][r] = sv;
@@ -211,7 +221,8 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
         const bool grow = mloc > m[cg] + RESCALE_LOG2;
         if (__ballot(grow)) {
           const float m_new = grow ? mloc : m[cg];
-          const float alpha = __builtin_amdgcn_exp2f(m[cg] - m_new);
+          // non-growing lanes keep their scale (and a still -inf m must not meet -inf - -inf)
+          const float alpha = grow ? __builtin_amdgcn_exp2f(m[cg] - m_new) : 1.f;
           m[cg] = m_new;
           l[cg] *= alpha;
 #pragma unroll
@@ -221,7 +232,10 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
         // scores per VALU op, two independent add chains instead of one 16-long chain).
         // Loop VALU 141 -> 128 instructions per tile at the same 148 VGPRs; kernel time within
         // run-to-run noise (633 us at 27 x 1,200, profiles/r1_prefill_valu).
-        const f32x2 sl2v = {sl2, sl2}, nmc = {-m[cg], -m[cg]};
+        // a tile can be fully masked for a row (sliding window): m may still be -inf then,
+        // and the offset must not become +inf (2^(-inf + inf) = NaN)
+        const float mo = m[cg] == -INFINITY ? 0.f : -m[cg];
+        const f32x2 sl2v = {sl2, sl2}, nmc = {mo, mo};
         f32x2 lsum = {0.f, 0.f};
 #pragma unroll
         for (int g = 0; g < 2; ++g)
@@ -251,8 +265,8 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
       }
   };
 
-  load_tile(0, kA, vA);
-  for (int t = 0; t < n_tiles; ++t) {
+  load_tile(t_first, kA, vA);
+  for (int t = t_first; t < n_tiles; ++t) {
     __syncthreads();  // previous tile's LDS reads are done
     store_tile(kA, vA);
     __syncthreads();
@@ -265,7 +279,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
     ll += __shfl_xor(ll, 16, 64);
     ll += __shfl_xor(ll, 32, 64);
     if (row_ok[cg]) {
-      const float inv = 1.f / ll;
+      const float inv = ll > 0.f ? 1.f / ll : 0.f;
       uint16_t* op = P.out + (int64_t)(q0 + qr[cg]) * P.out_stride + (int64_t)hq * D;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
@@ -301,7 +315,9 @@ void launch_prefill_attention(const PrefillParams& p, int num_seqs, int max_q_le
     if (ncg == 2) prefill_attn_kernel<DD, PG, CS, 2><<<grid, 256, 0, stream>>>(pp); \
     else prefill_attn_kernel<DD, PG, CS, 1><<<grid, 256, 0, stream>>>(pp);          \
   } while (0)
-  if (D == 128) {
+  if (D == 256 && paged) {   // Gemma (head_dim 256): paged causal prefill
+    if (causal) NGA_PF(256, true, true); else NGA_PF(256, true, false);
+  } else if (D == 128) {
     if (paged) {
       if (causal) NGA_PF(128, true, true); else NGA_PF(128, true, false);
     } else {

@@ -12,10 +12,15 @@ void launch_rmsnorm(uint16_t* out, uint16_t* resid, const uint16_t* delta, const
                     hipStream_t stream);
 void launch_layernorm(uint16_t* out, const uint16_t* x, const uint16_t* resid, const uint16_t* g,
                       const uint16_t* b, float eps, int64_t rows, int H, hipStream_t stream);
+// resid += delta (stored); out = LN(resid) * g + b
+void launch_add_layernorm(uint16_t* out, uint16_t* resid, const uint16_t* delta, const uint16_t* g,
+                          const uint16_t* b, float eps, int64_t rows, int H, hipStream_t stream);
 
 // activation.hip
 void launch_silu_mul(uint16_t* out, const uint16_t* in, int64_t T, int F, hipStream_t stream);
-void launch_bias_gelu(uint16_t* x, const uint16_t* bias, int64_t T, int F, hipStream_t stream);
+void launch_gelu_tanh_mul(uint16_t* out, const uint16_t* in, int64_t T, int F, hipStream_t stream);
+void launch_bias_gelu(uint16_t* x, const uint16_t* bias, int64_t T, int F, bool tanh_form,
+                      hipStream_t stream);
 
 // rope.hip
 void launch_rope_cache(uint16_t* qkv, const int32_t* pos, const float* cos_sin,
@@ -27,8 +32,8 @@ int decode_attn_pages_per_part(int num_seqs, int Hkv, int max_ctx);
 void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* q,
                              int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
                              const int32_t* block_tables, int max_blocks, const int32_t* ctx_lens,
-                             int num_seqs, int Hq, int Hkv, int max_ctx, float scale,
-                             int pages_per_part, float* part_ml, float* part_o,
+                             int num_seqs, int Hq, int Hkv, int D, int max_ctx, float scale,
+                             int pages_per_part, float* part_ml, float* part_o, int window,
                              hipStream_t stream);
 
 // attention_prefill.hip
@@ -52,6 +57,7 @@ struct PrefillParams {
   int ntiles;  // query tiles per (sequence, head) — set by the launcher
   int per_xcd; // workgroups per XCD slice of the 1-D grid — set by the launcher
   int total;   // ntiles * Hq * num_seqs — set by the launcher
+  int window;  // > 0: sliding-window causal attention (query i sees keys (i - window, i])
 };
 void launch_prefill_attention(const PrefillParams& p, int num_seqs, int max_q_len, int D,
                               bool paged, bool causal, hipStream_t stream);
@@ -83,5 +89,31 @@ void launch_resample_pcm(const float* x, int n, const float* h, int nh, int down
                          float gain, float* yf, int16_t* yi, hipStream_t stream);
 void launch_quant_fp8_rows(const uint16_t* x, int64_t ldx, int64_t rows, int H, int mode, uint8_t* y,
                            float* scale, hipStream_t stream);
+
+// moe.hip (sparse MoE MLP)
+struct MoeGemmParams {
+  const uint16_t* A;         // MODE 0: token rows x [T, K] (gathered); MODE 1: [M, K] sorted rows
+  int64_t lda;
+  const uint16_t* W;         // [E, w_rows, K] expert weights
+  int64_t w_rows;            // rows per expert (2F for gate|up, N for down)
+  int K;
+  int F;                     // MODE 0: features (up rows start at F)
+  int mt;                    // M tiles (table entries)
+  int nt;                    // N blocks: F / 64 (MODE 0) or N / 128 (MODE 1)
+  const int32_t* sorted_tok;
+  const float* sorted_w;
+  const int32_t* tiles;      // [mt, 3]: expert, first row, end row (expert -1: unused)
+  uint16_t* out;
+  int64_t ldo;
+  int act;                   // MODE 0: 0 silu, 1 gelu_tanh
+};
+void launch_moe_route(const uint16_t* logits, int64_t ld, int T, int E, int k, int32_t* ids,
+                      float* w, hipStream_t stream);
+void launch_moe_align(const int32_t* ids, const float* w, int M, int k, int e0, int E, int bm,
+                      int32_t* sorted_tok, float* sorted_w, int32_t* inv, int32_t* tiles,
+                      int mt_cap, hipStream_t stream);
+void launch_moe_gemm(const MoeGemmParams& p, int bm, int mode, hipStream_t stream);
+void launch_moe_combine(const uint16_t* y, const int32_t* inv, int T, int k, int H, uint16_t* out,
+                        hipStream_t stream);
 
 }  // namespace nga

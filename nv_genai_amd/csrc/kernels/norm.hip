@@ -52,14 +52,18 @@ __global__ void __launch_bounds__(1024) rmsnorm_kernel(uint16_t* __restrict__ ou
   }
 }
 
-// out = LN(x (+ resid)) * g + b ; if ADD, x+resid is also what is normalised.
-template <bool ADD>
+// MODE 0: out = LN(x) * g + b
+// MODE 1: out = LN(x + resid) * g + b            (BERT post-LN blocks; nothing written back)
+// MODE 2: x += resid (stored, bf16); out = LN(x)  (pre-LN decoders: StarCoder2's residual
+//         stream, x is the residual and `resid` the block output being added)
+template <int MODE>
 __global__ void __launch_bounds__(1024) layernorm_kernel(uint16_t* __restrict__ out,
-                                                         const uint16_t* __restrict__ x_in,
+                                                         uint16_t* __restrict__ x_in,
                                                          const uint16_t* __restrict__ resid,
                                                          const uint16_t* __restrict__ g,
                                                          const uint16_t* __restrict__ b, float eps,
                                                          int H) {
+  constexpr bool ADD = MODE != 0;
   __shared__ float red[16];
   const int64_t row = blockIdx.x;
   const int c = threadIdx.x * 8;
@@ -72,6 +76,15 @@ __global__ void __launch_bounds__(1024) layernorm_kernel(uint16_t* __restrict__ 
       u16x8 d = load8(resid + row * H + c);
 #pragma unroll
       for (int i = 0; i < 8; ++i) x[i] = bf2f(v[i]) + bf2f(d[i]);
+      if (MODE == 2) {
+        u16x8 sv;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          sv[i] = f2bf(x[i]);
+          x[i] = bf2f(sv[i]);  // normalise the stored bf16 residual
+        }
+        store8(x_in + row * H + c, sv);
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i) x[i] = bf2f(v[i]);
@@ -119,10 +132,18 @@ void launch_layernorm(uint16_t* out, const uint16_t* x, const uint16_t* resid, c
                       const uint16_t* b, float eps, int64_t rows, int H, hipStream_t stream) {
   if (rows == 0) return;
   dim3 grid((unsigned)rows), block(row_threads(H));
+  uint16_t* xm = const_cast<uint16_t*>(x);  // read-only in modes 0 / 1
   if (resid)
-    layernorm_kernel<true><<<grid, block, 0, stream>>>(out, x, resid, g, b, eps, H);
+    layernorm_kernel<1><<<grid, block, 0, stream>>>(out, xm, resid, g, b, eps, H);
   else
-    layernorm_kernel<false><<<grid, block, 0, stream>>>(out, x, resid, g, b, eps, H);
+    layernorm_kernel<0><<<grid, block, 0, stream>>>(out, xm, resid, g, b, eps, H);
+}
+
+void launch_add_layernorm(uint16_t* out, uint16_t* resid, const uint16_t* delta, const uint16_t* g,
+                          const uint16_t* b, float eps, int64_t rows, int H, hipStream_t stream) {
+  if (rows == 0) return;
+  dim3 grid((unsigned)rows), block(row_threads(H));
+  layernorm_kernel<2><<<grid, block, 0, stream>>>(out, resid, delta, g, b, eps, H);
 }
 
 }  // namespace nga

@@ -143,6 +143,8 @@ void launch_rope_cache(uint16_t* qkv, const int32_t* pos, const float* cos_sin,
     dim3 grid((unsigned)((T + RT - 1) / RT), (unsigned)(Hq + 2 * Hkv)), block(256);
     if (D == 128)
       rope_cache_tiled_kernel<128><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS);
+    else if (D == 256)
+      rope_cache_tiled_kernel<256><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS);
     else if (D == 64)
       rope_cache_tiled_kernel<64><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS);
     return;
@@ -150,6 +152,8 @@ void launch_rope_cache(uint16_t* qkv, const int32_t* pos, const float* cos_sin,
   dim3 grid((unsigned)T), block(256);
   if (D == 128)
     rope_cache_kernel<128><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, BS);
+  else if (D == 256)
+    rope_cache_kernel<256><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, BS);
   else if (D == 64)
     rope_cache_kernel<64><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, BS);
 }

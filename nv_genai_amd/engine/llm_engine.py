@@ -201,7 +201,11 @@ class LLMEngine:
         self.d_tok = dbuf(S)
         self.d_lp = dbuf(S, dtype=torch.float32)
         self.decode_ws = ops.DecodeWorkspace(S, self.model.hq, self.model.hkv, cfg.max_model_len,
-                                             dev, cfg.decode_pages_per_part) if self.gpu else None
+                                             dev, cfg.decode_pages_per_part,
+                                             D=self.model.D) if self.gpu else None
+        if self.gpu and self.mcfg.is_moe:
+            # routing buffers sized for the largest step before any hipGraph capture
+            ops.MoEWorkspace.get(T, self.mcfg.experts_per_tok, self.model.n_experts, dev)
         self.requests: Dict[int, Request] = {}
         self._ids = itertools.count(1)
         self._rng = random.Random(cfg.seed)
@@ -234,6 +238,11 @@ class LLMEngine:
             self._capture_graphs()
 
     # ------------------------------------------------------------------ requests
+    def apply_chat_template(self, messages, add_generation_prompt: bool = True) -> List[int]:
+        """Prompt ids of a chat in this model family's format (``LlamaConfig.chat_format``)."""
+        return self.tok.apply_chat_template(messages, add_generation_prompt,
+                                            fmt=self.mcfg.chat_format)
+
     def add_request(self, prompt_ids: List[int], params: Optional[SamplingParams] = None,
                     request_id: Optional[int] = None,
                     on_token: Optional[Callable[[Request, str], None]] = None) -> Request:

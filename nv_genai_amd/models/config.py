@@ -15,6 +15,19 @@ from typing import Optional
 
 @dataclass(frozen=True)
 class LlamaConfig:
+    """Decoder-only LM config. The defaults are Llama-3-8B; the architecture switches below
+    cover every decoder family the reference names:
+
+    * ``mistral`` — Llama layout, optional sliding-window attention (Mistral-7B NIM config,
+      experimental/fm-asr-streaming-rag/nim/configs/mistral-7b.yaml:3);
+    * ``mixtral`` — sparse MoE MLP, ``num_experts`` SwiGLU experts, top-``experts_per_tok``
+      softmax routing (the reference's default chat model ``ai-mixtral-8x7b-instruct``,
+      RetrievalAugmentedGeneration/common/configuration.py:75);
+    * ``gemma`` — GeGLU (tanh GELU), RMSNorm with a (1 + w) scale, sqrt(hidden) embedding
+      scale, tied embeddings, head_dim 256 (models/Gemma/*.ipynb, models/Codegemma/lora.ipynb);
+    * ``starcoder2`` — LayerNorm with bias, biased projections, non-gated tanh-GELU MLP,
+      sliding-window attention (models/StarCoder2/*.ipynb)."""
+
     name: str = "llama3-8b"
     vocab_size: int = 128256
     hidden: int = 4096
@@ -29,15 +42,35 @@ class LlamaConfig:
     max_position: int = 8192
     bos_id: int = 128000
     eos_ids: tuple = (128001, 128009)
+    arch: str = "llama"            # llama | mistral | mixtral | gemma | starcoder2
+    norm: str = "rms"              # rms | layer (LayerNorm with bias)
+    act: str = "silu"              # silu | gelu_tanh
+    gated_mlp: bool = True         # act(gate) * up  (False: act(fc(x) + b) -> proj)
+    attn_bias: bool = False        # q/k/v/o projection biases
+    mlp_bias: bool = False
+    embed_scale: float = 1.0       # Gemma multiplies the embedding by sqrt(hidden)
+    tie_embeddings: bool = False
+    sliding_window: int = 0        # 0: full causal attention; W: key j visible to query i iff i - W < j <= i
+    num_experts: int = 0           # > 0: sparse MoE MLP
+    experts_per_tok: int = 2
+    chat_format: str = "llama3"    # llama3 | mistral | gemma | plain
+
+    @property
+    def is_moe(self) -> bool:
+        return self.num_experts > 0
 
     @property
     def qkv_dim(self) -> int:
         return (self.heads + 2 * self.kv_heads) * self.head_dim
 
     def num_params(self) -> int:
+        mlp = (3 if self.gated_mlp else 2) * self.hidden * self.ffn
+        if self.is_moe:
+            mlp = mlp * self.num_experts + self.num_experts * self.hidden
         per_layer = (self.hidden * self.qkv_dim + self.heads * self.head_dim * self.hidden
-                     + 3 * self.hidden * self.ffn + 2 * self.hidden)
-        return per_layer * self.layers + 2 * self.vocab_size * self.hidden + self.hidden
+                     + mlp + 2 * self.hidden)
+        heads = 1 if self.tie_embeddings else 2
+        return per_layer * self.layers + heads * self.vocab_size * self.hidden + self.hidden
 
     def kv_bytes_per_token(self, dtype_bytes: int = 2) -> int:
         return 2 * self.layers * self.kv_heads * self.head_dim * dtype_bytes
@@ -81,6 +114,50 @@ LLAMA_PRESETS = {
     # hidden 768) in this architecture, for training/pretrain.py
     "slm-125m": LlamaConfig(name="slm-125m", hidden=768, layers=12, heads=12, kv_heads=12,
                             head_dim=64, ffn=2048, rope_theta=10000.0, max_position=2048),
+    # ---- other decoder families (public model-card dimensions)
+    # Mistral-7B-Instruct v0.3 (32768-token vocabulary, full attention, theta 1e6)
+    "mistral-7b": LlamaConfig(name="mistral-7b", arch="mistral", vocab_size=32768, rope_theta=1e6,
+                              max_position=32768, bos_id=1, eos_ids=(2,), chat_format="mistral"),
+    # Mistral-7B v0.1: 4096-token sliding window
+    "mistral-7b-v0.1": LlamaConfig(name="mistral-7b-v0.1", arch="mistral", vocab_size=32000,
+                                   rope_theta=10000.0, sliding_window=4096, max_position=32768,
+                                   bos_id=1, eos_ids=(2,), chat_format="mistral"),
+    "mixtral-8x7b": LlamaConfig(name="mixtral-8x7b", arch="mixtral", vocab_size=32000,
+                                rope_theta=1e6, max_position=32768, num_experts=8,
+                                experts_per_tok=2, bos_id=1, eos_ids=(2,), chat_format="mistral"),
+    "gemma-7b": LlamaConfig(name="gemma-7b", arch="gemma", vocab_size=256000, hidden=3072,
+                            layers=28, heads=16, kv_heads=16, head_dim=256, ffn=24576,
+                            rope_theta=10000.0, eps=1e-6, act="gelu_tanh",
+                            embed_scale=3072 ** 0.5, tie_embeddings=True, bos_id=2, eos_ids=(1, 107),
+                            chat_format="gemma"),
+    "gemma-2b": LlamaConfig(name="gemma-2b", arch="gemma", vocab_size=256000, hidden=2048,
+                            layers=18, heads=8, kv_heads=1, head_dim=256, ffn=16384,
+                            rope_theta=10000.0, eps=1e-6, act="gelu_tanh",
+                            embed_scale=2048 ** 0.5, tie_embeddings=True, bos_id=2, eos_ids=(1, 107),
+                            chat_format="gemma"),
+    "codegemma-7b": LlamaConfig(name="codegemma-7b", arch="gemma", vocab_size=256000, hidden=3072,
+                                layers=28, heads=16, kv_heads=16, head_dim=256, ffn=24576,
+                                rope_theta=10000.0, eps=1e-6, act="gelu_tanh",
+                                embed_scale=3072 ** 0.5, tie_embeddings=True, bos_id=2,
+                                eos_ids=(1, 107), chat_format="gemma"),
+    "starcoder2-3b": LlamaConfig(name="starcoder2-3b", arch="starcoder2", vocab_size=49152,
+                                 hidden=3072, layers=30, heads=24, kv_heads=2, ffn=12288,
+                                 rope_theta=999999.4, norm="layer", act="gelu_tanh",
+                                 gated_mlp=False, attn_bias=True, mlp_bias=True,
+                                 tie_embeddings=True, sliding_window=4096, max_position=16384,
+                                 bos_id=0, eos_ids=(0,), chat_format="plain"),
+    "starcoder2-7b": LlamaConfig(name="starcoder2-7b", arch="starcoder2", vocab_size=49152,
+                                 hidden=4608, layers=32, heads=36, kv_heads=4, ffn=18432,
+                                 rope_theta=1e6, norm="layer", act="gelu_tanh", gated_mlp=False,
+                                 attn_bias=True, mlp_bias=True, tie_embeddings=True,
+                                 sliding_window=4096, max_position=16384, bos_id=0, eos_ids=(0,),
+                                 chat_format="plain"),
+    "starcoder2-15b": LlamaConfig(name="starcoder2-15b", arch="starcoder2", vocab_size=49152,
+                                  hidden=6144, layers=40, heads=48, kv_heads=4, ffn=24576,
+                                  rope_theta=100000.0, norm="layer", act="gelu_tanh",
+                                  gated_mlp=False, attn_bias=True, mlp_bias=True,
+                                  sliding_window=4096, max_position=16384, bos_id=0, eos_ids=(0,),
+                                  chat_format="plain"),
     # small configs with the same structure for CPU tests / smoke runs
     "llama-tiny": LlamaConfig(name="llama-tiny", vocab_size=32768, hidden=256, layers=2, heads=4,
                               kv_heads=2, head_dim=64, ffn=512, max_position=2048,
@@ -88,7 +165,49 @@ LLAMA_PRESETS = {
     "llama-small": LlamaConfig(name="llama-small", vocab_size=32768, hidden=1024, layers=4,
                                heads=8, kv_heads=2, head_dim=128, ffn=2816,
                                max_position=8192, bos_id=1, eos_ids=(2,)),
+    "mistral-tiny": LlamaConfig(name="mistral-tiny", arch="mistral", vocab_size=32768, hidden=256,
+                                layers=2, heads=4, kv_heads=2, head_dim=64, ffn=512,
+                                rope_theta=1e6, sliding_window=96, max_position=2048, bos_id=1,
+                                eos_ids=(2,), chat_format="mistral"),
+    "mixtral-tiny": LlamaConfig(name="mixtral-tiny", arch="mixtral", vocab_size=32768, hidden=256,
+                                layers=2, heads=4, kv_heads=2, head_dim=64, ffn=384,
+                                rope_theta=1e6, num_experts=4, experts_per_tok=2,
+                                max_position=2048, bos_id=1, eos_ids=(2,), chat_format="mistral"),
+    "gemma-tiny": LlamaConfig(name="gemma-tiny", arch="gemma", vocab_size=32768, hidden=256,
+                              layers=2, heads=2, kv_heads=1, head_dim=256, ffn=512,
+                              rope_theta=10000.0, eps=1e-6, act="gelu_tanh", embed_scale=16.0,
+                              tie_embeddings=True, max_position=2048, bos_id=1, eos_ids=(2,),
+                              chat_format="gemma"),
+    "starcoder2-tiny": LlamaConfig(name="starcoder2-tiny", arch="starcoder2", vocab_size=32768,
+                                   hidden=256, layers=2, heads=4, kv_heads=2, head_dim=64, ffn=512,
+                                   rope_theta=1e5, norm="layer", act="gelu_tanh", gated_mlp=False,
+                                   attn_bias=True, mlp_bias=True, tie_embeddings=True,
+                                   sliding_window=96, max_position=2048, bos_id=1, eos_ids=(2,),
+                                   chat_format="plain"),
+    # small models of the real families' shapes for GPU kernel tests (head_dim 128 / 256)
+    "mixtral-small": LlamaConfig(name="mixtral-small", arch="mixtral", vocab_size=32768,
+                                 hidden=1024, layers=2, heads=8, kv_heads=2, head_dim=128,
+                                 ffn=1792, rope_theta=1e6, num_experts=8, experts_per_tok=2,
+                                 max_position=8192, bos_id=1, eos_ids=(2,), chat_format="mistral"),
+    "mistral-small": LlamaConfig(name="mistral-small", arch="mistral", vocab_size=32768,
+                                 hidden=1024, layers=2, heads=8, kv_heads=2, head_dim=128,
+                                 ffn=2816, rope_theta=1e6, sliding_window=200, max_position=8192,
+                                 bos_id=1, eos_ids=(2,), chat_format="mistral"),
+    "starcoder2-small": LlamaConfig(name="starcoder2-small", arch="starcoder2", vocab_size=32768,
+                                    hidden=1024, layers=2, heads=8, kv_heads=2, head_dim=128,
+                                    ffn=4096, rope_theta=1e5, norm="layer", act="gelu_tanh",
+                                    gated_mlp=False, attn_bias=True, mlp_bias=True,
+                                    tie_embeddings=True, sliding_window=200, max_position=8192,
+                                    bos_id=1, eos_ids=(2,), chat_format="plain"),
+    "gemma-small": LlamaConfig(name="gemma-small", arch="gemma", vocab_size=32768, hidden=1024,
+                               layers=2, heads=8, kv_heads=1, head_dim=256, ffn=2048,
+                               rope_theta=10000.0, eps=1e-6, act="gelu_tanh", embed_scale=32.0,
+                               tie_embeddings=True, max_position=8192, bos_id=1, eos_ids=(2,),
+                               chat_format="gemma"),
 }
+
+# DecoderConfig is the family-neutral name of the same dataclass
+DecoderConfig = LlamaConfig
 
 ENCODER_PRESETS = {
     "arctic-embed-l": EncoderConfig(),

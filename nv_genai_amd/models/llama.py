@@ -1,7 +1,9 @@
-"""Llama-3 decoder (8B / 70B) on the gfx950 kernel set, tensor-parallel over RCCL.
+"""Decoder-only LMs (Llama-3 8B / 70B, Mistral, Mixtral MoE, Gemma, StarCoder2) on the
+gfx950 kernel set, tensor-parallel over RCCL.
 
 This is the MI355X-native replacement for the TensorRT-LLM engine inside NIM
-(SURVEY.md §2.B N1). Per layer:
+(SURVEY.md §2.B N1). Per layer (Llama form; the other families switch pieces through
+``LlamaConfig.arch`` flags, see :class:`nv_genai_amd.models.config.LlamaConfig`):
 
     x_norm = rmsnorm(resid)                          K3  (fused with the residual add)
     qkv    = x_norm @ Wqkv^T                         K6  hipBLASLt (column-parallel)
@@ -14,6 +16,17 @@ This is the MI355X-native replacement for the TensorRT-LLM engine inside NIM
 
 Only the rows that produce a token (the last prompt position of each sequence, every decode
 row) go through the final norm and the vocab-parallel LM head (+ all-gather, CC4).
+
+Family switches: LayerNorm+bias instead of RMSNorm (StarCoder2), biased projections
+(hipBLASLt bias epilogue through ``torch.addmm``; row-parallel biases added on TP rank 0
+only), GeGLU / non-gated GELU MLPs (``ops.gelu_tanh_mul`` / ``ops.bias_gelu_``), Gemma's
+(1 + w) norm scale (folded into the stored weight) and sqrt(hidden) embedding scale, tied
+embeddings, sliding-window attention (a kernel argument: pages older than the window are
+never read), head_dim 256, and the sparse MoE MLP of Mixtral (``ops.moe_ffn``: routing,
+gathered grouped MFMA GEMMs with a fused SwiGLU epilogue, weighted combine). Under TP the
+experts are partitioned over the ranks (expert parallelism) when their count divides the
+group, otherwise every expert's FFN is split like a dense MLP; either way the MoE output is
+a partial sum that joins the dense path's all-reduce.
 """
 from __future__ import annotations
 
@@ -48,6 +61,8 @@ class AttnMeta:
 
 
 class LlamaModel:
+    """Decoder LM (every family of :class:`LlamaConfig`); ``DecoderModel`` is an alias."""
+
     def __init__(self, cfg: LlamaConfig, device="cuda", dtype=torch.bfloat16,
                  pctx: Optional[ParallelContext] = None, seed: int = 0,
                  weights: Optional[Dict[str, torch.Tensor]] = None, fp8: bool = False):
@@ -56,12 +71,19 @@ class LlamaModel:
         self.dtype = dtype
         self.p = pctx or get_context()
         tp = self.p.tp_size
-        if cfg.heads % tp or cfg.kv_heads % tp or cfg.ffn % tp or cfg.vocab_size % tp:
+        # expert parallelism: each TP rank owns num_experts / tp whole experts when that
+        # divides; otherwise every expert's FFN is sharded like a dense MLP
+        self.expert_parallel = cfg.is_moe and tp > 1 and cfg.num_experts % tp == 0
+        ffn_tp = 1 if self.expert_parallel else tp
+        if cfg.heads % tp or cfg.kv_heads % tp or cfg.ffn % ffn_tp or cfg.vocab_size % tp:
             raise ValueError(f"{cfg.name}: dims not divisible by tp={tp}")
         self.hq = cfg.heads // tp
         self.hkv = cfg.kv_heads // tp
         self.D = cfg.head_dim
-        self.ffn = cfg.ffn // tp
+        self.ffn = cfg.ffn // ffn_tp
+        self.n_experts = (cfg.num_experts // tp if self.expert_parallel else cfg.num_experts)
+        self.expert0 = self.p.tp_rank * self.n_experts if self.expert_parallel else 0
+        self.window = int(cfg.sliding_window or 0)
         self.vocab_local = cfg.vocab_size // tp
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
         # pipeline stage: a contiguous slice of layers; stage 0 also holds the embedding and
@@ -106,6 +128,8 @@ class LlamaModel:
         the KV cache stay bf16."""
         if self.fp8:
             return
+        if self.cfg.is_moe or not self.cfg.gated_mlp or self.cfg.attn_bias or self.cfg.mlp_bias:
+            raise NotImplementedError(f"FP8 W8A8 mode covers bias-free gated dense decoders, not {self.cfg.arch}")
         for L in self.layers:
             for n in self._LINEARS:
                 L[n + "8"], L[n + "_s"] = ops.quantize_weight_fp8(L.pop(n))
@@ -140,32 +164,61 @@ class LlamaModel:
             t.normal_(0.0, std, generator=g)
             return t
 
+        def ones(n):
+            return torch.ones(n, device=dev, dtype=dt)
+
+        def zeros(n):
+            return torch.zeros(n, device=dev, dtype=dt)
+
         g.manual_seed(seed * 1000 + self.p.tp_rank)
         out_std = 0.02 / math.sqrt(2 * cfg.layers)
         reseed(0)
         self.embed = rnd(self.vocab_local, H) if self.first_stage else None
         self.layers: List[Dict[str, torch.Tensor]] = []
+        qkv_rows = (self.hq + 2 * self.hkv) * self.D
         for i in range(self.layer_lo, self.layer_hi):
             reseed(i + 2)
-            self.layers.append({
-                "attn_norm": torch.ones(H, device=dev, dtype=dt),
-                "wqkv": rnd((self.hq + 2 * self.hkv) * self.D, H),
+            L = {
+                "attn_norm": ones(H),
+                "wqkv": rnd(qkv_rows, H),
                 "wo": rnd(H, self.hq * self.D, std=out_std),
-                "mlp_norm": torch.ones(H, device=dev, dtype=dt),
-                "wgu": rnd(2 * self.ffn, H),
-                "wd": rnd(H, self.ffn, std=out_std),
-            })
-        self.final_norm = torch.ones(H, device=dev, dtype=dt)
+                "mlp_norm": ones(H),
+            }
+            if cfg.is_moe:
+                E, F = self.n_experts, self.ffn
+                L["router"] = rnd(cfg.num_experts, H)
+                L["w13"] = rnd(E, 2 * F, H)
+                L["w2"] = rnd(E, H, F, std=out_std)
+            else:
+                L["wgu"] = rnd((2 if cfg.gated_mlp else 1) * self.ffn, H)
+                L["wd"] = rnd(H, self.ffn, std=out_std)
+            if cfg.norm == "layer":
+                L["attn_norm_b"], L["mlp_norm_b"] = zeros(H), zeros(H)
+            if cfg.attn_bias:
+                L["bqkv"], L["bo"] = zeros(qkv_rows), zeros(H)
+            if cfg.mlp_bias:
+                L["bgu"] = zeros((2 if cfg.gated_mlp else 1) * self.ffn)
+                L["bd"] = zeros(H)
+            self.layers.append(L)
+        self.final_norm = ones(H)
+        self.final_norm_b = zeros(H) if cfg.norm == "layer" else None
         reseed(1)
-        self.lm_head = rnd(self.vocab_local, H) if self.first_stage else None
+        if not self.first_stage:
+            self.lm_head = None
+        elif cfg.tie_embeddings:
+            self.lm_head = self.embed
+        else:
+            self.lm_head = rnd(self.vocab_local, H)
 
     def _load(self, w: Dict[str, torch.Tensor]):
-        """Load HF-named Llama weights (model.layers.N.self_attn.q_proj.weight, ...),
-        fusing q/k/v and gate/up, and slicing this rank's TP shard."""
+        """Load HF-named decoder weights (model.layers.N.self_attn.q_proj.weight, ...) of any
+        supported family, fusing q/k/v (and gate/up), folding Gemma's (1 + w) norm scale, and
+        slicing this rank's TP shard (experts: this rank's experts under expert parallelism)."""
         cfg, dev, dt = self.cfg, self.device, self.dtype
         tp, r = self.p.tp_size, self.p.tp_rank
+        gemma = cfg.arch == "gemma"
 
-        def rows(t, n):  # column-parallel shard (output rows)
+        def rows(t, n=0):  # column-parallel shard (output rows)
             c = t.shape[0] // tp
             return t[r * c:(r + 1) * c]
 
@@ -176,47 +229,132 @@ class LlamaModel:
         def get(name):
             return w[name].to(dev, dt)
 
-        self.embed = rows(get("model.embed_tokens.weight"), 0).contiguous() if self.first_stage else None
+        def norm(name):
+            t = get(name)
+            return (t.float() + 1.0).to(dt) if gemma else t
+
+        self.embed = rows(get("model.embed_tokens.weight")).contiguous() if self.first_stage else None
         self.layers = []
         for i in range(self.layer_lo, self.layer_hi):
             p = f"model.layers.{i}."
-            q, k, v = get(p + "self_attn.q_proj.weight"), get(p + "self_attn.k_proj.weight"), get(p + "self_attn.v_proj.weight")
-            gt, up = get(p + "mlp.gate_proj.weight"), get(p + "mlp.up_proj.weight")
-            self.layers.append({
-                "attn_norm": get(p + "input_layernorm.weight"),
-                "wqkv": torch.cat([rows(q, 0), rows(k, 0), rows(v, 0)]).contiguous(),
-                "wo": cols(get(p + "self_attn.o_proj.weight")).contiguous(),
-                "mlp_norm": get(p + "post_attention_layernorm.weight"),
-                "wgu": torch.cat([rows(gt, 0), rows(up, 0)]).contiguous(),
-                "wd": cols(get(p + "mlp.down_proj.weight")).contiguous(),
-            })
-        self.final_norm = get("model.norm.weight")
+            a = p + "self_attn."
+            q, k, v = get(a + "q_proj.weight"), get(a + "k_proj.weight"), get(a + "v_proj.weight")
+            L = {
+                "attn_norm": norm(p + "input_layernorm.weight"),
+                "wqkv": torch.cat([rows(q), rows(k), rows(v)]).contiguous(),
+                "wo": cols(get(a + "o_proj.weight")).contiguous(),
+                "mlp_norm": norm(p + "post_attention_layernorm.weight"),
+            }
+            if cfg.norm == "layer":
+                L["attn_norm_b"] = get(p + "input_layernorm.bias")
+                L["mlp_norm_b"] = get(p + "post_attention_layernorm.bias")
+            if cfg.attn_bias:
+                L["bqkv"] = torch.cat([rows(get(a + "q_proj.bias")), rows(get(a + "k_proj.bias")),
+                                       rows(get(a + "v_proj.bias"))]).contiguous()
+                L["bo"] = get(a + "o_proj.bias")
+            if cfg.is_moe:
+                L.update(self._load_experts(w, p, get, rows))
+            elif cfg.gated_mlp:
+                gt, up = get(p + "mlp.gate_proj.weight"), get(p + "mlp.up_proj.weight")
+                L["wgu"] = torch.cat([rows(gt), rows(up)]).contiguous()
+                L["wd"] = cols(get(p + "mlp.down_proj.weight")).contiguous()
+            else:   # StarCoder2: c_fc -> gelu -> c_proj
+                L["wgu"] = rows(get(p + "mlp.c_fc.weight")).contiguous()
+                L["wd"] = cols(get(p + "mlp.c_proj.weight")).contiguous()
+                if cfg.mlp_bias:
+                    L["bgu"] = rows(get(p + "mlp.c_fc.bias")).contiguous()
+                    L["bd"] = get(p + "mlp.c_proj.bias")
+            self.layers.append(L)
+        self.final_norm = norm("model.norm.weight")
+        self.final_norm_b = get("model.norm.bias") if cfg.norm == "layer" else None
         self.lm_head = None
         if self.first_stage:
-            head = w.get("lm_head.weight", w["model.embed_tokens.weight"]).to(dev, dt)
-            self.lm_head = rows(head, 0).contiguous()
+            if cfg.tie_embeddings or "lm_head.weight" not in w:
+                self.lm_head = self.embed
+            else:
+                self.lm_head = rows(get("lm_head.weight")).contiguous()
+
+    def _load_experts(self, w, p, get, rows):
+        """Mixtral experts in either checkpoint form: per-expert ``block_sparse_moe.experts.E.
+        w1/w3/w2`` (the released checkpoints) or the fused ``mlp.experts.gate_up_proj`` /
+        ``down_proj`` tensors of current transformers."""
+        cfg = self.cfg
+        ep = self.expert_parallel
+        tp, r = self.p.tp_size, self.p.tp_rank
+        E0, E = self.expert0, self.n_experts
+        F = self.ffn
+
+        def fsplit(t, dim):   # expert-TP: this rank's slice of the FFN dim
+            if ep or tp == 1:
+                return t
+            return t.narrow(dim, r * F, F)
+
+        if p + "mlp.experts.gate_up_proj" in w:
+            gu = get(p + "mlp.experts.gate_up_proj")[E0:E0 + E]        # [E, 2F_full, H]
+            Ff = gu.shape[1] // 2
+            w13 = torch.cat([fsplit(gu[:, :Ff], 1), fsplit(gu[:, Ff:], 1)], 1)
+            w2 = fsplit(get(p + "mlp.experts.down_proj")[E0:E0 + E], 2)
+            router = get(p + "mlp.gate.weight")
+        else:
+            b = p + "block_sparse_moe."
+            w13 = torch.stack([torch.cat([fsplit(get(b + f"experts.{e}.w1.weight"), 0),
+                                          fsplit(get(b + f"experts.{e}.w3.weight"), 0)])
+                               for e in range(E0, E0 + E)])
+            w2 = torch.stack([fsplit(get(b + f"experts.{e}.w2.weight"), 1) for e in range(E0, E0 + E)])
+            router = get(b + "gate.weight")
+        assert router.shape[0] == cfg.num_experts
+        return {"router": router.contiguous(), "w13": w13.contiguous(), "w2": w2.contiguous()}
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
         """HF-named weights of this rank (unfused; TP shards are local slices; a pipeline
         stage holds only its layers, plus embedding and LM head on stage 0)."""
         if self.fp8:
             raise RuntimeError("state_dict of an FP8-quantised model: export the bf16 model before quantize_fp8()")
-        out = {"model.norm.weight": self.final_norm}
+        cfg = self.cfg
+        gemma = cfg.arch == "gemma"
+
+        def unnorm(t):
+            return (t.float() - 1.0).to(t.dtype) if gemma else t
+
+        out = {"model.norm.weight": unnorm(self.final_norm)}
+        if self.final_norm_b is not None:
+            out["model.norm.bias"] = self.final_norm_b
         if self.first_stage:
             out["model.embed_tokens.weight"] = self.embed
-            out["lm_head.weight"] = self.lm_head
+            if not cfg.tie_embeddings:
+                out["lm_head.weight"] = self.lm_head
         qd, kd = self.hq * self.D, self.hkv * self.D
         for i, L in enumerate(self.layers, start=self.layer_lo):
             p = f"model.layers.{i}."
-            out[p + "input_layernorm.weight"] = L["attn_norm"]
-            out[p + "self_attn.q_proj.weight"] = L["wqkv"][:qd]
-            out[p + "self_attn.k_proj.weight"] = L["wqkv"][qd:qd + kd]
-            out[p + "self_attn.v_proj.weight"] = L["wqkv"][qd + kd:]
-            out[p + "self_attn.o_proj.weight"] = L["wo"]
-            out[p + "post_attention_layernorm.weight"] = L["mlp_norm"]
-            out[p + "mlp.gate_proj.weight"] = L["wgu"][: self.ffn]
-            out[p + "mlp.up_proj.weight"] = L["wgu"][self.ffn:]
-            out[p + "mlp.down_proj.weight"] = L["wd"]
+            a = p + "self_attn."
+            out[p + "input_layernorm.weight"] = unnorm(L["attn_norm"])
+            out[a + "q_proj.weight"] = L["wqkv"][:qd]
+            out[a + "k_proj.weight"] = L["wqkv"][qd:qd + kd]
+            out[a + "v_proj.weight"] = L["wqkv"][qd + kd:]
+            out[a + "o_proj.weight"] = L["wo"]
+            out[p + "post_attention_layernorm.weight"] = unnorm(L["mlp_norm"])
+            if "attn_norm_b" in L:
+                out[p + "input_layernorm.bias"] = L["attn_norm_b"]
+                out[p + "post_attention_layernorm.bias"] = L["mlp_norm_b"]
+            if "bqkv" in L:
+                out[a + "q_proj.bias"] = L["bqkv"][:qd]
+                out[a + "k_proj.bias"] = L["bqkv"][qd:qd + kd]
+                out[a + "v_proj.bias"] = L["bqkv"][qd + kd:]
+                out[a + "o_proj.bias"] = L["bo"]
+            if cfg.is_moe:
+                out[p + "mlp.gate.weight"] = L["router"]
+                out[p + "mlp.experts.gate_up_proj"] = L["w13"]
+                out[p + "mlp.experts.down_proj"] = L["w2"]
+            elif cfg.gated_mlp:
+                out[p + "mlp.gate_proj.weight"] = L["wgu"][: self.ffn]
+                out[p + "mlp.up_proj.weight"] = L["wgu"][self.ffn:]
+                out[p + "mlp.down_proj.weight"] = L["wd"]
+            else:
+                out[p + "mlp.c_fc.weight"] = L["wgu"]
+                out[p + "mlp.c_proj.weight"] = L["wd"]
+                if "bgu" in L:
+                    out[p + "mlp.c_fc.bias"] = L["bgu"]
+                    out[p + "mlp.c_proj.bias"] = L["bd"]
         return out
 
     # ------------------------------------------------------------------ cache
@@ -243,21 +381,65 @@ class LlamaModel:
     # ------------------------------------------------------------------ forward
     def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
         if self.p.tp_size == 1:
-            return torch.nn.functional.embedding(ids.long(), self.embed)
-        lo = self.p.tp_rank * self.vocab_local
-        local = ids.long() - lo
-        ok = (local >= 0) & (local < self.vocab_local)
-        h = torch.nn.functional.embedding(local.clamp(0, self.vocab_local - 1), self.embed)
-        h = h * ok.unsqueeze(-1).to(h.dtype)
-        return tp_all_reduce(h, self.p)
+            h = torch.nn.functional.embedding(ids.long(), self.embed)
+        else:
+            lo = self.p.tp_rank * self.vocab_local
+            local = ids.long() - lo
+            ok = (local >= 0) & (local < self.vocab_local)
+            h = torch.nn.functional.embedding(local.clamp(0, self.vocab_local - 1), self.embed)
+            h = h * ok.unsqueeze(-1).to(h.dtype)
+            h = tp_all_reduce(h, self.p)
+        if self.cfg.embed_scale != 1.0:
+            # Gemma: the scale is a bf16 constant (HF multiplies by it in the model dtype)
+            h = h * torch.tensor(self.cfg.embed_scale, dtype=h.dtype)
+        return h
+
+    # norms: RMSNorm (Llama/Mistral/Mixtral/Gemma) or LayerNorm with bias (StarCoder2)
+    def _norm(self, x, w, b=None):
+        if b is None:
+            return ops.rmsnorm(x, w, self.cfg.eps)
+        return ops.layernorm(x, w, b, self.cfg.eps)
+
+    def _add_norm(self, resid, delta, w, b=None):
+        """resid += delta (in place); returns norm(resid)."""
+        if b is None:
+            return ops.add_rmsnorm(resid, delta, w, self.cfg.eps)
+        return ops.add_layernorm(resid, delta, w, b, self.cfg.eps)
+
+    def _bias_rank0(self, y: torch.Tensor, b: Optional[torch.Tensor]) -> torch.Tensor:
+        """A row-parallel projection's bias joins the TP partial sum on one rank only."""
+        if b is not None and self.p.tp_rank == 0:
+            y.add_(b)
+        return y
+
+    def _qkv(self, x, L):
+        if "bqkv" in L:
+            return torch.addmm(L["bqkv"], x, L["wqkv"].t())
+        return self._lin(x, L, "wqkv")
+
+    def _mlp(self, x, L):
+        """MLP of one layer on normed rows; returns the (TP partial) output."""
+        cfg = self.cfg
+        if cfg.is_moe:
+            return ops.moe_ffn(x, L["router"], L["w13"], L["w2"], cfg.experts_per_tok,
+                               expert0=self.expert0, act=cfg.act)
+        if cfg.gated_mlp:
+            gu = self._lin(x, L, "wgu")
+            if cfg.act == "silu":
+                return self._lin(gu, L, "wd", swiglu=True)
+            return ops.gelu_tanh_mul(gu) @ L["wd"].t()
+        h = x @ L["wgu"].t()
+        ops.bias_gelu_(h, L.get("bgu"), approximate=cfg.act == "gelu_tanh")
+        return self._bias_rank0(h @ L["wd"].t(), L.get("bd"))
 
     def _attention(self, q, qkv, li, meta: AttnMeta, T: int):
         hq, hkv, D = self.hq, self.hkv, self.D
         qdim = hq * D
+        W = self.window
         if meta.kind == "decode":
             return ops.decode_attention(q, self.k_cache[li], self.v_cache[li],
                                         meta.block_tables, meta.ctx_lens, hq, hkv,
-                                        meta.max_ctx, self.scale, ws=meta.decode_ws)
+                                        meta.max_ctx, self.scale, ws=meta.decode_ws, window=W)
         if meta.kind == "mixed":
             nd = meta.n_decode
             attn = torch.empty(T, qdim, dtype=qkv.dtype, device=qkv.device)
@@ -266,7 +448,7 @@ class LlamaModel:
                 ops.prefill_attention_paged(q[nd:], self.k_cache[li], self.v_cache[li],
                                             meta.block_tables[nd:], meta.cu_q_prefill,
                                             meta.ctx_lens[nd:], hq, hkv, D, meta.max_q_len,
-                                            self.scale, out=attn[nd:])
+                                            self.scale, out=attn[nd:], window=W)
 
             side = None
             if self.concurrent_attention and qkv.is_cuda and not torch.cuda.is_current_stream_capturing():
@@ -279,7 +461,8 @@ class LlamaModel:
                     prefill()
             ops.decode_attention(q[:nd], self.k_cache[li], self.v_cache[li],
                                  meta.block_tables[:nd], meta.ctx_lens[:nd], hq, hkv,
-                                 meta.max_ctx, self.scale, out=attn[:nd], ws=meta.decode_ws)
+                                 meta.max_ctx, self.scale, out=attn[:nd], ws=meta.decode_ws,
+                                 window=W)
             if side is not None:
                 main.wait_stream(side)           # attn (allocated on main) complete
             else:
@@ -287,48 +470,56 @@ class LlamaModel:
             return attn
         return ops.prefill_attention_paged(q, self.k_cache[li], self.v_cache[li],
                                            meta.block_tables, meta.cu_q, meta.ctx_lens,
-                                           hq, hkv, D, meta.max_q_len, self.scale)
+                                           hq, hkv, D, meta.max_q_len, self.scale, window=W)
 
-    def _reduce_add_norm(self, partial, resid, w):
-        """resid += all_reduce_TP(partial); returns rmsnorm(resid) * w. A small TP message
-        goes through the custom all-reduce's fused epilogue kernel (one launch, the sum never
-        round-trips through HBM); otherwise all-reduce, then the add+RMSNorm kernel."""
+    def _reduce_add_norm(self, partial, resid, w, b=None):
+        """resid += all_reduce_TP(partial); returns norm(resid). A small TP message goes
+        through the custom all-reduce's fused add+RMSNorm epilogue kernel (one launch, the
+        sum never round-trips through HBM); otherwise all-reduce, then the add+norm kernel."""
         if self.p.tp_size > 1:
             car = custom_all_reduce_for(self.p.tp_group)
-            if car is not None and car.fused_norm_eligible(partial):
+            if b is None and car is not None and car.fused_norm_eligible(partial):
                 return car.all_reduce_add_rmsnorm(partial, resid, w, self.cfg.eps)
             tp_all_reduce(partial, self.p)
-        return ops.add_rmsnorm(resid, partial, w, self.cfg.eps)
+        return self._add_norm(resid, partial, w, b)
+
+    def _attn_block(self, li: int, x, pos, meta: AttnMeta, T: int):
+        """qkv projection + RoPE/KV write + attention + o projection (TP partial)."""
+        L = self.layers[li]
+        qkv = self._qkv(x, L)
+        ops.rope_cache_(qkv, pos, self.cos_sin, meta.slots, self.k_cache[li],
+                        self.v_cache[li], self.hq, self.hkv, self.D)
+        attn = self._attention(qkv[:, :self.hq * self.D], qkv, li, meta, T)
+        return self._bias_rank0(self._lin(attn, L, "wo"), L.get("bo"))
 
     def _layer(self, li: int, x, resid, pos, meta: AttnMeta):
-        """One decoder layer on rows (x = rmsnorm(resid)); returns the MLP output d — still
+        """One decoder layer on rows (x = norm(resid)); returns the MLP output d — still
         a TP partial sum — which the caller reduces into resid with the next layer's (or
         the final) norm."""
         L = self.layers[li]
-        qkv = self._lin(x, L, "wqkv")
-        ops.rope_cache_(qkv, pos, self.cos_sin, meta.slots, self.k_cache[li],
-                        self.v_cache[li], self.hq, self.hkv, self.D)
-        attn = self._attention(qkv[:, :self.hq * self.D], qkv, li, meta, x.shape[0])
-        o = self._lin(attn, L, "wo")
-        x = self._reduce_add_norm(o, resid, L["mlp_norm"])
-        return self._lin(self._lin(x, L, "wgu"), L, "wd", swiglu=True)
+        o = self._attn_block(li, x, pos, meta, x.shape[0])
+        x = self._reduce_add_norm(o, resid, L["mlp_norm"], L.get("mlp_norm_b"))
+        return self._mlp(x, L)
+
+    def _final(self, resid, d, sample_idx):
+        """Final norm of resid + d (all rows, or only the sampling rows)."""
+        if sample_idx is not None:
+            rows = resid.index_select(0, sample_idx) + d.index_select(0, sample_idx)
+            return self._norm(rows.contiguous(), self.final_norm, self.final_norm_b)
+        return self._add_norm(resid, d, self.final_norm, self.final_norm_b)
 
     def _stack(self, resid, pos, meta: AttnMeta, sample_idx: Optional[torch.Tensor]):
-        cfg = self.cfg
-        x = ops.rmsnorm(resid, self.layers[0]["attn_norm"], cfg.eps)
+        L0 = self.layers[0]
+        x = self._norm(resid, L0["attn_norm"], L0.get("attn_norm_b"))
         n = len(self.layers)
         for li in range(n):
             d = self._layer(li, x, resid, pos, meta)
             if li + 1 < n:
-                x = self._reduce_add_norm(d, resid, self.layers[li + 1]["attn_norm"])
+                Ln = self.layers[li + 1]
+                x = self._reduce_add_norm(d, resid, Ln["attn_norm"], Ln.get("attn_norm_b"))
                 continue
             tp_all_reduce(d, self.p)
-            if sample_idx is not None:
-                # only rows that sample need the final norm
-                rows = resid.index_select(0, sample_idx) + d.index_select(0, sample_idx)
-                return ops.rmsnorm(rows.contiguous(), self.final_norm, cfg.eps)
-            else:
-                return ops.add_rmsnorm(resid, d, self.final_norm, cfg.eps)
+            return self._final(resid, d, sample_idx)
         raise RuntimeError("model has no layers")
 
     def forward(self, ids: torch.Tensor, pos: torch.Tensor, meta: AttnMeta,
@@ -364,30 +555,28 @@ class LlamaModel:
             meta = AttnMeta(kind=meta.kind, slots=slots, cu_q=meta.cu_q, ctx_lens=meta.ctx_lens,
                             block_tables=meta.block_tables, max_q_len=meta.max_q_len,
                             max_ctx=meta.max_ctx, decode_ws=meta.decode_ws)
-        rows = Tp // tp
         # vocab-parallel embedding: partial rows, reduce-scattered straight into the shard
         lo = r * self.vocab_local
         local = ids.long() - lo
         ok = (local >= 0) & (local < self.vocab_local)
         h = torch.nn.functional.embedding(local.clamp(0, self.vocab_local - 1), self.embed)
         resid = tp_reduce_scatter_rows(h * ok.unsqueeze(-1).to(h.dtype), p).contiguous()
-        x = ops.rmsnorm(resid, self.layers[0]["attn_norm"], cfg.eps)
+        if cfg.embed_scale != 1.0:
+            resid = resid * torch.tensor(cfg.embed_scale, dtype=resid.dtype)
+        L0 = self.layers[0]
+        x = self._norm(resid, L0["attn_norm"], L0.get("attn_norm_b"))
         n = len(self.layers)
         d = None
         for li in range(n):
             L = self.layers[li]
             xf = tp_all_gather_rows(x, p)
-            qkv = self._lin(xf, L, "wqkv")
-            ops.rope_cache_(qkv, pos, self.cos_sin, meta.slots, self.k_cache[li],
-                            self.v_cache[li], self.hq, self.hkv, self.D)
-            attn = self._attention(qkv[:, :self.hq * self.D], qkv, li, meta, Tp)
-            o = tp_reduce_scatter_rows(self._lin(attn, L, "wo"), p).contiguous()
-            x = ops.add_rmsnorm(resid, o, L["mlp_norm"], cfg.eps)
-            gu = self._lin(tp_all_gather_rows(x, p), L, "wgu")
-            d = tp_reduce_scatter_rows(self._lin(gu, L, "wd", swiglu=True), p).contiguous()
+            o = tp_reduce_scatter_rows(self._attn_block(li, xf, pos, meta, Tp), p).contiguous()
+            x = self._add_norm(resid, o, L["mlp_norm"], L.get("mlp_norm_b"))
+            d = tp_reduce_scatter_rows(self._mlp(tp_all_gather_rows(x, p), L), p).contiguous()
             if li + 1 < n:
-                x = ops.add_rmsnorm(resid, d, self.layers[li + 1]["attn_norm"], cfg.eps)
-        out = tp_all_gather_rows(ops.add_rmsnorm(resid, d, self.final_norm, cfg.eps), p)[:T]
+                Ln = self.layers[li + 1]
+                x = self._add_norm(resid, d, Ln["attn_norm"], Ln.get("attn_norm_b"))
+        out = tp_all_gather_rows(self._add_norm(resid, d, self.final_norm, self.final_norm_b), p)[:T]
         return out if sample_idx is None else out.index_select(0, sample_idx)
 
     def _forward_pp(self, ids, pos, meta: AttnMeta, sample_idx):
@@ -406,12 +595,14 @@ class LlamaModel:
         else:
             resid = torch.empty(T, cfg.hidden, dtype=self.dtype, device=self.device)
             dist.recv(resid, src=p.pp_prev)
-        x = ops.rmsnorm(resid, self.layers[0]["attn_norm"], cfg.eps)
+        L0 = self.layers[0]
+        x = self._norm(resid, L0["attn_norm"], L0.get("attn_norm_b"))
         n = len(self.layers)
         for li in range(n):
             d = self._layer(li, x, resid, pos, meta)
             if li + 1 < n:
-                x = self._reduce_add_norm(d, resid, self.layers[li + 1]["attn_norm"])
+                Ln = self.layers[li + 1]
+                x = self._reduce_add_norm(d, resid, Ln["attn_norm"], Ln.get("attn_norm_b"))
         tp_all_reduce(d, self.p)
         rows = T if sample_idx is None else int(sample_idx.shape[0])
         if not self.last_stage:
@@ -419,11 +610,7 @@ class LlamaModel:
             dist.send(resid, dst=p.pp_next)
             h = None
         else:
-            if sample_idx is not None:
-                r = resid.index_select(0, sample_idx) + d.index_select(0, sample_idx)
-                h = ops.rmsnorm(r.contiguous(), self.final_norm, cfg.eps)
-            else:
-                h = ops.add_rmsnorm(resid, d, self.final_norm, cfg.eps)
+            h = self._final(resid, d, sample_idx)
             dist.send(h.contiguous(), dst=p.pp_first_rank)
             h = None
         if self.first_stage:
@@ -472,3 +659,7 @@ class LlamaModel:
         """fp32 logits over the full vocabulary (vocab-parallel head + all-gather)."""
         lg = (h @ self.lm_head.t()).float()
         return tp_all_gather(lg, dim=-1, ctx=self.p)
+
+
+# family-neutral name
+DecoderModel = LlamaModel

@@ -76,6 +76,30 @@ def layernorm(x, g, b, eps, resid=None, out=None):
     return out
 
 
+def add_layernorm(resid, delta, g, b, eps, out=None):
+    """resid += delta (in place); returns LayerNorm(resid) * g + b."""
+    if not _gpu(resid):
+        r = ref.add_layernorm(resid, delta, g, b, eps)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    if out is None:
+        out = torch.empty_like(resid)
+    kernels().add_layernorm(out, resid, delta, g, b, float(eps))
+    return out
+
+
+def gelu_tanh_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None):
+    """GeGLU: [T, 2F] = [gate | up] -> gelu_tanh(gate) * up [T, F]."""
+    if not _gpu(x):
+        return ref.gelu_tanh_mul(x)
+    if out is None:
+        out = torch.empty(x.shape[0], x.shape[1] // 2, dtype=x.dtype, device=x.device)
+    kernels().gelu_tanh_mul(out, x)
+    return out
+
+
 def silu_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None):
     if not _gpu(x):
         return ref.silu_mul(x)
@@ -85,10 +109,11 @@ def silu_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None):
     return out
 
 
-def bias_gelu_(x: torch.Tensor, bias: Optional[torch.Tensor]):
+def bias_gelu_(x: torch.Tensor, bias: Optional[torch.Tensor], approximate: bool = False):
+    """x = gelu(x + bias) in place; ``approximate``: the tanh form (StarCoder2, Gemma)."""
     if not _gpu(x):
-        return ref.bias_gelu_(x, bias)
-    kernels().bias_gelu(x, bias)
+        return ref.bias_gelu_(x, bias, approximate)
+    kernels().bias_gelu(x, bias, bool(approximate))
     return x
 
 
@@ -117,14 +142,15 @@ class DecodeWorkspace:
     MAX_PARTS = 16
 
     def __init__(self, max_seqs: int, Hq: int, Hkv: int, max_ctx: int, device,
-                 pages_per_part: Optional[int] = None):
+                 pages_per_part: Optional[int] = None, D: int = 128):
         self.pages = (max_ctx + 63) // 64
         self.fixed = pages_per_part
         self.Hkv = Hkv
         self.max_ctx = max_ctx
         need = max(b * self.nparts(b) for b in range(1, max_seqs + 1))
         self.ml = torch.empty(need * Hq * 2, dtype=torch.float32, device=device)
-        self.o = torch.empty(need * Hq * 128, dtype=torch.float32, device=device)
+        self.o = torch.empty(need * Hq * D, dtype=torch.float32, device=device)
+        self.D = D
 
     def nparts(self, B: int) -> int:
         if self.fixed:
@@ -141,29 +167,33 @@ class DecodeWorkspace:
 
 
 def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, max_ctx, scale,
-                     out=None, ws: Optional[DecodeWorkspace] = None):
+                     out=None, ws: Optional[DecodeWorkspace] = None, window: int = 0):
+    """Paged GQA decode attention (head_dim 128 or 256); ``window`` > 0: sliding window."""
+    D = kc.shape[3]
     if not _gpu(q):
-        r = ref.decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, scale, D=kc.shape[3])
+        r = ref.decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, scale, D=D,
+                                 window=window)
         if out is not None:
             out[: r.shape[0], : r.shape[1]].copy_(r)
             return out
         return r
     B = ctx_lens.numel()
     if out is None:
-        out = torch.empty(B, Hq * 128, dtype=q.dtype, device=q.device)
+        out = torch.empty(B, Hq * D, dtype=q.dtype, device=q.device)
     if ws is None:
-        ws = DecodeWorkspace(B, Hq, Hkv, max_ctx, q.device)
-    assert max_ctx <= ws.max_ctx
+        ws = DecodeWorkspace(B, Hq, Hkv, max_ctx, q.device, D=D)
+    assert max_ctx <= ws.max_ctx and ws.D == D
     kernels().decode_attention(out, q, kc, vc, block_tables, ctx_lens, Hq, Hkv, int(max_ctx),
-                               float(scale), ws.pages_per_part(B, max_ctx), ws.ml, ws.o)
+                               float(scale), ws.pages_per_part(B, max_ctx), ws.ml, ws.o,
+                               int(window))
     return out
 
 
 def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D, max_q_len,
-                            scale, out=None, causal=True):
+                            scale, out=None, causal=True, window: int = 0):
     if not _gpu(q):
         r = ref.prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
-                                        scale, causal)
+                                        scale, causal, window)
         if out is not None:
             out[:, : r.shape[1]].copy_(r)
             return out
@@ -171,7 +201,7 @@ def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
     if out is None:
         out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
     kernels().prefill_attention(out, q, None, None, kc, vc, block_tables, cu_q, ctx_lens, Hq,
-                                Hkv, D, int(max_q_len), float(scale), bool(causal))
+                                Hkv, D, int(max_q_len), float(scale), bool(causal), int(window))
     return out
 
 
@@ -182,7 +212,80 @@ def varlen_attention(q, k, v, cu, Hq, Hkv, D, max_len, scale, causal=False, out=
     if out is None:
         out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
     kernels().prefill_attention(out, q, k, v, None, None, None, cu, None, Hq, Hkv, D,
-                                int(max_len), float(scale), bool(causal))
+                                int(max_len), float(scale), bool(causal), 0)
+    return out
+
+
+# ------------------------------------------------------------------------- MoE
+MOE_BN = 128       # weight rows per grouped-GEMM tile
+
+
+class MoEWorkspace:
+    """Routing / permutation buffers of the grouped MoE GEMMs for up to ``rows`` tokens,
+    cached per (device, top-k, local experts) and grown on demand (never inside a hipGraph
+    capture: the engine's warm-up forward sizes it for the largest step first)."""
+
+    _cache = {}
+
+    @classmethod
+    def get(cls, rows: int, k: int, E: int, device):
+        key = (str(device), k, E)
+        ws = cls._cache.get(key)
+        if ws is None or ws.rows < rows:
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("MoE workspace must be sized before graph capture")
+            ws = cls(max(rows, 64), k, E, device)
+            cls._cache[key] = ws
+        return ws
+
+    def __init__(self, rows: int, k: int, E: int, device):
+        self.rows, self.k, self.E = rows, k, E
+        M = rows * k
+        self.mt_cap = max(1, -(-M // 64)) + E          # M-tile bound at BM = 64 (the larger)
+        i32 = dict(dtype=torch.int32, device=device)
+        self.ids = torch.empty(M, **i32)
+        self.w = torch.empty(M, dtype=torch.float32, device=device)
+        self.sorted_tok = torch.empty(M, **i32)
+        self.sorted_w = torch.empty(M, dtype=torch.float32, device=device)
+        self.inv = torch.empty(M, **i32)
+        self.tiles = torch.empty(self.mt_cap * 3, **i32)
+
+
+def moe_ffn(x: torch.Tensor, router: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, k: int,
+            expert0: int = 0, act: str = "silu") -> torch.Tensor:
+    """Sparse MoE MLP on rows x [T, H] -> [T, H] (a TP partial sum when the experts or their
+    FFN dims are split over ranks). ``w13`` [E, 2F, H] = [gate | up] rows per local expert,
+    ``w2`` [E, H, F]; the router [num_experts, H] scores every expert.
+
+    GPU: router GEMM (hipBLASLt) -> ``moe_route`` (softmax top-k) -> ``moe_align`` (per-
+    expert counts, sorted token order, M-tile table) -> gathered grouped MFMA GEMM with the
+    activation fused in its epilogue (gate and up rows interleaved per 16-row MFMA tile) ->
+    grouped down GEMM scaled by the routing weight -> ``moe_combine`` (top-k rows summed in
+    fp32 per token)."""
+    if not _gpu(x):
+        return ref.moe_ffn(x, router, w13, w2, k, expert0, act)
+    C = kernels()
+    T, H = x.shape
+    E, F2, K = w13.shape
+    F = F2 // 2
+    out = torch.empty(T, H, dtype=x.dtype, device=x.device)
+    if T == 0:
+        return out
+    ws = MoEWorkspace.get(T, k, E, x.device)
+    M = T * k
+    # 64-row M tiles while the experts average <= 4 of them (decode), 128 beyond (prefill)
+    bm = 64 if M <= 256 * E else 128
+    mt = -(-M // bm) + E                                           # M-tile bound of this call
+    logits = x @ router.t()                                        # [T, num_experts] bf16
+    C.moe_route(logits, int(k), ws.ids, ws.w)
+    C.moe_align(ws.ids, ws.w, T, int(k), int(expert0), E, bm, ws.sorted_tok, ws.sorted_w, ws.inv,
+                ws.tiles, mt)
+    h = torch.empty(M, F, dtype=x.dtype, device=x.device)
+    C.moe_gemm(x, w13, ws.sorted_tok, ws.sorted_w, ws.tiles, mt, bm, h, 0,
+               0 if act == "silu" else 1)
+    y = torch.empty(M, H, dtype=x.dtype, device=x.device)
+    C.moe_gemm(h, w2, ws.sorted_tok, ws.sorted_w, ws.tiles, mt, bm, y, 1, 0)
+    C.moe_combine(y, ws.inv, T, int(k), out)
     return out
 
 

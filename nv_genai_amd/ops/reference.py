@@ -37,15 +37,29 @@ def layernorm(x, g, b, eps, resid=None):
     return y.to(x.dtype)
 
 
+def add_layernorm(resid, delta, g, b, eps):
+    """resid += delta (stored in the residual dtype); returns LayerNorm(resid) * g + b."""
+    s = (resid.float() + delta.float()).to(resid.dtype)
+    resid.copy_(s)
+    return layernorm(s, g, b, eps)
+
+
+def gelu_tanh_mul(x: torch.Tensor) -> torch.Tensor:
+    """GeGLU: x = [gate | up] -> gelu_tanh(gate) * up."""
+    F = x.shape[-1] // 2
+    g, u = x[..., :F].float(), x[..., F:].float()
+    return (torch.nn.functional.gelu(g, approximate="tanh") * u).to(x.dtype)
+
+
 def silu_mul(x: torch.Tensor) -> torch.Tensor:
     F = x.shape[-1] // 2
     g, u = x[..., :F].float(), x[..., F:].float()
     return (torch.nn.functional.silu(g) * u).to(x.dtype)
 
 
-def bias_gelu_(x: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+def bias_gelu_(x: torch.Tensor, bias: Optional[torch.Tensor], approximate: bool = False) -> torch.Tensor:
     xf = x.float() + (bias.float() if bias is not None else 0.0)
-    x.copy_(torch.nn.functional.gelu(xf).to(x.dtype))
+    x.copy_(torch.nn.functional.gelu(xf, approximate="tanh" if approximate else "none").to(x.dtype))
     return x
 
 
@@ -103,7 +117,9 @@ def _gather_kv(kc, vc, bt_row, ctx, kvh):
     return k.float(), v.float()
 
 
-def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, scale, D=128):
+def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, scale, D=128, window=0):
+    """One query per sequence at position ctx - 1; ``window`` > 0 keeps only the last
+    ``window`` keys (sliding-window attention: key j visible iff j > ctx - 1 - window)."""
     B = ctx_lens.numel()
     G = Hq // Hkv
     out = torch.zeros(B, Hq * D, dtype=q.dtype, device=q.device)
@@ -111,8 +127,10 @@ def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, scale, D=128):
         ctx = int(ctx_lens[b])
         if ctx == 0:
             continue
+        lo = max(0, ctx - window) if window > 0 else 0
         for kvh in range(Hkv):
             k, v = _gather_kv(kc, vc, block_tables[b], ctx, kvh)
+            k, v = k[lo:], v[lo:]
             qs = q[b, kvh * G * D:(kvh + 1) * G * D].view(G, D).float()
             p = torch.softmax(qs @ k.T * scale, dim=-1)
             out[b, kvh * G * D:(kvh + 1) * G * D] = (p @ v).reshape(-1).to(q.dtype)
@@ -120,7 +138,7 @@ def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, scale, D=128):
 
 
 def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D, scale,
-                            causal=True):
+                            causal=True, window=0):
     G = Hq // Hkv
     T = q.shape[0]
     out = torch.zeros(T, Hq * D, dtype=q.dtype, device=q.device)
@@ -133,6 +151,8 @@ def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
         qpos = torch.arange(ctx - ql, ctx, device=q.device)
         kpos = torch.arange(ctx, device=q.device)
         mask = kpos[None, :] <= qpos[:, None] if causal else torch.ones(ql, ctx, dtype=torch.bool, device=q.device)
+        if window > 0:
+            mask = mask & (kpos[None, :] > qpos[:, None] - window)
         for hq in range(Hq):
             k, v = _gather_kv(kc, vc, block_tables[b], ctx, hq // G)
             qs = q[s0:s1, hq * D:(hq + 1) * D].float()
@@ -162,6 +182,38 @@ def varlen_attention(q, k, v, cu, Hq, Hkv, D, scale, causal=False):
                 sc = sc.masked_fill(~m, float("-inf"))
             out[s0:s1, hq * D:(hq + 1) * D] = (torch.softmax(sc, -1) @ vs).to(q.dtype)
     return out
+
+
+# ----------------------------------------------------------------------------- MoE
+def moe_route(logits: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Mixtral routing: softmax over all experts (fp32), top-k, renormalised over the k.
+    Returns (ids int32 [T, k], weights fp32 [T, k]) in descending-probability order."""
+    p = torch.softmax(logits.float(), dim=-1)
+    w, ids = torch.topk(p, k, dim=-1)
+    w = w / w.sum(-1, keepdim=True)
+    return ids.to(torch.int32), w
+
+
+def moe_ffn(x, router, w13, w2, k, expert0=0, act="silu"):
+    """Sparse MoE MLP of one layer on rows x [T, H] (fp32 math per expert):
+    sum_j w_j * down_e(act(gate_e(x)) * up_e(x)) over the top-k experts e of each row that
+    this rank holds (experts [expert0, expert0 + w13.shape[0]))."""
+    logits = (x @ router.t())
+    ids, wts = moe_route(logits, k)
+    E, F2, _ = w13.shape
+    F = F2 // 2
+    out = torch.zeros(x.shape[0], w2.shape[1], dtype=torch.float32, device=x.device)
+    for e in range(E):
+        tok, slot = torch.where(ids == expert0 + e)
+        if tok.numel() == 0:
+            continue
+        gu = x[tok].float() @ w13[e].float().t()
+        g, u = gu[:, :F], gu[:, F:]
+        h = (torch.nn.functional.silu(g) if act == "silu" else
+             torch.nn.functional.gelu(g, approximate="tanh")) * u
+        y = h.to(x.dtype).float() @ w2[e].float().t()
+        out.index_add_(0, tok, y * wts[tok, slot].unsqueeze(1))
+    return out.to(x.dtype)
 
 
 # ----------------------------------------------------------------------------- sampling

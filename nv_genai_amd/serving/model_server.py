@@ -215,7 +215,7 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
         if req.stream and req.n > 1:
             return JSONResponse({"error": "stream supports n = 1"}, status_code=400)
         with tracer.span("chat.completions", {"model": req.model}, request.headers.get("traceparent")):
-            ids = svc.engine.tok.apply_chat_template(msgs)
+            ids = svc.engine.apply_chat_template(msgs)
             handles = _submit_n(svc, ids, req)
         rid = f"chatcmpl-{uuid.uuid4().hex}"
         model = req.model or llm_name

@@ -95,22 +95,67 @@ class LLMTokenizer:
         ids = [i % self.n for i in ids]
         return self.tok.decode(ids, skip_special_tokens=skip_special)
 
-    def apply_chat_template(self, messages: List[dict], add_generation_prompt: bool = True) -> List[int]:
-        """Llama-3 instruct format:
-        <|begin_of_text|><|start_header_id|>role<|end_header_id|>\n\ncontent<|eot_id|>..."""
-        ids = [self.bos_id]
-        for m in messages:
-            ids.append(self.header_start)
-            ids += self.encode(m.get("role", "user"))
-            ids.append(self.header_end)
-            ids += self.encode("\n\n" + str(m.get("content", "")))
-            ids.append(self.eot_id)
-        if add_generation_prompt:
-            ids.append(self.header_start)
-            ids += self.encode("assistant")
-            ids.append(self.header_end)
-            ids += self.encode("\n\n")
-        return ids
+    def apply_chat_template(self, messages: List[dict], add_generation_prompt: bool = True,
+                            fmt: str = "llama3") -> List[int]:
+        """Render a chat in the model family's prompt format:
+
+        * ``llama3``: <|begin_of_text|><|start_header_id|>role<|end_header_id|>\n\ncontent<|eot_id|>...
+        * ``mistral``: <s>[INST] (system\n\n)user [/INST] assistant</s>[INST] ... — the
+          template of the reference's Mistral NIM config (experimental/fm-asr-streaming-rag/
+          nim/configs/mistral-7b.yaml:15-17: system folded into the first user turn);
+        * ``gemma``: <bos><start_of_turn>user\ncontent<end_of_turn>\n<start_of_turn>model\n
+          (no system role: it is folded into the first user turn, as Gemma's template does);
+        * ``plain``: ``role: content`` lines (base / code models such as StarCoder2).
+
+        BOS/EOS are this tokenizer's <|begin_of_text|> / <|eot_id|> (synthetic vocabulary)."""
+        if fmt == "llama3":
+            ids = [self.bos_id]
+            for m in messages:
+                ids.append(self.header_start)
+                ids += self.encode(m.get("role", "user"))
+                ids.append(self.header_end)
+                ids += self.encode("\n\n" + str(m.get("content", "")))
+                ids.append(self.eot_id)
+            if add_generation_prompt:
+                ids.append(self.header_start)
+                ids += self.encode("assistant")
+                ids.append(self.header_end)
+                ids += self.encode("\n\n")
+            return ids
+        msgs = [dict(m) for m in messages]
+        system = ""
+        if msgs and msgs[0].get("role") == "system":
+            system = str(msgs.pop(0).get("content", "")).strip() + "\n\n"
+        if fmt == "mistral":
+            ids = [self.bos_id]
+            first = True
+            for m in msgs:
+                c = str(m.get("content", "")).strip()
+                if m.get("role") == "user":
+                    ids += self.encode("[INST] " + (system + c if first else c) + " [/INST]")
+                    first = False
+                elif m.get("role") == "assistant":
+                    ids += self.encode(" " + c + " ")
+                    ids.append(self.eot_id)
+            return ids
+        if fmt == "gemma":
+            ids = [self.bos_id]
+            first = True
+            for m in msgs:
+                role = "model" if m.get("role") == "assistant" else "user"
+                c = str(m.get("content", "")).strip()
+                if role == "user" and first:
+                    c, first = system + c, False
+                ids += self.encode(f"<start_of_turn>{role}\n{c}<end_of_turn>\n")
+            if add_generation_prompt:
+                ids += self.encode("<start_of_turn>model\n")
+            return ids
+        if fmt == "plain":
+            text = system + "".join(f"{m.get('role', 'user')}: {m.get('content', '')}\n" for m in msgs)
+            if add_generation_prompt:
+                text += "assistant: "
+            return [self.bos_id] + self.encode(text)
+        raise ValueError(f"unknown chat format {fmt!r}")
 
 
 def _byte_decoder() -> dict:
