@@ -41,12 +41,26 @@ def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.T
     return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(x.dtype)
 
 
+def _window_mask(S: int, W: int, device) -> torch.Tensor:
+    """[S, S] bool: key j visible to query i iff i - W < j <= i."""
+    i = torch.arange(S, device=device)
+    d = i[:, None] - i[None, :]
+    return (d >= 0) & (d < W)
+
+
 def llama_hidden(model, ids: torch.Tensor, linear: Optional[LinearFn] = None,
                  params: Optional[Dict] = None, grad_ckpt: bool = False,
                  pos: Optional[torch.Tensor] = None) -> torch.Tensor:
     """ids [B, S] → final-normed hidden [B, S, H] (causal). ``linear(x, layer, name)``
     computes a projection (base weight + adapter); ``params`` overrides the model's tensors
-    (fp32 masters for full fine-tuning)."""
+    (fp32 masters for full fine-tuning).
+
+    Every decoder family of ``LlamaConfig`` (the serving model's weights, same semantics as
+    models/llama.py): LayerNorm + biases and the non-gated GELU MLP (StarCoder2), GeGLU and
+    the scaled embedding (Gemma: its (1 + w) norm scale is already folded into the stored
+    weight), sliding-window attention (Mistral v0.1, StarCoder2) and the sparse MoE MLP
+    (Mixtral: dense per-expert loop over the routed rows, differentiable through the
+    router's top-k weights)."""
     cfg = model.cfg
     P = params or {}
     B, S = ids.shape
@@ -56,40 +70,77 @@ def llama_hidden(model, ids: torch.Tensor, linear: Optional[LinearFn] = None,
     cs = model.cos_sin.to(ids.device)[pos]                        # [B, S, D]
     cos, sin = cs[..., : D // 2].unsqueeze(2), cs[..., D // 2:].unsqueeze(2)
     dt = torch.bfloat16
+    layer_norm = cfg.norm == "layer"
+    amask = _window_mask(S, cfg.sliding_window, ids.device) if cfg.sliding_window and S > cfg.sliding_window else None
 
     def W(li, name):
-        return P.get((li, name), model.layers[li][name] if li >= 0 else None)
+        return P.get((li, name), model.layers[li].get(name) if li >= 0 else None)
 
-    def lin(x, li, name):
-        if linear is not None:
-            return linear(x, li, name)
-        return x @ W(li, name).to(dt).t()
+    def lin(x, li, name, bias=None):
+        y = linear(x, li, name) if linear is not None else x @ W(li, name).to(dt).t()
+        b = W(li, bias) if bias else None
+        return y if b is None else y + b.to(y.dtype)
+
+    def norm(x, li, name):
+        w = W(li, name) if li >= 0 else P.get(name, getattr(model, name))
+        if not layer_norm:
+            return rms_norm(x, w, cfg.eps)
+        b = W(li, name + "_b") if li >= 0 else P.get(name + "_b", getattr(model, name + "_b"))
+        return F.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), cfg.eps).to(x.dtype)
+
+    def act(g):
+        return F.silu(g) if cfg.act == "silu" else F.gelu(g, approximate="tanh")
+
+    def mlp(h, li):
+        if cfg.is_moe:
+            x2 = h.reshape(-1, h.shape[-1])
+            logits = (x2 @ W(li, "router").to(dt).t()).float()
+            pr = torch.softmax(logits, -1)
+            wk, ids_k = torch.topk(pr, cfg.experts_per_tok, -1)
+            wk = wk / wk.sum(-1, keepdim=True)
+            w13, w2 = W(li, "w13"), W(li, "w2")
+            Fe = w2.shape[2]
+            out = torch.zeros(x2.shape, dtype=torch.float32, device=x2.device)
+            for e in range(w13.shape[0]):
+                tok, slot = torch.where(ids_k == model.expert0 + e)
+                if tok.numel() == 0:
+                    continue
+                gu = x2[tok] @ w13[e].to(dt).t()
+                y = (act(gu[:, :Fe]) * gu[:, Fe:]) @ w2[e].to(dt).t()
+                out = out.index_add(0, tok, y.float() * wk[tok, slot].unsqueeze(1))
+            return out.to(h.dtype).view_as(h)
+        gu = lin(h, li, "wgu", "bgu")
+        if cfg.gated_mlp:
+            g, u = gu.chunk(2, dim=-1)
+            return lin(act(g) * u, li, "wd", "bd")
+        return lin(act(gu), li, "wd", "bd")
 
     emb = P.get("embed", model.embed)
     x = F.embedding(ids, emb).to(dt)
+    if cfg.embed_scale != 1.0:
+        x = x * torch.tensor(cfg.embed_scale, dtype=dt)
 
     def layer(x, li):
-        L = model.layers[li]
-        h = rms_norm(x, P.get((li, "attn_norm"), L["attn_norm"]), cfg.eps)
-        qkv = lin(h, li, "wqkv")
+        h = norm(x, li, "attn_norm")
+        qkv = lin(h, li, "wqkv", "bqkv")
         q, k, v = qkv.split([hq * D, hkv * D, hkv * D], dim=-1)
         q = apply_rope(q.view(B, S, hq, D), cos, sin).transpose(1, 2)
         k = apply_rope(k.view(B, S, hkv, D), cos, sin).transpose(1, 2)
         v = v.view(B, S, hkv, D).transpose(1, 2)
-        a = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=model.scale, enable_gqa=hq != hkv)
+        if amask is None:
+            a = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=model.scale, enable_gqa=hq != hkv)
+        else:
+            a = F.scaled_dot_product_attention(q, k, v, attn_mask=amask, scale=model.scale, enable_gqa=hq != hkv)
         a = a.transpose(1, 2).reshape(B, S, hq * D)
-        x = x + lin(a, li, "wo")
-        h = rms_norm(x, P.get((li, "mlp_norm"), L["mlp_norm"]), cfg.eps)
-        gu = lin(h, li, "wgu")
-        g, u = gu.chunk(2, dim=-1)
-        return x + lin(F.silu(g) * u, li, "wd")
+        x = x + lin(a, li, "wo", "bo")
+        return x + mlp(norm(x, li, "mlp_norm"), li)
 
     for li in range(len(model.layers)):
         if grad_ckpt and torch.is_grad_enabled():
             x = _ckpt(layer, x, li, use_reentrant=False)
         else:
             x = layer(x, li)
-    return rms_norm(x, P.get("final_norm", model.final_norm), cfg.eps)
+    return norm(x, -1, "final_norm")
 
 
 def lm_loss(model, hidden: torch.Tensor, labels: torch.Tensor, params: Optional[Dict] = None,
@@ -97,7 +148,9 @@ def lm_loss(model, hidden: torch.Tensor, labels: torch.Tensor, params: Optional[
     """Mean next-token cross entropy over positions with ``labels >= 0`` (labels are already
     shifted: labels[b, t] is the target for hidden[b, t]). The vocab projection is chunked
     over tokens so [tokens, 128256] fp32 logits never materialise at once."""
-    head = (params or {}).get("lm_head", model.lm_head).to(torch.bfloat16)
+    P = params or {}
+    head = P.get("lm_head", P.get("embed") if model.lm_head is model.embed else None)
+    head = (head if head is not None else model.lm_head).to(torch.bfloat16)
     h = hidden.reshape(-1, hidden.shape[-1])
     y = labels.reshape(-1)
     keep = (y >= 0).nonzero().squeeze(1)
@@ -157,7 +210,11 @@ def trainable_params(model, kind: str = "llama") -> Dict:
     """fp32 master copies of every weight (full fine-tuning), keyed like ``params``."""
     out: Dict = {}
     if kind == "llama":
-        out["embed"], out["final_norm"], out["lm_head"] = model.embed, model.final_norm, model.lm_head
+        out["embed"], out["final_norm"] = model.embed, model.final_norm
+        if getattr(model, "final_norm_b", None) is not None:
+            out["final_norm_b"] = model.final_norm_b
+        if model.lm_head is not model.embed:   # tied embeddings train through "embed"
+            out["lm_head"] = model.lm_head
         for li, L in enumerate(model.layers):
             for n, t in L.items():
                 out[(li, n)] = t

@@ -16,7 +16,7 @@ def _free_port():
     return p
 
 
-def _tp_worker(rank, world, port, q, tp=2, pp=1, sp=False):
+def _tp_worker(rank, world, port, q, tp=2, pp=1, sp=False, model="llama-tiny", over=None):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
@@ -26,9 +26,9 @@ def _tp_worker(rank, world, port, q, tp=2, pp=1, sp=False):
     from nv_genai_amd.parallel import dist as pd
 
     single = pd.ParallelContext()
-    cfg = llama_config("llama-tiny")
+    cfg = llama_config(model, **(over or {}))
     full = LlamaModel(cfg, "cpu", pctx=single, seed=7).state_dict()
-    ecfg = EngineConfig(model="llama-tiny", max_num_seqs=4, max_batched_tokens=256, max_model_len=512,
+    ecfg = EngineConfig(model=model, max_num_seqs=4, max_batched_tokens=256, max_model_len=512,
                         kv_cache_blocks=32, sequence_parallel=sp, sp_min_tokens=16)
     prompts = [[5, 6, 7, 8] * 20, [9, 10, 11] * 11]
     params = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
@@ -38,10 +38,11 @@ def _tp_worker(rank, world, port, q, tp=2, pp=1, sp=False):
     ref = None
     if rank == 0:
         m1 = LlamaModel(cfg, "cpu", dtype=f32, pctx=single, weights=full)
-        e1 = LLMEngine(ecfg, device="cpu", pctx=single, model=m1)
+        e1 = LLMEngine(ecfg, device="cpu", pctx=single, model=m1, model_cfg=cfg)
         ref = [r.output_ids for r in e1.generate(prompts, params)]
     pctx = pd.init_distributed(tp_size=tp, backend="gloo", device="cpu", pp_size=pp)
-    eng = LLMEngine(ecfg, device="cpu", pctx=pctx, model=LlamaModel(cfg, "cpu", dtype=f32, pctx=pctx, weights=full))
+    eng = LLMEngine(ecfg, device="cpu", pctx=pctx, model_cfg=cfg,
+                    model=LlamaModel(cfg, "cpu", dtype=f32, pctx=pctx, weights=full))
     if eng.is_driver:
         out = [r.output_ids for r in eng.generate(prompts, params)]
         eng.stop_followers()
@@ -78,6 +79,29 @@ def test_sequence_parallel_tp_matches_single():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert sp_steps >= 1
+    assert out == ref
+
+
+@pytest.mark.parametrize("model,over,sp", [
+    ("mixtral-tiny", None, False),                    # 4 experts / 2 ranks: expert parallel
+    ("mixtral-tiny", {"num_experts": 3}, False),       # 3 experts: each expert's FFN split
+    ("starcoder2-tiny", None, True),                   # biases on rank 0, LayerNorm, window
+    ("gemma-tiny", {"heads": 4, "kv_heads": 2}, False),
+])
+def test_tensor_parallel_families_match_single(model, over, sp):
+    """Every decoder family at TP=2 generates the TP=1 tokens (Mixtral in both MoE sharding
+    modes; StarCoder2 also with sequence-parallel prefill)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q, 2, 1, sp, model, over))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out, ref, _, _, _ = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
     assert out == ref
 
 

@@ -254,3 +254,40 @@ def test_pretrain_packing_loss_and_serving_handoff(tmp_path):
     st, _ = sft_trainer(m, tok, DATA, TrainConfig(lr=1e-3, warmup_steps=1, max_steps=2, micro_batch=4,
                                                   global_batch=4, max_seq_len=64, log_every=0))
     assert len(st.fit()) == 2
+
+
+@pytest.mark.parametrize("name", ["mistral-tiny", "mixtral-tiny", "gemma-tiny", "starcoder2-tiny"])
+def test_family_training_forward_matches_serving(name):
+    """The differentiable forward of every decoder family (sliding window over a 130-token
+    sequence, MoE routing, GeGLU / LayerNorm + biases) equals the serving forward."""
+    from nv_genai_amd.models.llama import AttnMeta, LlamaModel
+    from nv_genai_amd.training import functional as Fn
+
+    cfg = llama_config(name)
+    m = LlamaModel(cfg, "cpu", seed=2)
+    m.allocate_kv_cache(4, 64)
+    T = 130
+    ids = torch.randint(3, 30000, (T,), generator=torch.Generator().manual_seed(4))
+    meta = AttnMeta(kind="prefill", slots=torch.arange(T, dtype=torch.int32),
+                    cu_q=torch.tensor([0, T], dtype=torch.int32), ctx_lens=torch.tensor([T], dtype=torch.int32),
+                    block_tables=torch.arange(4, dtype=torch.int32).unsqueeze(0), max_q_len=T, max_ctx=T)
+    serve = m.forward(ids.int(), torch.arange(T, dtype=torch.int32), meta).float()
+    train = Fn.llama_hidden(m, ids.unsqueeze(0).long())[0].float()
+    rel = ((train - serve).norm() / serve.norm()).item()
+    assert rel < 0.03, (name, rel)
+
+
+@pytest.mark.parametrize("name", ["gemma-tiny", "starcoder2-tiny"])
+def test_family_lora_sft_loss_decreases(name):
+    """LoRA SFT of the model-customisation notebooks' families (models/Gemma/lora.ipynb,
+    models/Codegemma/lora.ipynb, models/StarCoder2/lora.ipynb)."""
+    from nv_genai_amd.models.llama import LlamaModel
+    from nv_genai_amd.training.lora import LoRAConfig
+    from nv_genai_amd.training.sft import TrainConfig, sft_trainer
+
+    m = LlamaModel(llama_config(name, max_position=256), "cpu", seed=0)
+    cfg = TrainConfig(lr=1e-2, warmup_steps=2, max_steps=12, micro_batch=4, global_batch=8,
+                      max_seq_len=64, log_every=0)
+    tr, _ = sft_trainer(m, CharTok(), DATA, cfg, LoRAConfig(r=8, alpha=16, targets=("qkv", "o", "gate_up", "down")))
+    hist = tr.fit()
+    assert min(hist[-4:]) < hist[0] * 0.9, hist
