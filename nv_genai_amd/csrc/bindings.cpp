@@ -94,14 +94,15 @@ void silu_mul(Tensor out, Tensor x) {
   nga::launch_silu_mul(bfp(out), bfp(x), x.size(0), (int)out.size(1), cur_stream(x));
 }
 
-void bias_gelu(Tensor x, c10::optional<Tensor> bias, bool tanh_form) {
+void bias_gelu(Tensor x, c10::optional<Tensor> bias, int64_t mode) {
+  TORCH_CHECK(mode >= 0 && mode <= 2, "bias_gelu: mode 0 (erf), 1 (tanh) or 2 (quick)");
   CHECK_BF16(x); CHECK_CONTIG(x);
   TORCH_CHECK(x.dim() == 2 && x.size(1) % 8 == 0);
   if (bias.has_value()) {
     CHECK_BF16(*bias);
     TORCH_CHECK(bias->numel() == x.size(1));
   }
-  nga::launch_bias_gelu(bfp(x), cbfp(bias), x.size(0), (int)x.size(1), tanh_form, cur_stream(x));
+  nga::launch_bias_gelu(bfp(x), cbfp(bias), x.size(0), (int)x.size(1), (int)mode, cur_stream(x));
 }
 
 // ------------------------------------------------------------------ rope + kv cache

@@ -52,8 +52,9 @@ __global__ void gelu_tanh_mul_kernel(uint16_t* __restrict__ out, const uint16_t*
   }
 }
 
-// x: [T, F] inout; x = gelu(x + bias), erf form or (TANH) the tanh approximation
-template <bool TANH>
+// x: [T, F] inout; x = gelu(x + bias): MODE 0 erf form, 1 tanh approximation, 2 CLIP's
+// quick_gelu x * sigmoid(1.702 x)
+template <int MODE>
 __global__ void bias_gelu_kernel(uint16_t* __restrict__ x, const uint16_t* __restrict__ bias,
                                  int64_t T, int F) {
   const int64_t vec_per_row = F / 8;
@@ -69,7 +70,11 @@ __global__ void bias_gelu_kernel(uint16_t* __restrict__ x, const uint16_t* __res
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float f = bf2f(v[j]) + (bias ? bf2f(b[j]) : 0.f);
-      o[j] = f2bf(TANH ? gelu_tanh(f) : 0.5f * f * (1.f + erff(f * 0.70710678118654752f)));
+      float y;
+      if (MODE == 1) y = gelu_tanh(f);
+      else if (MODE == 2) y = f / (1.f + __expf(-1.702f * f));
+      else y = 0.5f * f * (1.f + erff(f * 0.70710678118654752f));
+      o[j] = f2bf(y);
     }
     store8(x + t * F + c, o);
   }
@@ -92,13 +97,15 @@ void launch_gelu_tanh_mul(uint16_t* out, const uint16_t* in, int64_t T, int F, h
   gelu_tanh_mul_kernel<<<ew_grid(T * F / 8), 256, 0, stream>>>(out, in, T, F);
 }
 
-void launch_bias_gelu(uint16_t* x, const uint16_t* bias, int64_t T, int F, bool tanh_form,
+void launch_bias_gelu(uint16_t* x, const uint16_t* bias, int64_t T, int F, int mode,
                       hipStream_t stream) {
   if (T == 0) return;
-  if (tanh_form)
-    bias_gelu_kernel<true><<<ew_grid(T * F / 8), 256, 0, stream>>>(x, bias, T, F);
+  if (mode == 1)
+    bias_gelu_kernel<1><<<ew_grid(T * F / 8), 256, 0, stream>>>(x, bias, T, F);
+  else if (mode == 2)
+    bias_gelu_kernel<2><<<ew_grid(T * F / 8), 256, 0, stream>>>(x, bias, T, F);
   else
-    bias_gelu_kernel<false><<<ew_grid(T * F / 8), 256, 0, stream>>>(x, bias, T, F);
+    bias_gelu_kernel<0><<<ew_grid(T * F / 8), 256, 0, stream>>>(x, bias, T, F);
 }
 
 }  // namespace nga

@@ -19,7 +19,8 @@ void launch_add_layernorm(uint16_t* out, uint16_t* resid, const uint16_t* delta,
 // activation.hip
 void launch_silu_mul(uint16_t* out, const uint16_t* in, int64_t T, int F, hipStream_t stream);
 void launch_gelu_tanh_mul(uint16_t* out, const uint16_t* in, int64_t T, int F, hipStream_t stream);
-void launch_bias_gelu(uint16_t* x, const uint16_t* bias, int64_t T, int F, bool tanh_form,
+// mode 0: erf GELU, 1: tanh GELU, 2: quick_gelu (x * sigmoid(1.702 x))
+void launch_bias_gelu(uint16_t* x, const uint16_t* bias, int64_t T, int F, int mode,
                       hipStream_t stream);
 
 // rope.hip

@@ -81,6 +81,9 @@ class Request:
     cached_prefix: int = 0
     beams: List[tuple] = field(default_factory=list)   # beam search: (score, token ids, text)
     json_state: Optional[object] = None    # _rt.JsonState of a response_format=json_object request
+    # multimodal prompt: (position, features [n, hidden]) — rows whose input embeddings are
+    # replaced by projected image features (models/vision.py)
+    mm: Optional[list] = None
 
     @property
     def ttft(self) -> Optional[float]:
@@ -207,6 +210,7 @@ class LLMEngine:
             # routing buffers sized for the largest step before any hipGraph capture
             ops.MoEWorkspace.get(T, self.mcfg.experts_per_tok, self.model.n_experts, dev)
         self.requests: Dict[int, Request] = {}
+        self._has_mm = False   # any multimodal request seen (enables the embedding override pass)
         self._ids = itertools.count(1)
         self._rng = random.Random(cfg.seed)
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
@@ -245,8 +249,23 @@ class LLMEngine:
 
     def add_request(self, prompt_ids: List[int], params: Optional[SamplingParams] = None,
                     request_id: Optional[int] = None,
-                    on_token: Optional[Callable[[Request, str], None]] = None) -> Request:
+                    on_token: Optional[Callable[[Request, str], None]] = None,
+                    mm: Optional[list] = None) -> Request:
+        """Queue a request. ``mm``: [(position, features [n, hidden])] — the prompt rows
+        [position, position + n) take these embeddings instead of their token ids' (image
+        placeholders of a vision-language prompt)."""
         params = params or SamplingParams()
+        V = self.mcfg.vocab_size
+        if prompt_ids and max(prompt_ids) >= V:
+            # the synthetic tokenizer's id space (32768) exceeds a few real vocabularies
+            # (32000): fold, as detokenisation folds sampled ids the other way
+            prompt_ids = [t % V for t in prompt_ids]
+        if mm:
+            if self.p.mp_size > 1:
+                raise ValueError("multimodal requests run on single-rank engines")
+            for off, f in mm:
+                if off < 0 or off + f.shape[0] > len(prompt_ids) or f.shape[1] != self.mcfg.hidden:
+                    raise ValueError("multimodal features must cover prompt rows of the model's hidden size")
         rid = request_id if request_id is not None else next(self._ids)
         max_new = max(1, min(params.max_tokens, self.cfg.max_model_len - len(prompt_ids)))
         if len(prompt_ids) >= self.cfg.max_model_len:
@@ -254,10 +273,13 @@ class LLMEngine:
                              f"{self.cfg.max_model_len}")
         req = Request(rid, list(prompt_ids), params, arrival=time.perf_counter(),
                       seed=params.seed if params.seed is not None else self._rng.getrandbits(62),
-                      on_token=on_token)
+                      on_token=on_token,
+                      mm=[(int(o), f.to(self.device, self.model.dtype)) for o, f in mm] if mm else None)
         req.params = SamplingParams(**{**params.__dict__, "max_tokens": max_new})
         if self.cfg.detokenize:
             req.detok = IncrementalDetokenizer(self.tok)
+        if mm:
+            self._has_mm = True
         if params.response_format == "json_object":
             self._grammar()
             req.json_state = rt.JsonState(True)
@@ -860,10 +882,34 @@ class LLMEngine:
         tok, lp = self._sample(logits, n)
         return tok[:n].cpu(), lp[:n].cpu()
 
+    def _mm_override(self, n: int, nd: int):
+        """(token rows, features) of this step's prompt rows that carry image features."""
+        rows, feats = [], []
+        pos, cu, sid = self._np[1], self._np[3], self._np[6]
+        for r in range(nd, n):
+            req = self.requests.get(int(sid[r]))
+            if req is None or not req.mm:
+                continue
+            t0, t1 = int(cu[r]), int(cu[r + 1])
+            if t1 <= t0:
+                continue
+            p0 = int(pos[t0])
+            p1 = p0 + (t1 - t0)
+            for off, f in req.mm:
+                lo, hi = max(off, p0), min(off + f.shape[0], p1)
+                if lo < hi:
+                    rows.append(torch.arange(t0 + lo - p0, t0 + hi - p0))
+                    feats.append(f[lo - off:hi - off])
+        if not rows:
+            return None
+        return torch.cat(rows).to(self.device, non_blocking=True), torch.cat(feats)
+
     def _prefill_forward(self, n, ntok, max_q, max_ctx, nd: int = 0):
         meta = self._meta("prefill", n, ntok, max_q, max_ctx, nd)
         sample_idx = (self.d_cu[1: n + 1] - 1).long()
-        h = self.model.forward(self.d_ids[:ntok], self.d_pos[:ntok], meta, sample_idx)
+        ov = self._mm_override(n, nd) if self._has_mm else None
+        h = self.model.forward(self.d_ids[:ntok], self.d_pos[:ntok], meta, sample_idx,
+                               embed_override=ov)
         return None if h is None else self.model.logits(h)   # None: a later pipeline stage
 
     def _decode(self, n):

@@ -158,6 +158,13 @@ LLAMA_PRESETS = {
                                   gated_mlp=False, attn_bias=True, mlp_bias=True,
                                   sliding_window=4096, max_position=16384, bos_id=0, eos_ids=(0,),
                                   chat_format="plain"),
+    # LLaVA-1.5's language model (Vicuna-7B = Llama-2-7B dims) and the NeVA-22B-class decoder
+    "vicuna-7b": LlamaConfig(name="vicuna-7b", vocab_size=32000, hidden=4096, layers=32, heads=32,
+                             kv_heads=32, ffn=11008, rope_theta=10000.0, max_position=4096,
+                             bos_id=1, eos_ids=(2,), chat_format="plain"),
+    "neva-22b-llm": LlamaConfig(name="neva-22b-llm", vocab_size=32768, hidden=6144, layers=40,
+                                heads=48, kv_heads=8, ffn=24576, rope_theta=10000.0,
+                                max_position=4096, bos_id=1, eos_ids=(2,), chat_format="plain"),
     # small configs with the same structure for CPU tests / smoke runs
     "llama-tiny": LlamaConfig(name="llama-tiny", vocab_size=32768, hidden=256, layers=2, heads=4,
                               kv_heads=2, head_dim=64, ffn=512, max_position=2048,

@@ -523,17 +523,27 @@ class LlamaModel:
         raise RuntimeError("model has no layers")
 
     def forward(self, ids: torch.Tensor, pos: torch.Tensor, meta: AttnMeta,
-                sample_idx: Optional[torch.Tensor] = None) -> torch.Tensor:
+                sample_idx: Optional[torch.Tensor] = None, embed_override=None) -> torch.Tensor:
         """Returns the final-normed hidden rows selected by ``sample_idx`` (all rows if None).
-        With pipeline stages only stage 0 gets them (other stages return None)."""
+        With pipeline stages only stage 0 gets them (other stages return None).
+        ``embed_override = (rows, features)`` replaces those rows' input embeddings (the
+        projected image patches of a vision-language prompt)."""
         if self.p.pp_size > 1:
-            return self._forward_pp(ids, pos, meta, sample_idx)
+            return self._forward_pp(ids, pos, meta, sample_idx, embed_override)
         if (self.sequence_parallel and self.p.tp_size > 1 and meta.kind == "prefill"
-                and ids.shape[0] >= self.sp_min_tokens):
+                and ids.shape[0] >= self.sp_min_tokens and embed_override is None):
             return self._forward_sp(ids, pos, meta, sample_idx)
-        if meta.kind == "mixed" and self.split_mixed and ids.is_cuda and self.p.tp_size == 1:
+        if (meta.kind == "mixed" and self.split_mixed and ids.is_cuda and self.p.tp_size == 1
+                and embed_override is None):
             return self.forward_split(ids, pos, meta, sample_idx)
-        return self._stack(self.embed_tokens(ids), pos, meta, sample_idx)
+        return self._stack(self._embed(ids, embed_override), pos, meta, sample_idx)
+
+    def _embed(self, ids, embed_override=None):
+        h = self.embed_tokens(ids)
+        if embed_override is not None:
+            rows, feats = embed_override
+            h.index_copy_(0, rows, feats.to(h.dtype))
+        return h
 
     def _forward_sp(self, ids, pos, meta: AttnMeta, sample_idx):
         """Megatron-style sequence parallelism inside the TP group for long prefills: the
@@ -579,7 +589,7 @@ class LlamaModel:
         out = tp_all_gather_rows(self._add_norm(resid, d, self.final_norm, self.final_norm_b), p)[:T]
         return out if sample_idx is None else out.index_select(0, sample_idx)
 
-    def _forward_pp(self, ids, pos, meta: AttnMeta, sample_idx):
+    def _forward_pp(self, ids, pos, meta: AttnMeta, sample_idx, embed_override=None):
         """Layer-split pipeline (SURVEY.md §2.E "PP", CC6): stage s receives the residual
         stream from stage s-1, runs its layers and sends it on (RCCL p2p over xGMI); the
         last stage applies the final norm to the sampling rows and returns them to stage 0,
@@ -591,7 +601,7 @@ class LlamaModel:
         cfg, p = self.cfg, self.p
         T = ids.shape[0]
         if self.first_stage:
-            resid = self.embed_tokens(ids)
+            resid = self._embed(ids, embed_override)
         else:
             resid = torch.empty(T, cfg.hidden, dtype=self.dtype, device=self.device)
             dist.recv(resid, src=p.pp_prev)

@@ -109,11 +109,15 @@ def silu_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None):
     return out
 
 
-def bias_gelu_(x: torch.Tensor, bias: Optional[torch.Tensor], approximate: bool = False):
-    """x = gelu(x + bias) in place; ``approximate``: the tanh form (StarCoder2, Gemma)."""
+_GELU_MODES = {False: 0, "none": 0, True: 1, "tanh": 1, "quick": 2}
+
+
+def bias_gelu_(x: torch.Tensor, bias: Optional[torch.Tensor], approximate=False):
+    """x = gelu(x + bias) in place; ``approximate``: False / "none" (erf), True / "tanh"
+    (StarCoder2, Gemma) or "quick" (CLIP's x * sigmoid(1.702 x))."""
     if not _gpu(x):
         return ref.bias_gelu_(x, bias, approximate)
-    kernels().bias_gelu(x, bias, bool(approximate))
+    kernels().bias_gelu(x, bias, _GELU_MODES[approximate])
     return x
 
 

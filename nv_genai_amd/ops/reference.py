@@ -57,9 +57,14 @@ def silu_mul(x: torch.Tensor) -> torch.Tensor:
     return (torch.nn.functional.silu(g) * u).to(x.dtype)
 
 
-def bias_gelu_(x: torch.Tensor, bias: Optional[torch.Tensor], approximate: bool = False) -> torch.Tensor:
+def bias_gelu_(x: torch.Tensor, bias: Optional[torch.Tensor], approximate=False) -> torch.Tensor:
+    """approximate: False / "none" (erf GELU), True / "tanh", or "quick" (x * sigmoid(1.702 x))."""
     xf = x.float() + (bias.float() if bias is not None else 0.0)
-    x.copy_(torch.nn.functional.gelu(xf, approximate="tanh" if approximate else "none").to(x.dtype))
+    if approximate == "quick":
+        y = xf * torch.sigmoid(1.702 * xf)
+    else:
+        y = torch.nn.functional.gelu(xf, approximate="tanh" if approximate in (True, "tanh") else "none")
+    x.copy_(y.to(x.dtype))
     return x
 
 

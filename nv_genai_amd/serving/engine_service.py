@@ -162,10 +162,12 @@ class EngineService:
                 logging.shutdown()
                 os._exit(70)
 
-    def submit(self, prompt_ids: List[int], params: SamplingParams) -> StreamHandle:
+    def submit(self, prompt_ids: List[int], params: SamplingParams, mm=None) -> StreamHandle:
+        """Queue a request on the engine thread; ``mm``: image features of a vision-language
+        prompt (``LLMEngine.add_request``)."""
         h = StreamHandle(self)
         with self.cv:
-            req = self.engine.add_request(prompt_ids, params, on_token=h._on_token)
+            req = self.engine.add_request(prompt_ids, params, on_token=h._on_token, mm=mm)
             h.request = req
             self.handles[req.id] = h
             self.cv.notify()

@@ -119,9 +119,18 @@ def _content_text(c) -> str:
     return "".join(p.get("text", "") for p in c if isinstance(p, dict) and p.get("type", "text") == "text")
 
 
+def _has_images(messages) -> bool:
+    return any(isinstance(m.content, list) and any(isinstance(p, dict) and p.get("type") in ("image_url", "image")
+                                                   for p in m.content) for m in messages)
+
+
 def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name: str = "meta/llama3-8b-instruct",
                embed_name: str = "snowflake/arctic-embed-l", rerank_name: str = "nv-rerank-qa-mistral-4b:1",
-               batch_delay_s: float = 0.002) -> FastAPI:
+               batch_delay_s: float = 0.002, vlm=None, vlm_service=None, vlm_name: str = "ai-neva-22b") -> FastAPI:
+    """``vlm`` / ``vlm_service``: a :class:`~nv_genai_amd.models.vision.VisionLanguageModel`
+    and the :class:`EngineService` over its engine; chat requests with ``image_url`` parts
+    (or ``model == vlm_name``) go there — the NeVA / DePlot endpoint contract of the
+    reference's multimodal example (examples/multimodal_rag/llm/llm_client.py:37-42)."""
     app = FastAPI(title="nv_genai_amd model server")
     metrics = Registry()
 
@@ -139,6 +148,7 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
 
         batcher = DynamicBatcher(embed_engine, batch_delay_s)
     app.state.llm, app.state.embed, app.state.rerank, app.state.batcher = llm_service, embed_engine, rerank_engine, batcher
+    app.state.vlm, app.state.vlm_service = vlm, vlm_service
 
     def _need(x, what):
         if x is None:
@@ -208,15 +218,25 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
 
     @app.post("/v1/chat/completions")
     async def chat(req: ChatRequest, request: Request):
-        svc = _need(app.state.llm, "LLM")
         t0 = time.perf_counter()
         metrics.inc("chat_requests_total")
-        msgs = [{"role": m.role, "content": _content_text(m.content)} for m in req.messages]
         if req.stream and req.n > 1:
             return JSONResponse({"error": "stream supports n = 1"}, status_code=400)
-        with tracer.span("chat.completions", {"model": req.model}, request.headers.get("traceparent")):
-            ids = svc.engine.apply_chat_template(msgs)
-            handles = _submit_n(svc, ids, req)
+        use_vlm = app.state.vlm is not None and (_has_images(req.messages) or req.model == vlm_name)
+        if use_vlm:
+            svc = app.state.vlm_service
+            with tracer.span("chat.completions.vision", {"model": req.model}, request.headers.get("traceparent")):
+                msgs = [{"role": m.role, "content": m.content} for m in req.messages]
+                ids, mm = await asyncio.get_running_loop().run_in_executor(None, app.state.vlm.build_request, msgs)
+                handles = [svc.submit(ids, _params(req), mm=mm)]
+        else:
+            if _has_images(req.messages):
+                return JSONResponse({"error": "this server hosts no vision-language model"}, status_code=400)
+            svc = _need(app.state.llm, "LLM")
+            msgs = [{"role": m.role, "content": _content_text(m.content)} for m in req.messages]
+            with tracer.span("chat.completions", {"model": req.model}, request.headers.get("traceparent")):
+                ids = svc.engine.apply_chat_template(msgs)
+                handles = _submit_n(svc, ids, req)
         rid = f"chatcmpl-{uuid.uuid4().hex}"
         model = req.model or llm_name
         if req.stream:
@@ -342,6 +362,8 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
         out = []
         if app.state.llm is not None:
             out.append({"id": llm_name, "object": "model", "owned_by": "nv_genai_amd"})
+        if app.state.vlm is not None:
+            out.append({"id": vlm_name, "object": "model", "owned_by": "nv_genai_amd"})
         if app.state.embed is not None:
             out.append({"id": embed_name, "object": "model", "owned_by": "nv_genai_amd"})
         if app.state.rerank is not None:
@@ -379,6 +401,7 @@ def main(argv=None):
     ap.add_argument("--llm", default="llama3-8b", help="LLM preset ('' to disable)")
     ap.add_argument("--embed", default="arctic-embed-l", help="encoder preset ('' to disable)")
     ap.add_argument("--rerank", default="", help="reranker preset ('' to disable)")
+    ap.add_argument("--vlm", default="", help="vision-language preset, e.g. neva-22b ('' to disable)")
     ap.add_argument("--weights", default="", help="safetensors dir for the LLM")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=8000)
@@ -407,7 +430,16 @@ def main(argv=None):
         emb = EmbeddingEngine(args.embed, device=args.device)
     if args.rerank:
         rr = EmbeddingEngine(args.rerank, device=args.device)
-    app = create_app(svc, emb, rr)
+    vlm = vsvc = None
+    if args.vlm:
+        from ..models.vision import VisionLanguageModel, vlm_config
+
+        vc = vlm_config(args.vlm)
+        vlm = VisionLanguageModel(vc, device=args.device, engine_cfg=EngineConfig(
+            model=vc.llm, max_num_seqs=args.max_num_seqs, max_model_len=args.max_model_len,
+            kv_cache_fraction=args.kv_cache_fraction))
+        vsvc = EngineService(vlm.engine, name="vlm")
+    app = create_app(svc, emb, rr, vlm=vlm, vlm_service=vsvc, vlm_name=f"ai-{args.vlm}" if args.vlm else "ai-neva-22b")
     uvicorn.run(app, host=args.host, port=args.port, log_level=os.environ.get("LOGLEVEL", "info").lower())
 
 
