@@ -29,10 +29,19 @@ class EmbeddingEngine:
                  max_batch_tokens: int = 65536, seed: int = 0,
                  tokenizer: Optional[EmbedTokenizer] = None,
                  encoder: Optional[EncoderModel] = None):
-        self.cfg = encoder_config(model) if isinstance(model, str) else model
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
+        from ..models.ranker import DECODER_RANKERS
+
+        if isinstance(model, str) and model in DECODER_RANKERS:
+            # decoder-based cross-encoder (nv-rerank-qa-mistral-4b): models/ranker.py
+            from ..models.ranker import DecoderRanker, ranker_encoder_config
+
+            self.cfg = ranker_encoder_config(model)
+            encoder = encoder or DecoderRanker(model, self.device, seed=seed)
+        else:
+            self.cfg = encoder_config(model) if isinstance(model, str) else model
         self.model = encoder or EncoderModel(self.cfg, self.device, seed=seed)
         self.tok = tokenizer or embed_tokenizer()
         self.tok.max_len = min(self.tok.max_len, self.cfg.max_position)
@@ -139,6 +148,9 @@ class EmbeddingEngine:
             q = self.embed([query], "query", truncate)
             p = self.embed(passages, "passage", truncate)
             return (p @ q[0]).tolist()
+        pair = getattr(self.model, "encode_pair", None)
+        if pair is not None:   # decoder ranker: its own tokenizer and pair template
+            return self.embed_ids([pair(query, p, truncate) for p in passages])[:, 0].tolist()
         seqs, types = [], []
         for p in passages:
             enc = self.tok.tok.encode(query, p)

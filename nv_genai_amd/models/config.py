@@ -158,6 +158,10 @@ LLAMA_PRESETS = {
                                   gated_mlp=False, attn_bias=True, mlp_bias=True,
                                   sliding_window=4096, max_position=16384, bos_id=0, eos_ids=(0,),
                                   chat_format="plain"),
+    # nv-rerank-qa-mistral-4b: Mistral-7B v0.1 cut to its first 16 layers (bidirectional)
+    "mistral-4b-rerank": LlamaConfig(name="mistral-4b-rerank", arch="mistral", vocab_size=32000,
+                                     layers=16, rope_theta=10000.0, max_position=4096, bos_id=1,
+                                     eos_ids=(2,), chat_format="mistral"),
     # LLaVA-1.5's language model (Vicuna-7B = Llama-2-7B dims) and the NeVA-22B-class decoder
     "vicuna-7b": LlamaConfig(name="vicuna-7b", vocab_size=32000, hidden=4096, layers=32, heads=32,
                              kv_heads=32, ffn=11008, rope_theta=10000.0, max_position=4096,

@@ -230,3 +230,16 @@ def test_vision_tower_and_vlm_gpu(gpu):
                                           {"type": "image", "image": img}]}]
     r = vlm.generate([msgs, msgs], SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True))
     assert r[0].output_ids == r[1].output_ids and len(r[0].output_ids) == 8
+
+
+def test_decoder_ranker_gpu_matches_cpu(gpu):
+    """nv-rerank-qa-mistral-4b-layout reranker (bidirectional GQA varlen attention, head_dim
+    128, mean pool + head) on the HIP kernels vs the CPU reference path."""
+    from nv_genai_amd.engine.embed_engine import EmbeddingEngine
+
+    q = "what does the quarterly report say about revenue?"
+    ps = ["revenue grew twelve percent in the quarter", "the cafeteria menu changes weekly",
+          "guidance for the next quarter was raised " * 20]
+    g = torch.tensor(EmbeddingEngine("mistral-rerank-small", device="cuda").rerank(q, ps))
+    c = torch.tensor(EmbeddingEngine("mistral-rerank-small", device="cpu").rerank(q, ps))
+    assert torch.allclose(g, c, atol=0.03 * c.abs().max().item() + 1e-3), (g, c)

@@ -150,3 +150,47 @@ def test_moe_reference_matches_dense_expert_loop():
     y0 = ref.moe_ffn(x, router, w13[:2], w2[:2], k, expert0=0).float()
     y1 = ref.moe_ffn(x, router, w13[2:], w2[2:], k, expert0=2).float()
     assert torch.allclose(y0 + y1, y, atol=2e-2)
+
+
+def test_decoder_ranker_matches_dense_bidirectional_reference():
+    """nv-rerank-qa-mistral-4b layout: decoder layers with a bidirectional mask, masked mean
+    pool, linear head — our packed forward vs an explicit per-pair fp32 recomputation."""
+    from nv_genai_amd.engine.embed_engine import EmbeddingEngine
+    from nv_genai_amd.models.ranker import DecoderRanker
+    from nv_genai_amd.training import functional as Fn
+
+    eng = EmbeddingEngine("mistral-rerank-tiny", device="cpu")
+    assert isinstance(eng.model, DecoderRanker)
+    q = "which river flows through the capital?"
+    ps = ["the capital sits on a wide river delta", "widgets are sold in boxes of twelve",
+          "x " * 700]                                               # > 512 tokens: truncated END
+    got = torch.tensor(eng.rerank(q, ps))
+    m = eng.model.lm
+    want = []
+    for p in ps:
+        ids = torch.tensor(eng.model.encode_pair(q, p))
+        assert ids.numel() <= 512
+        S = ids.numel()
+        # bidirectional reference: the training forward with a full (non-causal) mask
+        B = 1
+        hq, hkv, D = m.hq, m.hkv, m.D
+        cs = m.cos_sin[torch.arange(S)]
+        cos, sin = cs[:, : D // 2].view(1, S, 1, -1), cs[:, D // 2:].view(1, S, 1, -1)
+        x = torch.nn.functional.embedding(ids.unsqueeze(0), m.embed).float()
+        for L in m.layers:
+            h = Fn.rms_norm(x, L["attn_norm"], m.cfg.eps).float()
+            qkv = h @ L["wqkv"].float().t()
+            qq, kk, vv = qkv.split([hq * D, hkv * D, hkv * D], -1)
+            qq = Fn.apply_rope(qq.view(B, S, hq, D), cos, sin).transpose(1, 2)
+            kk = Fn.apply_rope(kk.view(B, S, hkv, D), cos, sin).transpose(1, 2)
+            vv = vv.view(B, S, hkv, D).transpose(1, 2)
+            a = torch.nn.functional.scaled_dot_product_attention(qq, kk, vv, scale=m.scale, enable_gqa=True)
+            x = x + a.transpose(1, 2).reshape(B, S, -1) @ L["wo"].float().t()
+            h = Fn.rms_norm(x, L["mlp_norm"], m.cfg.eps).float()
+            gu = h @ L["wgu"].float().t()
+            g, u = gu.chunk(2, -1)
+            x = x + (torch.nn.functional.silu(g) * u) @ L["wd"].float().t()
+        x = Fn.rms_norm(x, m.final_norm, m.cfg.eps).float()
+        want.append((x[0].mean(0) @ eng.model.head_w.float().t() + eng.model.head_b).item())
+    want = torch.tensor(want)
+    assert torch.allclose(got, want, atol=0.05 * want.abs().max().item() + 1e-3), (got, want)
