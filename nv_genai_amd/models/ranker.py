@@ -47,6 +47,8 @@ class DecoderRanker:
                  weights: Optional[Dict[str, torch.Tensor]] = None, seed: int = 0, max_len: int = 512):
         cfg = llama_config(DECODER_RANKERS[name])
         # bidirectional: no sliding window either (every pair fits the 512-token window)
+        if weights is not None and "lm_head.weight" not in weights and not cfg.tie_embeddings:
+            weights = {**weights, "lm_head.weight": weights["model.embed_tokens.weight"]}
         self.lm = LlamaModel(cfg, device, dtype=dtype, weights=weights, seed=seed)
         self.lm.lm_head = None                    # scoring head instead of the LM head
         self.cfg = cfg
@@ -60,6 +62,13 @@ class DecoderRanker:
             self.head_w = torch.empty(1, cfg.hidden, device=dev, dtype=dtype).normal_(0, 0.02, generator=g)
             self.head_b = torch.zeros(1, device=dev, dtype=torch.float32)
         self._tok = None
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        """Decoder weights (HF names) plus the ``score`` head."""
+        out = {k: v for k, v in self.lm.state_dict().items() if k != "lm_head.weight"}
+        out["score.weight"] = self.head_w
+        out["score.bias"] = self.head_b
+        return out
 
     # ---------------------------------------------------------------- tokenisation
     @property

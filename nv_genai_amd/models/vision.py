@@ -160,6 +160,27 @@ class VisionTower:
                 "w2": get(p + "mlp.fc2.weight"), "b2": get(p + "mlp.fc2.bias"),
             })
 
+    def state_dict(self, prefix: str = "model.vision_tower.") -> Dict[str, torch.Tensor]:
+        """HF ``CLIPVisionModel`` names (inverse of ``_load``)."""
+        c = self.cfg
+        H = c.hidden
+        out = {prefix + "embeddings.patch_embedding.weight": self.patch_w.reshape(H, 3, c.patch, c.patch),
+               prefix + "embeddings.class_embedding": self.cls,
+               prefix + "embeddings.position_embedding.weight": self.pos,
+               prefix + "pre_layrnorm.weight": self.pre_ln[0], prefix + "pre_layrnorm.bias": self.pre_ln[1]}
+        for i, L in enumerate(self.layers):
+            p = prefix + f"encoder.layers.{i}."
+            a = p + "self_attn."
+            for j, n in enumerate(("q_proj", "k_proj", "v_proj")):
+                out[a + n + ".weight"] = L["wqkv"][j * H:(j + 1) * H]
+                out[a + n + ".bias"] = L["bqkv"][j * H:(j + 1) * H]
+            out.update({a + "out_proj.weight": L["wo"], a + "out_proj.bias": L["bo"],
+                        p + "layer_norm1.weight": L["ln1_g"], p + "layer_norm1.bias": L["ln1_b"],
+                        p + "layer_norm2.weight": L["ln2_g"], p + "layer_norm2.bias": L["ln2_b"],
+                        p + "mlp.fc1.weight": L["w1"], p + "mlp.fc1.bias": L["b1"],
+                        p + "mlp.fc2.weight": L["w2"], p + "mlp.fc2.bias": L["b2"]})
+        return out
+
     def patchify(self, pixels: torch.Tensor) -> torch.Tensor:
         """[B, 3, S, S] -> [B, P, 3 * p * p] (channel-major within a patch, like the conv weight)."""
         c = self.cfg

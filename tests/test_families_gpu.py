@@ -219,7 +219,8 @@ def test_vision_tower_and_vlm_gpu(gpu):
     img = buf.getvalue()
     pix = preprocess_image(img, cfg.vision).unsqueeze(0)
     want = cpu_t.forward(pix).float()
-    gpu_t = VisionTower(cfg.vision, "cuda", seed=3)
+    gpu_t = VisionTower(cfg.vision, "cuda", weights=cpu_t.state_dict())   # same weights (the CPU
+    # and GPU generators draw different random streams)
     got = gpu_t.forward(pix.to(gpu)).float().cpu()
     rel = ((got - want).norm() / want.norm()).item()
     assert rel < 0.03, rel
@@ -240,6 +241,10 @@ def test_decoder_ranker_gpu_matches_cpu(gpu):
     q = "what does the quarterly report say about revenue?"
     ps = ["revenue grew twelve percent in the quarter", "the cafeteria menu changes weekly",
           "guidance for the next quarter was raised " * 20]
-    g = torch.tensor(EmbeddingEngine("mistral-rerank-small", device="cuda").rerank(q, ps))
-    c = torch.tensor(EmbeddingEngine("mistral-rerank-small", device="cpu").rerank(q, ps))
+    from nv_genai_amd.models.ranker import DecoderRanker
+
+    cpu_r = DecoderRanker("mistral-rerank-small", "cpu", seed=1)
+    gpu_r = DecoderRanker("mistral-rerank-small", "cuda", weights=cpu_r.state_dict())
+    g = torch.tensor(EmbeddingEngine("mistral-rerank-small", device="cuda", encoder=gpu_r).rerank(q, ps))
+    c = torch.tensor(EmbeddingEngine("mistral-rerank-small", device="cpu", encoder=cpu_r).rerank(q, ps))
     assert torch.allclose(g, c, atol=0.03 * c.abs().max().item() + 1e-3), (g, c)
