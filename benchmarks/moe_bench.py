@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--F", type=int, default=14336)
     ap.add_argument("--E", type=int, default=8)
     ap.add_argument("--k", type=int, default=2)
+    ap.add_argument("--gemm-only", action="store_true",
+                    help="time the gate|up grouped GEMM alone (NGA_MOE_ABLATE picks a diagnostic build)")
     args = ap.parse_args()
     dev = "cuda"
     H, F, E, k = args.H, args.F, args.E, args.k
@@ -60,7 +62,22 @@ def main():
     w2 = (torch.randn(E, H, F, device=dev) * 0.02).to(torch.bfloat16)
     for T in [int(t) for t in args.tokens.split(",")]:
         x = torch.randn(T, H, device=dev).to(torch.bfloat16)
-        ops.MoEWorkspace.get(T, k, E, dev)
+        ws = ops.MoEWorkspace.get(T, k, E, dev)
+        if args.gemm_only:
+            C = ops.kernels()
+            M = T * k
+            bm = 64 if M <= 256 * E else 128
+            mt = -(-M // bm) + E
+            C.moe_route(x @ router.t(), k, ws.ids, ws.w)
+            C.moe_align(ws.ids, ws.w, T, k, 0, E, bm, ws.sorted_tok, ws.sorted_w, ws.inv, ws.tiles, mt)
+            h = torch.empty(M, F, dtype=x.dtype, device=dev)
+            y = torch.empty(M, H, dtype=x.dtype, device=dev)
+            t0 = timeit(lambda: C.moe_gemm(x, w13, ws.sorted_tok, ws.sorted_w, ws.tiles, mt, bm, h, 0, 0))
+            t1 = timeit(lambda: C.moe_gemm(h, w2, ws.sorted_tok, ws.sorted_w, ws.tiles, mt, bm, y, 1, 0))
+            print(json.dumps({"tokens": T, "ablate": os.environ.get("NGA_MOE_ABLATE", "0"),
+                              "gate_up_us": round(t0, 1), "gate_up_tflops": round(2.0 * M * 2 * F * H / t0 / 1e6, 1),
+                              "down_us": round(t1, 1), "down_tflops": round(2.0 * M * F * H / t1 / 1e6, 1)}), flush=True)
+            continue
         y = ops.moe_ffn(x, router, w13, w2, k)
         yr = eager(x, router, w13, w2, k)
         rel = ((y.float() - yr.float()).norm() / yr.float().norm()).item()

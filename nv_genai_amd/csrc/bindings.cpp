@@ -192,14 +192,14 @@ void moe_gemm(Tensor A, Tensor W, Tensor sorted_tok, Tensor sorted_w, Tensor til
   p.K = (int)K;
   p.mt = (int)mt;
   if (mode == 0) {
-    TORCH_CHECK(W.size(1) % 128 == 0, "moe_gemm: 2F must be a multiple of 128");
+    TORCH_CHECK(W.size(1) % 256 == 0, "moe_gemm: 2F must be a multiple of 256");
     p.F = (int)(W.size(1) / 2);
     TORCH_CHECK(out.size(1) == p.F, "moe_gemm: out must be [M, F]");
-    p.nt = p.F / 64;
+    p.nt = p.F / 128;
   } else {
-    TORCH_CHECK(W.size(1) % 128 == 0 && out.size(1) == W.size(1), "moe_gemm: out must be [M, N], N % 128 == 0");
+    TORCH_CHECK(W.size(1) % 256 == 0 && out.size(1) == W.size(1), "moe_gemm: out must be [M, N], N % 256 == 0");
     p.F = 0;
-    p.nt = (int)(W.size(1) / 128);
+    p.nt = (int)(W.size(1) / 256);
   }
   TORCH_CHECK(sorted_tok.numel() >= out.size(0) && sorted_w.numel() >= out.size(0));
   TORCH_CHECK(mode == 1 || A.size(0) >= 1);

@@ -100,7 +100,7 @@ struct MoeGemmParams {
   int K;
   int F;                     // MODE 0: features (up rows start at F)
   int mt;                    // M tiles (table entries)
-  int nt;                    // N blocks: F / 64 (MODE 0) or N / 128 (MODE 1)
+  int nt;                    // N blocks: F / 128 (MODE 0) or N / 256 (MODE 1)
   const int32_t* sorted_tok;
   const float* sorted_w;
   const int32_t* tiles;      // [mt, 3]: expert, first row, end row (expert -1: unused)

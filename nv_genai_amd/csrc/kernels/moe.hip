@@ -11,22 +11,20 @@
 //                rows and scales by the routing weight
 //   moe_combine  sums each token's top-k rows (fp32) into [T, H]
 //
-// GEMM tile: 256 threads = 4 waves as 2 (weight rows) x 2 (token rows); a block computes
-// 128 weight rows x BM token rows, K in steps of 64 staged through XOR-swizzled LDS (the
-// ds_read_b128 operand reads of a 16-row MFMA fragment hit 16 distinct 16-B bank slots), the
-// next K tile held in registers while the current one is multiplied (issue-early /
-// write-late). Weight rows are the MFMA A operand and token rows the B operand, so each lane
+// GEMM: see the block comment above moe_gemm_kernel. Weight rows are the MFMA A operand and
+// token rows the B operand, so each lane
 // ends with 4 consecutive output features of one token: 8-byte stores, and in MODE 0 the
 // gate and up values of the same feature in the same lane — the tile's weight rows are
 // ordered [gate f..f+15 | up f..f+15] per 32-row group, read straight from the standard
 // [gate rows | up rows] layout by index (no repacked copy of the weights).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
 namespace nga {
 
 namespace {
-constexpr int BN = 128;  // weight rows per block tile
 constexpr int BK = 64;   // K per stage (one 128-B row of bf16)
 constexpr int MAX_E = 64;
 
@@ -127,21 +125,60 @@ __global__ void __launch_bounds__(1024) moe_align_kernel(
 }
 
 // ------------------------------------------------------------------ grouped GEMM
-template <int BM, int MODE>
+// Block tile: BN = 256 weight rows x BM token rows (BM = 128 prefill / 64 decode), K in steps
+// of 64; 4 waves as 2 (weight rows) x 2 (token rows), each wave 128 x BM/2 (8 x BM/32 MFMA
+// tiles: 43 FLOP per LDS byte read at BM = 128, against 32 for a 64 x 64 wave tile). Both
+// operands are staged with LDS-DMA (global_load_lds, 16 B per lane) into two stage buffers of
+// one __shared__ array: a wave's DMA instruction fills 1 KiB of LDS lane-linearly, so the XOR
+// swizzle that keeps the ds_read_b128 fragment reads conflict-free is applied to each lane's
+// global SOURCE chunk instead of the LDS address. NSTAGE stage buffers (3 at BM = 128:
+// 144 KiB of the CU's 160; the DMA gets two K steps of MFMA time to land, one wave per SIMD
+// hides nothing else). One barrier per K step: a counted vmcnt retires this stage's DMA while
+// the next stage's stays in flight, a raw s_barrier (no __syncthreads: its fence would drain
+// every DMA in flight) makes every wave's DMA visible and guarantees every wave is done with
+// the buffer the DMA of stage k + NSTAGE - 1 then refills, and the stage is multiplied.
+namespace {
+constexpr int GEMM_BN = 256;
+
+typedef __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+// 16 B per lane global -> LDS (the wave's 64 lanes fill lds_wave_base + lane * 16)
+__device__ __forceinline__ void glds16(const uint16_t* src, uint16_t* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gptr_t)(src), (lptr_t)(lds_wave_base), 16, 0, 0);
+}
+}  // namespace
+
+// s_waitcnt vmcnt(N) with a compile-time N (the asm operand must be a literal)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N == 0 || N == 10 || N == 12, "add the count");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+}
+
+// ABL (diagnostic builds, NGA_MOE_ABLATE): 1 = no DMA inside the K loop (MFMA + LDS-read
+// bound), 2 = no MFMAs (DMA + barrier bound), 3 = no DMA and no LDS fragment reads (MFMA +
+// barrier), 4 = no DMA and no barrier; results are wrong in all of them
+template <int BM, int MODE, int ABL = 0, int NSTAGE = 3>
 __global__ void __launch_bounds__(256) moe_gemm_kernel(MoeGemmParams P) {
-  constexpr int MTW = BM / 32;         // 16-row token tiles per wave (wave covers BM / 2 rows)
-  constexpr int W_PER_T = BN * 8 / 256;  // 16-B weight chunks per thread per stage (4)
-  constexpr int A_PER_T = BM * 8 / 256;  // token chunks per thread per stage (BM / 32)
-  __shared__ __attribute__((aligned(16))) uint16_t ws[BN * BK];
-  __shared__ __attribute__((aligned(16))) uint16_t as[BM * BK];
+  constexpr int BN = GEMM_BN;
+  constexpr int MTW = BM / 32;            // 16-row token tiles per wave
+  constexpr int NTW = 8;                  // 16-row weight tiles per wave (128 rows)
+  constexpr int STAGE = (BN + BM) * BK;   // uint16 elements per stage
+  constexpr int W_GL = BN * 8 / 64 / 4;   // DMA instructions per wave per stage, weights (8)
+  constexpr int X_GL = BM * 8 / 64 / 4;   // ... tokens (4 / 2)
+  constexpr int NPS = W_GL + X_GL;         // DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NSTAGE * STAGE];
 
   // XCD-aware order (workgroups are dealt round-robin over the 8 XCDs): each XCD gets a
   // contiguous range of (n block, m tile) with m fastest, so the m tiles of one expert that
   // re-read the same weight tile share an L2.
   const int nblk = P.mt * P.nt;
   const int pblk = blockIdx.x;
-  const int q8 = nblk / 8, r8 = nblk % 8, x = pblk % 8;
-  const int L = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + pblk / 8;
+  const int q8 = nblk / 8, r8 = nblk % 8, x8 = pblk % 8;
+  const int L = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + pblk / 8;
   const int mti = L % P.mt, nb = L / P.mt;
   const int e = P.tiles[3 * mti];
   if (e < 0) return;
@@ -152,79 +189,100 @@ __global__ void __launch_bounds__(256) moe_gemm_kernel(MoeGemmParams P) {
   const int col = lane & 15, h = lane >> 4;
   const uint16_t* We = P.W + (int64_t)e * P.w_rows * P.K;
 
-  // global source rows of this thread's staging chunks (fixed over K)
-  const uint16_t* wsrc[W_PER_T];
+  // per-lane DMA sources (fixed over K): instruction i of wave wv fills LDS rows
+  // [8 (wv * N + i), +8) lane-linearly; lane l lands in row + l/8, physical chunk l%8, which
+  // holds logical chunk (l%8) ^ swizzle(row)
+  const uint16_t* wsrc[W_GL];
 #pragma unroll
-  for (int i = 0; i < W_PER_T; ++i) {
-    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+  for (int i = 0; i < W_GL; ++i) {
+    const int r = (wv * W_GL + i) * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((r >> 1) & 7);
     int wrow;
-    if (MODE == 0) {
-      const int f = nb * 64 + (r >> 6) * 32 + ((r >> 5) & 1) * 16 + (r & 15);
+    if (MODE == 0) {   // [gate f..f+15 | up f..f+15] per 32-row group
+      const int f = nb * 128 + (r >> 7) * 64 + ((r >> 5) & 3) * 16 + (r & 15);
       wrow = (r & 16) ? P.F + f : f;
     } else {
       wrow = nb * BN + r;
     }
     wsrc[i] = We + (int64_t)wrow * P.K + ch * 8;
   }
-  const uint16_t* asrc[A_PER_T];
+  const uint16_t* xsrc[X_GL];
 #pragma unroll
-  for (int i = 0; i < A_PER_T; ++i) {
-    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+  for (int i = 0; i < X_GL; ++i) {
+    const int r = (wv * X_GL + i) * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((r >> 1) & 7);
     int pos = row0 + r;
     if (pos >= row1) pos = row0;   // padding rows of a partial tile: any valid row (not stored)
     const int64_t arow = MODE == 0 ? (int64_t)P.sorted_tok[pos] : (int64_t)pos;
-    asrc[i] = P.A + arow * P.lda + ch * 8;
+    xsrc[i] = P.A + arow * P.lda + ch * 8;
   }
-
-  u16x8 wreg[W_PER_T], areg[A_PER_T];
-  auto load = [&](int k0) {
+  auto issue = [&](int kt, int buf) {
+    uint16_t* base = smem + buf * STAGE;
+    const int k0 = kt * BK;   // stage index kt (callers clamp it to the last stage)
 #pragma unroll
-    for (int i = 0; i < W_PER_T; ++i) wreg[i] = load8(wsrc[i] + k0);
+    for (int i = 0; i < W_GL; ++i) glds16(wsrc[i] + k0, base + (wv * W_GL + i) * 8 * BK);
 #pragma unroll
-    for (int i = 0; i < A_PER_T; ++i) areg[i] = load8(asrc[i] + k0);
-  };
-  auto store = [&]() {
-#pragma unroll
-    for (int i = 0; i < W_PER_T; ++i) {
-      const int c = tid + 256 * i;
-      *reinterpret_cast<u16x8*>(&ws[swz(c >> 3, c & 7)]) = wreg[i];
-    }
-#pragma unroll
-    for (int i = 0; i < A_PER_T; ++i) {
-      const int c = tid + 256 * i;
-      *reinterpret_cast<u16x8*>(&as[swz(c >> 3, c & 7)]) = areg[i];
-    }
+    for (int i = 0; i < X_GL; ++i) glds16(xsrc[i] + k0, base + BN * BK + (wv * X_GL + i) * 8 * BK);
   };
 
-  f32x4 acc[4][MTW];
+  f32x4 acc[NTW][MTW];
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt)
+  for (int nt = 0; nt < NTW; ++nt)
 #pragma unroll
     for (int mt = 0; mt < MTW; ++mt) acc[nt][mt] = (f32x4)(0.f);
 
   const int nk = P.K / BK;
-  load(0);
+  bf16x8 af[2][NTW], bfr[2][MTW];
+  auto read_frags = [&](const uint16_t* ws, int s) {
+    const uint16_t* xs = ws + BN * BK;
+    const int ch = 4 * s + h;
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt)
+      bfr[s][mt] = as_bf16x8(*reinterpret_cast<const u16x8*>(&xs[swz(wm * (BM / 2) + mt * 16 + col, ch)]));
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt)
+      af[s][nt] = as_bf16x8(*reinterpret_cast<const u16x8*>(&ws[swz(wn * 128 + nt * 16 + col, ch)]));
+  };
+  auto mfmas = [&](int s) {
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < MTW; ++mt) acc[nt][mt] = mfma16(af[s][nt], bfr[s][mt], acc[nt][mt]);
+  };
+  constexpr int NR = NTW + MTW, NM = NTW * MTW;   // reads / MFMAs per k-step
+
+  // (Measured and rejected: reading k-step 0's fragments of the next stage under this stage's
+  // k-step-1 MFMAs, with the next stage's barrier moved between the two halves — 1015 ->
+  // 1205 us on the Mixtral gate|up GEMM at 1536 tokens.)
+#pragma unroll
+  for (int st = 0; st < NSTAGE - 1; ++st)
+    if (st < nk) issue(st, st);
   for (int kt = 0; kt < nk; ++kt) {
-    __syncthreads();  // the previous stage's fragment reads are done
-    store();
-    __syncthreads();
-    if (kt + 1 < nk) load((kt + 1) * BK);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int ch = 4 * s + h;
-      bf16x8 af[4], bf[MTW];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        af[nt] = as_bf16x8(*reinterpret_cast<const u16x8*>(&ws[swz(wn * 64 + nt * 16 + col, ch)]));
-#pragma unroll
-      for (int mt = 0; mt < MTW; ++mt)
-        bf[mt] = as_bf16x8(*reinterpret_cast<const u16x8*>(&as[swz(wm * (BM / 2) + mt * 16 + col, ch)]));
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int mt = 0; mt < MTW; ++mt) acc[nt][mt] = mfma16(af[nt], bf[mt], acc[nt][mt]);
+    // stage kt landed (this wave's part); the DMA of the next NSTAGE - 2 stages stays in flight
+    if (ABL == 1 || ABL >= 3 || NSTAGE == 2 || kt + 1 >= nk) wait_vmcnt<0>();
+    else wait_vmcnt<NPS>();
+    if (ABL != 4) __builtin_amdgcn_s_barrier();
+    if (ABL != 1 && ABL < 3 && kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
+    if (ABL == 2) continue;
+    const uint16_t* ws = smem + (kt % NSTAGE) * STAGE;
+    // k-step 0's fragments first; then its MFMAs with k-step 1's reads interleaved (one wave
+    // per SIMD: nothing else would hide the LDS latency). hipcc left alone sinks every read
+    // next to its first use and waits lgkmcnt(0) every 8 MFMAs.
+    if (ABL != 3 || kt == 0) {
+      read_frags(ws, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      read_frags(ws, 1);
     }
+    mfmas(0);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, NM / 4, 0);   // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, NR / 4, 0);   // DS read
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(1);
   }
+  wait_vmcnt<0>();   // no DMA may still target this CU's LDS when the workgroup ends
 
   // epilogue: acc[nt][mt][r] = out[token col][weight row 4h + r] of the 16 x 16 tile
 #pragma unroll
@@ -234,8 +292,8 @@ __global__ void __launch_bounds__(256) moe_gemm_kernel(MoeGemmParams P) {
     uint16_t* op = P.out + (int64_t)pos * P.ldo;
     if (MODE == 0) {
 #pragma unroll
-      for (int g = 0; g < 2; ++g) {
-        const int f = nb * 64 + wn * 32 + g * 16 + 4 * h;
+      for (int g = 0; g < 4; ++g) {
+        const int f = nb * 128 + wn * 64 + g * 16 + 4 * h;
         u16x4 v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -247,8 +305,8 @@ __global__ void __launch_bounds__(256) moe_gemm_kernel(MoeGemmParams P) {
     } else {
       const float sc = P.sorted_w[pos];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int n = nb * BN + wn * 64 + nt * 16 + 4 * h;
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int n = nb * BN + wn * 128 + nt * 16 + 4 * h;
         u16x4 v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = f2bf(acc[nt][mt][r] * sc);
@@ -301,8 +359,17 @@ void launch_moe_gemm(const MoeGemmParams& p, int bm, int mode, hipStream_t strea
   const int nblk = p.mt * p.nt;
   if (nblk == 0) return;
   dim3 grid(nblk);
+  static const int ablate = [] {
+    const char* e = getenv("NGA_MOE_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
   if (mode == 0) {
-    if (bm == 64) moe_gemm_kernel<64, 0><<<grid, 256, 0, stream>>>(p);
+    if (ablate == 5 && bm == 128) moe_gemm_kernel<128, 0, 0, 2><<<grid, 256, 0, stream>>>(p);   // 2-stage
+    else if (bm == 64) moe_gemm_kernel<64, 0><<<grid, 256, 0, stream>>>(p);
+    else if (ablate == 1) moe_gemm_kernel<128, 0, 1><<<grid, 256, 0, stream>>>(p);
+    else if (ablate == 2) moe_gemm_kernel<128, 0, 2><<<grid, 256, 0, stream>>>(p);
+    else if (ablate == 3) moe_gemm_kernel<128, 0, 3><<<grid, 256, 0, stream>>>(p);
+    else if (ablate == 4) moe_gemm_kernel<128, 0, 4><<<grid, 256, 0, stream>>>(p);
     else moe_gemm_kernel<128, 0><<<grid, 256, 0, stream>>>(p);
   } else {
     if (bm == 64) moe_gemm_kernel<64, 1><<<grid, 256, 0, stream>>>(p);
