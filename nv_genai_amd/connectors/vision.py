@@ -1,5 +1,7 @@
 """Vision-language client (Neva-22B "is it a graph?", DePlot chart->table,
-examples/multimodal_rag/llm/llm_client.py:37-42).
+examples/multimodal_rag/llm/llm_client.py:37-42). The framework serves such a model itself
+(models/vision.py behind ``model_server --vlm``); this client talks to it, or to any other
+OpenAI-compatible vision endpoint.
 
 Images go as ``HumanMessage`` content with an ``image_url`` base64 JPEG data URI to any
 OpenAI-compatible vision endpoint (``VLM_SERVER_URL`` / ``APP_VLM_SERVERURL``), with the Neva
@@ -49,12 +51,13 @@ class VisionClient:
         self.model = model
         self.timeout = timeout
 
-    def describe(self, image: bytes, prompt: str = "Describe this image in detail", **steer) -> str:
+    def describe(self, image: bytes, prompt: str = "Describe this image in detail",
+                 max_tokens: int = 1024, **steer) -> str:
         fmt, _, _ = image_size(image)
         b64 = base64.b64encode(image).decode()
         labels = ",".join(f"{k}:{v}" for k, v in steer.items())
         text = prompt + (f" [labels: {labels}]" if labels else "")
-        body = {"model": self.model, "max_tokens": 1024, "messages": [{"role": "user", "content": [
+        body = {"model": self.model, "max_tokens": max_tokens, "messages": [{"role": "user", "content": [
             {"type": "text", "text": text},
             {"type": "image_url", "image_url": {"url": f"data:image/{'jpeg' if fmt != 'png' else 'png'};base64,{b64}"}}]}]}
         r = requests.post(f"{self.base}/chat/completions", json=body, timeout=self.timeout)
@@ -67,7 +70,7 @@ class ImageHeuristics:
 
     model = "local-image-heuristics"
 
-    def describe(self, image: bytes, prompt: str = "", **steer) -> str:
+    def describe(self, image: bytes, prompt: str = "", max_tokens: int = 0, **steer) -> str:
         fmt, w, h = image_size(image)
         return f"An embedded {fmt} image of {w}x{h} pixels ({len(image)} bytes)."
 
