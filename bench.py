@@ -223,7 +223,10 @@ def main():
     p50 = statistics.median(lat)
     p95 = lat[min(len(lat) - 1, int(0.95 * len(lat)))]
     line = {
-        "metric": "end-to-end RAG QPS + p50 latency, Llama-3-8B + arctic-embed-l, 1M-doc index",
+        "metric": ("end-to-end RAG QPS + p50 latency, Llama-3-8B + arctic-embed-l, 1M-doc index"
+                   if (args.model, args.embed_model, args.index_size) == ("llama3-8b", "arctic-embed-l", 1_000_000)
+                   else f"end-to-end RAG QPS + p50 latency, {args.model} + {args.embed_model}, "
+                        f"{args.index_size}-doc index"),
         "value": round(qps, 4),
         "unit": "requests/s",
         "n_gpus": world,

@@ -319,7 +319,7 @@ void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p,
             c10::optional<Tensor> rep_penalty, c10::optional<Tensor> history, Tensor seeds,
             Tensor steps, Tensor out_tok, Tensor out_logprob) {
   CHECK_DEV(logits); CHECK_DT(logits, at::kFloat); CHECK_CONTIG(logits);
-  TORCH_CHECK(logits.dim() == 2 && logits.size(1) <= 131072, "sample: vocab must be <= 131072");
+  TORCH_CHECK(logits.dim() == 2 && logits.size(1) <= 262144, "sample: vocab must be <= 262144");
   const int64_t B = logits.size(0);
   CHECK_DT(temperature, at::kFloat); CHECK_DT(top_k, at::kInt); CHECK_DT(top_p, at::kFloat);
   CHECK_DT(seeds, at::kLong); CHECK_DT(steps, at::kLong);

@@ -1,4 +1,4 @@
-// Token sampling over a full 128K vocabulary row (K7 in SURVEY.md §2.C), one 1024-thread
+// Token sampling over a full vocabulary row (up to 256K: Gemma) (K7 in SURVEY.md §2.C), one 1024-thread
 // workgroup per sequence, no sort:
 //   * repetition penalty (TRT-LLM semantics: divide positive / multiply negative logits of
 //     every token seen in prompt+output) through an LDS bitmap of the row's history;
@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(NT) sample_kernel(
     const float* __restrict__ rep_penalty, const int32_t* __restrict__ history, int hist_len,
     const int64_t* __restrict__ seeds, const int64_t* __restrict__ steps,
     int32_t* __restrict__ out_tok, float* __restrict__ out_logprob) {
-  __shared__ uint32_t bitmap[4096];  // history bitmap, V <= 131072
+  __shared__ uint32_t bitmap[8192];  // history bitmap, V <= 262144 (Gemma: 256000)
   __shared__ uint32_t hcnt[NBINS];
   __shared__ float hmass[NBINS];
   __shared__ uint32_t scan_u[NT];
@@ -135,7 +135,7 @@ __global__ void __launch_bounds__(NT) sample_kernel(
   const float pen = rep_penalty ? rep_penalty[row] : 1.f;
 
   if (pen != 1.f && history != nullptr) {
-    for (int i = t; i < 4096; i += NT) bitmap[i] = 0;
+    for (int i = t; i < 8192; i += NT) bitmap[i] = 0;
     __syncthreads();
     const int32_t* hs = history + (int64_t)row * hist_len;
     for (int i = t; i < hist_len; i += NT) {

@@ -248,3 +248,28 @@ def test_decoder_ranker_gpu_matches_cpu(gpu):
     g = torch.tensor(EmbeddingEngine("mistral-rerank-small", device="cuda", encoder=gpu_r).rerank(q, ps))
     c = torch.tensor(EmbeddingEngine("mistral-rerank-small", device="cpu", encoder=cpu_r).rerank(q, ps))
     assert torch.allclose(g, c, atol=0.03 * c.abs().max().item() + 1e-3), (g, c)
+
+
+def test_sample_gemma_vocab_with_penalty(gpu):
+    """256000-token rows (Gemma): penalty bitmap covers ids past 131072, sampling and greedy
+    agree with the reference sampler."""
+    B, V = 3, 256000
+    torch.manual_seed(4)
+    logits = torch.randn(B, V, device=gpu)
+    logits[:, 200001] = 9.0
+    logits[:, 150000] = 8.0
+    hist = torch.tensor([[200001, -1], [5, 5], [150000, 200001]], dtype=torch.int32, device=gpu)
+    pen = torch.tensor([2.0, 2.0, 3.0], device=gpu)
+    zero_t = torch.zeros(B, device=gpu)
+    tok, _ = ops.sample(logits.clone(), zero_t, torch.zeros(B, dtype=torch.int32, device=gpu), torch.ones(B, device=gpu),
+                        torch.zeros(B, dtype=torch.int64, device=gpu), torch.zeros(B, dtype=torch.int64, device=gpu),
+                        pen, hist)
+    assert tok.tolist()[:2] == [150000, 200001]
+    temp = torch.full((B,), 0.7, device=gpu)
+    topk = torch.tensor([50, 0, 10], dtype=torch.int32, device=gpu)
+    topp = torch.tensor([0.9, 0.7, 1.0], device=gpu)
+    seeds = torch.arange(B, dtype=torch.int64, device=gpu)
+    steps = torch.ones(B, dtype=torch.int64, device=gpu)
+    t1, lp = ops.sample(logits.clone(), temp, topk, topp, seeds, steps)
+    t2, _ = ref.sample(logits.cpu(), temp.cpu(), topk.cpu(), topp.cpu(), seeds.cpu(), steps.cpu())
+    assert torch.isfinite(lp).all() and (t1.cpu() == t2).all()
