@@ -82,7 +82,8 @@ def main():
         if args.only == "search":
             print(json.dumps(out))
             return
-    for name, lens in (("prefill_1x1196", [1196]), ("prefill_27x1200", [1200] * 27)):
+    for name, lens in (("prefill_1x1196", [1196]), ("prefill_6x1200", [1200] * 6),
+                       ("prefill_27x1200", [1200] * 27), ("prefill_4x4096", [4096] * 4)):
         if args.only and args.only != "prefill":
             break
         kc, vc, bt = paged_setup(lens)

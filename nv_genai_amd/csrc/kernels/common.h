@@ -48,6 +48,15 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// LDS-DMA: 16 B per lane global -> LDS; the wave's 64 lanes fill lds_wave_base + lane * 16
+// (the LDS address is wave-uniform, it goes through M0). Completion is tracked by vmcnt, not
+// lgkmcnt; other waves see the bytes after the issuing wave's vmcnt wait + a barrier.
+typedef __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+__device__ __forceinline__ void glds16(const uint16_t* src, uint16_t* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gptr_t)(src), (lptr_t)(lds_wave_base), 16, 0, 0);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

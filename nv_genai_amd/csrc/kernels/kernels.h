@@ -62,6 +62,9 @@ struct PrefillParams {
 };
 void launch_prefill_attention(const PrefillParams& p, int num_seqs, int max_q_len, int D,
                               bool paged, bool causal, hipStream_t stream);
+// 32x32-MFMA prefill (paged, head_dim 128); returns false when the shape is not covered
+bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q_len, int D,
+                                 bool paged, bool causal, hipStream_t stream);
 
 // sampling.hip
 void launch_sample(float* logits, int B, int V, const float* temperature, const int32_t* top_k,

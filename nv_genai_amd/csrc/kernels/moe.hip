@@ -139,14 +139,6 @@ __global__ void __launch_bounds__(1024) moe_align_kernel(
 // the buffer the DMA of stage k + NSTAGE - 1 then refills, and the stage is multiplied.
 namespace {
 constexpr int GEMM_BN = 256;
-
-typedef __attribute__((address_space(1))) void* gptr_t;
-typedef __attribute__((address_space(3))) void* lptr_t;
-
-// 16 B per lane global -> LDS (the wave's 64 lanes fill lds_wave_base + lane * 16)
-__device__ __forceinline__ void glds16(const uint16_t* src, uint16_t* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((gptr_t)(src), (lptr_t)(lds_wave_base), 16, 0, 0);
-}
 }  // namespace
 
 // s_waitcnt vmcnt(N) with a compile-time N (the asm operand must be a literal)

@@ -137,6 +137,38 @@ def test_prefill_attention_paged(gpu):
     _close(out, o_ref, 0.02)
 
 
+@pytest.mark.parametrize("Hkv,G,window,causal", [
+    (8, 4, 0, True),      # Llama-3-8B: 4 query heads of a GQA group per workgroup
+    (2, 8, 0, True),      # Llama-70B-style G = 8: two head groups per KV head
+    (4, 1, 0, True),      # MHA: 4 x 32-row blocks of one head per workgroup
+    (2, 2, 0, True),      # 2 heads x 2 row blocks
+    (1, 3, 0, True),      # odd G: row blocks
+    (2, 4, 200, True),    # sliding window (Mistral)
+    (2, 4, 0, False),     # bidirectional over the paged cache
+])
+def test_prefill_attention_v2_layouts(gpu, Hkv, G, window, causal):
+    """The 32x32-MFMA paged prefill kernel (attention_prefill_v2.hip) in each of its
+    wave-to-(head, row block) layouts, against the fp32 reference: ragged query lengths
+    (not multiples of 32), chunked prefill after a cached prefix, single-token rows."""
+    D = 128
+    Hq = Hkv * G
+    ctxs = [100, 700, 64, 1, 1500, 33]
+    qls = [100, 300, 64, 1, 1500, 1]
+    kc, vc, bt = _paged_setup(ctxs, Hkv, D, gpu, seed=11)
+    cu = [0]
+    for ql in qls:
+        cu.append(cu[-1] + ql)
+    q = _bf(cu[-1], Hq * D, dev=gpu)
+    cu_t = torch.tensor(cu, dtype=torch.int32, device=gpu)
+    ctx_t = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
+    scale = 1 / math.sqrt(D)
+    out = ops.prefill_attention_paged(q, kc, vc, bt, cu_t, ctx_t, Hq, Hkv, D, max(qls), scale,
+                                      causal=causal, window=window)
+    o_ref = ref.prefill_attention_paged(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cu_t.cpu(), ctx_t.cpu(),
+                                        Hq, Hkv, D, scale, causal, window)
+    _close(out, o_ref, 0.02)
+
+
 @pytest.mark.parametrize("D,H,causal", [(64, 16, False), (128, 8, True), (32, 12, False)])
 def test_varlen_attention(gpu, D, H, causal):
     torch.manual_seed(4)
