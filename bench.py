@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    ap.add_argument("--step-timing", action="store_true",
+                    help="GPU events around every engine step: in-step time vs idle between steps")
     ap.add_argument("--mode", choices=("closed", "wave"), default="closed")
     ap.add_argument("--fp8", action="store_true",
                     help="W8A8 FP8 projections (not the headline: that is measured in bf16)")
@@ -71,6 +73,36 @@ def parse():
     ap.add_argument("--retrieval-delay-ms", type=float, default=50.0,
                     help="max time a query waits for its retrieval batch to fill (Triton max_queue_delay)")
     return ap.parse_args()
+
+
+def host_step_summary(llm) -> dict:
+    """Median / p90 / max (ms) of each host segment of the timed pipelined steps, and the
+    same for the steps whose wait for the previous step was < 1 ms (the GPU had already
+    finished it: a pipeline bubble unless the step was already queued)."""
+    st = list(llm._host_steps)
+    if not st:
+        return {}
+    names = ("outside", "pre_sched", "sched", "launch", "between", "wait", "finalize")
+    seg = []
+    prev_exit = None
+    for e in st:
+        enter, sch, h0, h1, h2, h3, ex = e
+        seg.append((enter - prev_exit if prev_exit is not None else 0.0, sch - enter, h0 - sch,
+                    h1 - h0, h2 - h1, h3 - h2, ex - h3))
+        prev_exit = ex
+
+    def stats(rows):
+        out = {}
+        for i, n in enumerate(names):
+            v = sorted(r[i] for r in rows)
+            if v:
+                out[n] = [round(1e3 * v[len(v) // 2], 2), round(1e3 * v[int(0.9 * (len(v) - 1))], 2),
+                          round(1e3 * v[-1], 2)]
+        return out
+
+    short = [r for r in seg if r[5] < 1e-3]
+    return {"steps": len(seg), "all": stats(seg), "short_wait_steps": len(short),
+            "short_wait": stats(short)}
 
 
 def main():
@@ -194,6 +226,9 @@ def main():
         prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA])
         prof.__enter__()
     llm.stats.update({k: 0 if isinstance(v, int) else 0.0 for k, v in llm.stats.items()})
+    llm._host_steps.clear()
+    llm._step_events.clear()
+    llm.step_timing = args.step_timing
     for v in hostprof.values():
         v.clear()
     t0 = time.perf_counter()
@@ -266,6 +301,8 @@ def main():
                              sum(1 for x in v if x > 4e-3)] for k, v in hostprof.items()},
         "host_s": {k[5:-2]: round(llm.stats[k], 3) for k in ("host_sched_s", "host_launch_s", "host_between_s",
                                                              "host_wait_s", "host_finalize_s")},
+        "host_step_ms": host_step_summary(llm),
+        **({"gpu_step_timing": llm.gpu_step_timing()} if args.step_timing and gpu else {}),
         "setup_s": round(setup_s, 1),
         "prefix_cache_hit_blocks": int(llm.sched.prefix_hits()),
         "distinct_docs_retrieved": len({d for r in results for d in r.doc_ids}),

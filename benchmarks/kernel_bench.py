@@ -91,9 +91,12 @@ def main():
         q = torch.randn(T, Hq * D, device=dev, dtype=torch.bfloat16)
         cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0).tolist()), dtype=torch.int32, device=dev)
         ctx = torch.tensor(lens, dtype=torch.int32, device=dev)
-        us = timeit(lambda: ops.prefill_attention_paged(q, kc, vc, bt, cu, ctx, Hq, Hkv, D, max(lens), D ** -0.5))
         flops = sum(2 * 2 * l * (l + 1) / 2 * D * Hq for l in lens)
-        out[name] = {"us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1)}
+        out[name] = {}
+        for impl, tag in ((0, "auto"), (1, "mfma16"), (2, "mfma32")):
+            us = timeit(lambda: ops.prefill_attention_paged(q, kc, vc, bt, cu, ctx, Hq, Hkv, D, max(lens),
+                                                            D ** -0.5, impl=impl))
+            out[name][tag] = {"us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1)}
     B, L = 256, 1400
     if args.only == "prefill":
         print(json.dumps(out))

@@ -268,8 +268,10 @@ void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optio
                        c10::optional<Tensor> kc, c10::optional<Tensor> vc,
                        c10::optional<Tensor> block_tables, Tensor cu_q,
                        c10::optional<Tensor> ctx_lens, int64_t Hq, int64_t Hkv, int64_t D,
-                       int64_t max_q_len, double scale, bool causal, int64_t window) {
+                       int64_t max_q_len, double scale, bool causal, int64_t window,
+                       int64_t impl) {
   CHECK_BF16(out); CHECK_BF16(q);
+  TORCH_CHECK(impl >= 0 && impl <= 2, "prefill_attention: impl is 0 (auto), 1 or 2");
   CHECK_DEV(cu_q); CHECK_DT(cu_q, at::kInt); CHECK_CONTIG(cu_q);
   TORCH_CHECK(D == 64 || D == 128 || (D == 32 && !kc.has_value()) || (D == 256 && kc.has_value()),
               "prefill_attention: head_dim must be 64 or 128 (32: packed only, 256: paged only)");
@@ -311,6 +313,7 @@ void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optio
     p.v = bfp(*v);
     p.kv_stride = k->stride(0);
   }
+  p.impl = (int)impl;
   nga::launch_prefill_attention(p, (int)B, (int)max_q_len, (int)D, paged, causal, cur_stream(q));
 }
 

@@ -295,8 +295,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
 void launch_prefill_attention(const PrefillParams& p, int num_seqs, int max_q_len, int D,
                               bool paged, bool causal, hipStream_t stream) {
   if (num_seqs == 0 || max_q_len == 0) return;
-  // paged head_dim-128 prefill (the serving hot path) runs the 32x32-MFMA kernel
-  // (attention_prefill_v2.hip; NGA_PREFILL_V1=1 keeps it on this one for A/B runs)
+  // large paged head_dim-128 prefills run the 32x32-MFMA kernel (attention_prefill_v2.hip)
   if (launch_prefill_attention_v2(p, num_seqs, max_q_len, D, paged, causal, stream)) return;
   // 64-row query tiles. The 128-row variant (two column groups per wave) halves the LDS
   // fragment traffic per MFMA but needs ~300 VGPR+AGPR, i.e. one wave per SIMD, and measured

@@ -54,19 +54,21 @@ __device__ __forceinline__ int vswz(int row) { return (row >> 1) & 7; }
 }  // namespace
 
 // ABL (diagnostic, NGA_PV2_ABLATE; results are wrong): 1 = no DMA inside the loop, 2 = no
-// compute, 3 = no softmax (P = S), 4 = no DMA and no barrier inside the loop
+// compute, 4 = no DMA and no barrier inside the loop
 template <bool CAUSAL, int HPW, int ABL = 0>
 __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P) {
   constexpr int D = 128, KT = 64;
   constexpr int TILE = KT * D;          // elements of one K (or V^T) tile: 16 KiB
   constexpr int RB = 4 / HPW;           // 32-row query blocks per workgroup
   constexpr int RW = 32 * RB;           // query rows per workgroup
-  // ONE LDS object: [buffer 0: K | V^T][buffer 1: K | V^T][block ids of the sequence].
+  // ONE LDS object: [K buffer 0 | K buffer 1 | V^T buffer 0 | V^T buffer 1 | block ids].
   // (With several LDS variables the compiler gives their accesses alias scopes and then waits
   // vmcnt(0) before fragment reads of a buffer whose earlier DMA it cannot see retired —
   // serialising the prefetch; a VMEM block-table load inside the loop did the same.)
   __shared__ __attribute__((aligned(16))) uint16_t smem[4 * TILE + 2 * V2_MAX_TILES];
   int32_t* sbt = reinterpret_cast<int32_t*>(smem + 4 * TILE);
+  uint16_t* const kbuf = smem;
+  uint16_t* const vbuf = smem + 2 * TILE;
 
   // XCD-aware order (as the 16x16 kernel): each XCD gets a contiguous range of
   // (sequence, kv head, head group, query block), longest causal blocks first.
@@ -89,15 +91,13 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
   const int rb = w / HPW;
   const int r32 = lane & 31, h = lane >> 5;
 
-  // this lane's query row (a column of the S^T / O^T tiles)
-  const int row_first = qb * RW + rb * 32;       // wave-uniform
-  const bool wave_active = row_first < qlen;
-  int qr = row_first + r32;
+  // this lane's query row (a column of the S^T / O^T tiles). Every wave walks the
+  // workgroup's whole tile range (uniform control flow for the software pipeline below); with
+  // several row blocks per workgroup the earlier blocks' extra tiles are fully masked.
+  int qr = qb * RW + rb * 32 + r32;
   const bool row_ok = qr < qlen;
   if (!row_ok) qr = qlen - 1;
   const int qpos = ctx - qlen + qr;
-  const int qmin_w = ctx - qlen + row_first;                       // wave's first query position
-  const int qmax_w = ctx - qlen + min(qlen - 1, row_first + 31);   // and its last
   const int W = CAUSAL ? P.window : 0;
 
   bf16x8 qf[8];
@@ -107,41 +107,58 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
     for (int s = 0; s < 8; ++s) qf[s] = as_bf16x8(load8(qp + 16 * s));
   }
 
-  // tile range of the workgroup
-  const int last_key = CAUSAL ? ctx - qlen + min(qlen - 1, qb * RW + RW - 1) : ctx - 1;
+  // tile range of the workgroup; tiles needing a mask: at / past the first query's diagonal,
+  // and (window) before the last query's window start
+  const int wq_lo = ctx - qlen + qb * RW;
+  const int wq_hi = ctx - qlen + min(qlen - 1, qb * RW + RW - 1);
+  const int last_key = CAUSAL ? wq_hi : ctx - 1;
   const int n_tiles = last_key / KT + 1;
-  const int t_first = W > 0 ? max(0, ctx - qlen + qb * RW - W + 1) / KT : 0;
+  const int t_first = W > 0 ? max(0, wq_lo - W + 1) / KT : 0;
+  const int nt = n_tiles - t_first;
 
   // per-lane DMA source offsets (fixed over tiles): wave instruction i fills LDS chunk
   // positions [64 (4w + i), +64) of the K tile (16 chunks per row) and of the V^T tile
   // (8 per row); position p holds logical chunk (p % n) ^ swizzle(row)
-  int koff[4], voff[4];
+  // (byte offsets from a wave-uniform page base: the saddr + 32-bit voffset form, one VGPR
+  // per DMA instead of a 64-bit lane address)
+  uint32_t koff[4], voff[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int p = (4 * w + i) * 64 + lane;
     const int kr = p >> 4, vr = p >> 3;
-    koff[i] = kr * D + (((p & 15) ^ kswz(kr)) << 3);
-    voff[i] = vr * KT + (((p & 7) ^ vswz(vr)) << 3);
+    koff[i] = 2u * (kr * D + (((p & 15) ^ kswz(kr)) << 3));
+    voff[i] = 2u * (vr * KT + (((p & 7) ^ vswz(vr)) << 3));
   }
   {
     const int32_t* btab = P.block_tables + (int64_t)b * P.max_blocks;
     for (int i = t_first + tid; i < n_tiles; i += 256) sbt[i] = btab[i];
     __syncthreads();
   }
-  auto issue = [&](int t, uint16_t* ks) {
-    const int64_t blk = sbt[t];
-    const uint16_t* kp = P.kc + (blk * P.Hkv + kvh) * (int64_t)TILE;
-    const uint16_t* vp = P.vc + (blk * P.Hkv + kvh) * (int64_t)TILE;
+  auto page = [&](int t) { return ((int64_t)sbt[t] * P.Hkv + kvh) * (int64_t)TILE; };
+  auto issue_k = [&](int t, uint16_t* dst) {
+    const char* src = reinterpret_cast<const char*>(P.kc + page(t));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(kp + koff[i], ks + (4 * w + i) * 512);
+    for (int i = 0; i < 4; ++i)
+      glds16(reinterpret_cast<const uint16_t*>(src + koff[i]), dst + (4 * w + i) * 512);
+  };
+  auto issue_v = [&](int t, uint16_t* dst) {
+    const char* src = reinterpret_cast<const char*>(P.vc + page(t));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(vp + voff[i], ks + TILE + (4 * w + i) * 512);
+    for (int i = 0; i < 4; ++i)
+      glds16(reinterpret_cast<const uint16_t*>(src + voff[i]), dst + (4 * w + i) * 512);
+  };
+  auto sync_tiles = [&]() {
+    // this wave's DMA has landed; the barrier makes every wave's visible and guarantees every
+    // wave is done reading the buffers the next DMA refills. (Raw s_barrier: __syncthreads'
+    // fence would also wait for the DMA issued after it.)
+    if constexpr (ABL != 1 && ABL != 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (ABL != 4) __builtin_amdgcn_s_barrier();
   };
 
   // fragment read addresses (elements, within a buffer)
   const int prow = (r32 & ~12) | ((r32 & 4) << 1) | ((r32 & 8) >> 1);   // perm(r32)
-  const int ksw = kswz(prow);                                           // same for prow + 32
-  const int vsw = vswz(r32);                                            // same for r32 + 32 dt
+  const int koffr = prow * D, ksw = kswz(prow);      // same swizzle for prow + 32
+  const int voffr = r32 * KT, vsw = vswz(r32);       // same swizzle for r32 + 32 dt
 
   const float sl2 = P.scale * V2_LOG2E;
   float m = -INFINITY, l = 0.f;
@@ -149,99 +166,142 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x16)(0.f);
 
-  auto compute = [&](int t, const uint16_t* ks) {
-    const uint16_t* vs = ks + TILE;
-    f32x16 sacc[2];
+  // The loop works in 32-key halves of the 64-key DMA tiles. Half h2 of tile t:
+  //   S^T = K . Q^T  (8 MFMAs; K rows 32 h2 + perm(r) of the K tile)
+  //   softmax        (16 scores per lane; keys (j & 7) + 8h + 16 (j >> 3) of the half)
+  //   O^T += V^T . P^T (4 d-tiles x 2 key-steps; V^T chunks 4 h2 + 2 s + h)
+  auto qk = [&](f32x16& S, const uint16_t* ks, int h2) {
+    S = (f32x16)(0.f);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      sacc[kk] = (f32x16)(0.f);
-      const uint16_t* kr = ks + (32 * kk + prow) * D;
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const bf16x8 a = as_bf16x8(*reinterpret_cast<const u16x8*>(kr + (((2 * s + h) ^ ksw) << 3)));
-        sacc[kk] = mfma32(a, qf[s], sacc[kk]);
-      }
+    for (int s = 0; s < 8; ++s) {
+      const bf16x8 a = as_bf16x8(*reinterpret_cast<const u16x8*>(
+          ks + 32 * h2 * D + koffr + (((2 * s + h) ^ ksw) << 3)));
+      S = mfma32(a, qf[s], S);
     }
-    const int kbase = t * KT;
-    const bool need_mask = CAUSAL ? (kbase + KT - 1 > qmin_w || (W > 0 && kbase <= qmax_w - W))
-                                  : (kbase + KT > ctx);
-    if (need_mask) {   // raw scores; the scale is folded into the exp
+  };
+  auto mask = [&](f32x16& S, int t, int h2) {
+    const int kbase = t * KT + 32 * h2;
+    const bool need = CAUSAL ? (kbase + 31 > wq_lo || (W > 0 && kbase <= wq_hi - W))
+                             : (kbase + 32 > ctx);
+    if (need) {   // raw scores; the scale is folded into the exp
       const int k0 = kbase + 8 * h;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int key = k0 + 32 * kk + 16 * (j >> 3) + (j & 7);
-          const bool ok = CAUSAL ? (key <= qpos && (W == 0 || key > qpos - W)) : (key < ctx);
-          sacc[kk][j] = ok ? sacc[kk][j] : -INFINITY;
-        }
+      for (int j = 0; j < 16; ++j) {
+        const int key = k0 + 16 * (j >> 3) + (j & 7);
+        const bool ok = CAUSAL ? (key <= qpos && (W == 0 || key > qpos - W)) : (key < ctx);
+        S[j] = ok ? S[j] : -INFINITY;
+      }
     }
-    bf16x8 pf[4];
-    if constexpr (ABL == 3) {
+  };
+  // Softmax of one half, all VALU except the rare O rescale, which it returns as a factor:
+  // lazy rescale — m only moves (and O / l are only rescaled) when a row's max over the half
+  // exceeds it by more than 2^8; P <= 2^8 is harmless in fp32 sums and bf16 P.
+  auto softmax = [&](const f32x16& S, bf16x8 (&pf)[2], float& alpha) -> bool {
+    float mloc = S[0];
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) pf[2 * kk + (j >> 3)][j & 7] = (__bf16)sacc[kk][j];
-    } else {
-    float mloc = -INFINITY;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = 0; j < 16; ++j) mloc = fmaxf(mloc, sacc[kk][j]);
+    for (int j = 1; j < 16; ++j) mloc = fmaxf(mloc, S[j]);
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
     mloc *= sl2;
     const bool grow = mloc > m + V2_RESCALE_LOG2;
-    if (__ballot(grow)) {
-      const float m_new = grow ? mloc : m;
-      const float alpha = grow ? __builtin_amdgcn_exp2f(m - m_new) : 1.f;
-      m = m_new;
-      l *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
-    }
+    const float m_new = grow ? mloc : m;
+    // non-growing lanes keep their scale (and a still -inf m must not meet -inf - -inf)
+    alpha = grow ? __builtin_amdgcn_exp2f(m - m_new) : 1.f;
+    m = m_new;
+    // a half can be fully masked for a row (window, or a row block before the diagonal):
+    // m may still be -inf then and the offset must not become +inf
     const float mo = m == -INFINITY ? 0.f : -m;
     float ls0 = 0.f, ls1 = 0.f;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = 0; j < 16; j += 2) {
-        const float e0 = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kk][j], sl2, mo));
-        const float e1 = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kk][j + 1], sl2, mo));
-        ls0 += e0;
-        ls1 += e1;
-        pf[2 * kk + (j >> 3)][j & 7] = (__bf16)e0;
-        pf[2 * kk + (j >> 3)][(j & 7) + 1] = (__bf16)e1;
-      }
-    l += ls0 + ls1;
+    for (int j = 0; j < 16; j += 2) {
+      const float e0 = __builtin_amdgcn_exp2f(__builtin_fmaf(S[j], sl2, mo));
+      const float e1 = __builtin_amdgcn_exp2f(__builtin_fmaf(S[j + 1], sl2, mo));
+      ls0 += e0;
+      ls1 += e1;
+      pf[j >> 3][j & 7] = (__bf16)e0;
+      pf[j >> 3][(j & 7) + 1] = (__bf16)e1;
     }
+    l = l * alpha + (ls0 + ls1);
+    return grow;
+  };
+  auto rescale = [&](bool grow, float alpha) {
+    if (__ballot(grow)) {
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const uint16_t* vr = vs + (32 * dt + r32) * KT;
+      for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+    }
+  };
+  auto pv = [&](const bf16x8 (&pf)[2], const uint16_t* vs, int h2) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 a = as_bf16x8(*reinterpret_cast<const u16x8*>(vr + (((2 * s + h) ^ vsw) << 3)));
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 a = as_bf16x8(*reinterpret_cast<const u16x8*>(
+            vs + 32 * dt * KT + voffr + (((4 * h2 + 2 * s + h) ^ vsw) << 3)));
         o[dt] = mfma32(a, pf[s], o[dt]);
       }
+  };
+  // one pipeline stage: softmax + P.V of the previous half (S, V^T buffer vs, half vh2); the
+  // softmax VALU is interleaved with the next half's S^T MFMAs (Sn, K buffer ks, half kh2)
+  auto stage = [&](const f32x16& S, const uint16_t* vs, int vh2, f32x16& Sn, const uint16_t* ks,
+                   int kh2, int t_next) {
+    bf16x8 pf[2];
+    float alpha;
+    qk(Sn, ks, kh2);
+    const bool grow = softmax(S, pf, alpha);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);     // DS read
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);  // VALU
     }
+    // keep P in this block: otherwise the exps sink past the rescale branch to their P.V use,
+    // out of the region the MFMAs above cover
+    asm volatile("" ::"v"(pf[0]), "v"(pf[1]), "v"(l));
+    rescale(grow, alpha);
+    pv(pf, vs, vh2);
+    mask(Sn, t_next, kh2);
   };
 
-  auto step = [&](int t, const uint16_t* cur, uint16_t* nxt) {
-    // this wave's DMA of tile t has landed; the barrier makes every wave's visible and
-    // guarantees every wave is done reading the buffer the next DMA refills. (Raw s_barrier:
-    // __syncthreads' fence would also wait for the DMA issued below.)
-    if constexpr (ABL != 1 && ABL != 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (ABL != 4) __builtin_amdgcn_s_barrier();
-    if (ABL != 1 && ABL != 4 && t + 1 < n_tiles) issue(t + 1, nxt);
-    if constexpr (ABL == 2) return;
-    const int kbase = t * KT;
-    const bool wave_needs = wave_active && (!CAUSAL || kbase <= qmax_w) &&
-                            (W == 0 || kbase + KT - 1 > qmin_w - W);
-    if (wave_needs) compute(t, cur);
+  // Software pipeline over tiles i = 0 .. nt-1 (t = t_first + i), in 32-key halves: each
+  // stage runs the softmax + P.V of one half while the next half's S^T MFMAs overlap the
+  // softmax VALU in the same wave (otherwise QK -> softmax -> PV is one serial chain per
+  // wave). Iteration i: [stage A: PV(i-1, 1) || QK(i, 0)] [stage B: PV(i, 0) || QK(i, 1)].
+  // It reads K(i), V(i-1), V(i); the DMA of K(i+1) goes out at its top (into the buffer of
+  // K(i-1)) and that of V(i+1) after a mid-iteration barrier (into the buffer of V(i-1),
+  // whose last reader was stage A).
+  f32x16 Sa, Sb;
+  auto iter = [&](int i, int par, bool first) {
+    const int t = t_first + i;
+    const uint16_t* kc_ = kbuf + par * TILE;
+    sync_tiles();   // K(i), V(i) landed; every wave is done with iteration i-1
+    if constexpr (ABL != 1 && ABL != 4)
+      if (i + 1 < nt) issue_k(t + 1, kbuf + (par ^ 1) * TILE);
+    if constexpr (ABL != 2) {
+      if (first) {
+        qk(Sa, kc_, 0);
+        mask(Sa, t, 0);
+      } else {
+        stage(Sb, vbuf + (par ^ 1) * TILE, 1, Sa, kc_, 0, t);
+      }
+    }
+    if constexpr (ABL != 4) __builtin_amdgcn_s_barrier();   // V(i-1) is free
+    if constexpr (ABL != 1 && ABL != 4)
+      if (i + 1 < nt) issue_v(t + 1, vbuf + (par ^ 1) * TILE);
+    if constexpr (ABL != 2) stage(Sa, vbuf + par * TILE, 0, Sb, kc_, 1, t);
   };
-  issue(t_first, smem);
-  for (int t = t_first; t < n_tiles; ++t) {
-    const int bb = (t - t_first) & 1;
-    step(t, smem + bb * 2 * TILE, smem + (bb ^ 1) * 2 * TILE);
+
+  issue_k(t_first, kbuf);
+  issue_v(t_first, vbuf);
+  iter(0, 0, true);
+  for (int i = 1; i < nt; i += 2) {
+    iter(i, 1, false);
+    if (i + 1 < nt) iter(i + 1, 0, false);
+  }
+  if constexpr (ABL != 2) {   // the last half: V(nt-1) landed before iteration nt-1
+    bf16x8 pf[2];
+    float alpha;
+    rescale(softmax(Sb, pf, alpha), alpha);
+    pv(pf, vbuf + ((nt - 1) & 1) * TILE, 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may outlive the workgroup
 
@@ -268,7 +328,8 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
     const char* e = getenv("NGA_PREFILL_V1");
     return e && atoi(e) != 0;
   }();
-  if (disabled || D != 128 || !paged || p.max_blocks > V2_MAX_TILES) return false;
+  if (p.impl == 1 || (p.impl == 0 && disabled) || D != 128 || !paged || p.max_blocks > V2_MAX_TILES)
+    return false;
   if (num_seqs == 0 || max_q_len == 0) return true;
   const int G = p.Hq / p.Hkv;
   const int hpw = G % 4 == 0 ? 4 : G % 2 == 0 ? 2 : 1;
@@ -276,6 +337,13 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
   PrefillParams pp = p;
   pp.ntiles = (max_q_len + rw - 1) / rw;
   const int64_t total = (int64_t)pp.ntiles * (p.Hq / hpw) * num_seqs;
+  // Size rule: this kernel needs about two of its workgroups per CU (two waves per SIMD) to
+  // overlap one wave's softmax with the other's MFMAs. A single ~1K-token prompt is ~300
+  // workgroups of 128 (row, head) pairs — one wave per SIMD, measured no faster than the
+  // 16x16 kernel's ~500 half-size workgroups standalone and 1.6% slower end to end when it
+  // shares the chip with the decode attention of a mixed step (benchmarks/kernel_bench.py
+  // and scripts/gpu_r2_attn_ab.sh). From ~6 such prompts (or long ones) up it is 15-25% faster.
+  if (p.impl == 0 && total < 2 * 256 * 2) return false;
   pp.total = (int)total;
   pp.per_xcd = (int)((total + 7) / 8);
   dim3 grid(8 * pp.per_xcd);
@@ -287,7 +355,6 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
   if (abl && causal && hpw == 4) {
     if (abl == 1) prefill_attn_v2_kernel<true, 4, 1><<<grid, 256, 0, stream>>>(pp);
     else if (abl == 2) prefill_attn_v2_kernel<true, 4, 2><<<grid, 256, 0, stream>>>(pp);
-    else if (abl == 3) prefill_attn_v2_kernel<true, 4, 3><<<grid, 256, 0, stream>>>(pp);
     else prefill_attn_v2_kernel<true, 4, 4><<<grid, 256, 0, stream>>>(pp);
     return true;
   }

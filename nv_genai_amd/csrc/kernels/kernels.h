@@ -59,10 +59,11 @@ struct PrefillParams {
   int per_xcd; // workgroups per XCD slice of the 1-D grid — set by the launcher
   int total;   // ntiles * Hq * num_seqs — set by the launcher
   int window;  // > 0: sliding-window causal attention (query i sees keys (i - window, i])
+  int impl;    // 0: pick by size, 1: the 16x16 kernel, 2: the 32x32 kernel where it applies
 };
 void launch_prefill_attention(const PrefillParams& p, int num_seqs, int max_q_len, int D,
                               bool paged, bool causal, hipStream_t stream);
-// 32x32-MFMA prefill (paged, head_dim 128); returns false when the shape is not covered
+// 32x32-MFMA prefill (paged, head_dim 128); returns false when it does not take the call
 bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q_len, int D,
                                  bool paged, bool causal, hipStream_t stream);
 

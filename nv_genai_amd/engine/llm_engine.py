@@ -24,7 +24,7 @@ import random
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional, Sequence
+from typing import Callable, Deque, Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -222,6 +222,14 @@ class LLMEngine:
         self._pending: Optional[dict] = None
         self._tok_flip = 0
         self._up_ev = None  # marks the last host->device upload of the pinned step buffers
+        # host-side timestamps of recent pipelined steps: (enter, schedule start, launch start,
+        # launch end, between end, wait end, exit) — where the host spends a step (bench.py)
+        self._host_steps: Deque[tuple] = collections.deque(maxlen=4096)
+        # optional GPU-side step timing (events at each launched step's start and end):
+        # ``gpu_step_timing()`` splits the GPU timeline into in-step time and idle gaps
+        # between steps
+        self.step_timing = False
+        self._step_events: Deque[tuple] = collections.deque(maxlen=8192)
         self._timeline = collections.deque(maxlen=4096)
         self._tok_host = [(hbuf(S), hbuf(S, dtype=torch.float32)) for _ in range(2)]
         self._step_reqs: List[Request] = []
@@ -351,6 +359,7 @@ class LLMEngine:
         return done
 
     def _step(self, between) -> List[Request]:
+        t_enter = time.perf_counter()
         pend = self._pending
         done: List[Request] = []
         if pend is not None:
@@ -408,7 +417,7 @@ class LLMEngine:
             h1 = time.perf_counter()
             if between is not None:
                 between()
-            h2 = time.perf_counter()
+            h2 = h3 = time.perf_counter()
             if pend is not None:
                 if pend["ev"] is not None:
                     pend["ev"].synchronize()
@@ -419,6 +428,7 @@ class LLMEngine:
             self.stats["host_launch_s"] += h1 - h0
             self.stats["host_between_s"] += h2 - h1
             self.stats["host_sched_s"] += h0 - t_sched
+            self._host_steps.append((t_enter, t_sched, h0, h1, h2, h3, time.perf_counter()))
             self._pending = nxt
             self.stats[key] += time.perf_counter() - t0
             return done
@@ -438,6 +448,22 @@ class LLMEngine:
         if between is not None:
             between()
         return done
+
+    def gpu_step_timing(self) -> dict:
+        """From the step events (``step_timing = True``): total ms the GPU spent inside
+        steps (first upload to last token copy), total ms of gaps between consecutive steps
+        (the GPU had finished a step before the next one's first command ran), and the
+        largest gap."""
+        evs = list(self._step_events)
+        if not evs:
+            return {}
+        torch.cuda.synchronize()
+        inside = sum(a.elapsed_time(b) for a, b in evs)
+        gaps = [max(0.0, evs[i - 1][1].elapsed_time(evs[i][0])) for i in range(1, len(evs))]
+        span = evs[0][0].elapsed_time(evs[-1][1])
+        return {"steps": len(evs), "span_ms": round(span, 1), "in_step_ms": round(inside, 1),
+                "between_steps_ms": round(sum(gaps), 1), "max_gap_ms": round(max(gaps, default=0.0), 2),
+                "gaps_over_1ms": sum(1 for g in gaps if g > 1.0)}
 
     def timeline(self, last: int = 256) -> List[dict]:
         """Recent scheduler steps: wall time at launch, kind, rows, tokens, decode rows and
@@ -469,6 +495,10 @@ class LLMEngine:
         input ids the previous in-flight step is still producing from its device output.
         Tokens are copied to pinned host memory right after sampling, so the next step may
         overwrite the device buffers."""
+        t_ev = None
+        if self.gpu and self.step_timing:
+            t_ev = torch.cuda.Event(enable_timing=True)
+            t_ev.record()
         if kind == 2:
             with gpu_range(f"decode n={n}"):
                 self._decode_launch(n, src)
@@ -488,8 +518,10 @@ class LLMEngine:
         buf[1][:n].copy_(self.d_lp[:n], non_blocking=self.gpu)
         ev = None
         if self.gpu:
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(enable_timing=t_ev is not None)
             ev.record()
+            if t_ev is not None:
+                self._step_events.append((t_ev, ev))
         reqs = [self.requests.get(int(s)) for s in self._np[6][:n].tolist()]
         smp = self._np[7][:n].tolist()
         return {"reqs": reqs, "smp": smp, "rows": {int(s): i for i, s in enumerate(self._np[6][:n].tolist())},

@@ -194,7 +194,9 @@ def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, max_ctx, scale,
 
 
 def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D, max_q_len,
-                            scale, out=None, causal=True, window: int = 0):
+                            scale, out=None, causal=True, window: int = 0, impl: int = 0):
+    """Paged prefill attention. ``impl``: 0 picks the kernel by problem size, 1 forces the
+    16x16-MFMA kernel, 2 the 32x32-MFMA kernel (head_dim 128) — for tests and A/B runs."""
     if not _gpu(q):
         r = ref.prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
                                         scale, causal, window)
@@ -205,7 +207,8 @@ def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
     if out is None:
         out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
     kernels().prefill_attention(out, q, None, None, kc, vc, block_tables, cu_q, ctx_lens, Hq,
-                                Hkv, D, int(max_q_len), float(scale), bool(causal), int(window))
+                                Hkv, D, int(max_q_len), float(scale), bool(causal), int(window),
+                                int(impl))
     return out
 
 
@@ -216,7 +219,7 @@ def varlen_attention(q, k, v, cu, Hq, Hkv, D, max_len, scale, causal=False, out=
     if out is None:
         out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
     kernels().prefill_attention(out, q, k, v, None, None, None, cu, None, Hq, Hkv, D,
-                                int(max_len), float(scale), bool(causal), 0)
+                                int(max_len), float(scale), bool(causal), 0, 0)
     return out
 
 

@@ -163,9 +163,36 @@ def test_prefill_attention_v2_layouts(gpu, Hkv, G, window, causal):
     ctx_t = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
     scale = 1 / math.sqrt(D)
     out = ops.prefill_attention_paged(q, kc, vc, bt, cu_t, ctx_t, Hq, Hkv, D, max(qls), scale,
-                                      causal=causal, window=window)
+                                      causal=causal, window=window, impl=2)
     o_ref = ref.prefill_attention_paged(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cu_t.cpu(), ctx_t.cpu(),
                                         Hq, Hkv, D, scale, causal, window)
+    _close(out, o_ref, 0.02)
+
+
+@pytest.mark.parametrize("impl", [0, 1, 2])
+@pytest.mark.parametrize("ctxs,qls,window", [
+    ([1200], [940], 0),            # one prompt after a 260-token prefix hit
+    ([1200] * 6, [1200] * 6, 0),   # six prompts (the size rule picks the 32x32 kernel)
+    ([3000, 64], [2000, 64], 0),   # long + short sequence
+    ([1200], [940], 300),          # sliding window
+])
+def test_prefill_attention_kernel_choice(gpu, ctxs, qls, window, impl):
+    """Serving-size prefills through the size rule (impl 0) and through each kernel forced,
+    against the fp32 reference."""
+    Hkv, G, D = 8, 4, 128
+    Hq = Hkv * G
+    kc, vc, bt = _paged_setup(ctxs, Hkv, D, gpu, seed=13)
+    cu = [0]
+    for ql in qls:
+        cu.append(cu[-1] + ql)
+    q = _bf(cu[-1], Hq * D, dev=gpu)
+    cu_t = torch.tensor(cu, dtype=torch.int32, device=gpu)
+    ctx_t = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
+    scale = 1 / math.sqrt(D)
+    out = ops.prefill_attention_paged(q, kc, vc, bt, cu_t, ctx_t, Hq, Hkv, D, max(qls), scale,
+                                      window=window, impl=impl)
+    o_ref = ref.prefill_attention_paged(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cu_t.cpu(), ctx_t.cpu(),
+                                        Hq, Hkv, D, scale, True, window)
     _close(out, o_ref, 0.02)
 
 
