@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--mode", choices=("closed", "wave"), default="closed")
     ap.add_argument("--fp8", action="store_true",
                     help="W8A8 FP8 projections (not the headline: that is measured in bf16)")
+    ap.add_argument("--kv-fp8", action="store_true",
+                    help="FP8 e4m3fn KV cache (not the headline: that is measured in bf16)")
     ap.add_argument("--mixed-prefill-tokens", type=int, default=2048)
     ap.add_argument("--mixed-min-tokens", type=int, default=0,
                     help="accumulate this many prompt tokens before forming a mixed step")
@@ -135,7 +137,7 @@ def main():
                         graph_batch_sizes=sizes, seed=rank, kv_cache_fraction=0.3,
                         mixed_prefill_tokens=args.mixed_prefill_tokens,
                         mixed_min_tokens=args.mixed_min_tokens, mixed_max_wait=args.mixed_max_wait,
-                        fp8=args.fp8)
+                        fp8=args.fp8, kv_cache_dtype="fp8" if args.kv_fp8 else "auto")
     llm = LLMEngine(ecfg, device=dev, pctx=pctx)
     emb = EmbeddingEngine(args.embed_model, device=dev, seed=rank)
     index = FlatIndex(emb.dim, "cosine", dev, capacity=args.index_size)
@@ -273,7 +275,8 @@ def main():
         # reference-equivalent stack (HF eager + torch brute-force search) measured on the
         # same MI355X: 4.40 QPS per GPU (BASELINE.md "Measured on MI355X")
         "vs_baseline": round(qps / (REF_EQUIV_QPS_PER_GPU * world), 3),
-        "dtype": "fp8-w8a8 (bf16 attention + KV)" if args.fp8 else "bf16",
+        "dtype": ("fp8-w8a8" if args.fp8 else "bf16") + (" + fp8 KV cache" if args.kv_fp8 else
+                                                           (" (bf16 attention + KV)" if args.fp8 else "")),
         "data": "synthetic: random-init weights; 1M random unit-vector index + generated ~500-token chunks; generated questions",
         "config": {
             "model": f"{args.model} + {args.embed_model}",

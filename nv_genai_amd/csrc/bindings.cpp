@@ -27,6 +27,15 @@ hipStream_t cur_stream(const Tensor& t) {
   CHECK_DT(x, at::kBFloat16)
 
 uint16_t* bfp(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+// paged KV caches: bf16, or fp8 e4m3fn (returns true); both caches must agree
+bool kv_is_fp8(const Tensor& kc, const Tensor& vc) {
+  TORCH_CHECK(kc.scalar_type() == vc.scalar_type(), "k and v caches must have the same dtype");
+  TORCH_CHECK(kc.scalar_type() == at::kBFloat16 || kc.scalar_type() == at::kFloat8_e4m3fn,
+              "KV caches must be bfloat16 or float8_e4m3fn");
+  TORCH_CHECK(kc.is_cuda() && vc.is_cuda(), "KV caches must be on the GPU");
+  return kc.scalar_type() == at::kFloat8_e4m3fn;
+}
 const uint16_t* cbfp(const c10::optional<Tensor>& t) {
   return t.has_value() ? reinterpret_cast<const uint16_t*>(t->data_ptr()) : nullptr;
 }
@@ -108,7 +117,7 @@ void bias_gelu(Tensor x, c10::optional<Tensor> bias, int64_t mode) {
 // ------------------------------------------------------------------ rope + kv cache
 void rope_cache(Tensor qkv, Tensor pos, Tensor cos_sin, c10::optional<Tensor> slots,
                 c10::optional<Tensor> kc, c10::optional<Tensor> vc, int64_t Hq, int64_t Hkv,
-                int64_t D) {
+                int64_t D, double k_scale, double v_scale) {
   CHECK_BF16(qkv); CHECK_CONTIG(qkv);
   CHECK_DEV(pos); CHECK_DT(pos, at::kInt);
   CHECK_DEV(cos_sin); CHECK_DT(cos_sin, at::kFloat); CHECK_CONTIG(cos_sin);
@@ -116,24 +125,28 @@ void rope_cache(Tensor qkv, Tensor pos, Tensor cos_sin, c10::optional<Tensor> sl
   TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == (Hq + 2 * Hkv) * D, "rope_cache: qkv must be [T, (Hq+2Hkv)*D]");
   TORCH_CHECK(pos.numel() == qkv.size(0));
   TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D);
+  TORCH_CHECK(k_scale > 0 && v_scale > 0, "rope_cache: KV scales must be positive");
   int BS = 64;
   const int32_t* sp = nullptr;
-  uint16_t *kp = nullptr, *vp = nullptr;
+  void *kp = nullptr, *vp = nullptr;
+  bool fp8 = false;
   if (slots.has_value()) {
     TORCH_CHECK(kc.has_value() && vc.has_value());
     CHECK_DEV(*slots); CHECK_DT(*slots, at::kInt);
     TORCH_CHECK(slots->numel() == qkv.size(0));
-    CHECK_BF16(*kc); CHECK_BF16(*vc); CHECK_CONTIG(*kc); CHECK_CONTIG(*vc);
+    fp8 = kv_is_fp8(*kc, *vc);
+    CHECK_CONTIG(*kc); CHECK_CONTIG(*vc);
     TORCH_CHECK(kc->dim() == 4 && kc->size(1) == Hkv && kc->size(3) == D, "k cache must be [nb, Hkv, BS, D]");
     TORCH_CHECK(vc->dim() == 4 && vc->size(1) == Hkv && vc->size(2) == D, "v cache must be [nb, Hkv, D, BS]");
     BS = (int)kc->size(2);
     TORCH_CHECK(vc->size(3) == BS && kc->size(0) == vc->size(0));
     sp = slots->data_ptr<int32_t>();
-    kp = bfp(*kc);
-    vp = bfp(*vc);
+    kp = kc->data_ptr();
+    vp = vc->data_ptr();
   }
   nga::launch_rope_cache(bfp(qkv), pos.data_ptr<int32_t>(), cos_sin.data_ptr<float>(), sp, kp, vp,
-                         qkv.size(0), (int)Hq, (int)Hkv, (int)D, BS, cur_stream(qkv));
+                         qkv.size(0), (int)Hq, (int)Hkv, (int)D, BS, fp8, (float)(1.0 / k_scale),
+                         (float)(1.0 / v_scale), cur_stream(qkv));
 }
 
 // ------------------------------------------------------------------ MoE
@@ -229,8 +242,10 @@ int64_t decode_pages_per_part(int64_t num_seqs, int64_t Hkv, int64_t max_ctx) {
 
 void decode_attention(Tensor out, Tensor q, Tensor kc, Tensor vc, Tensor block_tables,
                       Tensor ctx_lens, int64_t Hq, int64_t Hkv, int64_t max_ctx, double scale,
-                      int64_t pages_per_part, Tensor part_ml, Tensor part_o, int64_t window) {
-  CHECK_BF16(out); CHECK_BF16(q); CHECK_BF16(kc); CHECK_BF16(vc);
+                      int64_t pages_per_part, Tensor part_ml, Tensor part_o, int64_t window,
+                      double k_scale, double v_scale) {
+  CHECK_BF16(out); CHECK_BF16(q);
+  const bool fp8 = kv_is_fp8(kc, vc);
   CHECK_CONTIG(kc); CHECK_CONTIG(vc);
   CHECK_DEV(block_tables); CHECK_DT(block_tables, at::kInt); CHECK_CONTIG(block_tables);
   CHECK_DEV(ctx_lens); CHECK_DT(ctx_lens, at::kInt);
@@ -255,13 +270,14 @@ void decode_attention(Tensor out, Tensor q, Tensor kc, Tensor vc, Tensor block_t
     TORCH_CHECK(part_ml.numel() >= B * Hq * nparts * 2 && part_o.numel() >= B * Hq * nparts * D,
                 "decode_attention: partition workspace too small");
   }
-  nga::launch_decode_attention(bfp(out), out.stride(0), bfp(q), q.stride(0), bfp(kc), bfp(vc),
-                               block_tables.data_ptr<int32_t>(), (int)block_tables.size(1),
-                               ctx_lens.data_ptr<int32_t>(), (int)B, (int)Hq, (int)Hkv, (int)D,
-                               (int)max_ctx, (float)scale, (int)pages_per_part,
+  nga::launch_decode_attention(bfp(out), out.stride(0), bfp(q), q.stride(0), kc.data_ptr(),
+                               vc.data_ptr(), block_tables.data_ptr<int32_t>(),
+                               (int)block_tables.size(1), ctx_lens.data_ptr<int32_t>(), (int)B,
+                               (int)Hq, (int)Hkv, (int)D, (int)max_ctx, (float)scale,
+                               (int)pages_per_part,
                                nparts > 1 ? part_ml.data_ptr<float>() : nullptr,
-                               nparts > 1 ? part_o.data_ptr<float>() : nullptr, (int)window,
-                               cur_stream(q));
+                               nparts > 1 ? part_o.data_ptr<float>() : nullptr, (int)window, fp8,
+                               (float)k_scale, (float)v_scale, cur_stream(q));
 }
 
 void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optional<Tensor> v,
@@ -269,7 +285,7 @@ void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optio
                        c10::optional<Tensor> block_tables, Tensor cu_q,
                        c10::optional<Tensor> ctx_lens, int64_t Hq, int64_t Hkv, int64_t D,
                        int64_t max_q_len, double scale, bool causal, int64_t window,
-                       int64_t impl) {
+                       int64_t impl, double k_scale, double v_scale) {
   CHECK_BF16(out); CHECK_BF16(q);
   TORCH_CHECK(impl >= 0 && impl <= 2, "prefill_attention: impl is 0 (auto), 1 or 2");
   CHECK_DEV(cu_q); CHECK_DT(cu_q, at::kInt); CHECK_CONTIG(cu_q);
@@ -293,7 +309,12 @@ void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optio
   const bool paged = kc.has_value();
   if (paged) {
     TORCH_CHECK(vc.has_value() && block_tables.has_value() && ctx_lens.has_value());
-    CHECK_BF16(*kc); CHECK_BF16(*vc); CHECK_CONTIG(*kc); CHECK_CONTIG(*vc);
+    p.kv_fp8 = kv_is_fp8(*kc, *vc) ? 1 : 0;
+    CHECK_CONTIG(*kc); CHECK_CONTIG(*vc);
+    if (p.kv_fp8) {
+      p.scale = (float)(scale * k_scale);
+      p.v_scale = (float)v_scale;
+    }
     TORCH_CHECK(kc->dim() == 4 && kc->size(1) == Hkv && kc->size(2) == 64 && kc->size(3) == D);
     TORCH_CHECK(vc->sizes() == at::IntArrayRef({kc->size(0), Hkv, D, 64}));
     CHECK_DEV(*block_tables); CHECK_DT(*block_tables, at::kInt); CHECK_CONTIG(*block_tables);

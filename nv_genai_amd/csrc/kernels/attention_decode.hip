@@ -37,13 +37,20 @@ constexpr float RESCALE_LOG2 = 8.f;
 // 256 VGPRs, so the page is processed as two 32-key passes with their own online-softmax
 // update (KH = 1). WINDOW > 0 (sliding-window attention): the query at position ctx - 1 sees
 // keys (ctx - 1 - window, ctx - 1]; pages wholly before the window are never read.
-template <int D>
+// CT = cache element: uint16_t (bf16) or uint8_t (fp8 e4m3fn: 8-byte fragment loads widened
+// to bf16 in registers; the K scale is folded into `scale` by the launcher, the V scale
+// multiplies the output)
+template <int D, typename CT>
 __global__ void __launch_bounds__(256) decode_attn_kernel(
     uint16_t* __restrict__ out, int64_t out_stride, const uint16_t* __restrict__ q,
-    int64_t q_stride, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    int64_t q_stride, const CT* __restrict__ kc, const CT* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int max_blocks,
     const int32_t* __restrict__ ctx_lens, int Hq, int Hkv, float scale, int pages_per_part,
-    float* __restrict__ part_ml, float* __restrict__ part_o, int window) {
+    float* __restrict__ part_ml, float* __restrict__ part_o, int window, float v_scale) {
+  auto ld8 = [](const CT* p) -> u16x8 {
+    if constexpr (sizeof(CT) == 2) return load8(p);
+    else return load8_fp8(p);
+  };
   constexpr int DS = D / 32;   // d-steps of the QK^T MFMA
   constexpr int DT = D / 16;   // d-tiles of the PV MFMA
   constexpr int KH = D <= 128 ? 2 : 1;  // 32-key groups per softmax pass
@@ -103,8 +110,8 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   const int32_t* bt = block_tables + (int64_t)b * max_blocks;
   for (int p = p_begin + w; p < p_end; p += NW) {
     const int64_t blk = bt[p];
-    const uint16_t* kp = kc + (blk * Hkv + kvh) * (int64_t)(BS * D);
-    const uint16_t* vp = vc + (blk * Hkv + kvh) * (int64_t)(D * BS);
+    const CT* kp = kc + (blk * Hkv + kvh) * (int64_t)(BS * D);
+    const CT* vp = vc + (blk * Hkv + kvh) * (int64_t)(D * BS);
     const int kbase = p * BS;
     const bool full = kbase + BS <= ctx && kbase >= key_lo;
 #pragma unroll
@@ -116,14 +123,14 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
         const int tau = 2 * KH * pass + ti;
         const int key = 32 * (tau >> 1) + 8 * (col >> 2) + 4 * (tau & 1) + (col & 3);
 #pragma unroll
-        for (int s = 0; s < DS; ++s) kf[ti][s] = load8(kp + key * D + 32 * s + 8 * h);
+        for (int s = 0; s < DS; ++s) kf[ti][s] = ld8(kp + key * D + 32 * s + 8 * h);
       }
       u16x8 vf[KH][DT];
 #pragma unroll
       for (int gi = 0; gi < KH; ++gi) {
         const int g = KH * pass + gi;
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) vf[gi][dt] = load8(vp + (16 * dt + col) * BS + 32 * g + 8 * h);
+        for (int dt = 0; dt < DT; ++dt) vf[gi][dt] = ld8(vp + (16 * dt + col) * BS + 32 * g + 8 * h);
       }
 
       f32x4 sacc[2 * KH];
@@ -212,6 +219,7 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
       L += f * l_s[ww][qi];
       acc += f * o_s[ww][qi][d];
     }
+    acc *= v_scale;
     const int hq = kvh * G + qi;
     if (nparts == 1) {
       out[(int64_t)b * out_stride + (int64_t)hq * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
@@ -259,30 +267,34 @@ int decode_attn_pages_per_part(int num_seqs, int Hkv, int max_ctx) {
 }
 
 void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* q,
-                             int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
+                             int64_t q_stride, const void* kc, const void* vc,
                              const int32_t* block_tables, int max_blocks, const int32_t* ctx_lens,
                              int num_seqs, int Hq, int Hkv, int D, int max_ctx, float scale,
                              int pages_per_part, float* part_ml, float* part_o, int window,
-                             hipStream_t stream) {
+                             bool kv_fp8, float k_scale, float v_scale, hipStream_t stream) {
   if (num_seqs == 0) return;
   int pages = (max_ctx + BS - 1) / BS;
   if (window > 0) pages = min(pages, (window + BS - 1) / BS + 1);  // visible pages at most
   const int nparts = (pages + pages_per_part - 1) / pages_per_part;
   dim3 grid(num_seqs, Hkv, nparts);
   dim3 g2(num_seqs, Hq);
+  if (!kv_fp8) k_scale = v_scale = 1.f;
+  const float sc = scale * k_scale;
+#define NGA_DEC(DD, CT)                                                                        \
+  decode_attn_kernel<DD, CT><<<grid, 256, 0, stream>>>(                                        \
+      out, out_stride, q, q_stride, static_cast<const CT*>(kc), static_cast<const CT*>(vc),   \
+      block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, pages_per_part, part_ml, part_o, window, \
+      v_scale)
   if (D == 256) {
-    decode_attn_kernel<256><<<grid, 256, 0, stream>>>(out, out_stride, q, q_stride, kc, vc,
-                                                      block_tables, max_blocks, ctx_lens, Hq, Hkv,
-                                                      scale, pages_per_part, part_ml, part_o, window);
+    if (kv_fp8) NGA_DEC(256, uint8_t); else NGA_DEC(256, uint16_t);
     if (nparts > 1)
       decode_attn_reduce_kernel<256><<<g2, 256, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts);
   } else {
-    decode_attn_kernel<128><<<grid, 256, 0, stream>>>(out, out_stride, q, q_stride, kc, vc,
-                                                      block_tables, max_blocks, ctx_lens, Hq, Hkv,
-                                                      scale, pages_per_part, part_ml, part_o, window);
+    if (kv_fp8) NGA_DEC(128, uint8_t); else NGA_DEC(128, uint16_t);
     if (nparts > 1)
       decode_attn_reduce_kernel<128><<<g2, 128, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts);
   }
+#undef NGA_DEC
 }
 
 }  // namespace nga

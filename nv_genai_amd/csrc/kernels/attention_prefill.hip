@@ -17,7 +17,8 @@
 //        prefix-cache hits work unchanged).  Otherwise: K and V rows come from packed
 //        [T, H, D] tensors with per-sequence offsets (cu_q), V is transposed while staging.
 // D is 64 or 128 (either mode), 256 (paged: Gemma) or 32 (packed mode only: the
-// all-MiniLM-L6-v2 encoder). P.window > 0: sliding-window causal attention (query i sees keys
+// all-MiniLM-L6-v2 encoder). Paged caches may be fp8 e4m3fn (P.kv_fp8): widened to bf16 in
+// registers before staging; P.scale carries the K scale, P.v_scale the V scale. P.window > 0: sliding-window causal attention (query i sees keys
 // (i - window, i]); key tiles wholly before every query's window are skipped.
 #include <cstdlib>
 
@@ -109,13 +110,25 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
   auto load_tile = [&](int t, u16x8 (&kreg)[PER_T], u16x8 (&vreg)[PER_T]) {
     if (PAGED) {
       const int64_t blk = P.block_tables[(int64_t)b * P.max_blocks + t];
-      const uint16_t* kp = P.kc + (blk * P.Hkv + kvh) * (int64_t)(KT * D);
-      const uint16_t* vp = P.vc + (blk * P.Hkv + kvh) * (int64_t)(D * KT);
+      const int64_t pg = (blk * P.Hkv + kvh) * (int64_t)(KT * D);   // elements (= bytes for fp8)
+      if (P.kv_fp8) {   // 8-byte fp8 chunks widened to bf16 before they are staged
+        const uint8_t* kp = reinterpret_cast<const uint8_t*>(P.kc) + pg;
+        const uint8_t* vp = reinterpret_cast<const uint8_t*>(P.vc) + pg;
 #pragma unroll
-      for (int i = 0; i < PER_T; ++i) {
-        const int c = tid + 256 * i;
-        kreg[i] = load8(kp + (int64_t)c * 8);
-        vreg[i] = load8(vp + (int64_t)c * 8);
+        for (int i = 0; i < PER_T; ++i) {
+          const int c = tid + 256 * i;
+          kreg[i] = load8_fp8(kp + (int64_t)c * 8);
+          vreg[i] = load8_fp8(vp + (int64_t)c * 8);
+        }
+      } else {
+        const uint16_t* kp = P.kc + pg;
+        const uint16_t* vp = P.vc + pg;
+#pragma unroll
+        for (int i = 0; i < PER_T; ++i) {
+          const int c = tid + 256 * i;
+          kreg[i] = load8(kp + (int64_t)c * 8);
+          vreg[i] = load8(vp + (int64_t)c * 8);
+        }
       }
     } else {
 #pragma unroll
@@ -279,7 +292,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
     ll += __shfl_xor(ll, 16, 64);
     ll += __shfl_xor(ll, 32, 64);
     if (row_ok[cg]) {
-      const float inv = ll > 0.f ? 1.f / ll : 0.f;
+      const float inv = (ll > 0.f ? 1.f / ll : 0.f) * (PAGED && P.kv_fp8 ? P.v_scale : 1.f);
       uint16_t* op = P.out + (int64_t)(q0 + qr[cg]) * P.out_stride + (int64_t)hq * D;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {

@@ -328,7 +328,8 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
     const char* e = getenv("NGA_PREFILL_V1");
     return e && atoi(e) != 0;
   }();
-  if (p.impl == 1 || (p.impl == 0 && disabled) || D != 128 || !paged || p.max_blocks > V2_MAX_TILES)
+  if (p.impl == 1 || (p.impl == 0 && disabled) || D != 128 || !paged || p.kv_fp8 ||
+      p.max_blocks > V2_MAX_TILES)
     return false;
   if (num_seqs == 0 || max_q_len == 0) return true;
   const int G = p.Hq / p.Hkv;

@@ -48,6 +48,38 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// FP8 (OCP e4m3fn) KV cache helpers. 8 cache bytes <-> 8 bf16 values; every e4m3 value is
+// exact in bf16, so reads are lossless. Writes saturate to +-448 (the format has no inf).
+// (fp8 -> f32 pairs, then bf16: exact. The one-step v_cvt_scalef32_pk_bf16_fp8 gave the even
+// byte's value for the odd one of each pair in a device check, scripts/dev/fp8_cvt_check.hip.)
+__device__ __forceinline__ u16x8 fp8x8_to_bf16x8(uint2 w) {
+  u16x8 r;
+  const uint32_t ws[2] = {w.x, w.y};
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(ws[i], false);
+    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8(ws[i], true);
+    r[4 * i] = f2bf(lo[0]);
+    r[4 * i + 1] = f2bf(lo[1]);
+    r[4 * i + 2] = f2bf(hi[0]);
+    r[4 * i + 3] = f2bf(hi[1]);
+  }
+  return r;
+}
+
+__device__ __forceinline__ u16x8 load8_fp8(const uint8_t* p) {
+  return fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(p));
+}
+
+__device__ __forceinline__ float fp8_sat(float x) { return fminf(fmaxf(x, -448.f), 448.f); }
+
+// two floats -> two fp8 bytes in the low half of the result
+__device__ __forceinline__ uint32_t f32x2_to_fp8(float a, float b) {
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(fp8_sat(a), fp8_sat(b), 0, false) & 0xffffu;
+}
+
+__device__ __forceinline__ uint8_t f32_to_fp8(float a) { return (uint8_t)(f32x2_to_fp8(a, 0.f) & 0xffu); }
+
 // LDS-DMA: 16 B per lane global -> LDS; the wave's 64 lanes fill lds_wave_base + lane * 16
 // (the LDS address is wave-uniform, it goes through M0). Completion is tracked by vmcnt, not
 // lgkmcnt; other waves see the bytes after the issuing wave's vmcnt wait + a barrier.

@@ -24,18 +24,21 @@ void launch_bias_gelu(uint16_t* x, const uint16_t* bias, int64_t T, int F, int m
                       hipStream_t stream);
 
 // rope.hip
+// kc / vc: bf16 caches, or fp8 e4m3fn ones (kv_fp8) storing k * inv_ks and v * inv_vs
 void launch_rope_cache(uint16_t* qkv, const int32_t* pos, const float* cos_sin,
-                       const int32_t* slots, uint16_t* kc, uint16_t* vc, int64_t T, int Hq,
-                       int Hkv, int D, int BS, hipStream_t stream);
+                       const int32_t* slots, void* kc, void* vc, int64_t T, int Hq,
+                       int Hkv, int D, int BS, bool kv_fp8, float inv_ks, float inv_vs,
+                       hipStream_t stream);
 
 // attention_decode.hip
 int decode_attn_pages_per_part(int num_seqs, int Hkv, int max_ctx);
+// kc / vc: bf16, or fp8 e4m3fn holding k / k_scale and v / v_scale (kv_fp8)
 void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* q,
-                             int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
+                             int64_t q_stride, const void* kc, const void* vc,
                              const int32_t* block_tables, int max_blocks, const int32_t* ctx_lens,
                              int num_seqs, int Hq, int Hkv, int D, int max_ctx, float scale,
                              int pages_per_part, float* part_ml, float* part_o, int window,
-                             hipStream_t stream);
+                             bool kv_fp8, float k_scale, float v_scale, hipStream_t stream);
 
 // attention_prefill.hip
 struct PrefillParams {
@@ -60,6 +63,8 @@ struct PrefillParams {
   int total;   // ntiles * Hq * num_seqs — set by the launcher
   int window;  // > 0: sliding-window causal attention (query i sees keys (i - window, i])
   int impl;    // 0: pick by size, 1: the 16x16 kernel, 2: the 32x32 kernel where it applies
+  int kv_fp8;      // paged caches hold fp8 e4m3fn (k / k_scale, v / v_scale); 16x16 kernel only
+  float v_scale;   // output multiplier (fp8 caches; `scale` already includes k_scale)
 };
 void launch_prefill_attention(const PrefillParams& p, int num_seqs, int max_q_len, int D,
                               bool paged, bool causal, hipStream_t stream);

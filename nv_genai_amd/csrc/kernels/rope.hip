@@ -6,16 +6,52 @@
 //   Vt cache: [num_blocks, Hkv, D, BS]   (V stored transposed: keys contiguous per d, so the
 //                                          P.V MFMA operand is one 16-B load per lane)
 // qkv: [T, (Hq + 2*Hkv) * D] (the fused QKV projection output); q and k are rotated in place.
+// The caches hold bf16, or fp8 e4m3fn (half the KV bytes; k / v multiplied by 1 / scale
+// before rounding, the attention kernels fold the scales back in).
 #include "common.h"
 #include "kernels.h"
 
 namespace nga {
 
-template <int D>
+// CT = cache element: uint16_t (bf16) or uint8_t (fp8 e4m3fn, values multiplied by
+// inv_ks / inv_vs before rounding: the per-layer K / V scales)
+template <typename CT>
+__device__ __forceinline__ void put4(CT* dst, u16x4 v, float inv_s) {
+  if constexpr (sizeof(CT) == 2) {
+    *reinterpret_cast<u16x4*>(dst) = v;
+  } else {
+    *reinterpret_cast<uint32_t*>(dst) =
+        f32x2_to_fp8(bf2f(v[0]) * inv_s, bf2f(v[1]) * inv_s) |
+        (f32x2_to_fp8(bf2f(v[2]) * inv_s, bf2f(v[3]) * inv_s) << 16);
+  }
+}
+
+template <typename CT>
+__device__ __forceinline__ void put8(CT* dst, u16x8 v, float inv_s) {
+  if constexpr (sizeof(CT) == 2) {
+    store8(dst, v);
+  } else {
+    uint2 w;
+    w.x = f32x2_to_fp8(bf2f(v[0]) * inv_s, bf2f(v[1]) * inv_s) |
+          (f32x2_to_fp8(bf2f(v[2]) * inv_s, bf2f(v[3]) * inv_s) << 16);
+    w.y = f32x2_to_fp8(bf2f(v[4]) * inv_s, bf2f(v[5]) * inv_s) |
+          (f32x2_to_fp8(bf2f(v[6]) * inv_s, bf2f(v[7]) * inv_s) << 16);
+    *reinterpret_cast<uint2*>(dst) = w;
+  }
+}
+
+template <typename CT>
+__device__ __forceinline__ void put1(CT* dst, uint16_t v, float inv_s) {
+  if constexpr (sizeof(CT) == 2) *dst = v;
+  else *dst = f32_to_fp8(bf2f(v) * inv_s);
+}
+
+template <int D, typename CT>
 __global__ void rope_cache_kernel(uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos,
                                   const float* __restrict__ cos_sin,
-                                  const int32_t* __restrict__ slots, uint16_t* __restrict__ kc,
-                                  uint16_t* __restrict__ vc, int Hq, int Hkv, int BS) {
+                                  const int32_t* __restrict__ slots, CT* __restrict__ kc,
+                                  CT* __restrict__ vc, int Hq, int Hkv, int BS, float inv_ks,
+                                  float inv_vs) {
   constexpr int HALF = D / 2;
   constexpr int G4 = HALF / 4;  // 4-element groups per half
   const int64_t t = blockIdx.x;
@@ -48,18 +84,18 @@ __global__ void rope_cache_kernel(uint16_t* __restrict__ qkv, const int32_t* __r
       *reinterpret_cast<u16x4*>(x + HALF + i0) = ob;
       if (h >= Hq && slot >= 0) {
         const int kh = h - Hq;
-        uint16_t* dst = kc + ((blk * Hkv + kh) * BS + off) * D;
-        *reinterpret_cast<u16x4*>(dst + i0) = oa;
-        *reinterpret_cast<u16x4*>(dst + HALF + i0) = ob;
+        CT* dst = kc + ((blk * Hkv + kh) * BS + off) * D;
+        put4(dst + i0, oa, inv_ks);
+        put4(dst + HALF + i0, ob, inv_ks);
       }
     } else if (slot >= 0) {
       const int r = w - n_rot;
       const int vh = r / (D / 8);
       const int d0 = (r % (D / 8)) * 8;
       u16x8 v = load8(base + (int64_t)(Hq + Hkv + vh) * D + d0);
-      uint16_t* dst = vc + ((blk * Hkv + vh) * D + d0) * BS + off;
+      CT* dst = vc + ((blk * Hkv + vh) * D + d0) * BS + off;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dst[(int64_t)j * BS] = v[j];
+      for (int j = 0; j < 8; ++j) put1(dst + (int64_t)j * BS, v[j], inv_vs);
     }
   }
 }
@@ -72,11 +108,11 @@ __global__ void rope_cache_kernel(uint16_t* __restrict__ qkv, const int32_t* __r
 // per token (the per-token kernel above wrote Vt at ~2 TB/s effective).
 constexpr int RT = 64;  // tokens per tile
 
-template <int D>
+template <int D, typename CT>
 __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos, const float* __restrict__ cos_sin,
-    const int32_t* __restrict__ slots, uint16_t* __restrict__ kc, uint16_t* __restrict__ vc,
-    int64_t T, int Hq, int Hkv, int BS) {
+    const int32_t* __restrict__ slots, CT* __restrict__ kc, CT* __restrict__ vc,
+    int64_t T, int Hq, int Hkv, int BS, float inv_ks, float inv_vs) {
   constexpr int HALF = D / 2;
   constexpr int CH = HALF / 8;       // 8-element chunks per half
   constexpr int LDP = D + 2;         // padded LDS row (bank-conflict-free column reads)
@@ -109,9 +145,9 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
       store8(x + HALF + i0, ob);
       const int slot = (slots && h >= Hq) ? slots[t] : -1;
       if (slot >= 0) {
-        uint16_t* dst = kc + (((int64_t)(slot / BS) * Hkv + (h - Hq)) * BS + slot % BS) * D;
-        store8(dst + i0, oa);
-        store8(dst + HALF + i0, ob);
+        CT* dst = kc + (((int64_t)(slot / BS) * Hkv + (h - Hq)) * BS + slot % BS) * D;
+        put8(dst + i0, oa, inv_ks);
+        put8(dst + HALF + i0, ob, inv_ks);
       }
     }
     return;
@@ -131,31 +167,38 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
   const int64_t t = t0 + lane;
   const int slot = t < T ? slots[t] : -1;
   if (slot < 0) return;
-  uint16_t* dst = vc + ((int64_t)(slot / BS) * Hkv + vh) * D * BS + slot % BS;
-  for (int d = w; d < D; d += nw) dst[(int64_t)d * BS] = tile[lane * LDP + d];
+  CT* dst = vc + ((int64_t)(slot / BS) * Hkv + vh) * D * BS + slot % BS;
+  for (int d = w; d < D; d += nw) put1(dst + (int64_t)d * BS, tile[lane * LDP + d], inv_vs);
 }
 
-void launch_rope_cache(uint16_t* qkv, const int32_t* pos, const float* cos_sin,
-                       const int32_t* slots, uint16_t* kc, uint16_t* vc, int64_t T, int Hq,
-                       int Hkv, int D, int BS, hipStream_t stream) {
-  if (T == 0) return;
+template <typename CT>
+static void rope_dispatch(uint16_t* qkv, const int32_t* pos, const float* cos_sin,
+                          const int32_t* slots, CT* kc, CT* vc, int64_t T, int Hq, int Hkv, int D,
+                          int BS, float inv_ks, float inv_vs, hipStream_t stream) {
   if (T >= RT) {
     dim3 grid((unsigned)((T + RT - 1) / RT), (unsigned)(Hq + 2 * Hkv)), block(256);
-    if (D == 128)
-      rope_cache_tiled_kernel<128><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS);
-    else if (D == 256)
-      rope_cache_tiled_kernel<256><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS);
-    else if (D == 64)
-      rope_cache_tiled_kernel<64><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS);
+#define NGA_RT(DD) rope_cache_tiled_kernel<DD, CT><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS, inv_ks, inv_vs)
+    if (D == 128) NGA_RT(128); else if (D == 256) NGA_RT(256); else if (D == 64) NGA_RT(64);
+#undef NGA_RT
     return;
   }
   dim3 grid((unsigned)T), block(256);
-  if (D == 128)
-    rope_cache_kernel<128><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, BS);
-  else if (D == 256)
-    rope_cache_kernel<256><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, BS);
-  else if (D == 64)
-    rope_cache_kernel<64><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, BS);
+#define NGA_R1(DD) rope_cache_kernel<DD, CT><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, BS, inv_ks, inv_vs)
+  if (D == 128) NGA_R1(128); else if (D == 256) NGA_R1(256); else if (D == 64) NGA_R1(64);
+#undef NGA_R1
+}
+
+void launch_rope_cache(uint16_t* qkv, const int32_t* pos, const float* cos_sin,
+                       const int32_t* slots, void* kc, void* vc, int64_t T, int Hq,
+                       int Hkv, int D, int BS, bool kv_fp8, float inv_ks, float inv_vs,
+                       hipStream_t stream) {
+  if (T == 0) return;
+  if (kv_fp8)
+    rope_dispatch(qkv, pos, cos_sin, slots, static_cast<uint8_t*>(kc), static_cast<uint8_t*>(vc), T,
+                  Hq, Hkv, D, BS, inv_ks, inv_vs, stream);
+  else
+    rope_dispatch(qkv, pos, cos_sin, slots, static_cast<uint16_t*>(kc), static_cast<uint16_t*>(vc),
+                  T, Hq, Hkv, D, BS, 1.f, 1.f, stream);
 }
 
 }  // namespace nga

@@ -24,7 +24,7 @@ import random
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Callable, Deque, Dict, List, Optional, Sequence
+from typing import Callable, Deque, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -116,7 +116,9 @@ class EngineConfig:
     mixed_max_wait: int = 4       # ... unless the oldest waiting request waited this many steps
     tuned_gemms: bool = True   # load the per-shape hipBLASLt/rocBLAS table (ops/gemm_tuning.py)
     sequence_parallel: bool = False  # TP prefill >= sp_min_tokens: reduce-scatter/all-gather
-    fp8: bool = False   # W8A8 FP8 projections (LlamaModel.quantize_fp8); KV cache stays bf16
+    fp8: bool = False   # W8A8 FP8 projections (LlamaModel.quantize_fp8)
+    kv_cache_dtype: str = "auto"   # "fp8": e4m3fn KV pages (2x the cached tokens, half the KV reads)
+    kv_scales: Tuple[float, float] = (1.0, 1.0)   # fp8 KV: the per-tensor K / V scales
     sp_min_tokens: int = 512
 
 
@@ -153,11 +155,12 @@ class LLMEngine:
         if nb is None:
             if self.gpu:
                 free, _ = torch.cuda.mem_get_info(self.device)
-                nb = int(free * cfg.kv_cache_fraction) // self.model.kv_block_bytes(cfg.block_size)
+                nb = int(free * cfg.kv_cache_fraction) // self.model.kv_block_bytes(cfg.block_size,
+                                                                                    cfg.kv_cache_dtype)
             else:
                 nb = 256
         self.num_blocks = int(nb)
-        self.model.allocate_kv_cache(self.num_blocks, cfg.block_size)
+        self.model.allocate_kv_cache(self.num_blocks, cfg.block_size, cfg.kv_cache_dtype, cfg.kv_scales)
         self.max_blocks = (cfg.max_model_len + cfg.block_size - 1) // cfg.block_size
         self.sched = rt.Scheduler(self.num_blocks, cfg.block_size, cfg.max_num_seqs,
                                   cfg.max_batched_tokens, cfg.max_model_len,

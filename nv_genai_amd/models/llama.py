@@ -69,6 +69,7 @@ class LlamaModel:
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
+        self.kv_dtype, self.kv_scales = "auto", (1.0, 1.0)   # set by allocate_kv_cache
         self.p = pctx or get_context()
         tp = self.p.tp_size
         # expert parallelism: each TP rank owns num_experts / tp whole experts when that
@@ -358,25 +359,40 @@ class LlamaModel:
         return out
 
     # ------------------------------------------------------------------ cache
-    def allocate_kv_cache(self, num_blocks: int, block_size: int = 64):
+    def allocate_kv_cache(self, num_blocks: int, block_size: int = 64, kv_dtype: str = "auto",
+                          kv_scales=(1.0, 1.0)):
+        """Paged K [layers, blocks, Hkv, 64, D] and Vᵀ [layers, blocks, Hkv, D, 64] caches.
+        ``kv_dtype``: "auto" (the model dtype) or "fp8" — OCP e4m3fn pages holding k / k_scale
+        and v / v_scale (half the bytes: twice the cached tokens, half the decode KV stream;
+        the attention kernels widen the pages to bf16 in registers and fold the scales in)."""
         if block_size != 64:
             raise ValueError("the gfx950 attention kernels use 64-token KV pages")
+        if kv_dtype not in ("auto", "bf16", "fp8"):
+            raise ValueError(f"kv_dtype must be auto, bf16 or fp8, not {kv_dtype!r}")
         shape_k = (len(self.layers), num_blocks, self.hkv, block_size, self.D)
         shape_v = (len(self.layers), num_blocks, self.hkv, self.D, block_size)
+        self.kv_dtype = kv_dtype if kv_dtype == "fp8" else "auto"
+        self.kv_scales = (float(kv_scales[0]), float(kv_scales[1])) if kv_dtype == "fp8" else (1.0, 1.0)
         # zero-filled: masked keys of a partially filled page must stay finite
-        self.k_cache = torch.zeros(shape_k, device=self.device, dtype=self.dtype)
-        self.v_cache = torch.zeros(shape_v, device=self.device, dtype=self.dtype)
+        if kv_dtype == "fp8":
+            self.k_cache = torch.zeros(shape_k, device=self.device, dtype=torch.uint8).view(torch.float8_e4m3fn)
+            self.v_cache = torch.zeros(shape_v, device=self.device, dtype=torch.uint8).view(torch.float8_e4m3fn)
+        else:
+            self.k_cache = torch.zeros(shape_k, device=self.device, dtype=self.dtype)
+            self.v_cache = torch.zeros(shape_v, device=self.device, dtype=self.dtype)
         return self.k_cache, self.v_cache
 
     def copy_kv_blocks(self, src: torch.Tensor, dst: torch.Tensor) -> None:
         """Copy-on-fork (beam search): page ``dst[i]`` of every layer takes the K and Vᵀ of
         page ``src[i]`` — one gather/scatter per cache over the [layers, blocks] dims."""
         src, dst = src.to(self.device).long(), dst.to(self.device).long()
-        self.k_cache.index_copy_(1, dst, self.k_cache.index_select(1, src))
-        self.v_cache.index_copy_(1, dst, self.v_cache.index_select(1, src))
+        for c in (self.k_cache, self.v_cache):
+            raw = c.view(torch.uint8) if c.dtype == torch.float8_e4m3fn else c
+            raw.index_copy_(1, dst, raw.index_select(1, src))
 
-    def kv_block_bytes(self, block_size: int = 64) -> int:
-        return 2 * len(self.layers) * self.hkv * self.D * block_size * torch.finfo(self.dtype).bits // 8
+    def kv_block_bytes(self, block_size: int = 64, kv_dtype: str = "auto") -> int:
+        elem = 1 if kv_dtype == "fp8" else torch.finfo(self.dtype).bits // 8
+        return 2 * len(self.layers) * self.hkv * self.D * block_size * elem
 
     # ------------------------------------------------------------------ forward
     def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
@@ -439,7 +455,8 @@ class LlamaModel:
         if meta.kind == "decode":
             return ops.decode_attention(q, self.k_cache[li], self.v_cache[li],
                                         meta.block_tables, meta.ctx_lens, hq, hkv,
-                                        meta.max_ctx, self.scale, ws=meta.decode_ws, window=W)
+                                        meta.max_ctx, self.scale, ws=meta.decode_ws, window=W,
+                                        kv_scales=self.kv_scales)
         if meta.kind == "mixed":
             nd = meta.n_decode
             attn = torch.empty(T, qdim, dtype=qkv.dtype, device=qkv.device)
@@ -448,7 +465,8 @@ class LlamaModel:
                 ops.prefill_attention_paged(q[nd:], self.k_cache[li], self.v_cache[li],
                                             meta.block_tables[nd:], meta.cu_q_prefill,
                                             meta.ctx_lens[nd:], hq, hkv, D, meta.max_q_len,
-                                            self.scale, out=attn[nd:], window=W)
+                                            self.scale, out=attn[nd:], window=W,
+                                            kv_scales=self.kv_scales)
 
             side = None
             if self.concurrent_attention and qkv.is_cuda and not torch.cuda.is_current_stream_capturing():
@@ -462,7 +480,7 @@ class LlamaModel:
             ops.decode_attention(q[:nd], self.k_cache[li], self.v_cache[li],
                                  meta.block_tables[:nd], meta.ctx_lens[:nd], hq, hkv,
                                  meta.max_ctx, self.scale, out=attn[:nd], ws=meta.decode_ws,
-                                 window=W)
+                                 window=W, kv_scales=self.kv_scales)
             if side is not None:
                 main.wait_stream(side)           # attn (allocated on main) complete
             else:
@@ -470,7 +488,8 @@ class LlamaModel:
             return attn
         return ops.prefill_attention_paged(q, self.k_cache[li], self.v_cache[li],
                                            meta.block_tables, meta.cu_q, meta.ctx_lens,
-                                           hq, hkv, D, meta.max_q_len, self.scale, window=W)
+                                           hq, hkv, D, meta.max_q_len, self.scale, window=W,
+                                           kv_scales=self.kv_scales)
 
     def _reduce_add_norm(self, partial, resid, w, b=None):
         """resid += all_reduce_TP(partial); returns norm(resid). A small TP message goes
@@ -488,7 +507,7 @@ class LlamaModel:
         L = self.layers[li]
         qkv = self._qkv(x, L)
         ops.rope_cache_(qkv, pos, self.cos_sin, meta.slots, self.k_cache[li],
-                        self.v_cache[li], self.hq, self.hkv, self.D)
+                        self.v_cache[li], self.hq, self.hkv, self.D, kv_scales=self.kv_scales)
         attn = self._attention(qkv[:, :self.hq * self.D], qkv, li, meta, T)
         return self._bias_rank0(self._lin(attn, L, "wo"), L.get("bo"))
 

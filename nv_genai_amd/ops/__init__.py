@@ -122,10 +122,14 @@ def bias_gelu_(x: torch.Tensor, bias: Optional[torch.Tensor], approximate=False)
 
 
 # ------------------------------------------------------------------------- rope / kv
-def rope_cache_(qkv, pos, cos_sin, slots, kc, vc, Hq: int, Hkv: int, D: int):
+def rope_cache_(qkv, pos, cos_sin, slots, kc, vc, Hq: int, Hkv: int, D: int,
+                kv_scales=(1.0, 1.0)):
+    """RoPE on q / k in place + paged KV write. The caches are bf16, or fp8 e4m3fn holding
+    k / kv_scales[0] and v / kv_scales[1]."""
     if not _gpu(qkv):
-        return ref.rope_cache_(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, D)
-    kernels().rope_cache(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, D)
+        return ref.rope_cache_(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, D, kv_scales)
+    kernels().rope_cache(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, D, float(kv_scales[0]),
+                         float(kv_scales[1]))
     return qkv
 
 
@@ -171,12 +175,14 @@ class DecodeWorkspace:
 
 
 def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, max_ctx, scale,
-                     out=None, ws: Optional[DecodeWorkspace] = None, window: int = 0):
-    """Paged GQA decode attention (head_dim 128 or 256); ``window`` > 0: sliding window."""
+                     out=None, ws: Optional[DecodeWorkspace] = None, window: int = 0,
+                     kv_scales=(1.0, 1.0)):
+    """Paged GQA decode attention (head_dim 128 or 256); ``window`` > 0: sliding window;
+    bf16 or fp8 e4m3fn caches (``kv_scales`` = the fp8 caches' K / V scales)."""
     D = kc.shape[3]
     if not _gpu(q):
         r = ref.decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, scale, D=D,
-                                 window=window)
+                                 window=window, kv_scales=kv_scales)
         if out is not None:
             out[: r.shape[0], : r.shape[1]].copy_(r)
             return out
@@ -189,17 +195,19 @@ def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, max_ctx, scale,
     assert max_ctx <= ws.max_ctx and ws.D == D
     kernels().decode_attention(out, q, kc, vc, block_tables, ctx_lens, Hq, Hkv, int(max_ctx),
                                float(scale), ws.pages_per_part(B, max_ctx), ws.ml, ws.o,
-                               int(window))
+                               int(window), float(kv_scales[0]), float(kv_scales[1]))
     return out
 
 
 def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D, max_q_len,
-                            scale, out=None, causal=True, window: int = 0, impl: int = 0):
+                            scale, out=None, causal=True, window: int = 0, impl: int = 0,
+                            kv_scales=(1.0, 1.0)):
     """Paged prefill attention. ``impl``: 0 picks the kernel by problem size, 1 forces the
-    16x16-MFMA kernel, 2 the 32x32-MFMA kernel (head_dim 128) — for tests and A/B runs."""
+    16x16-MFMA kernel, 2 the 32x32-MFMA kernel (head_dim 128, bf16 caches) — for tests and
+    A/B runs. fp8 e4m3fn caches (``kv_scales``) run the 16x16 kernel."""
     if not _gpu(q):
         r = ref.prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
-                                        scale, causal, window)
+                                        scale, causal, window, kv_scales)
         if out is not None:
             out[:, : r.shape[1]].copy_(r)
             return out
@@ -208,7 +216,7 @@ def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
         out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
     kernels().prefill_attention(out, q, None, None, kc, vc, block_tables, cu_q, ctx_lens, Hq,
                                 Hkv, D, int(max_q_len), float(scale), bool(causal), int(window),
-                                int(impl))
+                                int(impl), float(kv_scales[0]), float(kv_scales[1]))
     return out
 
 
@@ -219,7 +227,7 @@ def varlen_attention(q, k, v, cu, Hq, Hkv, D, max_len, scale, causal=False, out=
     if out is None:
         out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
     kernels().prefill_attention(out, q, k, v, None, None, None, cu, None, Hq, Hkv, D,
-                                int(max_len), float(scale), bool(causal), 0, 0)
+                                int(max_len), float(scale), bool(causal), 0, 0, 1.0, 1.0)
     return out
 
 

@@ -92,7 +92,14 @@ def rope_cos_sin(max_pos: int, D: int, theta: float = 500000.0,
     return torch.cat([f.cos(), f.sin()], dim=-1).float()
 
 
-def rope_cache_(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, D):
+def _to_cache(x: torch.Tensor, cache: torch.Tensor, scale: float) -> torch.Tensor:
+    """Cache element type: bf16 as is; fp8 e4m3fn stores x / scale, saturated to +-448."""
+    if cache.dtype == torch.float8_e4m3fn:
+        return (x.float() * (1.0 / scale)).clamp(-448.0, 448.0).to(cache.dtype)
+    return x.to(cache.dtype)
+
+
+def rope_cache_(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, D, kv_scales=(1.0, 1.0)):
     T = qkv.shape[0]
     x = qkv.view(T, Hq + 2 * Hkv, D)
     cs = cos_sin[pos.long()]  # [T, D]
@@ -108,21 +115,24 @@ def rope_cache_(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, D):
         blk, off = sl[ok] // BS, sl[ok] % BS
         k = x[ok, Hq: Hq + Hkv]  # [n, Hkv, D]
         v = x[ok, Hq + Hkv:]
-        kc[blk, :, off, :] = k
-        vc[blk, :, :, off] = v
+        kc[blk, :, off, :] = _to_cache(k, kc, kv_scales[0])
+        vc[blk, :, :, off] = _to_cache(v, vc, kv_scales[1])
     return qkv
 
 
-def _gather_kv(kc, vc, bt_row, ctx, kvh):
+def _gather_kv(kc, vc, bt_row, ctx, kvh, kv_scales=(1.0, 1.0)):
     BS = kc.shape[2]
     n_pages = (ctx + BS - 1) // BS
     blocks = bt_row[:n_pages].long()
     k = kc[blocks, kvh].reshape(-1, kc.shape[3])[:ctx]  # [ctx, D]
     v = vc[blocks, kvh].permute(0, 2, 1).reshape(-1, vc.shape[2])[:ctx]
+    if kc.dtype == torch.float8_e4m3fn:
+        return k.float() * kv_scales[0], v.float() * kv_scales[1]
     return k.float(), v.float()
 
 
-def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, scale, D=128, window=0):
+def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, scale, D=128, window=0,
+                     kv_scales=(1.0, 1.0)):
     """One query per sequence at position ctx - 1; ``window`` > 0 keeps only the last
     ``window`` keys (sliding-window attention: key j visible iff j > ctx - 1 - window)."""
     B = ctx_lens.numel()
@@ -134,7 +144,7 @@ def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, scale, D=128, w
             continue
         lo = max(0, ctx - window) if window > 0 else 0
         for kvh in range(Hkv):
-            k, v = _gather_kv(kc, vc, block_tables[b], ctx, kvh)
+            k, v = _gather_kv(kc, vc, block_tables[b], ctx, kvh, kv_scales)
             k, v = k[lo:], v[lo:]
             qs = q[b, kvh * G * D:(kvh + 1) * G * D].view(G, D).float()
             p = torch.softmax(qs @ k.T * scale, dim=-1)
@@ -143,7 +153,7 @@ def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, scale, D=128, w
 
 
 def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D, scale,
-                            causal=True, window=0):
+                            causal=True, window=0, kv_scales=(1.0, 1.0)):
     G = Hq // Hkv
     T = q.shape[0]
     out = torch.zeros(T, Hq * D, dtype=q.dtype, device=q.device)
@@ -159,7 +169,7 @@ def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
         if window > 0:
             mask = mask & (kpos[None, :] > qpos[:, None] - window)
         for hq in range(Hq):
-            k, v = _gather_kv(kc, vc, block_tables[b], ctx, hq // G)
+            k, v = _gather_kv(kc, vc, block_tables[b], ctx, hq // G, kv_scales)
             qs = q[s0:s1, hq * D:(hq + 1) * D].float()
             sc = (qs @ k.T) * scale
             sc = sc.masked_fill(~mask, float("-inf"))

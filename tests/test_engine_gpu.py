@@ -229,3 +229,36 @@ def test_fp8_engine_gpu(gpu, weights):
     g = [r.output_ids for r in _engine(weights, "cuda", fp8=True).generate(PROMPTS[:3], p)]
     e = [r.output_ids for r in _engine(weights, "cuda", fp8=True, use_graphs=False).generate(PROMPTS[:3], p)]
     assert g == e
+
+
+def test_fp8_kv_cache_engine_gpu(gpu, weights):
+    """FP8 (e4m3fn) KV cache: twice the pages in the same bytes, decode logits of the GPU
+    engine close to the bf16-cache engine, hipGraph decode == eager, and the GPU fp8 engine
+    agrees with the CPU reference engine reading the same fp8 pages."""
+    from nv_genai_amd.engine.llm_engine import SamplingParams
+
+    def last_logits(e, prompt):
+        cap = []
+        orig = e._sample
+
+        def sample(logits, n):
+            cap.append(logits[:n].float().cpu())
+            return orig(logits, n)
+        e._sample = sample
+        e.generate([prompt], SamplingParams(temperature=0.0, max_tokens=4, ignore_eos=True))
+        return cap[-1][-1]
+
+    e8 = _engine(weights, "cuda", use_graphs=False, kv_cache_dtype="fp8", kv_scales=(2.0, 0.5))
+    assert e8.model.k_cache.dtype == torch.float8_e4m3fn
+    assert e8.model.kv_block_bytes(64, "fp8") * 2 == e8.model.kv_block_bytes(64)
+    a = last_logits(_engine(weights, "cuda", use_graphs=False), PROMPTS[1])
+    b = last_logits(e8, PROMPTS[1])
+    c = last_logits(_engine(weights, "cpu", use_graphs=False, kv_cache_dtype="fp8", kv_scales=(2.0, 0.5)),
+                    PROMPTS[1])
+    assert float((a - b).norm() / a.norm()) < 0.1
+    assert float((c - b).norm() / c.norm()) < 0.05
+    assert int(b.argmax()) == int(c.argmax())
+    p = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
+    g = [r.output_ids for r in _engine(weights, "cuda", kv_cache_dtype="fp8").generate(PROMPTS, p)]
+    e = [r.output_ids for r in _engine(weights, "cuda", kv_cache_dtype="fp8", use_graphs=False).generate(PROMPTS, p)]
+    assert g == e

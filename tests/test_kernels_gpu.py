@@ -196,6 +196,57 @@ def test_prefill_attention_kernel_choice(gpu, ctxs, qls, window, impl):
     _close(out, o_ref, 0.02)
 
 
+@pytest.mark.parametrize("D,scales", [(128, (1.0, 1.0)), (128, (3.0, 0.5)), (256, (2.0, 2.0))])
+def test_fp8_kv_cache_kernels(gpu, D, scales):
+    """FP8 e4m3fn KV pages: the RoPE/KV-write kernel stores exactly the reference's rounded
+    bytes (k / k_scale, v / v_scale, saturated), and decode + prefill attention over those
+    pages match the fp32 reference reading the same bytes."""
+    torch.manual_seed(21)
+    Hkv, G = 2, 4
+    Hq = Hkv * G
+    ctxs, qls = [700, 64, 130], [300, 64, 1]
+    nb = sum((c + 63) // 64 for c in ctxs) + 2
+    kc = torch.zeros(nb, Hkv, 64, D, dtype=torch.uint8, device=gpu).view(torch.float8_e4m3fn)
+    vc = torch.zeros(nb, Hkv, D, 64, dtype=torch.uint8, device=gpu).view(torch.float8_e4m3fn)
+    kc_r, vc_r = kc.cpu().clone(), vc.cpu().clone()
+    # write every context position through the kernel (tiled path: T >= 64; per-token: T < 64)
+    perm = torch.randperm(nb).tolist()
+    bt = torch.zeros(len(ctxs), max((c + 63) // 64 for c in ctxs), dtype=torch.int32)
+    k = 0
+    for i, c in enumerate(ctxs):
+        for j in range((c + 63) // 64):
+            bt[i, j] = perm[k]
+            k += 1
+    cs = ops.rope_cos_sin(4096, D).to(gpu)
+    for i, c in enumerate(ctxs):
+        for lo, hi in ((0, c - 7), (c - 7, c)):
+            T = hi - lo
+            qkv = _bf(T, (Hq + 2 * Hkv) * D, dev=gpu, scale=4.0)
+            pos = torch.arange(lo, hi, dtype=torch.int32, device=gpu)
+            slots = (bt[i, pos.cpu().long() // 64] * 64 + pos.cpu() % 64).to(torch.int32).to(gpu)
+            q_r = qkv.cpu().clone()
+            ops.rope_cache_(qkv, pos, cs, slots, kc, vc, Hq, Hkv, D, kv_scales=scales)
+            ref.rope_cache_(q_r, pos.cpu(), cs.cpu(), slots.cpu(), kc_r, vc_r, Hq, Hkv, D, kv_scales=scales)
+    for got, want in ((kc, kc_r), (vc, vc_r)):
+        diff = (got.cpu().view(torch.uint8).int() - want.view(torch.uint8).int()).abs()
+        assert (diff > 1).sum() == 0 and (diff == 1).float().mean() < 1e-3   # RNE ties aside
+    bt = bt.to(gpu)
+    kc_r, vc_r = kc.cpu(), vc.cpu()   # the reference reads the kernel's bytes
+    scale = 1 / math.sqrt(D)
+    q = _bf(len(ctxs), Hq * D, dev=gpu)
+    ctx = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
+    ws = ops.DecodeWorkspace(len(ctxs), Hq, Hkv, max(ctxs), gpu, D=D)
+    out = ops.decode_attention(q, kc, vc, bt, ctx, Hq, Hkv, max(ctxs), scale, ws=ws, kv_scales=scales)
+    o_ref = ref.decode_attention(q.cpu(), kc_r, vc_r, bt.cpu(), ctx.cpu(), Hq, Hkv, scale, D=D, kv_scales=scales)
+    _close(out, o_ref, 0.03, 0.02)
+    cu = torch.tensor([0] + list(torch.tensor(qls).cumsum(0).tolist()), dtype=torch.int32, device=gpu)
+    qp = _bf(sum(qls), Hq * D, dev=gpu)
+    out = ops.prefill_attention_paged(qp, kc, vc, bt, cu, ctx, Hq, Hkv, D, max(qls), scale, kv_scales=scales)
+    o_ref = ref.prefill_attention_paged(qp.cpu(), kc_r, vc_r, bt.cpu(), cu.cpu(), ctx.cpu(), Hq, Hkv, D, scale,
+                                        kv_scales=scales)
+    _close(out, o_ref, 0.03, 0.02)
+
+
 @pytest.mark.parametrize("D,H,causal", [(64, 16, False), (128, 8, True), (32, 12, False)])
 def test_varlen_attention(gpu, D, H, causal):
     torch.manual_seed(4)
