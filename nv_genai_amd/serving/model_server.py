@@ -408,6 +408,9 @@ def main(argv=None):
     ap.add_argument("--max-num-seqs", type=int, default=256)
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--kv-cache-fraction", type=float, default=0.3)
+    ap.add_argument("--kv-cache-dtype", default="auto", choices=("auto", "fp8"),
+                    help="fp8: e4m3fn KV pages (twice the cached tokens)")
+    ap.add_argument("--fp8", action="store_true", help="W8A8 FP8 projections")
     ap.add_argument("--device", default=None)
     args = ap.parse_args(argv)
     import uvicorn
@@ -424,7 +427,9 @@ def main(argv=None):
 
             weights = load_weights(args.weights)
         eng = LLMEngine(EngineConfig(model=args.llm, max_num_seqs=args.max_num_seqs, max_model_len=args.max_model_len,
-                                     kv_cache_fraction=args.kv_cache_fraction), device=args.device, weights=weights)
+                                     kv_cache_fraction=args.kv_cache_fraction,
+                                     kv_cache_dtype=args.kv_cache_dtype, fp8=args.fp8),
+                        device=args.device, weights=weights)
         svc = EngineService(eng)
     if args.embed:
         emb = EmbeddingEngine(args.embed, device=args.device)
