@@ -108,6 +108,20 @@ def main():
         ws = ops.DecodeWorkspace(B, Hq, Hkv, 8192, torch.device(dev), ppp)
         us = timeit(lambda: ops.decode_attention(q, kc, vc, bt, ctx, Hq, Hkv, 8192, D ** -0.5, ws=ws))
         out[f"decode_256x1400_ppp{ppp}"] = {"us": round(us, 1), "TBps": round(B * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
+    # fp8 e4m3fn KV pages (half the bytes; TB/s counted on the bytes actually read)
+    kc8, vc8 = kc.to(torch.float8_e4m3fn), vc.to(torch.float8_e4m3fn)
+    ws = ops.DecodeWorkspace(B, Hq, Hkv, 8192, torch.device(dev))
+    us = timeit(lambda: ops.decode_attention(q, kc8, vc8, bt, ctx, Hq, Hkv, 8192, D ** -0.5, ws=ws))
+    out["decode_256x1400_fp8kv"] = {"us": round(us, 1), "TBps": round(B * L * Hkv * D * 2 / us / 1e6, 2)}
+    del kc8, vc8
+    # head_dim 256, MHA (Gemma-7B: 16 q = 16 kv heads)
+    kc6, vc6, bt6 = paged_setup([L] * 64, Hkv=16, D=256, width=8192 // 64)
+    q6 = torch.randn(64, 16 * 256, device=dev, dtype=torch.bfloat16)
+    ctx6 = torch.full((64,), L, dtype=torch.int32, device=dev)
+    ws = ops.DecodeWorkspace(64, 16, 16, 8192, torch.device(dev), D=256)
+    us = timeit(lambda: ops.decode_attention(q6, kc6, vc6, bt6, ctx6, 16, 16, 8192, 256 ** -0.5, ws=ws))
+    out["decode_d256_64x1400"] = {"us": round(us, 1), "TBps": round(64 * L * 16 * 256 * 2 * 2 / us / 1e6, 2)}
+    del kc6, vc6
     # adaptive split at other batch sizes (max_ctx 8192 as in the captured decode graphs)
     for Bs in (250, 64, 16, 4):
         kc2, vc2, bt2 = paged_setup([L] * Bs, width=8192 // 64)
