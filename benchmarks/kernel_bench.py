@@ -56,15 +56,20 @@ def main():
         nb = 4096
         kc = torch.zeros(nb, Hkv, 64, D, device=dev, dtype=torch.bfloat16)
         vc = torch.zeros(nb, Hkv, D, 64, device=dev, dtype=torch.bfloat16)
-        for T, contiguous in ((1536, True), (256, False)):
+        for T, kind in ((1536, "prefill"), (256, "decode"), (1190, "mixed")):
             qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
             pos = torch.arange(T, dtype=torch.int32, device=dev) % 4096
-            slots = (torch.arange(T, device=dev) if contiguous
-                     else torch.randperm(nb, device=dev)[:T] * 64 + 17).to(torch.int32)
+            scattered = torch.randperm(nb, device=dev)[:T] * 64 + 17
+            if kind == "prefill":
+                slots = torch.arange(T, device=dev)
+            elif kind == "decode":
+                slots = scattered
+            else:   # a mixed step: 256 decode rows, then one prompt's contiguous slots
+                slots = torch.cat([scattered[:256], torch.arange(T - 256, device=dev) + 64 * 4000])
+            slots = slots.to(torch.int32)
             us = timeit(lambda: ops.rope_cache_(qkv, pos, cs, slots, kc, vc, Hq, Hkv, D))
             moved = T * (Hq + 2 * Hkv) * D * 2 + T * (Hq + Hkv) * D * 2 + 2 * T * Hkv * D * 2
-            out[f"rope_cache_T{T}_{'prefill' if contiguous else 'decode'}"] = {
-                "us": round(us, 1), "TBps": round(moved / us / 1e6, 2)}
+            out[f"rope_cache_T{T}_{kind}"] = {"us": round(us, 1), "TBps": round(moved / us / 1e6, 2)}
         del kc, vc
         if args.only == "rope":
             print(json.dumps(out))

@@ -124,6 +124,9 @@ class EngineConfigSection(ConfigWizard):
     max_batched_tokens: int = configfield("max_batched_tokens", default=16384,
                                           help_txt="Token budget of one prefill step")
     device: str = configfield("device", default="", help_txt="Device ('' = cuda if available)")
+    kv_cache_dtype: str = configfield("kv_cache_dtype", default="auto",
+                                      help_txt="auto | fp8 (e4m3fn KV pages: twice the cached tokens)")
+    fp8: bool = configfield("fp8", default=False, help_txt="W8A8 FP8 projections of the LLM")
 
 
 @configclass

@@ -79,7 +79,8 @@ def get_llm_service():
             eng = LLMEngine(EngineConfig(model=e.llm_preset, max_num_seqs=e.max_num_seqs,
                                          max_model_len=e.max_model_len,
                                          max_batched_tokens=e.max_batched_tokens,
-                                         kv_cache_fraction=e.kv_cache_fraction),
+                                         kv_cache_fraction=e.kv_cache_fraction,
+                                         kv_cache_dtype=e.kv_cache_dtype, fp8=e.fp8),
                             device=_device(cfg), weights=weights)
             svc = EngineService(eng)
             _RUNTIME["llm_service"] = svc

@@ -198,3 +198,57 @@ def test_n_choices_sampling_and_beams(client):
                                              "beam_width": 3, "n": 2}).json()
     assert len(b["choices"]) == 2
     assert client.post("/v1/chat/completions", json={**body, "stream": True}).status_code == 400
+
+
+def test_reference_connector_names_http_and_local(http_url):
+    """The reference's client classes as drop-ins (connectors/compat.py): ChatNVIDIA /
+    NVIDIAEmbeddings / NVIDIARerank and the LlamaIndex-style NVIDIA / NVIDIAEmbedding /
+    LangchainEmbedding, over HTTP against the model server and in-process on the engines."""
+    from types import SimpleNamespace
+
+    from nv_genai_amd.connectors import compat
+    from nv_genai_amd.engine.embed_engine import EmbeddingEngine
+    from nv_genai_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from nv_genai_amd.serving.engine_service import EngineService
+
+    # HTTP (base_url as the reference passes it: http://host:port/v1)
+    llm = compat.ChatNVIDIA(base_url=f"{http_url}/v1", model="tiny-llm", temperature=0.0, max_tokens=4)
+    msg = llm.invoke("hello", ignore_eos=True)
+    assert isinstance(msg, compat.AIMessage) and isinstance(msg.content, str)
+    chunks = list(llm.stream([("system", "be brief"), ("user", "hello")], ignore_eos=True))
+    whole = llm.invoke([("system", "be brief"), ("user", "hello")], ignore_eos=True)
+    assert sum(chunks[1:], chunks[0]).content == whole.content
+    assert len(llm.batch(["a", "b"], ignore_eos=True)) == 2
+    emb_q = compat.NVIDIAEmbeddings(model="tiny-embed", base_url=f"{http_url}/v1")
+    emb_p = compat.NVIDIAEmbeddings(model="tiny-embed", base_url=http_url, model_type="passage")
+    q = emb_q.embed_query("alpha")
+    assert len(q) == 128 and emb_p.embed_query("alpha") == emb_q.embed_documents(["alpha"])[0]
+    docs = [SimpleNamespace(page_content=t, metadata={"source": i}) for i, t in enumerate(["x y", "z", "w v u"])]
+    top = compat.NVIDIARerank(model="tiny-rerank", base_url=http_url, top_n=2).compress_documents(docs, "q")
+    assert len(top) == 2 and all("relevance_score" in d.metadata and "source" in d.metadata for d in top)
+    assert "relevance_score" not in docs[0].metadata          # inputs untouched
+    li = compat.NVIDIA(model="tiny-llm", base_url=http_url, temperature=0.0, max_tokens=4)
+    parts = list(li.stream_complete("hi", ignore_eos=True))
+    assert parts[-1].text == li.complete("hi", ignore_eos=True).text == "".join(p.delta for p in parts)
+    assert li.chat([compat.ChatMessage("user", "hi")], ignore_eos=True).message.role == "assistant"
+    e = compat.LangchainEmbedding(emb_q, embed_batch_size=2)
+    assert len(e.get_text_embedding_batch(["a", "b", "c"])) == 3
+    assert e.get_query_embedding("alpha") == q
+
+    # in-process: the same classes on the engines, no HTTP
+    eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=4, max_batched_tokens=256, max_model_len=512,
+                                 kv_cache_blocks=32), device="cpu")
+    svc = EngineService(eng)
+    try:
+        local = compat.ChatNVIDIA(engine=svc, temperature=0.0, max_tokens=3)
+        a = local.invoke("hello", ignore_eos=True).content
+        assert "".join(c.content for c in local.stream("hello", ignore_eos=True)) == a
+        assert local.bind(max_tokens=1).invoke("hello", ignore_eos=True).content == a[: len(
+            local.bind(max_tokens=1).invoke("hello", ignore_eos=True).content)]
+    finally:
+        svc.shutdown()
+    enc = EmbeddingEngine("encoder-tiny", device="cpu")
+    le = compat.NVIDIAEmbedding(engine=enc)
+    assert len(le.get_query_embedding("alpha")) == enc.dim
+    rr = compat.NVIDIARerank(engine=EmbeddingEngine("reranker-tiny", device="cpu"), top_n=1)
+    assert len(rr.compress_documents(docs, "q")) == 1
