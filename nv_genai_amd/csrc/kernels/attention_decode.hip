@@ -47,10 +47,13 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     const int32_t* __restrict__ block_tables, int max_blocks,
     const int32_t* __restrict__ ctx_lens, int Hq, int Hkv, float scale, int pages_per_part,
     float* __restrict__ part_ml, float* __restrict__ part_o, int window, float v_scale) {
-  auto ld8 = [](const CT* p) -> u16x8 {
-    if constexpr (sizeof(CT) == 2) return load8(p);
-    else return load8_fp8(p);
-  };
+  // fp8 pages at head_dim 128: 16-byte loads (half as many load instructions as 8-byte ones).
+  // Each lane's 16 K bytes cover two d-steps (Q is loaded with the same d order, the dot
+  // product does not care) and its 16 Vt bytes cover 16 consecutive keys of both key
+  // groups: tile rows map to keys as key = 16 (row >> 2) + 8 g + 4 t1 + (row & 3), so lane
+  // group h holds keys 16h + 8g .. 16h + 8g + 7 (bf16 pages keep the 32g + 8h + ... order).
+  constexpr bool F8 = sizeof(CT) == 1;
+  constexpr bool W16 = F8 && D == 128;
   constexpr int DS = D / 32;   // d-steps of the QK^T MFMA
   constexpr int DT = D / 16;   // d-tiles of the PV MFMA
   constexpr int KH = D <= 128 ? 2 : 1;  // 32-key groups per softmax pass
@@ -95,7 +98,7 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     const uint16_t* qp = q + (int64_t)b * q_stride + (int64_t)(kvh * G + (qv ? col : 0)) * D;
 #pragma unroll
     for (int s = 0; s < DS; ++s) {
-      u16x8 v = load8(qp + 32 * s + 8 * h);
+      u16x8 v = load8(qp + (W16 ? 64 * (s >> 1) + 16 * h + 8 * (s & 1) : 32 * s + 8 * h));
       if (!qv) v = (u16x8)(0);
       qf[s] = as_bf16x8(v);
     }
@@ -117,20 +120,52 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 #pragma unroll
     for (int pass = 0; pass < NPASS; ++pass) {
       // K operand loads: tile tau (g = tau>>1, t1 = tau&1), row = col
+      // bf16 fragments, or the raw fp8 words: widened right before their MFMA, so the loads
+      // in flight take half the registers
       u16x8 kf[2 * KH][DS];
-#pragma unroll
-      for (int ti = 0; ti < 2 * KH; ++ti) {
-        const int tau = 2 * KH * pass + ti;
-        const int key = 32 * (tau >> 1) + 8 * (col >> 2) + 4 * (tau & 1) + (col & 3);
-#pragma unroll
-        for (int s = 0; s < DS; ++s) kf[ti][s] = ld8(kp + key * D + 32 * s + 8 * h);
-      }
       u16x8 vf[KH][DT];
+      uint2 kw[2 * KH][DS], vw[KH][DT];
+      if constexpr (W16) {
+        const uint8_t* kb = reinterpret_cast<const uint8_t*>(kp);
+        const uint8_t* vb = reinterpret_cast<const uint8_t*>(vp);
 #pragma unroll
-      for (int gi = 0; gi < KH; ++gi) {
-        const int g = KH * pass + gi;
+        for (int ti = 0; ti < 2 * KH; ++ti) {
+          const int key = 16 * (col >> 2) + 8 * (ti >> 1) + 4 * (ti & 1) + (col & 3);
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) vf[gi][dt] = ld8(vp + (16 * dt + col) * BS + 32 * g + 8 * h);
+          for (int pp = 0; pp < DS / 2; ++pp) {
+            const uint4 w = *reinterpret_cast<const uint4*>(kb + key * D + 64 * pp + 16 * h);
+            kw[ti][2 * pp] = make_uint2(w.x, w.y);
+            kw[ti][2 * pp + 1] = make_uint2(w.z, w.w);
+          }
+        }
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const uint4 w = *reinterpret_cast<const uint4*>(vb + (16 * dt + col) * BS + 16 * h);
+          vw[0][dt] = make_uint2(w.x, w.y);
+          vw[1][dt] = make_uint2(w.z, w.w);
+        }
+      } else {
+#pragma unroll
+        for (int ti = 0; ti < 2 * KH; ++ti) {
+          const int tau = 2 * KH * pass + ti;
+          const int key = 32 * (tau >> 1) + 8 * (col >> 2) + 4 * (tau & 1) + (col & 3);
+#pragma unroll
+          for (int s = 0; s < DS; ++s) {
+            const CT* src = kp + key * D + 32 * s + 8 * h;
+            if constexpr (F8) kw[ti][s] = *reinterpret_cast<const uint2*>(src);
+            else kf[ti][s] = load8(src);
+          }
+        }
+#pragma unroll
+        for (int gi = 0; gi < KH; ++gi) {
+          const int g = KH * pass + gi;
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            const CT* src = vp + (16 * dt + col) * BS + 32 * g + 8 * h;
+            if constexpr (F8) vw[gi][dt] = *reinterpret_cast<const uint2*>(src);
+            else vf[gi][dt] = load8(src);
+          }
+        }
       }
 
       f32x4 sacc[2 * KH];
@@ -138,7 +173,8 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
       for (int ti = 0; ti < 2 * KH; ++ti) {
         sacc[ti] = (f32x4)(0.f);
 #pragma unroll
-        for (int s = 0; s < DS; ++s) sacc[ti] = mfma16(as_bf16x8(kf[ti][s]), qf[s], sacc[ti]);
+        for (int s = 0; s < DS; ++s)
+          sacc[ti] = mfma16(as_bf16x8(F8 ? fp8x8_to_bf16x8(kw[ti][s]) : kf[ti][s]), qf[s], sacc[ti]);
       }
       // mask (the sequence's last, partial page; the window's first page); lane's keys:
       // 32g + 8h + 4t1 + r for tile tau = 2g + t1, reg r. Raw scores: the softmax scale is
@@ -155,7 +191,8 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int tau = 2 * KH * pass + ti;
-            const int key = kbase + 32 * (tau >> 1) + 8 * h + 4 * (tau & 1) + r;
+            const int key = kbase + (W16 ? 16 * h + 8 * (tau >> 1) : 32 * (tau >> 1) + 8 * h) +
+                            4 * (tau & 1) + r;
             const float sv = (key < ctx && key >= key_lo) ? sacc[ti][r] : -INFINITY;
             sacc[ti][r] = sv;
             mloc = fmaxf(mloc, sv);
@@ -190,7 +227,8 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 #pragma unroll
       for (int gi = 0; gi < KH; ++gi)
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16(as_bf16x8(vf[gi][dt]), pf[gi], o[dt]);
+        for (int dt = 0; dt < DT; ++dt)
+          o[dt] = mfma16(as_bf16x8(F8 ? fp8x8_to_bf16x8(vw[gi][dt]) : vf[gi][dt]), pf[gi], o[dt]);
     }
   }
   l += __shfl_xor(l, 16, 64);
