@@ -100,61 +100,75 @@ __global__ void rope_cache_kernel(uint16_t* __restrict__ qkv, const int32_t* __r
   }
 }
 
-// Tiled form for multi-token steps: grid = (token tiles of 64, Hq + 2*Hkv heads). A q/k head
-// block rotates its 64 tokens with 16-B loads/stores (8-element chunks of each half, cos/sin
-// as two float4 pairs) and writes k heads to the K cache; a v head block stages the 64 tokens
-// x D tile in LDS and writes the transposed page rows with lanes = tokens, so the consecutive
-// slots of a prefill chunk become one 128-B store per d row instead of 64 scattered 2-B ones
-// per token (the per-token kernel above wrote Vt at ~2 TB/s effective).
-constexpr int RT = 64;  // tokens per tile
-
+// Tiled form for multi-token steps: a workgroup covers RT = 4096 / D tokens (32 at head_dim
+// 128) and either a group of `hg` rotary heads (q, then k) or one v head.
+// * rotary group: thread = (token, 8-element chunk of each half); it loads its cos/sin once
+//   and rotates the chunk in every head of the group (the loads of all heads issued before
+//   the math), writing k heads to the K cache too. (One workgroup per head re-read the
+//   fp32 cos/sin rows — twice the bytes of the activations — once per head.)
+// * v head: stages the RT tokens x D tile in LDS and writes the transposed page rows with
+//   lanes = tokens, so the consecutive slots of a prefill chunk become one store per d row
+//   instead of scattered 2-B ones per token.
 template <int D, typename CT>
 __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos, const float* __restrict__ cos_sin,
     const int32_t* __restrict__ slots, CT* __restrict__ kc, CT* __restrict__ vc,
-    int64_t T, int Hq, int Hkv, int BS, float inv_ks, float inv_vs) {
+    int64_t T, int Hq, int Hkv, int BS, int hg, float inv_ks, float inv_vs) {
   constexpr int HALF = D / 2;
   constexpr int CH = HALF / 8;       // 8-element chunks per half
+  constexpr int RT = 256 / CH;       // tokens per tile (one thread per token and chunk)
   constexpr int LDP = D + 2;         // padded LDS row (bank-conflict-free column reads)
+  constexpr int HGMAX = 8;
   __shared__ uint16_t tile[RT * LDP];
   const int64_t t0 = (int64_t)blockIdx.x * RT;
-  const int h = blockIdx.y;
+  const int nrot = Hq + Hkv;
+  const int ngroups = (nrot + hg - 1) / hg;
   const int64_t row = (int64_t)(Hq + 2 * Hkv) * D;
-  if (h < Hq + Hkv) {
-    for (int i = threadIdx.x; i < RT * CH; i += blockDim.x) {
-      const int64_t t = t0 + i / CH;
-      if (t >= T) break;
-      const int i0 = (i % CH) * 8;
-      uint16_t* x = qkv + t * row + (int64_t)h * D;
-      const float* cs = cos_sin + (int64_t)pos[t] * D;
-      const u16x8 a = load8(x + i0), b = load8(x + HALF + i0);
-      const float4 c0 = *reinterpret_cast<const float4*>(cs + i0);
-      const float4 c1 = *reinterpret_cast<const float4*>(cs + i0 + 4);
-      const float4 s0 = *reinterpret_cast<const float4*>(cs + HALF + i0);
-      const float4 s1 = *reinterpret_cast<const float4*>(cs + HALF + i0 + 4);
-      const float c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-      const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  if ((int)blockIdx.y < ngroups) {
+    const int64_t t = t0 + threadIdx.x / CH;
+    if (t >= T) return;
+    const int i0 = (threadIdx.x % CH) * 8;
+    const int h0 = blockIdx.y * hg, h1 = min(nrot, h0 + hg);
+    const float* cs = cos_sin + (int64_t)pos[t] * D;
+    const float4 c0 = *reinterpret_cast<const float4*>(cs + i0);
+    const float4 c1 = *reinterpret_cast<const float4*>(cs + i0 + 4);
+    const float4 s0 = *reinterpret_cast<const float4*>(cs + HALF + i0);
+    const float4 s1 = *reinterpret_cast<const float4*>(cs + HALF + i0 + 4);
+    uint16_t* xr = qkv + t * row + i0;
+    u16x8 a[HGMAX], b[HGMAX];
+#pragma unroll
+    for (int j = 0; j < HGMAX; ++j)
+      if (h0 + j < h1) {
+        a[j] = load8(xr + (int64_t)(h0 + j) * D);
+        b[j] = load8(xr + (int64_t)(h0 + j) * D + HALF);
+      }
+    const float c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const int slot = slots ? slots[t] : -1;
+#pragma unroll
+    for (int j = 0; j < HGMAX; ++j) {
+      const int h = h0 + j;
+      if (h >= h1) break;
       u16x8 oa, ob;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x1 = bf2f(a[j]), x2 = bf2f(b[j]);
-        oa[j] = f2bf(x1 * c[j] - x2 * sn[j]);
-        ob[j] = f2bf(x2 * c[j] + x1 * sn[j]);
+      for (int e = 0; e < 8; ++e) {
+        const float x1 = bf2f(a[j][e]), x2 = bf2f(b[j][e]);
+        oa[e] = f2bf(x1 * c[e] - x2 * sn[e]);
+        ob[e] = f2bf(x2 * c[e] + x1 * sn[e]);
       }
-      store8(x + i0, oa);
-      store8(x + HALF + i0, ob);
-      const int slot = (slots && h >= Hq) ? slots[t] : -1;
-      if (slot >= 0) {
-        CT* dst = kc + (((int64_t)(slot / BS) * Hkv + (h - Hq)) * BS + slot % BS) * D;
-        put8(dst + i0, oa, inv_ks);
-        put8(dst + HALF + i0, ob, inv_ks);
+      store8(xr + (int64_t)h * D, oa);
+      store8(xr + (int64_t)h * D + HALF, ob);
+      if (h >= Hq && slot >= 0) {
+        CT* dst = kc + (((int64_t)(slot / BS) * Hkv + (h - Hq)) * BS + slot % BS) * D + i0;
+        put8(dst, oa, inv_ks);
+        put8(dst + HALF, ob, inv_ks);
       }
     }
     return;
   }
   if (slots == nullptr) return;
-  const int vh = h - Hq - Hkv;
-  // stage V[t0:t0+64, vh, :] (4-byte pairs; padded rows keep 4-B alignment)
+  const int vh = blockIdx.y - ngroups;
+  // stage V[t0:t0+RT, vh, :] (4-byte pairs; padded rows keep 4-B alignment)
   for (int i = threadIdx.x; i < RT * (D / 2); i += blockDim.x) {
     const int r = i / (D / 2), c2 = i % (D / 2);
     const int64_t t = t0 + r;
@@ -163,21 +177,31 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     *reinterpret_cast<uint32_t*>(tile + r * LDP + 2 * c2) = v;
   }
   __syncthreads();
+  // lane -> (token = lane % RT, d-phase = lane / RT): RT lanes store one d row's tokens
+  constexpr int PH = 64 / RT;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int64_t t = t0 + lane;
+  const int tl = lane % RT, ph = lane / RT;
+  const int64_t t = t0 + tl;
   const int slot = t < T ? slots[t] : -1;
   if (slot < 0) return;
   CT* dst = vc + ((int64_t)(slot / BS) * Hkv + vh) * D * BS + slot % BS;
-  for (int d = w; d < D; d += nw) put1(dst + (int64_t)d * BS, tile[lane * LDP + d], inv_vs);
+  for (int d = w * PH + ph; d < D; d += nw * PH) put1(dst + (int64_t)d * BS, tile[tl * LDP + d], inv_vs);
 }
 
 template <typename CT>
 static void rope_dispatch(uint16_t* qkv, const int32_t* pos, const float* cos_sin,
                           const int32_t* slots, CT* kc, CT* vc, int64_t T, int Hq, int Hkv, int D,
                           int BS, float inv_ks, float inv_vs, hipStream_t stream) {
-  if (T >= RT) {
-    dim3 grid((unsigned)((T + RT - 1) / RT), (unsigned)(Hq + 2 * Hkv)), block(256);
-#define NGA_RT(DD) rope_cache_tiled_kernel<DD, CT><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS, inv_ks, inv_vs)
+  const int rt = 4096 / D;   // tokens per tile of the tiled kernel
+  if (T >= rt) {
+    // rotary heads per workgroup: enough workgroups to fill the chip, up to 8 heads sharing
+    // one cos/sin load
+    const int64_t tiles = (T + rt - 1) / rt;
+    const int nrot = Hq + Hkv;
+    int hg = 8;
+    while (hg > 1 && tiles * ((nrot + hg - 1) / hg) < 512) hg /= 2;
+    dim3 grid((unsigned)tiles, (unsigned)((nrot + hg - 1) / hg + Hkv)), block(256);
+#define NGA_RT(DD) rope_cache_tiled_kernel<DD, CT><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS, hg, inv_ks, inv_vs)
     if (D == 128) NGA_RT(128); else if (D == 256) NGA_RT(256); else if (D == 64) NGA_RT(64);
 #undef NGA_RT
     return;
