@@ -106,45 +106,51 @@ def main():
     if args.only == "prefill":
         print(json.dumps(out))
         return
-    kc, vc, bt = paged_setup([L] * B, width=8192 // 64)
-    q = torch.randn(B, Hq * D, device=dev, dtype=torch.bfloat16)
-    ctx = torch.full((B,), L, dtype=torch.int32, device=dev)
-    for ppp in (None, 16, 32):
-        ws = ops.DecodeWorkspace(B, Hq, Hkv, 8192, torch.device(dev), ppp)
-        us = timeit(lambda: ops.decode_attention(q, kc, vc, bt, ctx, Hq, Hkv, 8192, D ** -0.5, ws=ws))
-        out[f"decode_256x1400_ppp{ppp}"] = {"us": round(us, 1), "TBps": round(B * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
-    # fp8 e4m3fn KV pages (half the bytes; TB/s counted on the bytes actually read)
-    kc8, vc8 = kc.to(torch.float8_e4m3fn), vc.to(torch.float8_e4m3fn)
-    ws = ops.DecodeWorkspace(B, Hq, Hkv, 8192, torch.device(dev))
-    us = timeit(lambda: ops.decode_attention(q, kc8, vc8, bt, ctx, Hq, Hkv, 8192, D ** -0.5, ws=ws))
-    out["decode_256x1400_fp8kv"] = {"us": round(us, 1), "TBps": round(B * L * Hkv * D * 2 / us / 1e6, 2)}
-    del kc8, vc8
-    # head_dim 256, MHA (Gemma-7B: 16 q = 16 kv heads)
-    kc6, vc6, bt6 = paged_setup([L] * 64, Hkv=16, D=256, width=8192 // 64)
-    q6 = torch.randn(64, 16 * 256, device=dev, dtype=torch.bfloat16)
-    ctx6 = torch.full((64,), L, dtype=torch.int32, device=dev)
-    ws = ops.DecodeWorkspace(64, 16, 16, 8192, torch.device(dev), D=256)
-    us = timeit(lambda: ops.decode_attention(q6, kc6, vc6, bt6, ctx6, 16, 16, 8192, 256 ** -0.5, ws=ws))
-    out["decode_d256_64x1400"] = {"us": round(us, 1), "TBps": round(64 * L * 16 * 256 * 2 * 2 / us / 1e6, 2)}
-    del kc6, vc6
-    # adaptive split at other batch sizes (max_ctx 8192 as in the captured decode graphs)
-    for Bs in (250, 64, 16, 4):
-        kc2, vc2, bt2 = paged_setup([L] * Bs, width=8192 // 64)
-        q2 = torch.randn(Bs, Hq * D, device=dev, dtype=torch.bfloat16)
-        ctx2 = torch.full((Bs,), L, dtype=torch.int32, device=dev)
-        ws = ops.DecodeWorkspace(Bs, Hq, Hkv, 8192, torch.device(dev))
-        us = timeit(lambda: ops.decode_attention(q2, kc2, vc2, bt2, ctx2, Hq, Hkv, 8192, D ** -0.5, ws=ws))
-        out[f"decode_{Bs}x1400_auto"] = {"us": round(us, 1), "parts": ws.nparts(Bs),
-                                         "TBps": round(Bs * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
-    if args.only == "decode":
-        print(json.dumps(out))
-        return
+    if args.only in ("", "decode"):
+        kc, vc, bt = paged_setup([L] * B, width=8192 // 64)
+        q = torch.randn(B, Hq * D, device=dev, dtype=torch.bfloat16)
+        ctx = torch.full((B,), L, dtype=torch.int32, device=dev)
+        for ppp in (None, 16, 32):
+            ws = ops.DecodeWorkspace(B, Hq, Hkv, 8192, torch.device(dev), ppp)
+            us = timeit(lambda: ops.decode_attention(q, kc, vc, bt, ctx, Hq, Hkv, 8192, D ** -0.5, ws=ws))
+            out[f"decode_256x1400_ppp{ppp}"] = {"us": round(us, 1), "TBps": round(B * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
+        # fp8 e4m3fn KV pages (half the bytes; TB/s counted on the bytes actually read)
+        kc8, vc8 = kc.to(torch.float8_e4m3fn), vc.to(torch.float8_e4m3fn)
+        ws = ops.DecodeWorkspace(B, Hq, Hkv, 8192, torch.device(dev))
+        us = timeit(lambda: ops.decode_attention(q, kc8, vc8, bt, ctx, Hq, Hkv, 8192, D ** -0.5, ws=ws))
+        out["decode_256x1400_fp8kv"] = {"us": round(us, 1), "TBps": round(B * L * Hkv * D * 2 / us / 1e6, 2)}
+        del kc8, vc8
+        # head_dim 256, MHA (Gemma-7B: 16 q = 16 kv heads)
+        kc6, vc6, bt6 = paged_setup([L] * 64, Hkv=16, D=256, width=8192 // 64)
+        q6 = torch.randn(64, 16 * 256, device=dev, dtype=torch.bfloat16)
+        ctx6 = torch.full((64,), L, dtype=torch.int32, device=dev)
+        ws = ops.DecodeWorkspace(64, 16, 16, 8192, torch.device(dev), D=256)
+        us = timeit(lambda: ops.decode_attention(q6, kc6, vc6, bt6, ctx6, 16, 16, 8192, 256 ** -0.5, ws=ws))
+        out["decode_d256_64x1400"] = {"us": round(us, 1), "TBps": round(64 * L * 16 * 256 * 2 * 2 / us / 1e6, 2)}
+        del kc6, vc6
+        # adaptive split at other batch sizes (max_ctx 8192 as in the captured decode graphs)
+        for Bs in (250, 64, 16, 4):
+            kc2, vc2, bt2 = paged_setup([L] * Bs, width=8192 // 64)
+            q2 = torch.randn(Bs, Hq * D, device=dev, dtype=torch.bfloat16)
+            ctx2 = torch.full((Bs,), L, dtype=torch.int32, device=dev)
+            ws = ops.DecodeWorkspace(Bs, Hq, Hkv, 8192, torch.device(dev))
+            us = timeit(lambda: ops.decode_attention(q2, kc2, vc2, bt2, ctx2, Hq, Hkv, 8192, D ** -0.5, ws=ws))
+            out[f"decode_{Bs}x1400_auto"] = {"us": round(us, 1), "parts": ws.nparts(Bs),
+                                             "TBps": round(Bs * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
+        if args.only == "decode":
+            print(json.dumps(out))
+            return
     V = 128256
     logits = torch.randn(B, V, device=dev) * 3
     z = lambda v, dt=torch.float32: torch.full((B,), v, dtype=dt, device=dev)  # noqa: E731
+    flat = torch.randn(B, V, device=dev) * 0.5
     for nm, (t, k, p) in {"sample_greedy": (0.0, 0, 1.0), "sample_t0.2_p0.7": (0.2, 0, 0.7),
-                          "sample_t1_k50": (1.0, 50, 1.0)}.items():
-        us = timeit(lambda: ops.sample(logits, z(t), z(k, torch.int32), z(p), z(1, torch.int64), z(0, torch.int64)))
+                          "sample_t1_k50": (1.0, 50, 1.0), "sample_t1_k50_p0.9": (1.0, 50, 0.9),
+                          "sample_flat_t1_p0.95": (1.0, 0, 0.95),
+                          "sample_flat_t1_p0.9999": (1.0, 0, 0.9999)}.items():
+        lg = flat if nm.startswith("sample_flat") else logits
+        prm = (z(t), z(k, torch.int32), z(p), z(1, torch.int64), z(0, torch.int64))
+        us = timeit(lambda: ops.sample(lg, *prm))
         out[nm] = {"us": round(us, 1)}
     print(json.dumps(out))
 

@@ -1,13 +1,20 @@
 // Token sampling over a full vocabulary row (up to 256K: Gemma) (K7 in SURVEY.md §2.C), one 1024-thread
-// workgroup per sequence, no sort:
+// workgroup per sequence, no full sort:
 //   * repetition penalty (TRT-LLM semantics: divide positive / multiply negative logits of
 //     every token seen in prompt+output) through an LDS bitmap of the row's history;
 //   * temperature; greedy when temperature <= 0 or top_k == 1;
-//   * top-k and top-p thresholds by a 3-level (11/11/10-bit) radix descent on order-preserving
-//     float keys — top-k descends on counts, top-p on probability mass restricted to the
-//     top-k set — so each costs 3 L2-resident passes over the row instead of a 128K sort;
+//   * top-k / top-p thresholds, fast path: one pass bins every token with v > M - 16 by its
+//     distance to the row max (2048 linear bins, so the LDS atomics spread out instead of piling
+//     onto a few exponent bins; the far tail takes no atomic), a scan finds the bin where the
+//     running count / probability mass reaches the target, a second pass gathers that bin's keys
+//     (at most 2048) into LDS, and a bitonic sort + scan there gives the exact threshold;
+//   * exact fallback when the crossing lies in the far tail or its bin is too full (flat rows,
+//     p close to 1): 3-level (11/11/10-bit) radix descent on order-preserving float keys;
 //   * the draw itself is Gumbel-max over the kept tokens with a counter-based RNG keyed on
 //     (seed, step, token): deterministic for a given seed, no global RNG state.
+// Every pass over the row keeps eight 16-byte loads in flight per thread. Histogram weights are
+// 64-bit fixed point (2^-40 units of exp(v - M)) so the LDS atomics are ds_add_u64: LDS
+// ds_add_f32 measured ~8x slower on gfx950 (scripts/dev/lds_atomic_bench.hip).
 // Also returns the chosen token's log-probability under the temperature-scaled distribution.
 #include "common.h"
 #include "kernels.h"
@@ -17,21 +24,60 @@ namespace nga {
 namespace {
 constexpr int NT = 1024;
 constexpr int NBINS = 2048;
+constexpr int CAP = 2048;        // keys the fast path sorts in LDS
+constexpr float DRANGE = 16.f;   // fast-path bins cover v in (M - DRANGE, M]
+constexpr float DSCALE = NBINS / DRANGE;
+constexpr int UNROLL = 8;
 
 __device__ __forceinline__ uint32_t fkey(float f) {
   const uint32_t u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-// Inclusive suffix scan (from the top bin) of NBINS values held 2 per thread; returns the
-// bin where the running total first reaches `target`, and the total strictly above it.
+__device__ __forceinline__ float fval(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+struct ArgMax {
+  float v;
+  int i;
+};
+
+constexpr double FIX = 1099511627776.0;  // 2^40: fixed-point unit of the mass histograms
+
+struct Smem {
+  union {
+    uint32_t bitmap[8192];  // history bitmap (repetition penalty only), V <= 262144 (Gemma: 256000)
+    struct {
+      union {
+        uint64_t q[NBINS];  // bin weights: counts or fixed-point mass
+        float w[NBINS];     // candidate weights (fast path, after the bin scan)
+      } h;
+      uint32_t cand[CAP];
+      union {
+        uint64_t q[NT];
+        float f[NT];
+      } scan;
+    } s;
+  } u;
+  float red[NT / 64];
+  ArgMax ared[NT / 64];
+  int ncand;
+  int sel;
+  float sel_above_f;
+  uint64_t sel_above_q;
+};
+
+// Top-down crossing over nb <= 2*NT values (bins[nb-1] is the top): inclusive suffix scan,
+// returns the bin where the running total first reaches `target` and the total strictly above
+// it, or -1 (with the grand total in *above_out) when the total stays below target.
 template <typename T>
-__device__ int find_crossing(T* bins, T target, T* above_out, T* scan) {
+__device__ __forceinline__ int find_crossing(const T* bins, int nb, T target, T* above_out, T* scan, Smem& sm) {
   const int t = threadIdx.x;
-  // thread t owns bins (NBINS-1-2t) and (NBINS-2-2t): descending order
-  const int b0 = NBINS - 1 - 2 * t, b1 = b0 - 1;
-  T v0 = bins[b0], v1 = bins[b1];
-  T mine = v0 + v1;
+  // thread t owns bins (nb-1-2t) and (nb-2-2t): descending order
+  const int b0 = nb - 1 - 2 * t, b1 = b0 - 1;
+  const T v0 = b0 >= 0 ? bins[b0] : (T)0, v1 = b1 >= 0 ? bins[b1] : (T)0;
+  const T mine = v0 + v1;
   scan[t] = mine;
   __syncthreads();
   for (int off = 1; off < NT; off <<= 1) {
@@ -42,43 +88,53 @@ __device__ int find_crossing(T* bins, T target, T* above_out, T* scan) {
   }
   const T incl = scan[t];
   const T excl = incl - mine;
-  __shared__ int sel;
-  __shared__ T sel_above;
-  if (t == 0) {
-    sel = -1;
-    sel_above = (T)0;
-  }
+  if (t == 0) sm.sel = -1;
   __syncthreads();
   if (excl < target && incl >= target) {
-    if (excl + v0 >= target) {
-      sel = b0;
-      sel_above = excl;
-    } else {
-      sel = b1;
-      sel_above = excl + v0;
-    }
+    const bool first = excl + v0 >= target;
+    sm.sel = first ? b0 : b1;
+    const T a = first ? excl : excl + v0;
+    if constexpr (sizeof(T) == 8)
+      sm.sel_above_q = a;
+    else
+      sm.sel_above_f = a;
   }
   __syncthreads();
-  int s = sel;
-  T a = sel_above;
-  if (s < 0) {  // target beyond total (rounding): take the lowest populated bin
-    s = 0;
-    a = scan[NT - 1] - bins[0];
-  }
-  *above_out = a;
+  const int s = sm.sel;
+  T a;
+  if constexpr (sizeof(T) == 8)
+    a = sm.sel_above_q;
+  else
+    a = sm.sel_above_f;
+  *above_out = s >= 0 ? a : scan[NT - 1];
   __syncthreads();
   return s;
 }
 
-// Visit every element of a row: float4 loads for the body (rows of the [B, V] fp32 logits
-// are 16-B aligned when V % 4 == 0), scalar loads for any tail. f(index, value).
+// Visit every element of a row: UNROLL float4 loads in flight per thread for the body (rows
+// of the [B, V] fp32 logits are 16-B aligned when V % 4 == 0), scalar loads for any tail.
+// f(index, value) is called by every lane of the workgroup in step for the unrolled body.
 template <typename F>
 __device__ __forceinline__ void for_row(const float* __restrict__ x, int V, F f) {
   const int t = threadIdx.x;
   if ((V & 3) == 0) {
     const float4* x4 = reinterpret_cast<const float4*>(x);
     const int n4 = V >> 2;
-    for (int j = t; j < n4; j += NT) {
+    int j = t;
+    for (; j + (UNROLL - 1) * NT < n4; j += UNROLL * NT) {
+      float4 v[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) v[u] = x4[j + u * NT];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const int i = 4 * (j + u * NT);
+        f(i, v[u].x);
+        f(i + 1, v[u].y);
+        f(i + 2, v[u].z);
+        f(i + 3, v[u].w);
+      }
+    }
+    for (; j < n4; j += NT) {
       const float4 v = x4[j];
       f(4 * j, v.x);
       f(4 * j + 1, v.y);
@@ -89,11 +145,6 @@ __device__ __forceinline__ void for_row(const float* __restrict__ x, int V, F f)
     for (int i = t; i < V; i += NT) f(i, x[i]);
   }
 }
-
-struct ArgMax {
-  float v;
-  int i;
-};
 
 __device__ __forceinline__ ArgMax am_max(ArgMax a, ArgMax b) {
   return (b.v > a.v || (b.v == a.v && b.i < a.i)) ? b : a;
@@ -114,6 +165,143 @@ __device__ ArgMax block_argmax(ArgMax a, ArgMax* red) {
   for (int k = 1; k < NT / 64; ++k) r = am_max(r, red[k]);
   return r;
 }
+
+__device__ __forceinline__ int dist_bin(float d) { return min((int)(d * DSCALE), NBINS - 1); }
+
+// exp(v - M) <= 1 in units of 2^-40; a row's total stays below 2^58
+__device__ __forceinline__ uint64_t fixed_mass(float dv) {
+  return (uint64_t)(__expf(dv) * (float)FIX);
+}
+template <bool MASS>
+__device__ __forceinline__ uint64_t to_fixed(float w) {
+  return MASS ? (uint64_t)((double)w * FIX) : (uint64_t)w;
+}
+template <bool MASS>
+__device__ __forceinline__ float from_fixed(uint64_t q) {
+  return MASS ? (float)((double)q * (1.0 / FIX)) : (float)q;
+}
+
+// Fast threshold: the largest key thr >= floor_key whose weight {key >= thr} reaches target,
+// weight = 1 per token (MASS = false: top-k) or exp(v - M) (MASS = true: top-p). Also returns
+// the probability mass (relative to exp(M)) kept by that threshold. Returns false, uniformly
+// over the workgroup, when the caller must take the radix descent instead.
+template <bool MASS>
+__device__ __forceinline__ bool fast_select(const float* __restrict__ x, int V, float inv_t, float M,
+                            uint32_t floor_key, float target, Smem& sm, uint32_t* thr_out,
+                            float* kept_out) {
+  const int t = threadIdx.x, lane = t & 63;
+  for (int i = t; i < NBINS; i += NT) sm.u.s.h.q[i] = 0ull;
+  if (t == 0) sm.ncand = 0;
+  __syncthreads();
+  for_row(x, V, [&](int, float raw) {
+    const float v = raw * inv_t;
+    const float d = M - v;
+    if (d < DRANGE && fkey(v) >= floor_key)
+      atomicAdd(&sm.u.s.h.q[NBINS - 1 - dist_bin(d)], MASS ? fixed_mass(v - M) : 1ull);
+  });
+  __syncthreads();
+  uint64_t above_q;
+  const int bin = find_crossing<uint64_t>(sm.u.s.h.q, NBINS, to_fixed<MASS>(target), &above_q,
+                                          sm.u.s.scan.q, sm);
+  if (bin < 0) return false;
+  const float above = from_fixed<MASS>(above_q);
+  const int cbin = NBINS - 1 - bin;  // crossing bin in distance order
+
+  // gather the crossing bin's keys (wave-aggregated slots), and the mass of the bins above it
+  float m_above = 0.f;
+  for_row(x, V, [&](int, float raw) {
+    const float v = raw * inv_t;
+    const float d = M - v;
+    const uint32_t key = fkey(v);
+    bool want = false;
+    if (d < DRANGE && key >= floor_key) {
+      const int db = dist_bin(d);
+      if (db < cbin) m_above += __expf(v - M);
+      want = db == cbin;
+    }
+    const uint64_t m = __ballot(want);
+    if (m != 0) {
+      const int leader = __ffsll((unsigned long long)m) - 1;
+      int base = 0;
+      if (lane == leader) base = atomicAdd(&sm.ncand, __popcll(m));
+      base = __shfl(base, leader, 64);
+      if (want) {
+        const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+        if (pos < CAP) sm.u.s.cand[pos] = key;
+      }
+    }
+  });
+  m_above = block_sum(m_above, sm.red);  // starts and ends with a barrier
+  const int n = sm.ncand;
+  if (n > CAP || n == 0) return false;
+  int sn = 2;
+  while (sn < n) sn <<= 1;
+  for (int i = n + t; i < sn; i += NT) sm.u.s.cand[i] = 0u;  // pads sort below every real key
+  // bitonic sort, ascending
+  for (int size = 2; size <= sn; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      if (t < (sn >> 1)) {
+        const int i = 2 * t - (t & (stride - 1));
+        const int j = i + stride;
+        const uint32_t a = sm.u.s.cand[i], b = sm.u.s.cand[j];
+        if ((a > b) == ((i & size) == 0)) {
+          sm.u.s.cand[i] = b;
+          sm.u.s.cand[j] = a;
+        }
+      }
+    }
+  __syncthreads();
+  const int lo = sn - n;  // first real key
+  for (int i = t; i < sn; i += NT)
+    sm.u.s.h.w[i] = i < lo ? 0.f : (MASS ? __expf(fval(sm.u.s.cand[i]) - M) : 1.f);
+  __syncthreads();
+  float above2;
+  int c = find_crossing<float>(sm.u.s.h.w, sn, target - above, &above2, sm.u.s.scan.f, sm);
+  if (c < lo) c = lo;  // rounding: keep the whole bin
+  const uint32_t thr = sm.u.s.cand[c];
+  float km = 0.f;
+  for (int i = lo + t; i < sn; i += NT)
+    if (sm.u.s.cand[i] >= thr) km += __expf(fval(sm.u.s.cand[i]) - M);
+  km = block_sum(km, sm.red);
+  *thr_out = thr;
+  *kept_out = m_above + km;
+  return true;
+}
+
+// Exact radix descent (11/11/10 bits of the key) on counts (top-k) or fixed-point mass (top-p,
+// restricted to key >= floor_key). Used when the fast path declines.
+template <bool MASS>
+__device__ __forceinline__ uint32_t radix_select(const float* __restrict__ x, int V, float inv_t,
+                                                 float M, uint32_t floor_key, float target, Smem& sm) {
+  const int t = threadIdx.x;
+  uint32_t prefix = 0, mask = 0;
+  uint64_t remaining = to_fixed<MASS>(target);
+  for (int lvl = 0; lvl < 3; ++lvl) {
+    for (int i = t; i < NBINS; i += NT) sm.u.s.h.q[i] = 0ull;
+    __syncthreads();
+    const int sh = lvl == 0 ? 21 : lvl == 1 ? 10 : 0;
+    const uint32_t bm = lvl == 2 ? 0x3ffu : 0x7ffu;
+    for_row(x, V, [&](int, float raw) {
+      const float v = raw * inv_t;
+      const uint32_t key = fkey(v);
+      if ((key & mask) == prefix && key >= floor_key)
+        atomicAdd(&sm.u.s.h.q[(key >> sh) & bm], MASS ? fixed_mass(v - M) : 1ull);
+    });
+    __syncthreads();
+    uint64_t above;
+    int bin = find_crossing<uint64_t>(sm.u.s.h.q, NBINS, remaining, &above, sm.u.s.scan.q, sm);
+    if (bin < 0) {  // target beyond total (rounding): take the lowest populated bin
+      bin = 0;
+      above -= sm.u.s.h.q[0];
+    }
+    remaining -= above;
+    prefix |= ((uint32_t)bin) << sh;
+    mask |= bm << sh;
+    __syncthreads();
+  }
+  return prefix;
+}
 }  // namespace
 
 __global__ void __launch_bounds__(NT) sample_kernel(
@@ -122,29 +310,23 @@ __global__ void __launch_bounds__(NT) sample_kernel(
     const float* __restrict__ rep_penalty, const int32_t* __restrict__ history, int hist_len,
     const int64_t* __restrict__ seeds, const int64_t* __restrict__ steps,
     int32_t* __restrict__ out_tok, float* __restrict__ out_logprob) {
-  __shared__ uint32_t bitmap[8192];  // history bitmap, V <= 262144 (Gemma: 256000)
-  __shared__ uint32_t hcnt[NBINS];
-  __shared__ float hmass[NBINS];
-  __shared__ uint32_t scan_u[NT];
-  __shared__ float scan_f[NT];
-  __shared__ float red[NT / 64];
-  __shared__ ArgMax ared[NT / 64];
+  __shared__ Smem sm;
 
   const int row = blockIdx.x, t = threadIdx.x;
   float* x = logits + (int64_t)row * V;
   const float pen = rep_penalty ? rep_penalty[row] : 1.f;
 
   if (pen != 1.f && history != nullptr) {
-    for (int i = t; i < 8192; i += NT) bitmap[i] = 0;
+    for (int i = t; i < 8192; i += NT) sm.u.bitmap[i] = 0;
     __syncthreads();
     const int32_t* hs = history + (int64_t)row * hist_len;
     for (int i = t; i < hist_len; i += NT) {
       const int tok = hs[i];
-      if (tok >= 0 && tok < V) atomicOr(&bitmap[tok >> 5], 1u << (tok & 31));
+      if (tok >= 0 && tok < V) atomicOr(&sm.u.bitmap[tok >> 5], 1u << (tok & 31));
     }
     __syncthreads();
     for (int i = t; i < V; i += NT)
-      if (bitmap[i >> 5] & (1u << (i & 31))) {
+      if (sm.u.bitmap[i >> 5] & (1u << (i & 31))) {
         const float v = x[i];
         x[i] = v > 0.f ? v / pen : v * pen;
       }
@@ -171,9 +353,9 @@ __global__ void __launch_bounds__(NT) sample_kernel(
     }
   });
   const float m_thr = am.v;
-  am = block_argmax(am, ared);
+  am = block_argmax(am, sm.ared);
   const float M = am.v;
-  const float Z = block_sum(m_thr == -INFINITY ? 0.f : z * __expf(m_thr - M), red);
+  const float Z = block_sum(m_thr == -INFINITY ? 0.f : z * __expf(m_thr - M), sm.red);
   const float logZ = __logf(Z);
 
   if (greedy) {
@@ -187,57 +369,22 @@ __global__ void __launch_bounds__(NT) sample_kernel(
   uint32_t thr = 0u;  // keep tokens with fkey(x * inv_t) >= thr
   float kept_mass = Z;
   if (k > 0 && k < V) {
-    uint32_t prefix = 0, mask = 0;
-    int remaining = k;
-    const int shifts[3] = {21, 10, 0};
-    const int widths[3] = {11, 11, 10};
-    for (int lvl = 0; lvl < 3; ++lvl) {
-      for (int i = t; i < NBINS; i += NT) hcnt[i] = 0;
-      __syncthreads();
-      const int sh = shifts[lvl];
-      const uint32_t bm = (1u << widths[lvl]) - 1u;
-      for_row(x, V, [&](int, float raw) {
-        const uint32_t key = fkey(raw * inv_t);
-        if ((key & mask) == prefix) atomicAdd(&hcnt[(key >> sh) & bm], 1u);
-      });
-      __syncthreads();
-      uint32_t above;
-      const int bin = find_crossing<uint32_t>(hcnt, (uint32_t)remaining, &above, scan_u);
-      remaining -= (int)above;
-      prefix |= ((uint32_t)bin) << sh;
-      mask |= bm << sh;
-    }
-    thr = prefix;
-    float km = 0.f;
-    for_row(x, V, [&](int, float raw) {
-      const float v = raw * inv_t;
-      if (fkey(v) >= thr) km += __expf(v - M);
-    });
-    kept_mass = block_sum(km, red);
-  }
-  if (p < 1.f) {
-    uint32_t prefix = 0, mask = 0;
-    float remaining = p * kept_mass;
-    const int shifts[3] = {21, 10, 0};
-    const int widths[3] = {11, 11, 10};
-    for (int lvl = 0; lvl < 3; ++lvl) {
-      for (int i = t; i < NBINS; i += NT) hmass[i] = 0.f;
-      __syncthreads();
-      const int sh = shifts[lvl];
-      const uint32_t bm = (1u << widths[lvl]) - 1u;
+    if (!fast_select<false>(x, V, inv_t, M, 0u, (float)k, sm, &thr, &kept_mass)) {
+      thr = radix_select<false>(x, V, inv_t, M, 0u, (float)k, sm);
+      float km = 0.f;
       for_row(x, V, [&](int, float raw) {
         const float v = raw * inv_t;
-        const uint32_t key = fkey(v);
-        if ((key & mask) == prefix && key >= thr) atomicAdd(&hmass[(key >> sh) & bm], __expf(v - M));
+        if (fkey(v) >= thr) km += __expf(v - M);
       });
-      __syncthreads();
-      float above;
-      const int bin = find_crossing<float>(hmass, remaining, &above, scan_f);
-      remaining -= above;
-      prefix |= ((uint32_t)bin) << sh;
-      mask |= bm << sh;
+      kept_mass = block_sum(km, sm.red);
     }
-    thr = prefix > thr ? prefix : thr;
+  }
+  if (p < 1.f) {
+    uint32_t tp;
+    float unused;
+    if (!fast_select<true>(x, V, inv_t, M, thr, p * kept_mass, sm, &tp, &unused))
+      tp = radix_select<true>(x, V, inv_t, M, thr, p * kept_mass, sm);
+    thr = tp > thr ? tp : thr;
   }
 
   // Gumbel-max draw over kept tokens
@@ -252,7 +399,7 @@ __global__ void __launch_bounds__(NT) sample_kernel(
       best = am_max(best, ArgMax{v + g, i});
     }
   });
-  best = block_argmax(best, ared);
+  best = block_argmax(best, sm.ared);
   if (t == 0) {
     const int tok = best.i == 0x7fffffff ? am.i : best.i;
     out_tok[row] = tok;

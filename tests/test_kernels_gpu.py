@@ -407,6 +407,63 @@ def test_sample_odd_vocab_and_masked_logits(gpu):
     assert (tok.cpu() == tok_r).float().mean() >= 0.8
 
 
+def _kept_set(xs, k, p, slack):
+    """Reference truncation in float64: top-k, then the top-p nucleus widened by `slack`."""
+    xs = xs.double()
+    keep = torch.ones_like(xs, dtype=torch.bool)
+    if 0 < k < xs.numel():
+        keep &= xs >= torch.topk(xs, k).values[-1]
+    if p < 1.0:
+        pm = torch.exp(xs - xs.max()) * keep
+        order = torch.argsort(xs, descending=True)
+        cs = torch.cumsum(pm[order], 0)
+        cut = int(torch.searchsorted(cs, torch.tensor([min(p + slack, 1.0) * float(pm.sum())], dtype=cs.dtype)))
+        keep &= xs >= xs[order[min(cut, xs.numel() - 1)]]
+    return keep
+
+
+def test_sample_threshold_fast_path_and_fallbacks(gpu):
+    """Rows chosen to take each threshold route of sampling.hip: the binned fast path (peaky and
+    flat rows), the radix fallback for a crossing in the far tail (p close to 1), for a crossing
+    bin with more than 2048 keys (quantised logits, a constant row), and top-k followed by top-p.
+    Every draw must lie in the reference's kept set, and most draws equal the reference's."""
+    torch.manual_seed(21)
+    V = 128256
+    rows = [
+        (torch.randn(V) * 3, 0.2, 0, 0.7),                   # peaky, fast
+        (torch.randn(V) * 0.5, 1.0, 0, 0.95),                # flat, fast
+        (torch.randn(V) * 0.5, 1.0, 0, 0.9999),              # crossing in the tail: radix
+        (torch.round(torch.randn(V) * 4) / 2, 1.0, 0, 0.5),  # thousands of ties per bin: radix
+        (torch.zeros(V), 1.0, 0, 0.5),                       # constant row: keep everything
+        (torch.randn(V) * 3, 1.0, 50, 1.0),                  # top-k fast
+        (torch.round(torch.randn(V) * 4) / 2, 1.0, 3000, 1.0),  # top-k over a tie bin: radix
+        (torch.randn(V) * 2, 0.8, 200, 0.8),                 # top-k then top-p
+        (torch.randn(V) * 2, 0.05, 0, 0.9),                  # near-greedy temperature
+    ]
+    B = len(rows)
+    logits = torch.stack([r[0] for r in rows]).float()
+    temp = torch.tensor([r[1] for r in rows])
+    topk = torch.tensor([r[2] for r in rows], dtype=torch.int32)
+    topp = torch.tensor([r[3] for r in rows])
+    seeds = torch.arange(B, dtype=torch.int64) * 131 + 7
+    steps = torch.arange(B, dtype=torch.int64)
+    agree = 0
+    for rep in range(4):
+        st = steps + rep * 17
+        tok, lp = ops.sample(logits.to(gpu), temp.to(gpu), topk.to(gpu), topp.to(gpu), seeds.to(gpu), st.to(gpu))
+        tok_r, lp_r = ref.sample(logits.clone(), temp, topk, topp, seeds, st)
+        tok = tok.cpu()
+        assert torch.isfinite(lp).all()
+        agree += int((tok == tok_r).sum())
+        for b in range(B):
+            xs = logits[b] / temp[b]
+            keep = _kept_set(xs, int(topk[b]), float(topp[b]), 1e-4)
+            assert keep[int(tok[b])], f"row {b}: token {int(tok[b])} outside the kept set"
+        same = tok == tok_r
+        assert torch.allclose(lp.cpu()[same], lp_r[same], atol=1e-3)
+    assert agree >= 0.9 * 4 * B, f"{agree} of {4 * B} draws agree with the reference"
+
+
 def test_debug_sync_mode_checks_launches(gpu):
     """NGA_DEBUG_SYNC=1: every kernel binding checks its launch and synchronises its stream
     (fault localisation without a debugger); results are unchanged."""
