@@ -98,6 +98,10 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
     inc, defs, libs = _torch_flags()
     hip_srcs = sorted((CSRC / "kernels").glob("*.hip"))
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+    if os.environ.get("NGA_DIAG_BUILD", "0") != "0":
+        # kernel ablation variants (NGA_PV2_ABLATE / NGA_MOE_ABLATE: timings only, results
+        # wrong by design) exist only in this build; rebuild with force=True when switching
+        common.append("-DNGA_DIAG_ABLATION")
     jobs_list = []
     objs = []
     for s in hip_srcs:

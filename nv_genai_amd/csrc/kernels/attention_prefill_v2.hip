@@ -53,8 +53,8 @@ __device__ __forceinline__ int kswz(int row) { return (row & 3) | (((row >> 3) &
 __device__ __forceinline__ int vswz(int row) { return (row >> 1) & 7; }
 }  // namespace
 
-// ABL (diagnostic, NGA_PV2_ABLATE; results are wrong): 1 = no DMA inside the loop, 2 = no
-// compute, 4 = no DMA and no barrier inside the loop
+// ABL (diagnostic builds with NGA_DIAG_BUILD=1, picked by NGA_PV2_ABLATE; results are wrong):
+// 1 = no DMA inside the loop, 2 = no compute, 4 = no DMA and no barrier inside the loop
 template <bool CAUSAL, int HPW, int ABL = 0>
 __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P) {
   constexpr int D = 128, KT = 64;
@@ -349,6 +349,7 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
   pp.per_xcd = (int)((total + 7) / 8);
   dim3 grid(8 * pp.per_xcd);
 #define NGA_PF2(CS, HP) prefill_attn_v2_kernel<CS, HP><<<grid, 256, 0, stream>>>(pp)
+#ifdef NGA_DIAG_ABLATION  // diagnostic builds only (NGA_DIAG_BUILD=1): results are wrong
   static const int abl = [] {
     const char* e = getenv("NGA_PV2_ABLATE");
     return e ? atoi(e) : 0;
@@ -359,6 +360,7 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
     else prefill_attn_v2_kernel<true, 4, 4><<<grid, 256, 0, stream>>>(pp);
     return true;
   }
+#endif
   if (causal) {
     if (hpw == 4) NGA_PF2(true, 4); else if (hpw == 2) NGA_PF2(true, 2); else NGA_PF2(true, 1);
   } else {

@@ -150,9 +150,9 @@ __device__ __forceinline__ void wait_vmcnt() {
   else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
 }
 
-// ABL (diagnostic builds, NGA_MOE_ABLATE): 1 = no DMA inside the K loop (MFMA + LDS-read
-// bound), 2 = no MFMAs (DMA + barrier bound), 3 = no DMA and no LDS fragment reads (MFMA +
-// barrier), 4 = no DMA and no barrier; results are wrong in all of them
+// ABL (diagnostic builds with NGA_DIAG_BUILD=1, picked by NGA_MOE_ABLATE): 1 = no DMA inside
+// the K loop (MFMA + LDS-read bound), 2 = no MFMAs (DMA + barrier bound), 3 = no DMA and no LDS
+// fragment reads (MFMA + barrier), 4 = no DMA and no barrier; results are wrong in all of them
 template <int BM, int MODE, int ABL = 0, int NSTAGE = 3>
 __global__ void __launch_bounds__(256) moe_gemm_kernel(MoeGemmParams P) {
   constexpr int BN = GEMM_BN;
@@ -351,17 +351,22 @@ void launch_moe_gemm(const MoeGemmParams& p, int bm, int mode, hipStream_t strea
   const int nblk = p.mt * p.nt;
   if (nblk == 0) return;
   dim3 grid(nblk);
+#ifdef NGA_DIAG_ABLATION  // diagnostic builds only (NGA_DIAG_BUILD=1): timings, not results
   static const int ablate = [] {
     const char* e = getenv("NGA_MOE_ABLATE");
     return e ? atoi(e) : 0;
   }();
-  if (mode == 0) {
-    if (ablate == 5 && bm == 128) moe_gemm_kernel<128, 0, 0, 2><<<grid, 256, 0, stream>>>(p);   // 2-stage
-    else if (bm == 64) moe_gemm_kernel<64, 0><<<grid, 256, 0, stream>>>(p);
+  if (mode == 0 && bm == 128 && ablate >= 1 && ablate <= 5) {
+    if (ablate == 5) moe_gemm_kernel<128, 0, 0, 2><<<grid, 256, 0, stream>>>(p);   // 2-stage
     else if (ablate == 1) moe_gemm_kernel<128, 0, 1><<<grid, 256, 0, stream>>>(p);
     else if (ablate == 2) moe_gemm_kernel<128, 0, 2><<<grid, 256, 0, stream>>>(p);
     else if (ablate == 3) moe_gemm_kernel<128, 0, 3><<<grid, 256, 0, stream>>>(p);
-    else if (ablate == 4) moe_gemm_kernel<128, 0, 4><<<grid, 256, 0, stream>>>(p);
+    else moe_gemm_kernel<128, 0, 4><<<grid, 256, 0, stream>>>(p);
+    return;
+  }
+#endif
+  if (mode == 0) {
+    if (bm == 64) moe_gemm_kernel<64, 0><<<grid, 256, 0, stream>>>(p);
     else moe_gemm_kernel<128, 0><<<grid, 256, 0, stream>>>(p);
   } else {
     if (bm == 64) moe_gemm_kernel<64, 1><<<grid, 256, 0, stream>>>(p);

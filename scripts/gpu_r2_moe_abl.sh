@@ -1,5 +1,6 @@
 #!/usr/bin/env bash
 # MoE grouped GEMM ablation: normal, no-DMA, no-MFMA builds.
+# needs the diagnostic build: NGA_DIAG_BUILD=1 python -c 'from nv_genai_amd._build import build_kernels; build_kernels(force=True)'
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"
