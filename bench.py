@@ -64,7 +64,8 @@ def parse():
                     help="W8A8 FP8 projections (not the headline: that is measured in bf16)")
     ap.add_argument("--kv-fp8", action="store_true",
                     help="FP8 e4m3fn KV cache (not the headline: that is measured in bf16)")
-    ap.add_argument("--mixed-prefill-tokens", type=int, default=2048)
+    ap.add_argument("--mixed-prefill-tokens", type=int, default=4096,
+                    help="prefill tokens per mixed step (sweep: profiles/r2_mixed_sweep)")
     ap.add_argument("--mixed-min-tokens", type=int, default=0,
                     help="accumulate this many prompt tokens before forming a mixed step")
     ap.add_argument("--mixed-max-wait", type=int, default=4)

@@ -110,7 +110,7 @@ class EngineConfig:
     seed: int = 0
     detokenize: bool = True
     async_decode: bool = True  # pipeline steps (host work overlaps the GPU)
-    mixed_prefill_tokens: int = 2048  # prefill tokens that ride along a decode step (0 = off)
+    mixed_prefill_tokens: int = 4096  # prefill tokens that ride along a decode step (0 = off)
     token_alignment: int = 256   # prefill/mixed steps carry a multiple of this many tokens
     mixed_min_tokens: int = 0     # accumulate this many prompt tokens before a mixed step ...
     mixed_max_wait: int = 4       # ... unless the oldest waiting request waited this many steps
