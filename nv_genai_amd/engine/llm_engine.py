@@ -235,6 +235,12 @@ class LLMEngine:
         self._step_events: Deque[tuple] = collections.deque(maxlen=8192)
         self._timeline = collections.deque(maxlen=4096)
         self._tok_host = [(hbuf(S), hbuf(S, dtype=torch.float32)) for _ in range(2)]
+        # pinned staging of the pipelined id gather (token index, row of the in-flight step):
+        # a pageable host->device copy is staged synchronously by the HIP runtime and can
+        # hold the launching thread while the GPU drains the previous step
+        self.h_gidx, self.h_gprev = hbuf(T, dtype=torch.int64), hbuf(T, dtype=torch.int64)
+        self.d_gidx = dbuf(T, dtype=torch.int64) if self.gpu else None
+        self.d_gprev = dbuf(T, dtype=torch.int64) if self.gpu else None
         self._step_reqs: List[Request] = []
         self._faults = FaultInjector(rank=self.p.rank)   # NGA_FAULT (utils/faults.py)
         self._nstep = 0
@@ -531,11 +537,24 @@ class LLMEngine:
                 "sampled": {r.id for r, m in zip(reqs, smp) if m and r is not None},
                 "n": n, "buf": buf, "ev": ev}
 
+    def _stage_gather(self, src):
+        """Device copies of the gather's (token index, previous row) lists, uploaded from the
+        pinned staging buffers; the upload event then covers them too."""
+        k = len(src[0])
+        self.h_gidx.numpy()[:k] = src[0]
+        self.h_gprev.numpy()[:k] = src[1]
+        if not self.gpu:
+            return self.h_gidx[:k], self.h_gprev[:k]
+        self.d_gidx[:k].copy_(self.h_gidx[:k], non_blocking=True)
+        self.d_gprev[:k].copy_(self.h_gprev[:k], non_blocking=True)
+        self._up_ev = torch.cuda.Event()
+        self._up_ev.record()
+        return self.d_gidx[:k], self.d_gprev[:k]
+
     def _gather_ids(self, src) -> None:
         if src is None or len(src[0]) == 0:
             return
-        idx = torch.as_tensor(src[0], dtype=torch.int64).to(self.device, non_blocking=True)
-        prev = torch.as_tensor(src[1], dtype=torch.int64).to(self.device, non_blocking=True)
+        idx, prev = self._stage_gather(src)
         self.d_ids.index_copy_(0, idx, self.d_tok.index_select(0, prev))
 
     def _decode_launch(self, n: int, src) -> None:
@@ -546,7 +565,7 @@ class LLMEngine:
         self._sync_step(2, n, n, 1, self.cfg.max_model_len, bs or 0)
         self._upload(bs or n, bs or n)
         if src is not None and len(src[0]) == n:
-            prev = torch.as_tensor(src[1], dtype=torch.int64).to(self.device, non_blocking=True)
+            _, prev = self._stage_gather(src)
             self.d_ids[:n] = self.d_tok.index_select(0, prev)
         else:
             self._gather_ids(src)
