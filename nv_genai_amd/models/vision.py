@@ -276,6 +276,34 @@ def image_placeholder_ids(data: bytes, n: int, vocab: int) -> List[int]:
     return [(base + 7919 * i) % (vocab - 16) + 16 for i in range(n)]
 
 
+def split_image_parts(content) -> Tuple[List[object], List[bytes]]:
+    """Split an OpenAI chat message content into ordered parts — text strings, or the index of
+    an image in the returned image list — and the image bytes (``image_url`` data URIs or raw
+    ``{"type": "image", "image": bytes}`` parts)."""
+    import base64
+
+    if isinstance(content, str):
+        return [content], []
+    parts, images = [], []
+    for p in content:
+        if not isinstance(p, dict):
+            continue
+        t = p.get("type", "text")
+        if t == "text":
+            parts.append(p.get("text", ""))
+        elif t in ("image_url", "image"):
+            if t == "image":
+                data = p["image"]
+            else:
+                url = p["image_url"]["url"] if isinstance(p["image_url"], dict) else p["image_url"]
+                if not url.startswith("data:"):
+                    raise ValueError("only data: URIs are accepted for images (no network access)")
+                data = base64.b64decode(url.split(",", 1)[1])
+            parts.append(len(images))
+            images.append(data)
+    return parts, images
+
+
 class VisionLanguageModel:
     """Tower + projector + a continuous-batching decoder engine.
 
@@ -316,29 +344,7 @@ class VisionLanguageModel:
         return self.projector(f.reshape(B * P, Hv).contiguous()).view(B, P, -1)
 
     def _images_of(self, content) -> Tuple[List[object], List[bytes]]:
-        """Split a message content into ordered text / image parts."""
-        import base64
-
-        if isinstance(content, str):
-            return [content], []
-        parts, images = [], []
-        for p in content:
-            if not isinstance(p, dict):
-                continue
-            t = p.get("type", "text")
-            if t == "text":
-                parts.append(p.get("text", ""))
-            elif t in ("image_url", "image"):
-                if t == "image":
-                    data = p["image"]
-                else:
-                    url = p["image_url"]["url"] if isinstance(p["image_url"], dict) else p["image_url"]
-                    if not url.startswith("data:"):
-                        raise ValueError("only data: URIs are accepted for images (no network access)")
-                    data = base64.b64decode(url.split(",", 1)[1])
-                parts.append(len(images))
-                images.append(data)
-        return parts, images
+        return split_image_parts(content)
 
     def build_request(self, messages: Sequence[dict]):
         """-> (prompt ids, [(offset, features)]) in the LLaVA-1.5 conversation format."""

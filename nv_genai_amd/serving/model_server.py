@@ -23,6 +23,7 @@ import json
 import logging
 import os
 import struct
+import threading
 import time
 import uuid
 from typing import Any, Dict, List, Optional, Union
@@ -126,11 +127,15 @@ def _has_images(messages) -> bool:
 
 def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name: str = "meta/llama3-8b-instruct",
                embed_name: str = "snowflake/arctic-embed-l", rerank_name: str = "nv-rerank-qa-mistral-4b:1",
-               batch_delay_s: float = 0.002, vlm=None, vlm_service=None, vlm_name: str = "ai-neva-22b") -> FastAPI:
+               batch_delay_s: float = 0.002, vlm=None, vlm_service=None, vlm_name: str = "ai-neva-22b",
+               deplot=None, deplot_names=("google/deplot", "ai-google-deplot")) -> FastAPI:
     """``vlm`` / ``vlm_service``: a :class:`~nv_genai_amd.models.vision.VisionLanguageModel`
     and the :class:`EngineService` over its engine; chat requests with ``image_url`` parts
     (or ``model == vlm_name``) go there — the NeVA / DePlot endpoint contract of the
-    reference's multimodal example (examples/multimodal_rag/llm/llm_client.py:37-42)."""
+    reference's multimodal example (examples/multimodal_rag/llm/llm_client.py:37-42).
+    ``deplot``: a :class:`~nv_genai_amd.models.pix2struct.DePlot` chart-to-table model; chat
+    requests naming one of ``deplot_names`` are answered by it (the images of the request, its
+    text as the rendered header prompt; custom_pdf_parser.py:55-71)."""
     app = FastAPI(title="nv_genai_amd model server")
     metrics = Registry()
 
@@ -149,6 +154,23 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
         batcher = DynamicBatcher(embed_engine, batch_delay_s)
     app.state.llm, app.state.embed, app.state.rerank, app.state.batcher = llm_service, embed_engine, rerank_engine, batcher
     app.state.vlm, app.state.vlm_service = vlm, vlm_service
+    app.state.deplot = deplot
+    deplot_lock = threading.Lock()
+
+    def _deplot_run(msgs, max_tokens):
+        from ..models.vision import split_image_parts
+
+        texts, images = [], []
+        for m in msgs:
+            parts, imgs = split_image_parts(m.content)
+            texts += [p for p in parts if isinstance(p, str) and p.strip()]
+            images += imgs
+        if not images:
+            raise ValueError("a DePlot request needs at least one image")
+        with deplot_lock:            # one model instance: requests run one batch at a time
+            outs = app.state.deplot.describe_batch(images, " ".join(texts) or None,
+                                                   max_new_tokens=min(max_tokens, 512))
+        return "\n".join(outs)
 
     def _need(x, what):
         if x is None:
@@ -222,6 +244,29 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
         metrics.inc("chat_requests_total")
         if req.stream and req.n > 1:
             return JSONResponse({"error": "stream supports n = 1"}, status_code=400)
+        if app.state.deplot is not None and req.model in deplot_names:
+            with tracer.span("chat.completions.deplot", {"model": req.model}, request.headers.get("traceparent")):
+                try:
+                    text = await asyncio.get_running_loop().run_in_executor(None, _deplot_run, req.messages,
+                                                                            req.max_tokens)
+                except ValueError as e:
+                    return JSONResponse({"error": str(e)}, status_code=400)
+            metrics.observe("request_seconds", time.perf_counter() - t0)
+            rid = f"chatcmpl-{uuid.uuid4().hex}"
+            if req.stream:
+                def one():
+                    for ch in ({"index": 0, "delta": {"role": "assistant", "content": text}, "finish_reason": None},
+                               {"index": 0, "delta": {}, "finish_reason": "stop"}):
+                        yield "data: " + json.dumps({"id": rid, "object": "chat.completion.chunk",
+                                                     "created": int(time.time()), "model": req.model,
+                                                     "choices": [ch]}) + "\n\n"
+                    yield "data: [DONE]\n\n"
+
+                return StreamingResponse(one(), media_type="text/event-stream")
+            return {"id": rid, "object": "chat.completion", "created": int(time.time()), "model": req.model,
+                    "choices": [{"index": 0, "message": {"role": "assistant", "content": text},
+                                 "finish_reason": "stop"}],
+                    "usage": {"prompt_tokens": 0, "completion_tokens": 0, "total_tokens": 0}}
         use_vlm = app.state.vlm is not None and (_has_images(req.messages) or req.model == vlm_name)
         if use_vlm:
             svc = app.state.vlm_service
@@ -364,6 +409,8 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
             out.append({"id": llm_name, "object": "model", "owned_by": "nv_genai_amd"})
         if app.state.vlm is not None:
             out.append({"id": vlm_name, "object": "model", "owned_by": "nv_genai_amd"})
+        if app.state.deplot is not None:
+            out.append({"id": deplot_names[0], "object": "model", "owned_by": "nv_genai_amd"})
         if app.state.embed is not None:
             out.append({"id": embed_name, "object": "model", "owned_by": "nv_genai_amd"})
         if app.state.rerank is not None:
@@ -402,6 +449,7 @@ def main(argv=None):
     ap.add_argument("--embed", default="arctic-embed-l", help="encoder preset ('' to disable)")
     ap.add_argument("--rerank", default="", help="reranker preset ('' to disable)")
     ap.add_argument("--vlm", default="", help="vision-language preset, e.g. neva-22b ('' to disable)")
+    ap.add_argument("--deplot", default="", help="Pix2Struct chart-to-table preset, e.g. deplot ('' to disable)")
     ap.add_argument("--weights", default="", help="safetensors dir for the LLM")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=8000)
@@ -444,7 +492,13 @@ def main(argv=None):
             model=vc.llm, max_num_seqs=args.max_num_seqs, max_model_len=args.max_model_len,
             kv_cache_fraction=args.kv_cache_fraction))
         vsvc = EngineService(vlm.engine, name="vlm")
-    app = create_app(svc, emb, rr, vlm=vlm, vlm_service=vsvc, vlm_name=f"ai-{args.vlm}" if args.vlm else "ai-neva-22b")
+    dp = None
+    if args.deplot:
+        from ..models.pix2struct import DePlot
+
+        dp = DePlot(args.deplot, device=args.device)
+    app = create_app(svc, emb, rr, vlm=vlm, vlm_service=vsvc, vlm_name=f"ai-{args.vlm}" if args.vlm else "ai-neva-22b",
+                     deplot=dp)
     uvicorn.run(app, host=args.host, port=args.port, log_level=os.environ.get("LOGLEVEL", "info").lower())
 
 
