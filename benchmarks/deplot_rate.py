@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--max-tokens", type=int, default=128)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--host-threads", type=int, default=8)
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     from nv_genai_amd.models.pix2struct import DePlot
@@ -58,22 +59,44 @@ def main():
                       use_graph=False if args.no_graph else None, ignore_eos=True)
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    from concurrent.futures import ThreadPoolExecutor
+
+    from nv_genai_amd.models.pix2struct import flatten_patches, render_header
+
+    cfg = dp.cfg
+
+    workers = ThreadPoolExecutor(args.host_threads)
+
+    def host(batch):
+        """PNG decode + VQA header render (PIL, host; PIL drops the GIL) for one batch, fanned
+        out over worker threads while the GPU decodes the previous batch."""
+        if not cfg.is_vqa:
+            return list(batch)
+        return list(workers.map(lambda im: render_header(im, dp.PROMPT), batch))
+
     t_pre = t_enc = t_gen = 0.0
     t0 = time.perf_counter()
     toks = 0
-    for s in range(0, args.images, args.batch):
-        a = time.perf_counter()
-        ps = [dp.patches(im) for im in imgs[s:s + args.batch]]
-        b = time.perf_counter()
-        out = dp.model.generate(ps, max_new_tokens=args.max_tokens, use_graph=False if args.no_graph else None,
-                                ignore_eos=True)
-        if dev.type == "cuda":
-            torch.cuda.synchronize()
-        c = time.perf_counter()
-        t_pre += b - a
-        t_gen += c - b
-        toks += sum(len(o) for o in out)
+    batches = [imgs[s:s + args.batch] for s in range(0, args.images, args.batch)]
+    with ThreadPoolExecutor(1) as pool:
+        fut = pool.submit(host, batches[0])
+        for i in range(len(batches)):
+            a = time.perf_counter()
+            arrs = fut.result()
+            if i + 1 < len(batches):
+                fut = pool.submit(host, batches[i + 1])
+            ps = [flatten_patches(x, cfg.max_patches, cfg.patch, device=dev) for x in arrs]
+            b = time.perf_counter()
+            out = dp.model.generate(ps, max_new_tokens=args.max_tokens,
+                                    use_graph=False if args.no_graph else None, ignore_eos=True)
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            c = time.perf_counter()
+            t_pre += b - a
+            t_gen += c - b
+            toks += sum(len(o) for o in out)
     wall = time.perf_counter() - t0
+    workers.shutdown()
     # encoder-only time of one batch (the rest of generate is decode)
     ps = [dp.patches(im) for im in imgs[: args.batch]]
     if dev.type == "cuda":
@@ -87,7 +110,7 @@ def main():
             "batch": args.batch, "max_tokens": args.max_tokens, "graph": not args.no_graph,
             "patches_per_image": int(ps[0].shape[0]), "images_per_s": round(args.images / wall, 2),
             "output_tok_per_s": round(toks / wall, 1), "wall_s": round(wall, 3),
-            "host_preprocess_s": round(t_pre, 3), "generate_s": round(t_gen, 3),
+            "host_preprocess_wait_s": round(t_pre, 3), "generate_s": round(t_gen, 3),
             "encoder_ms_per_batch": round(1e3 * t_enc, 2),
             "data": "synthetic bar charts; random-init weights of the architecture",
             "dtype": str(dp.model.dtype).replace("torch.", "")}

@@ -21,7 +21,9 @@ riding on the LLaVA-style VLM (models/vision.py):
 * **Decoder** (:meth:`Pix2StructModel.decode_logits` / :meth:`Pix2StructModel.generate`): T5 decoder layers (causal self-attention with the
   bucketed relative position bias of layer 0 shared by every layer, cross-attention to the
   encoder rows, gated-GELU MLP). Generation is batched over images: every layer's cross K/V
-  are computed once in a single GEMM, the self-attention KV cache is a static buffer, and on a
+  are computed once in a single GEMM into 64-token KV pages, so cross-attention runs on the
+  paged non-causal MFMA attention kernel (``ops.prefill_attention_paged``, each image's patch
+  count as its context length); the self-attention KV cache is a static buffer, and on a
   GPU the whole decode step — embedding, 12 layers, LM head, greedy pick, cache write — is
   captured once into a hipGraph and replayed per token (the step index lives on the device, so
   the relative-bias row and the cache slot are gathered by the kernels, not by the host).
@@ -133,17 +135,22 @@ def render_header(image, header: str, font_size: int = 36) -> np.ndarray:
     return np.asarray(out)
 
 
-def flatten_patches(image, max_patches: int, patch: int = 16, normalize: bool = True) -> torch.Tensor:
+def flatten_patches(image, max_patches: int, patch: int = 16, normalize: bool = True,
+                    device=None) -> torch.Tensor:
     """One image -> its real patches [rows * cols, 2 + 3 * patch^2] float32 (row id, column id,
     then the channel-last patch pixels); ``pad_patches`` pads to ``max_patches`` rows as the HF
     processor does. Same arithmetic as transformers' ``Pix2StructImageProcessorPil``:
     standardise with the image's mean / population std (std floored at 1 / sqrt(numel)), then
-    resize (bilinear, antialiased) to the largest patch grid with rows * cols <= max_patches."""
-    x = _to_rgb_array(image).astype(np.float32)
-    x = torch.from_numpy(np.ascontiguousarray(x.transpose(2, 0, 1)))     # [3, h, w]
+    resize (bilinear, antialiased) to the largest patch grid with rows * cols <= max_patches.
+    ``device``: run the standardise / resize / patchify on that device (the uint8 pixels are
+    uploaded once; on a GPU this takes the per-pixel work off the host)."""
+    x = torch.from_numpy(np.ascontiguousarray(_to_rgb_array(image).transpose(2, 0, 1)))   # [3, h, w] u8
+    if device is not None:
+        x = x.to(device, non_blocking=True)
+    x = x.float()
     if normalize:
-        mean, std = float(x.mean()), float(x.numpy().std())
-        x = (x - mean) / max(std, 1.0 / math.sqrt(x.numel()))
+        std = x.std(correction=0)
+        x = (x - x.mean()) / torch.clamp(std, min=1.0 / math.sqrt(x.numel()))
     _, h, w = x.shape
     scale = math.sqrt(max_patches * (patch / h) * (patch / w))
     rows = max(min(int(scale * h / patch), max_patches), 1)
@@ -151,8 +158,8 @@ def flatten_patches(image, max_patches: int, patch: int = 16, normalize: bool = 
     x = torch.nn.functional.interpolate(x[None], size=(rows * patch, cols * patch), mode="bilinear",
                                         align_corners=False, antialias=True)[0]
     p = x.reshape(3, rows, patch, cols, patch).permute(1, 3, 2, 4, 0).reshape(rows * cols, -1)
-    r = torch.arange(rows, dtype=torch.float32).repeat_interleave(cols) + 1
-    c = torch.arange(cols, dtype=torch.float32).repeat(rows) + 1
+    r = torch.arange(rows, dtype=torch.float32, device=x.device).repeat_interleave(cols) + 1
+    c = torch.arange(cols, dtype=torch.float32, device=x.device).repeat(rows) + 1
     return torch.cat([r[:, None], c[:, None], p], 1)
 
 
@@ -350,28 +357,42 @@ class Pix2StructModel:
         b = b.permute(2, 0, 1).contiguous()
         return b.masked_fill((rel > 0)[None], float("-inf"))
 
-    def _cross_kv(self, enc: torch.Tensor, cu: torch.Tensor):
-        """Padded cross-attention K / V of every layer [L, B, heads, Le, dkv] and the additive
-        key mask [B, 1, 1, Le] (0 on real rows, -inf on padding)."""
-        c = self.cfg
+    def _cross_kv(self, enc: torch.Tensor, cu: torch.Tensor) -> dict:
+        """Every layer's cross-attention K / V in the paged layout of the attention kernels
+        (K pages [L, blocks, heads, 64, dkv], V^T pages [L, blocks, heads, dkv, 64]; image b
+        owns blocks [b * nb, (b + 1) * nb)), computed by one GEMM over the encoder rows. The
+        decoder's cross-attention is then the paged non-causal MFMA attention kernel with
+        ``ctx_lens`` = each image's patch count (no mask tensor, padding never read)."""
+        c, dev = self.cfg, enc.device
         lens = (cu[1:] - cu[:-1]).tolist()
-        B, Le, H = len(lens), max(lens), c.t_hidden
+        B, L, h, d = len(lens), c.t_layers, c.t_heads, c.t_dkv
+        nb = -(-max(lens) // 64)
         kv = enc @ self.w_xkv.t()                                                   # [T, L*2H]
-        pad = torch.zeros(B, Le, kv.shape[1], dtype=kv.dtype, device=kv.device)
-        mask = torch.full((B, 1, 1, Le), float("-inf"), dtype=torch.float32, device=kv.device)
+        pad = torch.zeros(B, nb * 64, kv.shape[1], dtype=kv.dtype, device=dev)
         for b, (s, n) in enumerate(zip(cu[:-1].tolist(), lens)):
             pad[b, :n] = kv[s:s + n]
-            mask[b, ..., :n] = 0.0
-        pad = pad.view(B, Le, c.t_layers, 2, c.t_heads, c.t_dkv).permute(2, 3, 0, 4, 1, 5).contiguous()
-        return pad[:, 0], pad[:, 1], mask
+        pad = pad.view(B, nb, 64, L, 2, h, d)
+        kp = pad[:, :, :, :, 0].permute(3, 0, 1, 4, 2, 5).reshape(L, B * nb, h, 64, d).contiguous()
+        vp = pad[:, :, :, :, 1].permute(3, 0, 1, 4, 5, 2).reshape(L, B * nb, h, d, 64).contiguous()
+        return {"k": kp, "v": vp,
+                "bt": torch.arange(B * nb, dtype=torch.int32, device=dev).view(B, nb),
+                "lens": torch.tensor(lens, dtype=torch.int32, device=dev)}
+
+    def _cross(self, q: torch.Tensor, xa: dict, li: int, T: int) -> torch.Tensor:
+        """Cross-attention of q rows [B * T, H] (T decoder positions per image, image-major)."""
+        c = self.cfg
+        B = xa["lens"].numel()
+        cu_q = torch.arange(0, B * T + 1, T, dtype=torch.int32, device=q.device)
+        return ops.prefill_attention_paged(q, xa["k"][li], xa["v"][li], xa["bt"], cu_q, xa["lens"],
+                                           c.t_heads, c.t_heads, c.t_dkv, T, 1.0, causal=False)
 
     @staticmethod
     def _attend(q, k, v, bias):
-        """Unscaled T5 attention: softmax(q k^T + bias) v, fp32 softmax."""
-        s = torch.matmul(q.float(), k.float().transpose(-1, -2)) + bias
-        return torch.matmul(torch.softmax(s, -1).to(v.dtype), v)
+        """Unscaled T5 attention softmax(q k^T + bias) v as one fused SDPA call (fp32 softmax
+        inside; K / V are read once in their storage dtype, never widened in memory)."""
+        return torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=bias.to(q.dtype), scale=1.0)
 
-    def _dec_layer(self, L, x, self_k, self_v, q_bias, xk, xv, xmask, B, T):
+    def _dec_layer(self, L, x, self_k, self_v, q_bias, xa, li, B, T):
         """One decoder layer on x [B*T, H]; self_k / self_v [B, heads, S, dkv] already hold
         this step's keys. Returns x (updated in place through the fused add+norm)."""
         c = self.cfg
@@ -380,8 +401,7 @@ class Pix2StructModel:
         q = (n @ L["wqkv"][:H].t()).view(B, T, h, d).transpose(1, 2)
         a = self._attend(q, self_k, self_v, q_bias).transpose(1, 2).reshape(B * T, H)
         n = ops.add_rmsnorm(x, a @ L["wo"].t(), L["ln_x"], c.eps)
-        q = (n @ L["wq_x"].t()).view(B, T, h, d).transpose(1, 2)
-        a = self._attend(q, xk, xv, xmask).transpose(1, 2).reshape(B * T, H)
+        a = self._cross(n @ L["wq_x"].t(), xa, li, T)
         n = ops.add_rmsnorm(x, a @ L["wo_x"].t(), L["ln_f"], c.eps)
         m = ops.gelu_tanh_mul(n @ L["wi"].t()) @ L["wout"].t()
         x += m
@@ -393,14 +413,14 @@ class Pix2StructModel:
         c = self.cfg
         B, T = ids.shape
         H, h, d = c.t_hidden, c.t_heads, c.t_dkv
-        xk, xv, xmask = self._cross_kv(enc, cu)
+        xa = self._cross_kv(enc, cu)
         bias = self._bias_table(T)[None]
         x = self.embed.index_select(0, ids.reshape(-1).to(self.device)).contiguous()
         for li, L in enumerate(self.dec_layers):
             n = ops.rmsnorm(x, L["ln_s"], c.eps)
             kv = (n @ L["wqkv"][H:].t()).view(B, T, 2, h, d)
             k, v = kv[:, :, 0].transpose(1, 2), kv[:, :, 1].transpose(1, 2)
-            self._dec_layer(L, x, k, v, bias, xk[li], xv[li], xmask, B, T)
+            self._dec_layer(L, x, k, v, bias, xa, li, B, T)
         y = ops.rmsnorm(x, self.dec_norm, c.eps)
         return (y @ self.lm_head.t()).float().view(B, T, -1)
 
@@ -419,8 +439,7 @@ class Pix2StructModel:
             kv = (n @ L["wqkv"][H:].t()).view(B, 2, h, 1, d)
             st["k"][li].index_copy_(2, t, kv[:, 0])
             st["v"][li].index_copy_(2, t, kv[:, 1])
-            self._dec_layer(L, x, st["k"][li], st["v"][li], bias, st["xk"][li], st["xv"][li],
-                            st["xmask"], B, 1)
+            self._dec_layer(L, x, st["k"][li], st["v"][li], bias, st["xa"], li, B, 1)
         y = ops.rmsnorm(x, self.dec_norm, c.eps)
         logits = (y @ self.lm_head.t()).float()
         nxt = torch.argmax(logits, -1)
@@ -440,9 +459,8 @@ class Pix2StructModel:
         ``ignore_eos``: every row runs all ``max_new_tokens`` steps (fixed-work benchmarks)."""
         c, dev = self.cfg, self.device
         enc, cu = self.encode(patches)
-        xk, xv, xmask = self._cross_kv(enc, cu)
         B, S = len(patches), int(max_new_tokens)
-        st = {"xk": xk, "xv": xv, "xmask": xmask, "bias": self._bias_table(S),
+        st = {"xa": self._cross_kv(enc, cu), "bias": self._bias_table(S),
               "k": torch.zeros(c.t_layers, B, c.t_heads, S, c.t_dkv, dtype=self.dtype, device=dev),
               "v": torch.zeros(c.t_layers, B, c.t_heads, S, c.t_dkv, dtype=self.dtype, device=dev),
               "tok": torch.full((B,), c.decoder_start_id, dtype=torch.long, device=dev),
@@ -497,9 +515,10 @@ class DePlot:
         self.tok = tokenizer or llm_tokenizer()
 
     def patches(self, image, prompt: Optional[str] = None) -> torch.Tensor:
+        """Header render on the host (PIL text), the per-pixel work on the model's device."""
         if self.cfg.is_vqa:
             image = render_header(image, prompt or self.PROMPT)
-        return flatten_patches(image, self.cfg.max_patches, self.cfg.patch)
+        return flatten_patches(image, self.cfg.max_patches, self.cfg.patch, device=self.model.device)
 
     def describe_batch(self, images: Sequence, prompt: Optional[str] = None,
                        max_new_tokens: int = 512) -> List[str]:
