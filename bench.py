@@ -110,6 +110,12 @@ def host_step_summary(llm) -> dict:
 
 def main():
     args = parse()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env > 1:
+        # one rank per GPU on a shared host: give each rank's tokenizer thread pool (Rust
+        # rayon, sized to every core by default) its share of the cores, before first use
+        ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+        os.environ.setdefault("RAYON_NUM_THREADS", str(max(1, ncpu // world_env)))
     from nv_genai_amd.engine.embed_engine import EmbeddingEngine
     from nv_genai_amd.engine.llm_engine import EngineConfig, LLMEngine, SamplingParams
     from nv_genai_amd.index.docstore import SyntheticDocStore

@@ -528,5 +528,33 @@ class DePlot:
         # tokenizer's id space (``decode`` folds; random-init weights produce no real tables)
         return [self.tok.decode(o) for o in outs]
 
+    def generate_many(self, images: Sequence, prompt: Optional[str] = None, batch: int = 32,
+                      max_new_tokens: int = 512, threads: int = 8, ignore_eos: bool = False) -> List[List[int]]:
+        """Token ids for many images in batches of ``batch``. The host part of the next batch
+        (PNG decode + header render; PIL releases the GIL) runs on ``threads`` worker threads
+        while the GPU encodes and decodes the current one; the per-pixel preprocessing runs on
+        the device."""
+        from concurrent.futures import ThreadPoolExecutor
+
+        c = self.cfg
+        prompt = prompt or self.PROMPT
+        chunks = [list(images[i:i + batch]) for i in range(0, len(images), batch)]
+        if not chunks:
+            return []
+
+        def host(im):
+            return render_header(im, prompt) if c.is_vqa else _to_rgb_array(im)
+
+        out: List[List[int]] = []
+        with ThreadPoolExecutor(max(1, threads)) as pool:
+            fut = [pool.submit(host, im) for im in chunks[0]]
+            for i in range(len(chunks)):
+                arrs = [f.result() for f in fut]
+                if i + 1 < len(chunks):
+                    fut = [pool.submit(host, im) for im in chunks[i + 1]]
+                ps = [flatten_patches(a, c.max_patches, c.patch, device=self.model.device) for a in arrs]
+                out += self.model.generate(ps, max_new_tokens=max_new_tokens, ignore_eos=ignore_eos)
+        return out
+
     def describe(self, image, prompt: Optional[str] = None, max_new_tokens: int = 512) -> str:
         return self.describe_batch([image], prompt, max_new_tokens)[0]

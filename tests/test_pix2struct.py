@@ -166,3 +166,11 @@ def test_model_server_routes_deplot_requests():
     bad = c.post("/v1/chat/completions", json={"model": "google/deplot",
                                                "messages": [{"role": "user", "content": "no image"}]})
     assert bad.status_code == 400
+
+
+def test_generate_many_matches_per_batch_generation():
+    d = DePlot("pix2struct-tiny", device="cpu", seed=4)
+    imgs = [_image(30 + 7 * i, 50, i) for i in range(5)]
+    many = d.generate_many(imgs, batch=2, max_new_tokens=5, threads=3)
+    one = d.model.generate([d.patches(im) for im in imgs], max_new_tokens=5)
+    assert many == one
