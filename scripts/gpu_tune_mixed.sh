@@ -6,7 +6,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 O="$R/gpurun_out/tune"
 mkdir -p "$O"
 cp "$R/nv_genai_amd/assets/tunableop/gemm_gfx950.csv" "$O/gemm_gfx950.csv"
-MS=512,768,1024,1280,1536,1792,2048,2304
+MS=${MS:-512,768,1024,1280,1536,1792,2048,2304}
 timeout -k 10 900 python3 -u "$R/scripts/tune_gemms.py" --decode "" --prefill "$MS" --max-ms ${TUNE_MS:-1000} --iters ${TUNE_ITERS:-100} --out "$O/gemm_gfx950.csv" > "$O/tune.log" 2>&1 || exit $?
 tail -3 "$O/tune.log"
 timeout -k 10 300 python3 -u "$R/benchmarks/gemm_sweep.py" --ms "$MS" > "$O/sweep_default.log" 2>&1 || exit $?
