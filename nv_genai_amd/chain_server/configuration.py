@@ -131,7 +131,7 @@ class EngineConfigSection(ConfigWizard):
 
 @configclass
 class IndexConfig(ConfigWizard):
-    type: str = configfield("type", default="flat", help_txt="flat | ivf_flat")
+    type: str = configfield("type", default="flat", help_txt="flat | ivf_flat | hnsw")
     metric: str = configfield("metric", default="cosine", help_txt="cosine | ip | l2")
     persist_dir: str = configfield("persist_dir", default="",
                                    help_txt="Directory for index snapshots ('' = in-memory only)")

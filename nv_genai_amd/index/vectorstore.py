@@ -107,7 +107,8 @@ class VectorStore:
     def __init__(self, embedder, dim: int, index_type: str = "flat", metric: str = "cosine",
                  device: Optional[str] = None, nlist: int = 64, nprobe: int = 16,
                  name: str = "default", persist_dir: Optional[str] = None,
-                 batch_queries: Optional[bool] = None):
+                 batch_queries: Optional[bool] = None, hnsw_m: int = 16, hnsw_ef_construction: int = 200,
+                 hnsw_ef: int = 64):
         self.embedder = embedder
         self.dim = dim
         self.name = name
@@ -115,6 +116,10 @@ class VectorStore:
         self.index_type = index_type
         if index_type == "ivf_flat":
             self.index = IVFFlatIndex(dim, nlist, nprobe, metric, device)
+        elif index_type == "hnsw":
+            from .hnsw import HNSWIndex
+
+            self.index = HNSWIndex(dim, metric, M=hnsw_m, ef_construction=hnsw_ef_construction, ef=hnsw_ef)
         else:
             self.index = FlatIndex(dim, metric, device)
         self.docs = DocStore()
@@ -249,7 +254,12 @@ class VectorStore:
         p = Path(path)
         kind = json.loads((p / "index.json").read_text()).get("kind", "flat")
         dev = str(self.index.device)
-        self.index = IVFFlatIndex.load(path, dev) if kind == "ivf_flat" else FlatIndex.load(path, dev)
+        if kind == "hnsw":
+            from .hnsw import HNSWIndex
+
+            self.index = HNSWIndex.load(path)
+        else:
+            self.index = IVFFlatIndex.load(path, dev) if kind == "ivf_flat" else FlatIndex.load(path, dev)
         self.docs = DocStore.load(path)
 
 

@@ -397,6 +397,28 @@ def load_config(path: str) -> dict:
         return yaml.safe_load(f)
 
 
+def store_kwargs(vcfg: dict, name: str) -> dict:
+    """VectorStore arguments for a collection from the reference's vdb ``resource_schemas``
+    ``index_conf`` (kafka_config.yaml:109-125: ``metric_type`` L2 / IP / COSINE, ``index_type``
+    HNSW with ``M`` / ``efConstruction``, or IVF_FLAT / GPU_IVF_FLAT with ``nlist``; anything
+    else is the flat in-HBM scan)."""
+    conf = ((vcfg.get("resource_schemas") or {}).get(name) or {}).get("index_conf") or {}
+    if not conf:
+        return {}
+    params = conf.get("params") or {}
+    out = {"metric": {"L2": "l2", "IP": "ip", "COSINE": "cosine"}.get(str(conf.get("metric_type", "")).upper(),
+                                                                        "cosine")}
+    it = str(conf.get("index_type", "")).upper()
+    if it == "HNSW":
+        out.update(index_type="hnsw", hnsw_m=int(params.get("M", 16)),
+                   hnsw_ef_construction=int(params.get("efConstruction", 200)))
+    elif it in ("IVF_FLAT", "GPU_IVF_FLAT"):
+        out.update(index_type="ivf_flat", nlist=int(params.get("nlist", 64)))
+    else:
+        out["index_type"] = "flat"
+    return out
+
+
 def main(argv=None):
     import argparse
 
@@ -410,12 +432,15 @@ def main(argv=None):
     from ..index.vectorstore import VectorStore
 
     emb = EmbeddingEngine(a.embed_model)
+    cfg = load_config(a.config)
+    vcfg = cfg.get("vdb_pipeline", cfg).get("vdb", {}) if isinstance(cfg, dict) else {}
 
     def factory(name, recreate):
         return VectorStore(emb, emb.dim, name=name,
-                           persist_dir=os.path.join(a.persist_dir, name) if a.persist_dir else None)
+                           persist_dir=os.path.join(a.persist_dir, name) if a.persist_dir else None,
+                           **store_kwargs(vcfg, name))
 
-    mons = IngestPipeline(load_config(a.config), emb, factory).run(a.timeout)
+    mons = IngestPipeline(cfg, emb, factory).run(a.timeout)
     for m in mons.values():
         print(m)
 

@@ -94,7 +94,7 @@ def test_vectorstore_flat_ivf_and_persistence(tmp_path):
     emb = HashEmbeddings(128)
     texts = [f"document about topic {i} with keyword k{i % 7}" for i in range(300)]
     metas = [{"filename": f"f{i % 3}.txt"} for i in range(300)]
-    for itype in ("flat", "ivf_flat"):
+    for itype in ("flat", "ivf_flat", "hnsw"):
         vs = VectorStore(emb, 128, itype, "cosine", "cpu", nlist=8, nprobe=8, persist_dir=str(tmp_path / itype))
         vs.add_texts(texts, metas)
         hits = vs.similarity_search_with_score("topic 42 keyword k0", 3)

@@ -1,0 +1,78 @@
+"""HNSW graph index (csrc/runtime/hnsw.cpp via index/hnsw.py): recall against exact search
+for each metric, tombstone deletes, persistence, threaded batch search, the reference's
+``index_conf`` mapping (kafka_config.yaml:109-125) and the VectorStore integration."""
+import numpy as np
+import pytest
+import torch
+
+from nv_genai_amd.index.hnsw import HNSWIndex
+from nv_genai_amd.ingest.streaming import store_kwargs
+
+
+def _exact(X, Q, k, metric):
+    if metric == "l2":
+        s = -((Q[:, None, :] - X[None]) ** 2).sum(-1)
+    else:
+        if metric == "cosine":
+            X = X / np.linalg.norm(X, axis=1, keepdims=True)
+            Q = Q / np.linalg.norm(Q, axis=1, keepdims=True)
+        s = Q @ X.T
+    return np.argsort(-s, axis=1)[:, :k], np.sort(s, axis=1)[:, ::-1][:, :k]
+
+
+@pytest.mark.parametrize("metric", ["l2", "ip", "cosine"])
+def test_recall_against_exact_search(metric):
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((4000, 32)).astype(np.float32)
+    Q = rng.standard_normal((100, 32)).astype(np.float32)
+    idx = HNSWIndex(32, metric, M=16, ef_construction=200, ef=128)
+    idx.add(torch.from_numpy(X), torch.arange(4000) + 10)
+    assert len(idx) == 4000
+    s, i = idx.search(torch.from_numpy(Q), 10)
+    ref_i, ref_s = _exact(X, Q, 10, metric)
+    recall = np.mean([len(set(a) & set(b + 10)) / 10 for a, b in zip(i.numpy(), ref_i)])
+    assert recall >= 0.95, recall
+    # scores are the metric's similarity (-L2^2 / dot), sorted best first
+    assert np.all(np.diff(s.numpy(), axis=1) <= 1e-5)
+    hit = i.numpy()[:, 0] == ref_i[:, 0] + 10
+    np.testing.assert_allclose(s.numpy()[hit, 0], ref_s[hit, 0], rtol=1e-4, atol=1e-4)
+
+
+def test_delete_persist_threads_and_errors(tmp_path):
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((1500, 16)).astype(np.float32)
+    idx = HNSWIndex(16, "l2", M=8, ef_construction=64, ef=64, threads=4)
+    idx.add(X, np.arange(1500))
+    gone = list(range(0, 1500, 3))
+    assert idx.remove(gone) == len(gone)
+    assert idx.remove(gone[:5]) == 0                       # already deleted
+    assert len(idx) == 1000
+    s, i = idx.search(X[:64], 5)
+    assert not set(i.numpy().ravel().tolist()) & set(gone)
+    # threaded batch == one query at a time
+    for r in range(0, 64, 7):
+        s1, i1 = idx.search(X[r], 5)
+        assert i1.numpy()[0].tolist() == i.numpy()[r].tolist()
+    idx.save(str(tmp_path))
+    again = HNSWIndex.load(str(tmp_path))
+    s2, i2 = again.search(X[:64], 5)
+    assert torch.equal(i2, i) and torch.equal(s2, s) and len(again) == 1000
+    with pytest.raises(Exception):
+        idx.add(X[:1], np.array([1]))                       # duplicate live id
+    with pytest.raises(Exception):
+        idx.search(np.zeros((1, 15), np.float32), 3)        # wrong dim
+    e = HNSWIndex(16, "l2")
+    s, i = e.search(X[:2], 3)
+    assert (i.numpy() == -1).all()
+
+
+def test_reference_index_conf_mapping():
+    vcfg = {"resource_schemas": {
+        "vdb_kafka_scrape": {"index_conf": {"field_name": "embedding", "metric_type": "L2", "index_type": "HNSW",
+                                            "params": {"M": 8, "efConstruction": 64}}},
+        "gpu": {"index_conf": {"metric_type": "IP", "index_type": "GPU_IVF_FLAT", "params": {"nlist": 64}}},
+        "plain": {}}}
+    assert store_kwargs(vcfg, "vdb_kafka_scrape") == {"metric": "l2", "index_type": "hnsw", "hnsw_m": 8,
+                                                      "hnsw_ef_construction": 64}
+    assert store_kwargs(vcfg, "gpu") == {"metric": "ip", "index_type": "ivf_flat", "nlist": 64}
+    assert store_kwargs(vcfg, "plain") == {} and store_kwargs({}, "x") == {}

@@ -1,5 +1,5 @@
 """ASan + UBSan build of the native host runtime (_rt: paged-KV block manager, continuous-
-batching scheduler, BM25 index, splitters), driven by a randomized stress workload in a
+batching scheduler, BM25 index, splitters, HNSW graph index), driven by a randomized stress workload in a
 child interpreter (the reference has no sanitizer coverage at all).
 
 The instrumented module is built into a temp dir (the in-tree _rt stays uninstrumented) and
@@ -84,6 +84,30 @@ STRESS = textwrap.dedent(r'''
     text = "".join(rng.choice(["a", "b", " ", "\n", "\n\n", ". "]) for _ in range(20000))
     rt.char_split(text, 1000, 100, ["\n\n", "\n", " ", ""])
     rt.char_split("", 10, 0, ["\n"])
+
+    # HNSW: interleaved adds / deletes / threaded searches, save + load, error paths
+    import os, tempfile
+    nr = np.random.default_rng(0)
+    for metric in ("l2", "ip", "cosine"):
+        h = rt.HNSW(24, metric, 6, 32, 16, 7)
+        nid = 0
+        for rnd in range(6):
+            n = int(nr.integers(1, 400))
+            h.add(nr.standard_normal((n, 24)).astype(np.float32), np.arange(nid, nid + n, dtype=np.int64))
+            nid += n
+            h.remove([int(x) for x in nr.integers(0, nid, 50)])
+            h.search(nr.standard_normal((int(nr.integers(1, 40)), 24)).astype(np.float32), int(nr.integers(0, 20)),
+                     int(nr.integers(0, 64)), int(nr.integers(1, 5)))
+        f = os.path.join(tempfile.mkdtemp(), "g.hnsw")
+        h.save(f)
+        rt.HNSW.load(f).search(np.zeros((3, 24), np.float32), 5, 0, 2)
+        for bad in (lambda: h.add(np.zeros((1, 24), np.float32), np.array([1], np.int64)) if len(h) else None,
+                    lambda: h.search(np.zeros((1, 3), np.float32), 2, 0, 1),
+                    lambda: rt.HNSW.load(f + ".missing")):
+            try:
+                bad()
+            except (RuntimeError, ValueError):
+                pass
     print("STRESS_OK")
 ''')
 
