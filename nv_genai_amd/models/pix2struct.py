@@ -382,7 +382,9 @@ class Pix2StructModel:
         """Cross-attention of q rows [B * T, H] (T decoder positions per image, image-major)."""
         c = self.cfg
         B = xa["lens"].numel()
-        cu_q = torch.arange(0, B * T + 1, T, dtype=torch.int32, device=q.device)
+        cu_q = xa.get(("cu_q", T))
+        if cu_q is None:        # built once per decoder length (outside any graph replay)
+            cu_q = xa[("cu_q", T)] = torch.arange(0, B * T + 1, T, dtype=torch.int32, device=q.device)
         return ops.prefill_attention_paged(q, xa["k"][li], xa["v"][li], xa["bt"], cu_q, xa["lens"],
                                            c.t_heads, c.t_heads, c.t_dkv, T, 1.0, causal=False)
 
@@ -390,38 +392,39 @@ class Pix2StructModel:
     def _attend(q, k, v, bias):
         """Unscaled T5 attention softmax(q k^T + bias) v as one fused SDPA call (fp32 softmax
         inside; K / V are read once in their storage dtype, never widened in memory)."""
-        return torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=bias.to(q.dtype), scale=1.0)
+        return torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=bias, scale=1.0)
 
-    def _dec_layer(self, L, x, self_k, self_v, q_bias, xa, li, B, T):
-        """One decoder layer on x [B*T, H]; self_k / self_v [B, heads, S, dkv] already hold
-        this step's keys. Returns x (updated in place through the fused add+norm)."""
+    def _dec_stack(self, x, B, T, bias, xa, kv_sink):
+        """All decoder layers on the residual stream x [B*T, H] (updated in place) -> the
+        final-normed rows. Per layer: one fused QKV GEMM; ``kv_sink(li, k, v)`` with this call's
+        keys / values [B, heads, T, dkv] returns the (K, V) the self-attention reads (the
+        teacher-forced path: these; the decode step: the cache they were written into); each
+        residual add is fused into the following RMSNorm (``ops.add_rmsnorm``)."""
         c = self.cfg
         H, h, d = c.t_hidden, c.t_heads, c.t_dkv
-        n = ops.rmsnorm(x, L["ln_s"], c.eps)
-        q = (n @ L["wqkv"][:H].t()).view(B, T, h, d).transpose(1, 2)
-        a = self._attend(q, self_k, self_v, q_bias).transpose(1, 2).reshape(B * T, H)
-        n = ops.add_rmsnorm(x, a @ L["wo"].t(), L["ln_x"], c.eps)
-        a = self._cross(n @ L["wq_x"].t(), xa, li, T)
-        n = ops.add_rmsnorm(x, a @ L["wo_x"].t(), L["ln_f"], c.eps)
-        m = ops.gelu_tanh_mul(n @ L["wi"].t()) @ L["wout"].t()
-        x += m
-        return x
+        layers = self.dec_layers
+        n = ops.rmsnorm(x, layers[0]["ln_s"], c.eps)
+        for li, L in enumerate(layers):
+            qkv = (n @ L["wqkv"].t()).view(B, T, 3, h, d)
+            q = qkv[:, :, 0].transpose(1, 2)
+            K, V = kv_sink(li, qkv[:, :, 1].transpose(1, 2), qkv[:, :, 2].transpose(1, 2))
+            a = self._attend(q, K, V, bias).transpose(1, 2).reshape(B * T, H)
+            n = ops.add_rmsnorm(x, a @ L["wo"].t(), L["ln_x"], c.eps)
+            a = self._cross(n @ L["wq_x"].t(), xa, li, T)
+            n = ops.add_rmsnorm(x, a @ L["wo_x"].t(), L["ln_f"], c.eps)
+            m = ops.gelu_tanh_mul(n @ L["wi"].t()) @ L["wout"].t()
+            nxt = layers[li + 1]["ln_s"] if li + 1 < len(layers) else self.dec_norm
+            n = ops.add_rmsnorm(x, m, nxt, c.eps)
+        return n
 
     @torch.no_grad()
     def decode_logits(self, enc: torch.Tensor, cu: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
         """Teacher-forced decoder: ids [B, T] -> logits [B, T, vocab] (fp32)."""
-        c = self.cfg
         B, T = ids.shape
-        H, h, d = c.t_hidden, c.t_heads, c.t_dkv
         xa = self._cross_kv(enc, cu)
-        bias = self._bias_table(T)[None]
+        bias = self._bias_table(T)[None].to(self.dtype)
         x = self.embed.index_select(0, ids.reshape(-1).to(self.device)).contiguous()
-        for li, L in enumerate(self.dec_layers):
-            n = ops.rmsnorm(x, L["ln_s"], c.eps)
-            kv = (n @ L["wqkv"][H:].t()).view(B, T, 2, h, d)
-            k, v = kv[:, :, 0].transpose(1, 2), kv[:, :, 1].transpose(1, 2)
-            self._dec_layer(L, x, k, v, bias, xa, li, B, T)
-        y = ops.rmsnorm(x, self.dec_norm, c.eps)
+        y = self._dec_stack(x, B, T, bias, xa, lambda li, k, v: (k, v))
         return (y @ self.lm_head.t()).float().view(B, T, -1)
 
     # -- generation
@@ -430,17 +433,16 @@ class Pix2StructModel:
         index ``t`` is a device tensor; no host reads)."""
         c = self.cfg
         B = st["tok"].shape[0]
-        H, h, d = c.t_hidden, c.t_heads, c.t_dkv
         t = st["t"]
         x = self.embed.index_select(0, st["tok"]).contiguous()
         bias = st["bias"].index_select(1, t).unsqueeze(0)                 # [1, heads, 1, S]
-        for li, L in enumerate(self.dec_layers):
-            n = ops.rmsnorm(x, L["ln_s"], c.eps)
-            kv = (n @ L["wqkv"][H:].t()).view(B, 2, h, 1, d)
-            st["k"][li].index_copy_(2, t, kv[:, 0])
-            st["v"][li].index_copy_(2, t, kv[:, 1])
-            self._dec_layer(L, x, st["k"][li], st["v"][li], bias, st["xa"], li, B, 1)
-        y = ops.rmsnorm(x, self.dec_norm, c.eps)
+
+        def sink(li, k, v):                                               # k / v [B, heads, 1, dkv]
+            st["k"][li].index_copy_(2, t, k)
+            st["v"][li].index_copy_(2, t, v)
+            return st["k"][li], st["v"][li]
+
+        y = self._dec_stack(x, B, 1, bias, st["xa"], sink)
         logits = (y @ self.lm_head.t()).float()
         nxt = torch.argmax(logits, -1)
         # rows that already emitted EOS keep emitting padding
@@ -460,7 +462,7 @@ class Pix2StructModel:
         c, dev = self.cfg, self.device
         enc, cu = self.encode(patches)
         B, S = len(patches), int(max_new_tokens)
-        st = {"xa": self._cross_kv(enc, cu), "bias": self._bias_table(S),
+        st = {"xa": self._cross_kv(enc, cu), "bias": self._bias_table(S).to(self.dtype),
               "k": torch.zeros(c.t_layers, B, c.t_heads, S, c.t_dkv, dtype=self.dtype, device=dev),
               "v": torch.zeros(c.t_layers, B, c.t_heads, S, c.t_dkv, dtype=self.dtype, device=dev),
               "tok": torch.full((B,), c.decoder_start_id, dtype=torch.long, device=dev),
