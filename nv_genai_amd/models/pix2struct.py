@@ -560,3 +560,56 @@ class DePlot:
 
     def describe(self, image, prompt: Optional[str] = None, max_new_tokens: int = 512) -> str:
         return self.describe_batch([image], prompt, max_new_tokens)[0]
+
+
+class DePlotBatcher:
+    """Dynamic batching for a served DePlot: chart requests arriving within ``max_delay_s`` of
+    each other (up to ``max_batch`` images) share one encoder pass and one batched hipGraph
+    decode; each request's tokens are cut at its own ``max_new_tokens``. Header rendering is
+    per image, so requests with different prompts batch together."""
+
+    def __init__(self, deplot: DePlot, max_batch: int = 32, max_delay_s: float = 0.02):
+        import queue
+        import threading
+
+        self.dp, self.max_batch, self.max_delay_s = deplot, int(max_batch), float(max_delay_s)
+        self.q = queue.Queue()
+        self.batches = 0
+        self._t = threading.Thread(target=self._run, daemon=True, name="deplot-batcher")
+        self._t.start()
+
+    def submit(self, image, prompt: Optional[str] = None, max_new_tokens: int = 512):
+        from concurrent.futures import Future
+
+        f = Future()
+        self.q.put((image, prompt, int(max_new_tokens), f))
+        return f
+
+    def describe(self, image, prompt: Optional[str] = None, max_new_tokens: int = 512) -> str:
+        return self.submit(image, prompt, max_new_tokens).result()
+
+    def _run(self):
+        import queue
+        import time
+
+        while True:
+            items = [self.q.get()]
+            deadline = time.monotonic() + self.max_delay_s
+            while len(items) < self.max_batch:
+                rem = deadline - time.monotonic()
+                if rem <= 0:
+                    break
+                try:
+                    items.append(self.q.get(timeout=rem))
+                except queue.Empty:
+                    break
+            try:
+                ps = [self.dp.patches(im, pr) for im, pr, _, _ in items]
+                outs = self.dp.model.generate(ps, max_new_tokens=max(n for _, _, n, _ in items))
+                self.batches += 1
+                for (_, _, n, f), o in zip(items, outs):
+                    f.set_result(self.dp.tok.decode(o[:n]))
+            except Exception as e:  # noqa: BLE001 - delivered to every waiting request
+                for *_, f in items:
+                    if not f.done():
+                        f.set_exception(e)

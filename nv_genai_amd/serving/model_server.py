@@ -23,7 +23,6 @@ import json
 import logging
 import os
 import struct
-import threading
 import time
 import uuid
 from typing import Any, Dict, List, Optional, Union
@@ -155,7 +154,13 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
     app.state.llm, app.state.embed, app.state.rerank, app.state.batcher = llm_service, embed_engine, rerank_engine, batcher
     app.state.vlm, app.state.vlm_service = vlm, vlm_service
     app.state.deplot = deplot
-    deplot_lock = threading.Lock()
+    deplot_batcher = None
+    if deplot is not None:
+        from ..models.pix2struct import DePlotBatcher
+
+        # concurrent chart requests share one encoder pass and one batched graph decode
+        deplot_batcher = DePlotBatcher(deplot)
+    app.state.deplot_batcher = deplot_batcher
 
     def _deplot_run(msgs, max_tokens):
         from ..models.vision import split_image_parts
@@ -167,10 +172,8 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
             images += imgs
         if not images:
             raise ValueError("a DePlot request needs at least one image")
-        with deplot_lock:            # one model instance: requests run one batch at a time
-            outs = app.state.deplot.describe_batch(images, " ".join(texts) or None,
-                                                   max_new_tokens=min(max_tokens, 512))
-        return "\n".join(outs)
+        futs = [deplot_batcher.submit(im, " ".join(texts) or None, min(max_tokens, 512)) for im in images]
+        return "\n".join(f.result() for f in futs)
 
     def _need(x, what):
         if x is None:

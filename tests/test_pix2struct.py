@@ -174,3 +174,19 @@ def test_generate_many_matches_per_batch_generation():
     many = d.generate_many(imgs, batch=2, max_new_tokens=5, threads=3)
     one = d.model.generate([d.patches(im) for im in imgs], max_new_tokens=5)
     assert many == one
+
+
+def test_deplot_batcher_merges_concurrent_requests():
+    from concurrent.futures import ThreadPoolExecutor
+
+    from nv_genai_amd.models.pix2struct import DePlotBatcher
+
+    d = DePlot("pix2struct-tiny", device="cpu", seed=2)
+    imgs = [_image(30 + 5 * i, 40, 20 + i) for i in range(6)]
+    want = [d.tok.decode(o[:3 + i]) for i, o in
+            enumerate(d.model.generate([d.patches(im) for im in imgs], max_new_tokens=8))]
+    b = DePlotBatcher(d, max_batch=8, max_delay_s=0.5)
+    with ThreadPoolExecutor(6) as ex:
+        got = list(ex.map(lambda i: b.describe(imgs[i], None, 3 + i), range(6)))
+    assert got == want
+    assert b.batches < 6
