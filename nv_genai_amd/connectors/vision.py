@@ -75,6 +75,50 @@ class ImageHeuristics:
         return f"An embedded {fmt} image of {w}x{h} pixels ({len(image)} bytes)."
 
 
+_LOCAL = {}
+
+
+class LocalDePlot:
+    """In-process DePlot behind the ``describe`` contract (requests are dynamically batched)."""
+
+    def __init__(self, deplot):
+        from ..models.pix2struct import DePlotBatcher
+
+        self.model = "google/deplot"
+        self.batcher = DePlotBatcher(deplot)
+
+    def describe(self, image: bytes, prompt: str = "", max_tokens: int = 512, **steer) -> str:
+        return self.batcher.describe(image, prompt or None, min(int(max_tokens), 512))
+
+
+def register_local_vision(model: str, describer) -> None:
+    """Serve ``model`` in-process: ``describer`` has ``describe(image, prompt, max_tokens,
+    **steer)`` — a :class:`~nv_genai_amd.models.vision.VisionLanguageModel`, a
+    :class:`LocalDePlot`, or anything with that method."""
+    _LOCAL[model] = describer
+
+
+def load_local_vision(spec: str, device: Optional[str] = None) -> None:
+    """``spec`` = "ai-neva-22b=neva-22b,ai-google-deplot=deplot" (model name = preset): load
+    each preset in this process and register it (``APP_VISION_LOCAL`` at chain-server start)."""
+    for item in filter(None, (x.strip() for x in spec.split(","))):
+        name, preset = item.split("=", 1)
+        if preset in ("deplot",) or preset.startswith("pix2struct"):
+            from ..models.pix2struct import DePlot
+
+            register_local_vision(name, LocalDePlot(DePlot(preset, device=device)))
+        else:
+            from ..models.vision import VisionLanguageModel
+
+            register_local_vision(name, VisionLanguageModel(preset, device=device))
+
+
 def get_vision_client(model: str = "ai-neva-22b"):
+    """In-process model if one is registered under ``model``, else the configured endpoint,
+    else the endpoint-free heuristics."""
+    if not _LOCAL and os.environ.get("APP_VISION_LOCAL"):
+        load_local_vision(os.environ["APP_VISION_LOCAL"])
+    if model in _LOCAL:
+        return _LOCAL[model]
     url = os.environ.get("VLM_SERVER_URL") or os.environ.get("APP_VLM_SERVERURL")
     return VisionClient(url, model) if url else ImageHeuristics()

@@ -190,3 +190,23 @@ def test_deplot_batcher_merges_concurrent_requests():
         got = list(ex.map(lambda i: b.describe(imgs[i], None, 3 + i), range(6)))
     assert got == want
     assert b.batches < 6
+
+
+def test_local_vision_registry_serves_deplot_in_process(monkeypatch):
+    import io
+
+    from PIL import Image
+
+    from nv_genai_amd.connectors import vision as vc
+
+    monkeypatch.setattr(vc, "_LOCAL", {})
+    monkeypatch.delenv("VLM_SERVER_URL", raising=False)
+    monkeypatch.delenv("APP_VLM_SERVERURL", raising=False)
+    monkeypatch.setenv("APP_VISION_LOCAL", "ai-google-deplot=pix2struct-tiny")
+    buf = io.BytesIO()
+    Image.fromarray(_image(40, 40, 3)).save(buf, format="PNG")
+    c = vc.get_vision_client("ai-google-deplot")
+    assert isinstance(c, vc.LocalDePlot)
+    assert isinstance(c.describe(buf.getvalue(), DePlot.PROMPT, max_tokens=4), str)
+    # names that are not registered keep the endpoint / heuristics path
+    assert isinstance(vc.get_vision_client("ai-neva-22b"), vc.ImageHeuristics)
