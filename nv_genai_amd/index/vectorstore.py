@@ -127,8 +127,11 @@ class VectorStore:
         self._write_ev = None
         self._batcher = None
         dev = torch.device(device) if device is not None else self.index_device()
+        # the query batcher groups searches on the GPU index's stream; a host-side HNSW graph
+        # answers each query on the calling thread
         use = batch_queries if batch_queries is not None else (
-            dev.type == "cuda" and os.environ.get("NGA_BATCH_QUERIES", "1") != "0")
+            dev.type == "cuda" and self.index_device().type == "cuda"
+            and os.environ.get("NGA_BATCH_QUERIES", "1") != "0")
         if use:
             self._batcher = _QueryBatcher(self, dev)
         self.persist_dir = persist_dir
