@@ -12,12 +12,17 @@
 // diversity heuristic for neighbour selection and for shrinking overfull lists). Deletion
 // marks a tombstone: deleted nodes still route the search but are never returned.
 // Concurrency: a shared mutex — searches run in parallel (GIL released, batched queries are
-// split over threads), adds take it exclusively.
+// split over threads), adds take it exclusively; inside an add the batch is linked by worker
+// threads with striped per-node locks on the link lists (vectors, levels and storage are laid
+// out for the whole batch first, so nothing reallocates while the graph grows).
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <array>
+#include <atomic>
+#include <mutex>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -77,11 +82,13 @@ inline float l2sq(const float* a, const float* b, int d) {
 }
 
 using Cand = std::pair<float, int32_t>;  // (distance, node); smaller distance = closer
+constexpr int kMaxLinks = 2 * 512 + 1;   // level-0 capacity 2M for M up to 512
 
 class HNSW {
  public:
   HNSW(int dim, const std::string& metric, int M, int ef_construction, int ef_search, uint64_t seed)
-      : d_(dim), metric_(parse_metric(metric)), M_(std::max(2, M)), M0_(2 * std::max(2, M)),
+      : d_(dim), metric_(parse_metric(metric)), M_(std::min(512, std::max(2, M))),
+        M0_(2 * std::min(512, std::max(2, M))),
         efc_(std::max(ef_construction, M)), ef_(std::max(1, ef_search)), rng_(seed),
         ml_(1.0 / std::log(double(std::max(2, M)))) {
     if (dim <= 0) throw std::invalid_argument("dim must be positive");
@@ -94,18 +101,59 @@ class HNSW {
   int ef() const { return ef_; }
 
   void add(py::array_t<float, py::array::c_style | py::array::forcecast> vecs,
-           py::array_t<int64_t, py::array::c_style | py::array::forcecast> ids) {
+           py::array_t<int64_t, py::array::c_style | py::array::forcecast> ids, int threads) {
     auto v = vecs.unchecked<2>();
     auto id = ids.unchecked<1>();
     if (v.shape(1) != d_) throw std::invalid_argument("vector dim mismatch");
     if (v.shape(0) != id.shape(0)) throw std::invalid_argument("vecs / ids length mismatch");
     const int64_t n = v.shape(0);
-    std::vector<float> buf(d_);
     py::gil_scoped_release nogil;
     std::unique_lock<std::shared_mutex> lk(mu_);
+    // 1. sequential: ids, levels and storage for the whole batch (nothing reallocates while
+    //    the batch is being linked)
     for (int64_t r = 0; r < n; ++r) {
-      for (int j = 0; j < d_; ++j) buf[j] = v(r, j);
-      insert(buf.data(), id(r));
+      if (int_.count(id(r))) {
+        for (int64_t u = 0; u < r; ++u) int_.erase(id(u));   // leave the index unchanged
+        throw std::invalid_argument("duplicate id " + std::to_string(id(r)));
+      }
+      int_[id(r)] = (int32_t)(ext_.size() + r);
+    }
+    const int32_t first = (int32_t)ext_.size();
+    std::uniform_real_distribution<double> U(std::numeric_limits<double>::min(), 1.0);
+    data_.resize(data_.size() + (size_t)n * d_);
+    l0_.resize(l0_.size() + (size_t)n * (M0_ + 1), 0);
+    for (int64_t r = 0; r < n; ++r) {
+      const int32_t me = first + (int32_t)r;
+      float* x = &data_[(size_t)me * d_];
+      for (int j = 0; j < d_; ++j) x[j] = v(r, j);
+      normalise(x);
+      const int lvl = std::min(32, (int)std::floor(-std::log(U(rng_)) * ml_));
+      ext_.push_back(id(r));
+      deleted_.push_back(0);
+      level_.push_back(lvl);
+      up_.emplace_back(lvl);
+      for (int l = 1; l <= lvl; ++l) up_[me][l - 1].assign(M_ + 1, 0);
+    }
+    // 2. link: the first node of an empty graph becomes the entry point, then the batch is
+    //    inserted by ``threads`` workers (per-node striped locks guard the link lists)
+    int32_t start = first;
+    if (entry_ < 0 && n > 0) {
+      entry_ = first;
+      max_level_ = level_[first];
+      start = first + 1;
+    }
+    const int32_t end = first + (int32_t)n;
+    const int T = std::max(1, std::min<int>(threads, (int)((end - start + 63) / 64)));
+    if (T == 1) {
+      for (int32_t me = start; me < end; ++me) link(me);
+    } else {
+      std::atomic<int32_t> next(start);
+      std::vector<std::thread> pool;
+      for (int t = 0; t < T; ++t)
+        pool.emplace_back([&] {
+          for (int32_t me = next.fetch_add(1); me < end; me = next.fetch_add(1)) link(me);
+        });
+      for (auto& th : pool) th.join();
     }
   }
 
@@ -222,7 +270,6 @@ class HNSW {
       if (h.deleted_[i]) ++h.n_deleted_;
       else h.int_[h.ext_[i]] = (int32_t)i;
     }
-    h.seen_.assign(n * 2 + 1, 0);
     return hp;
   }
 
@@ -248,6 +295,21 @@ class HNSW {
   }
 
   // beam search of one layer from ``ep``; returns up to ef closest (max-heap order undone)
+  // copy of node i's level-l list (under its stripe lock while the graph is being linked)
+  template <bool LOCK>
+  int read_links(int32_t i, int l, int32_t* out) const {
+    if (LOCK) {
+      std::lock_guard<std::mutex> g(stripe(i));
+      const int32_t* ln = links(i, l);
+      std::memcpy(out, ln + 1, sizeof(int32_t) * ln[0]);
+      return ln[0];
+    }
+    const int32_t* ln = links(i, l);
+    std::memcpy(out, ln + 1, sizeof(int32_t) * ln[0]);
+    return ln[0];
+  }
+
+  template <bool LOCK = false>
   std::vector<Cand> search_layer(const float* q, int32_t ep, int ef, int l, std::vector<uint32_t>& seen,
                                  uint32_t& tag) const {
     if (++tag == 0) {  // wrapped: reset the visit marks
@@ -264,9 +326,10 @@ class HNSW {
       Cand c = cand.top();
       if (c.first > best.top().first && (int)best.size() >= ef) break;
       cand.pop();
-      const int32_t* ln = links(c.second, l);
-      for (int j = 1; j <= ln[0]; ++j) {
-        int32_t u = ln[j];
+      int32_t nb[kMaxLinks];
+      const int cnt = read_links<LOCK>(c.second, l, nb);
+      for (int j = 0; j < cnt; ++j) {
+        int32_t u = nb[j];
         if (seen[u] == tag) continue;
         seen[u] = tag;
         float du = dist(q, vec(u));
@@ -305,6 +368,7 @@ class HNSW {
   }
 
   void connect(int32_t a, int32_t b, int l) {
+    std::lock_guard<std::mutex> g(stripe(a));
     int32_t* ln = links(a, l);
     const int cap = l == 0 ? M0_ : M_;
     if (ln[0] < cap) {
@@ -322,56 +386,59 @@ class HNSW {
     for (size_t j = 0; j < keep.size(); ++j) ln[j + 1] = keep[j];
   }
 
-  void insert(float* x, int64_t ext_id) {
-    if (int_.count(ext_id)) throw std::invalid_argument("duplicate id " + std::to_string(ext_id));
-    normalise(x);
-    const int32_t me = (int32_t)ext_.size();
-    std::uniform_real_distribution<double> U(std::numeric_limits<double>::min(), 1.0);
-    const int lvl = std::min(32, (int)std::floor(-std::log(U(rng_)) * ml_));
-    data_.insert(data_.end(), x, x + d_);
-    ext_.push_back(ext_id);
-    deleted_.push_back(0);
-    level_.push_back(lvl);
-    l0_.resize(l0_.size() + M0_ + 1, 0);
-    up_.emplace_back(lvl);
-    for (int l = 1; l <= lvl; ++l) up_[me][l - 1].assign(M_ + 1, 0);
-    int_[ext_id] = me;
-    if (seen_.size() < ext_.size()) seen_.resize(ext_.size() * 2, 0);
-    if (entry_ < 0) {
-      entry_ = me;
-      max_level_ = lvl;
-      return;
+  // graph insertion of node ``me`` (vector, level and storage already in place); safe to run
+  // for several nodes at once
+  void link(int32_t me) {
+    const int lvl = level_[me];
+    int32_t ep;
+    int top;
+    {
+      std::lock_guard<std::mutex> g(entry_mu_);
+      ep = entry_;
+      top = max_level_;
     }
-    int32_t ep = entry_;
+    thread_local std::vector<uint32_t> seen;
+    thread_local uint32_t tag = 0;
+    if (seen.size() < ext_.size()) {
+      seen.assign(ext_.size() * 2, 0);
+      tag = 0;
+    }
     const float* q = vec(me);
-    for (int l = max_level_; l > lvl; --l) {  // greedy descent
+    int32_t nb[kMaxLinks];
+    for (int l = top; l > lvl; --l) {  // greedy descent
       bool moved = true;
       float de = dist(q, vec(ep));
       while (moved) {
         moved = false;
-        const int32_t* ln = links(ep, l);
-        for (int j = 1; j <= ln[0]; ++j) {
-          float du = dist(q, vec(ln[j]));
+        const int cnt = read_links<true>(ep, l, nb);
+        for (int j = 0; j < cnt; ++j) {
+          float du = dist(q, vec(nb[j]));
           if (du < de) {
             de = du;
-            ep = ln[j];
+            ep = nb[j];
             moved = true;
           }
         }
       }
     }
-    for (int l = std::min(lvl, max_level_); l >= 0; --l) {
-      std::vector<Cand> w = search_layer(q, ep, efc_, l, seen_, tag_);
-      std::vector<int32_t> nb = select(w, l == 0 ? M0_ : M_);
-      int32_t* ln = links(me, l);
-      ln[0] = (int32_t)nb.size();
-      for (size_t j = 0; j < nb.size(); ++j) ln[j + 1] = nb[j];
-      for (int32_t u : nb) connect(u, me, l);
+    for (int l = std::min(lvl, top); l >= 0; --l) {
+      std::vector<Cand> w = search_layer<true>(q, ep, efc_, l, seen, tag);
+      std::vector<int32_t> sel = select(w, l == 0 ? M0_ : M_);
+      {
+        std::lock_guard<std::mutex> g(stripe(me));
+        int32_t* ln = links(me, l);
+        ln[0] = (int32_t)sel.size();
+        for (size_t j = 0; j < sel.size(); ++j) ln[j + 1] = sel[j];
+      }
+      for (int32_t u : sel) connect(u, me, l);
       ep = w.front().second;
     }
-    if (lvl > max_level_) {
-      max_level_ = lvl;
-      entry_ = me;
+    if (lvl > top) {
+      std::lock_guard<std::mutex> g(entry_mu_);
+      if (lvl > max_level_) {
+        max_level_ = lvl;
+        entry_ = me;
+      }
     }
   }
 
@@ -435,9 +502,10 @@ class HNSW {
   std::vector<std::vector<std::vector<int32_t>>> up_;
   std::unordered_map<int64_t, int32_t> int_;
   int64_t n_deleted_ = 0;
-  std::vector<uint32_t> seen_;  // insertion-time visit marks (adds are exclusive)
-  uint32_t tag_ = 0;
-  mutable std::shared_mutex mu_;
+  mutable std::shared_mutex mu_;                 // searches shared, adds exclusive
+  std::mutex entry_mu_;                          // entry point / top level during a batch link
+  mutable std::array<std::mutex, 4096> stripes_; // link-list locks, striped by node id
+  std::mutex& stripe(int32_t i) const { return stripes_[(uint32_t)i & 4095u]; }
 };
 
 }  // namespace
@@ -447,7 +515,7 @@ void register_hnsw(py::module_& m) {
       .def(py::init<int, const std::string&, int, int, int, uint64_t>(), py::arg("dim"),
            py::arg("metric") = "l2", py::arg("M") = 16, py::arg("ef_construction") = 200,
            py::arg("ef_search") = 64, py::arg("seed") = 100)
-      .def("add", &HNSW::add, py::arg("vecs"), py::arg("ids"))
+      .def("add", &HNSW::add, py::arg("vecs"), py::arg("ids"), py::arg("threads") = 1)
       .def("remove", &HNSW::remove)
       .def("search", &HNSW::search, py::arg("queries"), py::arg("k"), py::arg("ef") = 0,
            py::arg("threads") = 1)

@@ -3,7 +3,8 @@ index of the reference's streaming-ingest collections:
 experimental/streaming_ingest_rag/morpheus_examples/streaming_ingest_rag/vdb_upload/kafka_config.yaml:112-122).
 
 The graph lives in host memory and is built and searched by the native runtime
-(``csrc/runtime/hnsw.cpp``; searches release the GIL and split a query batch over threads).
+(``csrc/runtime/hnsw.cpp``; adds link a batch with worker threads, searches release the GIL
+and split a query batch over threads).
 Same interface and score convention as :class:`~nv_genai_amd.index.flat.FlatIndex` —
 ``search`` returns (scores, ids) with scores = -squared L2, or the inner product (cosine: of
 the normalised vectors), and -1 ids for missing results — so ``VectorStore(index_type="hnsw")``
@@ -57,7 +58,7 @@ class HNSWIndex:
         if v.ndim == 1:
             v = v[None]
         i = np.ascontiguousarray(np.asarray(ids.cpu() if isinstance(ids, torch.Tensor) else ids, dtype=np.int64))
-        self.g.add(v, i)
+        self.g.add(v, i, self.threads)
 
     def remove(self, ids: Sequence[int]) -> int:
         return int(self.g.remove([int(i) for i in ids]))

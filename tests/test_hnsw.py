@@ -20,13 +20,15 @@ def _exact(X, Q, k, metric):
     return np.argsort(-s, axis=1)[:, :k], np.sort(s, axis=1)[:, ::-1][:, :k]
 
 
-@pytest.mark.parametrize("metric", ["l2", "ip", "cosine"])
-def test_recall_against_exact_search(metric):
+@pytest.mark.parametrize("metric,threads", [("l2", 1), ("ip", 4), ("cosine", 8), ("l2", 6)])
+def test_recall_against_exact_search(metric, threads):
     rng = np.random.default_rng(0)
     X = rng.standard_normal((4000, 32)).astype(np.float32)
     Q = rng.standard_normal((100, 32)).astype(np.float32)
-    idx = HNSWIndex(32, metric, M=16, ef_construction=200, ef=128)
-    idx.add(torch.from_numpy(X), torch.arange(4000) + 10)
+    idx = HNSWIndex(32, metric, M=16, ef_construction=200, ef=128, threads=threads)
+    # two batches: the second links into a graph that already exists
+    idx.add(torch.from_numpy(X[:1500]), torch.arange(1500) + 10)
+    idx.add(torch.from_numpy(X[1500:]), torch.arange(1500, 4000) + 10)
     assert len(idx) == 4000
     s, i = idx.search(torch.from_numpy(Q), 10)
     ref_i, ref_s = _exact(X, Q, 10, metric)
@@ -59,6 +61,12 @@ def test_delete_persist_threads_and_errors(tmp_path):
     assert torch.equal(i2, i) and torch.equal(s2, s) and len(again) == 1000
     with pytest.raises(Exception):
         idx.add(X[:1], np.array([1]))                       # duplicate live id
+    with pytest.raises(Exception):
+        idx.add(X[:2], np.array([5000, 5000]))              # duplicate inside a batch
+    assert len(idx) == 1000
+    idx.add(X[:1], np.array([5000]))                        # the failed batch left no trace
+    assert len(idx) == 1001
+    idx.remove([5000])
     with pytest.raises(Exception):
         idx.search(np.zeros((1, 15), np.float32), 3)        # wrong dim
     e = HNSWIndex(16, "l2")

@@ -142,3 +142,46 @@ def test_runtime_under_asan_ubsan(tmp_path):
     assert r.returncode == 0, report
     assert "STRESS_OK" in r.stdout, report
     assert "AddressSanitizer" not in r.stderr and "runtime error:" not in r.stderr, report
+
+
+TSAN_WORKLOAD = textwrap.dedent(r'''
+    import importlib.util, sys
+    import numpy as np
+    spec = importlib.util.spec_from_file_location("_rt", sys.argv[1])
+    rt = importlib.util.module_from_spec(spec); spec.loader.exec_module(rt)
+    rng = np.random.default_rng(0)
+    # multi-threaded HNSW batch linking (striped link-list locks) and threaded batch search
+    for metric in ("l2", "cosine"):
+        h = rt.HNSW(16, metric, 8, 48, 32, 1)
+        h.add(rng.standard_normal((2500, 16)).astype(np.float32), np.arange(2500, dtype=np.int64), 8)
+        h.add(rng.standard_normal((1500, 16)).astype(np.float32), np.arange(2500, 4000, dtype=np.int64), 8)
+        h.remove(list(range(0, 4000, 5)))
+        h.search(rng.standard_normal((400, 16)).astype(np.float32), 10, 64, 8)
+    print("TSAN_OK")
+''')
+
+
+@pytest.mark.timeout(600)
+def test_hnsw_parallel_build_under_tsan(tmp_path):
+    """ThreadSanitizer build of _rt driving the only multi-threaded native code path (HNSW)."""
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    libtsan = subprocess.run(["g++", "-print-file-name=libtsan.so"], capture_output=True,
+                             text=True).stdout.strip()
+    if not os.path.isabs(libtsan) or not os.path.exists(libtsan):
+        pytest.skip("libtsan not available")
+    sys.path.insert(0, ROOT)
+    from nv_genai_amd import _build
+
+    so = _build.build_runtime(force=True, out_dir=tmp_path, extra_flags=["-fsanitize=thread", "-g", "-O1"])
+    script = tmp_path / "tsan.py"
+    script.write_text(TSAN_WORKLOAD)
+    env = dict(os.environ)
+    env["LD_PRELOAD"] = " ".join(p for p in (libtsan, os.environ.get("LD_PRELOAD", "")) if p)
+    env["TSAN_OPTIONS"] = "report_signal_unsafe=0"
+    r = subprocess.run([sys.executable, str(script), str(so)], capture_output=True, text=True,
+                       env=env, timeout=500)
+    report = r.stdout[-3000:] + r.stderr[-6000:]
+    assert r.returncode == 0, report
+    assert "TSAN_OK" in r.stdout, report
+    assert "ThreadSanitizer" not in r.stderr, report
