@@ -26,13 +26,32 @@ Load model (``--mode``):
 Weights are random-init of the real architectures; the corpus is synthetic (index vectors
 are random unit vectors standing in for arctic-embed-l passage embeddings; chunk texts are
 generated prose of ~500 tokens). ``value`` is the whole-job QPS (all ranks).
+
+Launch: ``python bench.py --gpus N`` with N > 1 and no ``WORLD_SIZE`` in the environment starts
+``torch.distributed.run --nproc-per-node N`` on this same command line as a child process
+(before anything touches the GPU) and exits with its status; under torchrun the job checks
+``WORLD_SIZE == --gpus``.
+
+Model parallelism (``--tp T``, SURVEY.md §2.E TP; the reference's ``tensor_para_size`` /
+``enable_custom_all_reduce``, experimental/fm-asr-streaming-rag/nim/configs/mistral-7b.yaml:32-36,
+and NIM's ``count: ${INFERENCE_GPU_COUNT:-all}``, deploy/compose/docker-compose-nim-ms.yaml:20):
+the N ranks form N / T replicas of T ranks each; every replica's driver (tp rank 0) serves the
+RAG clients, its followers replay the driver's steps over RCCL (TP all-reduces on xGMI). With
+``--sharded-index`` the replica's index is striped over its T ranks and each search is a
+broadcast + per-shard MFMA top-k + all-gather merge (CC7/CC8) on the replica's step channel.
+
+``--workload agent`` runs the query-decomposition agent (BASELINE.json configs[3]: Llama-3-70B
+TP=N + a 10M-vector index sharded over the N ranks; ``benchmarks/agent_tp.py``) and reports
+agent queries/s in the same JSON shape.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -40,9 +59,11 @@ import torch
 
 
 REF_EQUIV_QPS_PER_GPU = 4.40   # profiles/r1_refeq/ref_eq.json
+SEARCH_CMD = -3    # replica step-channel command: sharded search (followers join the collectives)
+BARRIER_CMD = -4   # replica step-channel command: followers join a world barrier
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -75,7 +96,39 @@ def parse():
                     help="keep CPython's default GC (multi-ms host pauses stall the GPU)")
     ap.add_argument("--retrieval-delay-ms", type=float, default=50.0,
                     help="max time a query waits for its retrieval batch to fill (Triton max_queue_delay)")
-    return ap.parse_args()
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel ranks per replica (N / tp replicas)")
+    ap.add_argument("--sharded-index", action="store_true",
+                    help="stripe each replica's index over its tp ranks (broadcast + all-gather merge)")
+    ap.add_argument("--workload", choices=("rag", "agent"), default="rag",
+                    help="agent: query-decomposition agent, one TP=N replica + N-way sharded index")
+    ap.add_argument("--kv-cache-fraction", type=float, default=None)
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args) -> None:
+    """``--gpus N > 1`` outside torchrun: run this command line under
+    ``torch.distributed.run --nproc-per-node N`` as a child (no exec: nothing here has touched
+    the GPU, but the child owns the devices) and exit with its status. Rank 0 prints the JSON
+    line on the inherited stdout."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    root = os.path.dirname(os.path.abspath(__file__))
+    env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    sys.stdout.flush()
+    rc = subprocess.call(cmd, env=env)
+    sys.exit(rc)
 
 
 def host_step_summary(llm) -> dict:
@@ -108,9 +161,73 @@ def host_step_summary(llm) -> dict:
             "short_wait": stats(short)}
 
 
-def main():
-    args = parse()
+class ReplicaSearch:
+    """A replica-sharded index seen from the replica's driver: each search first announces
+    itself on the step channel so the followers join its broadcast / all-gather."""
+
+    def __init__(self, llm, index, src: int):
+        self.llm, self.index, self.src = llm, index, src
+        self.dim = index.dim
+
+    def search(self, q, k):
+        self.llm.broadcast_command(SEARCH_CMD, int(q.shape[0]))
+        return self.index.search(q, k, src=self.src)
+
+
+def run_agent(args, world: int) -> None:
+    """``--workload agent``: benchmarks/agent_tp.py (one TP=world replica, world-way sharded
+    index), ``--steps`` x ``--concurrency`` timed agent queries, reported in bench.py's shape."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from benchmarks import agent_tp
+
+    model = args.model if args.model != "llama3-8b" else "llama3-70b"
+    index_size = args.index_size if args.index_size != 1_000_000 else 10_000_000
+    conc = args.concurrency if args.concurrency != 256 else 32
+    argv = ["--model", model, "--embed-model", args.embed_model, "--index-size", str(index_size),
+            "--queries", str(max(1, args.steps * conc)), "--warmup", str(args.warmup * conc),
+            "--concurrency", str(conc), "--answer-tokens", str(args.max_tokens),
+            "--top-k", str(args.top_k)]
+    if args.no_graphs:
+        argv.append("--no-graphs")
+    if args.fp8:
+        argv.append("--fp8")
+    if args.kv_cache_fraction is not None:
+        argv += ["--kv-cache-fraction", str(args.kv_cache_fraction)]
+    res = agent_tp.main(argv, emit=False)
+    if res is None:          # follower rank
+        return
+    ms = 1000.0 * res["elapsed_s"] / max(1, args.steps)
+    line = {
+        "metric": f"query-decomposition agent QPS + p50 latency, {model} TP={world} + "
+                  f"{index_size}-vector index sharded over {world} ranks",
+        "value": res["value"], "unit": "agent queries/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": res["dtype"],
+        "data": res["data"] + " (scripted agent decisions: the weights are random)",
+        "config": {"model": f"{model} + {args.embed_model}", "global_batch": conc,
+                   "seq_len": int(res["mean_prompt_tokens"]) + args.max_tokens,
+                   "parallelism": f"tp{world}", "index_size": index_size, "sharded_index": world > 1,
+                   "workload": "agent"},
+        **{k: res[k] for k in ("p50_latency_ms", "p95_latency_ms", "llm_calls_per_s", "searches_per_s",
+                               "mean_prompt_tokens", "output_tokens_per_s", "setup_s")},
+        "world_size": world, "backend": res.get("backend"),
+    }
+    s = json.dumps(line)
+    print(s, flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(s + "\n")
+
+
+def main(argv=None):
+    args = parse(argv)
+    self_launch(args)
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env} ranks were launched")
+    if args.workload == "agent":
+        run_agent(args, world_env)
+        return
     if world_env > 1:
         # one rank per GPU on a shared host: give each rank's tokenizer thread pool (Rust
         # rayon, sized to every core by default) its share of the cores, before first use
@@ -124,8 +241,13 @@ def main():
     from nv_genai_amd.rag.pipeline import RAGPipeline
     from nv_genai_amd.utils.synthetic import TextGen
 
-    pctx = pd.init_distributed(tp_size=1)
+    tp = max(1, args.tp)
+    if world_env % tp:
+        raise SystemExit(f"bench.py: --tp {tp} does not divide {world_env} ranks")
+    pctx = pd.init_distributed(tp_size=tp)
     world, rank = pctx.world_size, pctx.rank
+    assert world == args.gpus, (world, args.gpus)
+    replicas = world // tp
     dev = str(pctx.device)
     gpu = pctx.device.type == "cuda"
     if world > 1:
@@ -139,19 +261,53 @@ def main():
     sizes = tuple(b for b in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256) if b <= R) or (1,)
     if sizes[-1] < R:
         sizes = sizes + (R,)
+    kv_frac = args.kv_cache_fraction if args.kv_cache_fraction is not None else 0.3
     ecfg = EngineConfig(model=args.model, max_num_seqs=max(R, 1), max_batched_tokens=args.max_batched_tokens,
                         max_model_len=8192, use_graphs=gpu and not args.no_graphs,
-                        graph_batch_sizes=sizes, seed=rank, kv_cache_fraction=0.3,
+                        graph_batch_sizes=sizes, seed=pctx.dp_rank, kv_cache_fraction=kv_frac,
+                        kv_cache_blocks=None if gpu else 512,
                         mixed_prefill_tokens=args.mixed_prefill_tokens,
                         mixed_min_tokens=args.mixed_min_tokens, mixed_max_wait=args.mixed_max_wait,
                         fp8=args.fp8, kv_cache_dtype="fp8" if args.kv_fp8 else "auto")
     llm = LLMEngine(ecfg, device=dev, pctx=pctx)
-    emb = EmbeddingEngine(args.embed_model, device=dev, seed=rank)
-    index = FlatIndex(emb.dim, "cosine", dev, capacity=args.index_size)
-    index.add_random(args.index_size, seed=1234)
+    from nv_genai_amd.models.config import encoder_config
+
+    dim = encoder_config(args.embed_model).hidden
+    sharded = args.sharded_index and tp > 1
+    if sharded:
+        from nv_genai_amd.index.sharded import ShardedIndex
+
+        shard = ShardedIndex(dim, "cosine", dev, pctx=pctx, group=pctx.mp_group,
+                             capacity=args.index_size // tp + 1)
+        shard.add_random(args.index_size, seed=1234)
+    if not llm.is_driver:
+        # follower of a TP replica: replay the driver's steps; join its sharded searches and
+        # the timing barriers; leave when the driver stops the replica
+        hooks = {BARRIER_CMD: lambda n: (torch.cuda.synchronize() if gpu else None, pd.barrier())}
+        if sharded:
+            hooks[SEARCH_CMD] = lambda n: shard.search(torch.zeros(n, dim, device=shard.comm_dev), args.top_k,
+                                                       src=pctx.mp_src)
+        llm.run_follower(hooks=hooks)
+        pd.all_reduce_max(0.0)
+        pd.all_gather_objects(None)
+        pd.destroy()
+        return
+    emb = EmbeddingEngine(args.embed_model, device=dev, seed=pctx.dp_rank)
+    if sharded:
+        index = ReplicaSearch(llm, shard, pctx.mp_src)
+    else:
+        index = FlatIndex(emb.dim, "cosine", dev, capacity=args.index_size)
+        index.add_random(args.index_size, seed=1234)
     docs = SyntheticDocStore(args.index_size)
     rag = RAGPipeline(llm, emb, index, docs, top_k=args.top_k)
-    gen = TextGen(seed=100 + rank)
+    gen = TextGen(seed=100 + pctx.dp_rank)
+
+    def world_barrier():
+        """Every rank, followers included (through the replica's step channel)."""
+        llm.broadcast_command(BARRIER_CMD)
+        if gpu:
+            torch.cuda.synchronize()
+        pd.barrier()
     # random-init encoder outputs are highly anisotropic (every query would retrieve the same
     # few passages and share KV through the prefix cache): PCA-whiten them so concurrent
     # queries retrieve different passages, as with a trained embedding model
@@ -225,9 +381,7 @@ def main():
         from nv_genai_amd.utils.runtime import quiet_gc
 
         quiet_gc()
-    pd.barrier()
-    if gpu:
-        torch.cuda.synchronize()
+    world_barrier()
     prof = None
     if args.profile_dir and rank == 0:
         from torch.profiler import ProfilerActivity, profile
@@ -247,10 +401,9 @@ def main():
             results += one_step()
     else:
         results = closed_loop(args.steps * R, ramping=False)
-    if gpu:
-        torch.cuda.synchronize()
-    pd.barrier()
+    world_barrier()
     elapsed = time.perf_counter() - t0
+    llm.stop_followers()
     if prof is not None:
         prof.__exit__(None, None, None)
         os.makedirs(args.profile_dir, exist_ok=True)
@@ -258,12 +411,13 @@ def main():
         with open(os.path.join(args.profile_dir, "top_kernels.txt"), "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40))
     t_max = pd.all_reduce_max(elapsed)
-    n_req = R * args.steps * world
+    per_replica = pd.all_gather_objects(round(R * args.steps / elapsed, 3))
+    n_req = R * args.steps * replicas
     qps = n_req / t_max
     lat = sorted(r.latency for r in results)
     ttft = sorted(r.ttft for r in results)
     ptoks = [r.prompt_tokens for r in results]
-    out_tok = sum(len(r.request.output_ids) for r in results) * world
+    out_tok = sum(len(r.request.output_ids) for r in results) * replicas
     p50 = statistics.median(lat)
     p95 = lat[min(len(lat) - 1, int(0.95 * len(lat)))]
     line = {
@@ -284,16 +438,18 @@ def main():
         "vs_baseline": round(qps / (REF_EQUIV_QPS_PER_GPU * world), 3),
         "dtype": ("fp8-w8a8" if args.fp8 else "bf16") + (" + fp8 KV cache" if args.kv_fp8 else
                                                            (" (bf16 attention + KV)" if args.fp8 else "")),
-        "data": "synthetic: random-init weights; 1M random unit-vector index + generated ~500-token chunks; generated questions",
+        "data": f"synthetic: random-init weights; {args.index_size:,}-vector random unit-vector index + generated "
+                "~500-token chunks; generated questions",
         "config": {
             "model": f"{args.model} + {args.embed_model}",
-            "global_batch": R * world,
+            "global_batch": R * replicas,
             "seq_len": int(statistics.mean(ptoks)) + args.max_tokens,
-            "parallelism": f"dp{world}",
+            "parallelism": f"dp{replicas}" + (f"xtp{tp}" if tp > 1 else ""),
+            "sharded_index": sharded,
             "index_size": args.index_size,
             "top_k": args.top_k,
             "max_tokens": args.max_tokens,
-            "concurrency_per_gpu": R,
+            "concurrency_per_replica": R,
             "load": args.mode,
             "mixed_prefill_tokens": args.mixed_prefill_tokens,
         },
@@ -314,6 +470,9 @@ def main():
         "host_step_ms": host_step_summary(llm),
         **({"gpu_step_timing": llm.gpu_step_timing()} if args.step_timing and gpu else {}),
         "setup_s": round(setup_s, 1),
+        "world_size": world,
+        "backend": pctx.backend,
+        "per_replica_qps": [x for x in per_replica if x is not None],
         "prefix_cache_hit_blocks": int(llm.sched.prefix_hits()),
         "distinct_docs_retrieved": len({d for r in results for d in r.doc_ids}),
     }

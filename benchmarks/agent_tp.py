@@ -64,7 +64,9 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def main(argv=None):
+def main(argv=None, emit: bool = True):
+    """Run the benchmark; the driver returns the result dict (and prints it when ``emit``),
+    follower ranks return None."""
     args = parse(argv)
     from nv_genai_amd.engine.llm_engine import EngineConfig, LLMEngine, SamplingParams
     from nv_genai_amd.examples.query_decomposition_rag.chains import EXTRACT_PROMPT, TEMPLATE, Ledger
@@ -91,7 +93,7 @@ def main(argv=None):
         comm_dev = index.comm_dev
         eng.run_follower(hooks={SEARCH_CMD: lambda n: index.search(torch.zeros(n, dim, device=comm_dev), k)})
         pd.destroy()
-        return
+        return None
 
     import jinja2
 
@@ -180,13 +182,15 @@ def main(argv=None):
            "output_tokens_per_s": round(stats["output_tokens"] / elapsed, 1),
            "dtype": "fp8-w8a8" if args.fp8 else "bf16",
            "data": "synthetic: random-init weights, random unit-vector index, generated questions",
-           "setup_s": round(setup_s, 1)}
+           "setup_s": round(setup_s, 1), "backend": pctx.backend}
     line = json.dumps(res)
-    print(line, flush=True)
+    if emit:
+        print(line, flush=True)
     if args.out:
         with open(args.out, "w") as f:
             f.write(line + "\n")
     pd.destroy()
+    return res
 
 
 if __name__ == "__main__":

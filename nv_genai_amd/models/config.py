@@ -173,6 +173,10 @@ LLAMA_PRESETS = {
     "llama-tiny": LlamaConfig(name="llama-tiny", vocab_size=32768, hidden=256, layers=2, heads=4,
                               kv_heads=2, head_dim=64, ffn=512, max_position=2048,
                               bos_id=1, eos_ids=(2,)),
+    # Llama-3-70B's attention layout (64 q : 8 kv heads: at TP=8 one KV head per rank) at tiny width
+    "llama70b-tiny": LlamaConfig(name="llama70b-tiny", vocab_size=32768, hidden=256, layers=2, heads=64,
+                                 kv_heads=8, head_dim=16, ffn=512, max_position=2048,
+                                 bos_id=1, eos_ids=(2,)),
     "llama-small": LlamaConfig(name="llama-small", vocab_size=32768, hidden=1024, layers=4,
                                heads=8, kv_heads=2, head_dim=128, ffn=2816,
                                max_position=8192, bos_id=1, eos_ids=(2,)),

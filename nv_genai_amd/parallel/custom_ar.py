@@ -26,6 +26,15 @@ import torch.distributed as dist
 log = logging.getLogger(__name__)
 
 ALGO_AUTO, ALGO_ONE_SHOT, ALGO_TWO_SHOT = 0, 1, 2
+TWO_SHOT_THRESHOLD_BYTES = 512 * 1024   # the kernel's default (custom_ar.h)
+
+
+def choose_algo(nbytes: int, world: int, threshold: int = TWO_SHOT_THRESHOLD_BYTES) -> int:
+    """One-shot (every rank reads all W-1 peers' full message: one flag round trip, W-1
+    times the bytes per link) below ``threshold``; two-shot (reduce-scatter of 1/W slices +
+    all-gather: two round trips, 2/W of the bytes per link) above it. At W = 2 the two-shot
+    saves nothing, so it is one-shot at every size."""
+    return ALGO_TWO_SHOT if world > 2 and nbytes > threshold else ALGO_ONE_SHOT
 
 
 class CustomAllReduce:
@@ -39,6 +48,9 @@ class CustomAllReduce:
         cap = int(capacity_mb * 2 ** 20) // 128 * 128
         self.capacity = cap
         self.fused_norm_max_bytes = 1 << 20
+        self.two_shot_threshold = (int(two_shot_threshold_kb * 1024) if two_shot_threshold_kb is not None
+                                   else TWO_SHOT_THRESHOLD_BYTES)
+        self.algo_counts = {ALGO_ONE_SHOT: 0, ALGO_TWO_SHOT: 0}
         self.enabled = False
         self.impl = None
         # every stage ends with an agreement among the ranks, so a failure on one rank
@@ -46,8 +58,7 @@ class CustomAllReduce:
         handle, err = b"", None
         try:
             self.impl = kernels().CustomAllReduce(self.rank, self.world, cap, float(timeout_s))
-            if two_shot_threshold_kb is not None:
-                self.impl.set_two_shot_threshold(int(two_shot_threshold_kb * 1024))
+            self.impl.set_two_shot_threshold(self.two_shot_threshold)
             handle = self.impl.handle()
         except Exception as e:  # noqa: BLE001
             err = e
@@ -75,9 +86,13 @@ class CustomAllReduce:
 
     def all_reduce(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
                    algo: int = ALGO_AUTO) -> torch.Tensor:
-        """Sum of ``x`` over the group (in place unless ``out`` is given)."""
+        """Sum of ``x`` over the group (in place unless ``out`` is given). ``ALGO_AUTO`` is
+        resolved here (:func:`choose_algo`), so the kernel always receives an explicit one."""
         if out is None:
             out = x
+        if algo == ALGO_AUTO:
+            algo = choose_algo(x.numel() * x.element_size(), self.world, self.two_shot_threshold)
+        self.algo_counts[algo] = self.algo_counts.get(algo, 0) + 1
         self.impl.all_reduce(x, out, algo)
         return out
 

@@ -230,6 +230,15 @@ def all_reduce_sum(v: float) -> float:
     return float(t.item())
 
 
+def all_gather_objects(obj) -> list:
+    """Every rank's ``obj`` in rank order (``[obj]`` outside a job)."""
+    if not dist.is_initialized():
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def destroy():
     if dist.is_initialized():
         dist.destroy_process_group()

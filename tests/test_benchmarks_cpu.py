@@ -59,3 +59,20 @@ def test_headline_bench_two_ranks_gloo():
     assert abs(res["value"] - 6 / (res["ms_per_step"] / 1000)) / res["value"] < 0.01
     for k in ("metric", "unit", "higher_is_better", "scaling", "vs_baseline", "dtype", "data"):
         assert k in res
+
+
+def test_headline_bench_self_launches_for_gpus_n():
+    """``python bench.py --gpus 2`` (no torchrun around it): bench.py starts the 2-rank job
+    itself as a child and relays rank 0's line, which reports both ranks."""
+    env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=os.getcwd())
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1",
+                        "--model", "llama-tiny", "--embed-model", "encoder-tiny", "--index-size", "2000",
+                        "--concurrency", "3", "--max-tokens", "4"],
+                       capture_output=True, text=True, timeout=400, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["world_size"] == 2 and res["config"]["parallelism"] == "dp2"
+    assert len(res["per_replica_qps"]) == 2 and res["config"]["global_batch"] == 6
