@@ -77,12 +77,38 @@ def main():
     if args.only in ("", "search"):
         N, Dx = 1_000_000, 1024
         X = torch.nn.functional.normalize(torch.randn(N, Dx, device=dev), dim=1).to(torch.bfloat16)
+        bias = torch.zeros(N, device=dev)
         for nq in (1, 8, 64):
             Q = torch.nn.functional.normalize(torch.randn(nq, Dx, device=dev), dim=1).to(torch.bfloat16)
             us = timeit(lambda: ops.score(Q, X, None, 1.0))
             us_all = timeit(lambda: ops.topk(ops.score(Q, X, None, 1.0), 4))
+            us_f = timeit(lambda: ops.search_topk(Q, X, bias, 1.0, 4))
             out[f"search_1Mx1024_q{nq}"] = {"score_us": round(us, 1), "score_TBps": round(N * Dx * 2 / us / 1e6, 2),
-                                             "score_topk_us": round(us_all, 1)}
+                                             "score_topk_us": round(us_all, 1),
+                                             "fused_us": round(us_f, 1),
+                                             "fused_TBps": round(N * Dx * 2 / us_f / 1e6, 2),
+                                             "fused_vs_score_only": round(us_f / us, 3)}
+        # one 1.25M-vector shard of the 10M index over 8 GPUs
+        Xs = X[:1_000_000]
+        Xs = torch.cat([Xs, Xs[:250_000]])
+        bs = torch.zeros(Xs.shape[0], device=dev)
+        for nq in (8, 64):
+            Q = torch.nn.functional.normalize(torch.randn(nq, Dx, device=dev), dim=1).to(torch.bfloat16)
+            us_f = timeit(lambda: ops.search_topk(Q, Xs, bs, 1.0, 4))
+            out[f"search_shard1.25Mx1024_q{nq}"] = {"fused_us": round(us_f, 1),
+                                                    "fused_TBps": round(Xs.numel() * 2 / us_f / 1e6, 2)}
+        del Xs, bs
+        # IVF-Flat, the reference's GPU_IVF_FLAT nlist 64 / nprobe 16 over 1M vectors
+        from nv_genai_amd.index.ivf import IVFFlatIndex
+
+        ivf = IVFFlatIndex(Dx, nlist=64, nprobe=16, metric="cosine", device=dev)
+        ivf.train(X[:200_000].float(), iters=5)
+        ivf.add(X, torch.arange(N))
+        for nq in (1, 8, 64):
+            Q = torch.nn.functional.normalize(torch.randn(nq, Dx, device=dev), dim=1)
+            us_i = timeit(lambda: ivf.search(Q, 4))
+            out[f"ivf_1Mx1024_nlist64_nprobe16_q{nq}"] = {"us": round(us_i, 1)}
+        del ivf
         del X
         if args.only == "search":
             print(json.dumps(out))

@@ -384,6 +384,77 @@ void score(Tensor Q, Tensor X, c10::optional<Tensor> row_bias, Tensor S, double 
                     (float)dot_scale, cur_stream(X));
 }
 
+// fused score + per-block top-k (flat: row_beg/row_end/qtab absent, n_items = ceil(nq / 64))
+void score_topk(Tensor Q, Tensor X, c10::optional<Tensor> row_bias, double dot_scale,
+                c10::optional<Tensor> row_beg, c10::optional<Tensor> row_end, c10::optional<Tensor> qtab,
+                c10::optional<Tensor> slot_rows, int64_t n_items, int64_t max_q_per_item, int64_t nblk,
+                int64_t k, Tensor out_v, Tensor out_r) {
+  CHECK_BF16(Q); CHECK_BF16(X); CHECK_CONTIG(Q); CHECK_CONTIG(X);
+  TORCH_CHECK(Q.dim() == 2 && X.dim() == 2 && Q.size(1) == X.size(1));
+  const int64_t D = X.size(1);
+  TORCH_CHECK(D % 32 == 0 && D <= 1216, "score_topk: D must be a multiple of 32 and <= 1216");
+  TORCH_CHECK(max_q_per_item >= 1 && max_q_per_item <= 64, "score_topk: 1..64 queries per item");
+  TORCH_CHECK(k >= 1 && k <= nga::score_topk_kmax((int)max_q_per_item), "score_topk: k too large");
+  TORCH_CHECK(n_items >= 1 && nblk >= 1 && nblk <= 65535 && n_items <= 65535, "score_topk: bad grid");
+  TORCH_CHECK(X.size(0) < (int64_t(1) << 31), "score_topk: rows must fit int32");
+  const bool items = row_beg.has_value();
+  TORCH_CHECK(items == row_end.has_value() && items == qtab.has_value(),
+              "score_topk: row_beg, row_end and qtab go together");
+  if (!items) TORCH_CHECK(n_items == (Q.size(0) + 63) / 64, "score_topk: flat search has ceil(nq/64) items");
+  const float* bp = nullptr;
+  if (row_bias.has_value()) {
+    CHECK_DEV(*row_bias); CHECK_DT(*row_bias, at::kFloat);
+    TORCH_CHECK(row_bias->numel() == X.size(0));
+    bp = row_bias->data_ptr<float>();
+  }
+  const int64_t *rb = nullptr, *re = nullptr;
+  const int32_t* qt = nullptr;
+  const int32_t* sr = nullptr;
+  int64_t out_rows = n_items * 64;
+  if (slot_rows.has_value()) {
+    TORCH_CHECK(items, "score_topk: slot_rows needs item tables");
+    CHECK_DEV(*slot_rows); CHECK_DT(*slot_rows, at::kInt); CHECK_CONTIG(*slot_rows);
+    TORCH_CHECK(slot_rows->numel() == n_items * 64, "score_topk: slot_rows must be [n_items, 64]");
+    sr = slot_rows->data_ptr<int32_t>();
+    // rows of the pair-ordered output: the caller sizes it to its pair count (every slot_rows
+    // entry must be < that; the plan kernel writes pair indices < nq * nprobe)
+    out_rows = out_v.size(0);
+  }
+  if (items) {
+    CHECK_DEV(*row_beg); CHECK_DEV(*row_end); CHECK_DEV(*qtab);
+    CHECK_DT(*row_beg, at::kLong); CHECK_DT(*row_end, at::kLong); CHECK_DT(*qtab, at::kInt);
+    CHECK_CONTIG(*row_beg); CHECK_CONTIG(*row_end); CHECK_CONTIG(*qtab);
+    TORCH_CHECK(row_beg->numel() == n_items && row_end->numel() == n_items && qtab->numel() == n_items * 64,
+                "score_topk: item tables must be [n_items], [n_items], [n_items, 64]");
+    rb = row_beg->data_ptr<int64_t>();
+    re = row_end->data_ptr<int64_t>();
+    qt = qtab->data_ptr<int32_t>();
+  }
+  CHECK_DEV(out_v); CHECK_DEV(out_r); CHECK_DT(out_v, at::kFloat); CHECK_DT(out_r, at::kLong);
+  CHECK_CONTIG(out_v); CHECK_CONTIG(out_r);
+  TORCH_CHECK(out_v.dim() == 3 && out_v.size(1) == nblk && out_v.size(2) == k && out_v.size(0) == out_rows &&
+                  out_r.sizes() == out_v.sizes(),
+              "score_topk: outputs must be [n_items * 64 (or the pair count with slot_rows), nblk, k]");
+  nga::launch_score_topk(bfp(Q), (int)Q.size(0), bfp(X), X.size(0), (int)D, bp, (float)dot_scale, rb, re, qt,
+                         sr, (int)n_items, (int)max_q_per_item, (int)nblk, (int)k, out_v.data_ptr<float>(),
+                         out_r.data_ptr<int64_t>(), cur_stream(X));
+}
+
+// (query, probe) pairs -> per-list work-item slots (qtab, slot_rows: [nlist * ceil(nq/64) * 64])
+void ivf_plan(Tensor probes, int64_t nlist, Tensor qtab, Tensor slot_rows) {
+  CHECK_DEV(probes); CHECK_DT(probes, at::kLong); CHECK_CONTIG(probes);
+  TORCH_CHECK(probes.dim() == 2, "ivf_plan: probes [nq, nprobe]");
+  TORCH_CHECK(nlist >= 1 && nlist <= nga::IVF_PLAN_MAX_LISTS, "ivf_plan: nlist out of range");
+  const int64_t nq = probes.size(0), nprobe = probes.size(1);
+  const int64_t slots = nlist * ((nq + 63) / 64) * 64;
+  CHECK_DEV(qtab); CHECK_DEV(slot_rows); CHECK_DT(qtab, at::kInt); CHECK_DT(slot_rows, at::kInt);
+  CHECK_CONTIG(qtab); CHECK_CONTIG(slot_rows);
+  TORCH_CHECK(qtab.numel() == slots && slot_rows.numel() == slots, "ivf_plan: tables must hold nlist*ceil(nq/64)*64");
+  if (nq == 0) return;
+  nga::launch_ivf_plan(probes.data_ptr<int64_t>(), (int)nq, (int)nprobe, (int)nlist, qtab.data_ptr<int32_t>(),
+                       slot_rows.data_ptr<int32_t>(), cur_stream(probes));
+}
+
 void topk(Tensor in, c10::optional<Tensor> in_idx, int64_t seg_len, int64_t k, Tensor out_v,
           Tensor out_i) {
   CHECK_DEV(in); CHECK_DT(in, at::kFloat); CHECK_CONTIG(in);
@@ -579,6 +650,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("sample", checked("sample", &sample));
   m.def("score", checked("score", &score));
   m.def("topk", checked("topk", &topk));
+  m.def("score_topk", checked("score_topk", &score_topk));
+  m.def("ivf_plan", checked("ivf_plan", &ivf_plan));
+  m.def("score_topk_kmax", [](int64_t q) { return (int64_t)nga::score_topk_kmax((int)q); });
   m.def("pool_l2norm", checked("pool_l2norm", &pool_l2norm));
   m.def("row_sqnorm", checked("row_sqnorm", &row_sqnorm));
   m.def("fir_c64", checked("fir_c64", &fir_c64));

@@ -81,6 +81,16 @@ void launch_sample(float* logits, int B, int V, const float* temperature, const 
 // vector_search.hip
 void launch_score(const uint16_t* Q, int nq, const uint16_t* X, int64_t N, int D,
                   const float* row_bias, float* S, float dot_scale, hipStream_t stream);
+// fused score + per-block top-k over work items (row range + <= 64 query slots); candidates
+// out [n_items * 64, nblk, k]; k <= score_topk_kmax(max_q_per_item)
+int score_topk_kmax(int nq_per_item);
+void launch_score_topk(const uint16_t* Q, int nq, const uint16_t* X, int64_t N, int D,
+                       const float* row_bias, float dot_scale, const int64_t* row_beg,
+                       const int64_t* row_end, const int32_t* qtab, const int32_t* slot_rows, int n_items,
+                       int max_q_per_item, int nblk, int k, float* out_v, int64_t* out_r, hipStream_t stream);
+constexpr int IVF_PLAN_MAX_LISTS = 16384;
+void launch_ivf_plan(const int64_t* probes, int nq, int nprobe, int nlist, int32_t* qtab,
+                     int32_t* slot_rows, hipStream_t stream);
 void launch_topk(const float* in, const int64_t* in_idx, int64_t rows, int64_t row_len,
                  int64_t seg_len, int k, float* out_v, int64_t* out_i, hipStream_t stream);
 

@@ -280,6 +280,356 @@ __global__ void __launch_bounds__(TK_NT) topk_select_kernel(
   }
 }
 
+// ---------------------------------------------------------------- fused score + top-k
+// score_topk_kernel: the score kernel's MFMA stream with the top-k folded in, so no [nq, N]
+// score matrix ever reaches HBM (only [queries, blocks, k] candidates).
+//
+// Work items (blockIdx.y): a row range of X plus up to 64 query slots. Flat search: one item
+// per 64-query chunk over all rows. IVF: one item per (inverted list, 64-query chunk) over the
+// list's contiguous rows, the slots holding the queries that probe that list (``qtab``), so a
+// list is streamed once for every query that probes it. Blocks of an item (blockIdx.x) stride
+// over its 32W-row tiles.
+//
+// Per lane and query group: a register top-K (descending, branch-free insertion) of the
+// scores that lane produced (a 16x16 MFMA tile gives lane (col, h) rows 4h..4h+3 of query
+// col). End of block: the 4 lanes of a query merge their lists through two xor-shuffle
+// bitonic merges, the W waves' lists meet in LDS (the query tile's space, free by then) and
+// one thread per query keeps the block's top k.
+namespace {
+template <int K>
+__device__ __forceinline__ void tk_insert(float (&v)[K], int (&r)[K], float x, int row) {
+  float cv = x;
+  int cr = row;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const bool sw = cv > v[j];
+    const float tv = v[j];
+    const int tr = r[j];
+    v[j] = sw ? cv : tv;
+    r[j] = sw ? cr : tr;
+    cv = sw ? tv : cv;
+    cr = sw ? tr : cr;
+  }
+}
+
+// (v, r) := top K of itself and the list held by lane ^ mask (both sorted descending)
+template <int K>
+__device__ __forceinline__ void tk_merge_xor(float (&v)[K], int (&r)[K], int mask) {
+  float ov[K];
+  int orr[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    ov[j] = __shfl_xor(v[j], mask, 64);
+    orr[j] = __shfl_xor(r[j], mask, 64);
+  }
+  // max(a[j], b[K-1-j]) is bitonic and holds the top K of both; a half-cleaner cascade sorts it
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const bool tb = ov[K - 1 - j] > v[j];
+    v[j] = tb ? ov[K - 1 - j] : v[j];
+    r[j] = tb ? orr[K - 1 - j] : r[j];
+  }
+#pragma unroll
+  for (int st = K / 2; st > 0; st >>= 1) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if ((j & st) == 0) {
+        const bool sw = v[j + st] > v[j];
+        const float a = v[j], b = v[j + st];
+        const int ra = r[j], rb = r[j + st];
+        v[j] = sw ? b : a;
+        v[j + st] = sw ? a : b;
+        r[j] = sw ? rb : ra;
+        r[j + st] = sw ? ra : rb;
+      }
+    }
+  }
+}
+}  // namespace
+
+template <int NG, int W, int K>
+__global__ void __launch_bounds__(64 * W) score_topk_kernel(
+    const uint16_t* __restrict__ Q, int nq, const uint16_t* __restrict__ X, int64_t N, int D,
+    const float* __restrict__ row_bias, float dot_scale, const int64_t* __restrict__ row_beg,
+    const int64_t* __restrict__ row_end, const int32_t* __restrict__ qtab,
+    const int32_t* __restrict__ slot_rows, int k, float* __restrict__ out_v, int64_t* __restrict__ out_r) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t q_s[];
+  __shared__ int s_nql;
+  constexpr int ROWS = 32 * W;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int col = lane & 15, h = lane >> 4;
+  const int item = blockIdx.y;
+  const int nch = D / 8;
+  const int64_t beg = row_beg ? row_beg[item] : 0;
+  const int64_t end = row_end ? row_end[item] : N;
+  const int nblk = gridDim.x;
+
+  // query slot -> query index (-1: empty)
+  auto slot_q = [&](int s) -> int {
+    if (qtab) return qtab[item * 64 + s];
+    const int q = item * 64 + s;
+    return q < nq ? q : -1;
+  };
+  if (tid == 0) s_nql = 0;
+  __syncthreads();
+  if (tid < 64 && slot_q(tid) >= 0) atomicMax(&s_nql, tid + 1);
+  __syncthreads();
+  const int nql = s_nql;
+  // candidate row of a slot: the slot itself (flat), or the (query, probe) pair it serves
+  // (IVF: candidates land in [nq * nprobe, nblk, k] order, -1 = unused slot)
+  auto slot_row = [&](int s) -> int64_t {
+    return slot_rows ? (int64_t)slot_rows[item * 64 + s] : (int64_t)item * 64 + s;
+  };
+  if (nql == 0 || end <= beg) {
+    // nothing to scan: every used slot still reports k empty candidates
+    for (int i = tid; i < 64 * k; i += 64 * W) {
+      const int s = i / k, j = i % k;
+      const int64_t cr = slot_row(s);
+      if (cr < 0) continue;
+      const int64_t o = (cr * nblk + blockIdx.x) * k + j;
+      out_v[o] = -INFINITY;
+      out_r[o] = -1;
+    }
+    return;
+  }
+  const int ngrp = min(NG, (nql + 15) / 16);
+
+  for (int c = tid; c < 16 * NG * nch; c += 64 * W) {
+    const int r = c / nch, ch = c % nch;
+    u16x8 v = (u16x8)(0);
+    const int q = r < nql ? slot_q(r) : -1;
+    if (q >= 0) v = load8(Q + (int64_t)q * D + ch * 8);
+    *reinterpret_cast<u16x8*>(&q_s[r * D + ((ch ^ (r & 15)) * 8)]) = v;
+  }
+  __syncthreads();
+
+  float tv[NG][K];
+  int tr[NG][K];
+#pragma unroll
+  for (int g = 0; g < NG; ++g)
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      tv[g][j] = -INFINITY;
+      tr[g][j] = -1;
+    }
+
+  const int64_t ntiles = (end - beg + ROWS - 1) / ROWS;
+  const int nsteps = D / 32;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += nblk) {
+    const int64_t row_base = beg + tile * ROWS + w * 32;
+    int64_t r0 = row_base + col, r1 = row_base + 16 + col;
+    if (r0 >= end) r0 = end - 1;
+    if (r1 >= end) r1 = end - 1;
+    const uint16_t* x0 = X + r0 * D + 8 * h;
+    const uint16_t* x1 = X + r1 * D + 8 * h;
+
+    f32x4 acc[2][NG];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int g = 0; g < NG; ++g) acc[i][g] = (f32x4)(0.f);
+
+    u16x8 a0[SC_KB], a1[SC_KB];
+#pragma unroll
+    for (int j = 0; j < SC_KB; ++j) {
+      if (j < nsteps) {
+        a0[j] = load8(x0 + 32 * j);
+        a1[j] = load8(x1 + 32 * j);
+      }
+    }
+    for (int s0 = 0; s0 < nsteps; s0 += SC_KB) {
+      u16x8 b0[SC_KB], b1[SC_KB];
+      const bool more = s0 + SC_KB < nsteps;
+#pragma unroll
+      for (int j = 0; j < SC_KB; ++j) {
+        if (more && s0 + SC_KB + j < nsteps) {
+          b0[j] = load8(x0 + 32 * (s0 + SC_KB + j));
+          b1[j] = load8(x1 + 32 * (s0 + SC_KB + j));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < SC_KB; ++j) {
+        const int s = s0 + j;
+        if (s < nsteps) {
+          const int ch = 4 * s + h;
+#pragma unroll
+          for (int g = 0; g < NG; ++g) {
+            if (g < ngrp) {
+              const int qr = 16 * g + col;
+              bf16x8 bq = as_bf16x8(*reinterpret_cast<const u16x8*>(&q_s[qr * D + ((ch ^ (qr & 15)) * 8)]));
+              acc[0][g] = mfma16(as_bf16x8(a0[j]), bq, acc[0][g]);
+              acc[1][g] = mfma16(as_bf16x8(a1[j]), bq, acc[1][g]);
+            }
+          }
+        }
+      }
+      if (more) {
+#pragma unroll
+        for (int j = 0; j < SC_KB; ++j) {
+          a0[j] = b0[j];
+          a1[j] = b1[j];
+        }
+      }
+    }
+    // acc[i][g][rr]: index row row_base + 16 i + 4 h + rr, query slot 16 g + col
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t rb = row_base + 16 * i + 4 * h;
+      float bias[4];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        bias[rr] = (row_bias && rb + rr < end) ? row_bias[rb + rr] : 0.f;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        if (g < ngrp) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const float sc = acc[i][g][rr] * dot_scale + bias[rr];
+            if (rb + rr < end && sc > tv[g][K - 1]) tk_insert<K>(tv[g], tr[g], sc, (int)(rb + rr));
+          }
+        }
+      }
+    }
+  }
+
+  // the 4 lanes (h = 0..3) of each query column merge their lists
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    if (g < ngrp) {
+      tk_merge_xor<K>(tv[g], tr[g], 16);
+      tk_merge_xor<K>(tv[g], tr[g], 32);
+    }
+  }
+  __syncthreads();   // every wave is done with the query tile: its LDS holds the wave lists now
+  float* mv = reinterpret_cast<float*>(q_s);                 // [64 slots][W][K]
+  int* mr = reinterpret_cast<int*>(mv + 64 * W * K);
+  if (h == 0) {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (g < ngrp) {
+        const int sl = 16 * g + col;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          mv[(sl * W + w) * K + j] = tv[g][j];
+          mr[(sl * W + w) * K + j] = tr[g][j];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < 64 && slot_row(tid) >= 0) {
+    const int sl = tid;
+    const int64_t o = (slot_row(sl) * nblk + blockIdx.x) * k;
+    if (sl >= nql || slot_q(sl) < 0) {
+      for (int j = 0; j < k; ++j) {
+        out_v[o + j] = -INFINITY;
+        out_r[o + j] = -1;
+      }
+    } else {
+      int head[W];
+#pragma unroll
+      for (int u = 0; u < W; ++u) head[u] = 0;
+      for (int j = 0; j < k; ++j) {
+        float best = -INFINITY;
+        int bu = -1;
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+          const float x = head[u] < K ? mv[(sl * W + u) * K + head[u]] : -INFINITY;
+          if (x > best) {
+            best = x;
+            bu = u;
+          }
+        }
+        int row = -1;
+        if (bu >= 0) {
+#pragma unroll
+          for (int u = 0; u < W; ++u)
+            if (u == bu) {
+              row = mr[(sl * W + u) * K + head[u]];
+              ++head[u];
+            }
+        }
+        out_v[o + j] = best;
+        out_r[o + j] = row;
+      }
+    }
+  }
+}
+
+int score_topk_kmax(int nq_per_item) { return nq_per_item <= 32 ? 16 : 8; }
+
+void launch_score_topk(const uint16_t* Q, int nq, const uint16_t* X, int64_t N, int D,
+                       const float* row_bias, float dot_scale, const int64_t* row_beg,
+                       const int64_t* row_end, const int32_t* qtab, const int32_t* slot_rows, int n_items,
+                       int max_q_per_item, int nblk, int k, float* out_v, int64_t* out_r, hipStream_t stream) {
+  if (n_items == 0 || nblk == 0) return;
+  const int ng = max_q_per_item <= 16 ? 1 : max_q_per_item <= 32 ? 2 : 4;
+  const int W = ng == 4 ? 8 : 4;
+  const int KR = k <= 4 ? 4 : k <= 8 ? 8 : 16;
+  const size_t qs = (size_t)16 * ng * D * sizeof(uint16_t);
+  const size_t mg = (size_t)64 * W * KR * 8;
+  const size_t lds = qs > mg ? qs : mg;
+  dim3 grid((unsigned)nblk, (unsigned)n_items);
+#define NGA_STK(NG_, W_, K_)                                                                    \
+  do {                                                                                           \
+    static bool attr_ = false;                                                                   \
+    if (!attr_) {                                                                                \
+      /* 160 KiB of LDS minus the kernel's static s_nql */                                     \
+      (void)hipFuncSetAttribute((const void*)score_topk_kernel<NG_, W_, K_>,                     \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64);    \
+      (void)hipGetLastError();                                                                   \
+      attr_ = true;                                                                              \
+    }                                                                                            \
+    score_topk_kernel<NG_, W_, K_><<<grid, 64 * W_, lds, stream>>>(Q, nq, X, N, D, row_bias,     \
+                                                                   dot_scale, row_beg, row_end,  \
+                                                                   qtab, slot_rows, k, out_v,    \
+                                                                   out_r);                       \
+  } while (0)
+  if (ng == 1) {
+    if (KR == 4) NGA_STK(1, 4, 4); else if (KR == 8) NGA_STK(1, 4, 8); else NGA_STK(1, 4, 16);
+  } else if (ng == 2) {
+    if (KR == 4) NGA_STK(2, 4, 4); else if (KR == 8) NGA_STK(2, 4, 8); else NGA_STK(2, 4, 16);
+  } else {
+    if (KR == 4) NGA_STK(4, 8, 4); else NGA_STK(4, 8, 8);
+  }
+#undef NGA_STK
+}
+
+// ---------------------------------------------------------------- IVF scan plan
+// One block groups the (query, probe) pairs by inverted list: pair i = (q = i / nprobe,
+// list p) takes slot rank % 64 of work item p * chunks + rank / 64, rank = its arrival
+// order among list p's pairs (LDS atomics). qtab[slot] = q, slot_rows[slot] = i; untouched
+// slots stay -1. nlist <= IVF_PLAN_MAX_LISTS.
+__global__ void __launch_bounds__(1024) ivf_plan_kernel(const int64_t* __restrict__ probes, int npairs,
+                                                        int nprobe, int nlist, int chunks,
+                                                        int32_t* __restrict__ qtab,
+                                                        int32_t* __restrict__ slot_rows) {
+  __shared__ int cnt[IVF_PLAN_MAX_LISTS];
+  const int t = threadIdx.x;
+  const int nslots = nlist * chunks * 64;
+  for (int i = t; i < nlist; i += 1024) cnt[i] = 0;
+  for (int i = t; i < nslots; i += 1024) {
+    qtab[i] = -1;
+    slot_rows[i] = -1;
+  }
+  __syncthreads();
+  for (int i = t; i < npairs; i += 1024) {
+    const int64_t p = probes[i];
+    if (p < 0 || p >= nlist) continue;   // a short coarse top-k pads with -1
+    const int rank = atomicAdd(&cnt[p], 1);
+    if (rank >= chunks * 64) continue;   // cannot happen: a list has <= nq probing queries
+    const int slot = ((int)p * chunks + rank / 64) * 64 + rank % 64;
+    qtab[slot] = i / nprobe;
+    slot_rows[slot] = i;
+  }
+}
+
+void launch_ivf_plan(const int64_t* probes, int nq, int nprobe, int nlist, int32_t* qtab,
+                     int32_t* slot_rows, hipStream_t stream) {
+  const int chunks = (nq + 63) / 64;
+  ivf_plan_kernel<<<1, 1024, 0, stream>>>(probes, nq * nprobe, nprobe, nlist, chunks, qtab, slot_rows);
+}
+
 void launch_score(const uint16_t* Q, int nq, const uint16_t* X, int64_t N, int D,
                   const float* row_bias, float* S, float dot_scale, hipStream_t stream) {
   if (nq == 0 || N == 0) return;

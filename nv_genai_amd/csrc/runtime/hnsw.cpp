@@ -266,6 +266,7 @@ class HNSW {
       }
     }
     if (!f) throw std::runtime_error("truncated HNSW index file: " + path);
+    h.validate(path);
     for (int64_t i = 0; i < n; ++i) {
       if (h.deleted_[i]) ++h.n_deleted_;
       else h.int_[h.ext_[i]] = (int32_t)i;
@@ -274,6 +275,61 @@ class HNSW {
   }
 
  private:
+  // a loaded graph is trusted by search (no bounds checks on the hot path): every list count
+  // must fit its capacity, every neighbour id must name a node, and the entry point must be a
+  // node whose level is the graph's top level
+  void validate(const std::string& path) const {
+    const int64_t n = (int64_t)ext_.size();
+    auto bad = [&](const char* what) { throw std::runtime_error(std::string("corrupt HNSW graph (") + what + "): " + path); };
+    if (entry_ < -1 || entry_ >= n) bad("entry point");
+    if (entry_ < 0 ? (max_level_ != -1 || n != 0) : (max_level_ < 0 || max_level_ != level_[entry_])) bad("top level");
+    if (M0_ + 1 > kMaxLinks || M_ + 1 > kMaxLinks) bad("link capacity");
+    for (int64_t i = 0; i < n; ++i) {
+      if (deleted_[i] > 1) bad("tombstone flag");
+      for (int l = 0; l <= level_[i]; ++l) {
+        const int32_t* ln = links((int32_t)i, l);
+        const int cap = l == 0 ? M0_ : M_;
+        if (ln[0] < 0 || ln[0] > cap) bad("link count");
+        for (int j = 1; j <= ln[0]; ++j)
+          if (ln[j] < 0 || ln[j] >= n) bad("neighbour id");
+      }
+    }
+  }
+
+  // visit marks of one search / link: a tag per node, bumped per layer search so the array
+  // is cleared only when the tag wraps. Buffers are owned by the index and reused across
+  // calls and threads (a fresh 2 x N array per thread per call dominated batched queries).
+  struct Visit {
+    std::vector<uint32_t> seen;
+    uint32_t tag = 0;
+  };
+  struct VisitLease {
+    const HNSW* h;
+    std::unique_ptr<Visit> v;
+    ~VisitLease() { h->release_visit(std::move(v)); }
+  };
+  VisitLease lease_visit() const {
+    std::unique_ptr<Visit> v;
+    {
+      std::lock_guard<std::mutex> g(visit_mu_);
+      if (!visit_pool_.empty()) {
+        v = std::move(visit_pool_.back());
+        visit_pool_.pop_back();
+      }
+    }
+    if (!v) v = std::make_unique<Visit>();
+    if (v->seen.size() < ext_.size()) {
+      v->seen.assign(ext_.size() + ext_.size() / 2 + 1024, 0);
+      v->tag = 0;
+    }
+    return VisitLease{this, std::move(v)};
+  }
+  void release_visit(std::unique_ptr<Visit> v) const {
+    if (!v) return;
+    std::lock_guard<std::mutex> g(visit_mu_);
+    visit_pool_.push_back(std::move(v));
+  }
+
   // neighbour list of node i at level l: [count, n_0, n_1, ...]
   int32_t* links(int32_t i, int l) {
     return l == 0 ? &l0_[(size_t)i * (M0_ + 1)] : up_[i][l - 1].data();
@@ -397,12 +453,9 @@ class HNSW {
       ep = entry_;
       top = max_level_;
     }
-    thread_local std::vector<uint32_t> seen;
-    thread_local uint32_t tag = 0;
-    if (seen.size() < ext_.size()) {
-      seen.assign(ext_.size() * 2, 0);
-      tag = 0;
-    }
+    VisitLease vis = lease_visit();
+    std::vector<uint32_t>& seen = vis.v->seen;
+    uint32_t& tag = vis.v->tag;
     const float* q = vec(me);
     int32_t nb[kMaxLinks];
     for (int l = top; l > lvl; --l) {  // greedy descent
@@ -467,13 +520,10 @@ class HNSW {
         }
       }
     }
-    // per-thread visit marks (searches run concurrently)
-    thread_local std::vector<uint32_t> seen;
-    thread_local uint32_t tag = 0;
-    if (seen.size() < ext_.size()) {
-      seen.assign(ext_.size() * 2, 0);
-      tag = 0;
-    }
+    // visit marks leased from the index's pool (searches run concurrently)
+    VisitLease vis = lease_visit();
+    std::vector<uint32_t>& seen = vis.v->seen;
+    uint32_t& tag = vis.v->tag;
     // tombstones still route; widen the beam by the deleted share so k live results survive
     int efd = ef + (int)std::min<int64_t>(n_deleted_, ef);
     std::vector<Cand> w = search_layer(qb, ep, efd, 0, seen, tag);
@@ -505,6 +555,8 @@ class HNSW {
   mutable std::shared_mutex mu_;                 // searches shared, adds exclusive
   std::mutex entry_mu_;                          // entry point / top level during a batch link
   mutable std::array<std::mutex, 4096> stripes_; // link-list locks, striped by node id
+  mutable std::mutex visit_mu_;                  // guards visit_pool_
+  mutable std::vector<std::unique_ptr<Visit>> visit_pool_;
   std::mutex& stripe(int32_t i) const { return stripes_[(uint32_t)i & 4095u]; }
 };
 

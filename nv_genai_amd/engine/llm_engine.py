@@ -210,8 +210,10 @@ class LLMEngine:
                                              dev, cfg.decode_pages_per_part,
                                              D=self.model.D) if self.gpu else None
         if self.gpu and self.mcfg.is_moe:
-            # routing buffers sized for the largest step before any hipGraph capture
-            ops.MoEWorkspace.get(T, self.mcfg.experts_per_tok, self.model.n_experts, dev)
+            # this engine's own routing buffers, sized for its largest step before any
+            # hipGraph capture (graphs keep pointing at them for the engine's lifetime)
+            self.model.moe_ws = ops.MoEWorkspace(max(T, 64), self.mcfg.experts_per_tok,
+                                                 self.model.n_experts, dev)
         self.requests: Dict[int, Request] = {}
         self._has_mm = False   # any multimodal request seen (enables the embedding override pass)
         self._ids = itertools.count(1)
@@ -273,7 +275,10 @@ class LLMEngine:
         placeholders of a vision-language prompt)."""
         params = params or SamplingParams()
         V = self.mcfg.vocab_size
-        if prompt_ids and max(prompt_ids) >= V:
+        if prompt_ids and (max(prompt_ids) >= V or min(prompt_ids) < 0):
+            if not getattr(self.tok, "synthetic", False) or min(prompt_ids) < 0:
+                raise ValueError(f"prompt token ids outside the model's vocabulary [0, {V}): "
+                                 "tokenizer / model mismatch")
             # the synthetic tokenizer's id space (32768) exceeds a few real vocabularies
             # (32000): fold, as detokenisation folds sampled ids the other way
             prompt_ids = [t % V for t in prompt_ids]

@@ -9,6 +9,9 @@ HBM (1M x 1024 = 2 GB; a 288 GB MI355X holds >100M at this width), scored by the
   added back on the host so returned scores are true negative squared distances);
 * deletes: bias = -inf tombstones (no re-packing on delete; compaction is lazy).
 
+Search is one fused kernel (``ops.search_topk``): the MFMA scoring stream keeps a per-lane
+register top-k, so only [queries, blocks, k] candidates reach HBM before the final k-merge.
+
 Metrics: ``ip`` (inner product), ``cosine`` (vectors/queries pre-normalised, then ip),
 ``l2``. Search returns (scores [nq, k], ids [nq, k]) with external int64 ids.
 """
@@ -145,12 +148,9 @@ class FlatIndex:
     def _search(self, q: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
         qb = q.to(self.dtype).contiguous()
         X = self.X[: self.n]
-        if self.metric == "l2":
-            S = ops.score(qb, X, self.bias[: self.n], 2.0)
-        else:
-            S = ops.score(qb, X, self.bias[: self.n], 1.0)
         k = min(k, self.n)
-        vals, rows = ops.topk(S, k)
+        # fused MFMA score + per-block top-k: the [nq, N] score matrix never reaches HBM
+        vals, rows = ops.search_topk(qb, X, self.bias[: self.n], 2.0 if self.metric == "l2" else 1.0, k)
         if self.metric == "l2":
             vals = vals - q.float().pow(2).sum(-1, keepdim=True)
         ids = torch.where(rows >= 0, self.ids[rows.clamp_min(0)], torch.full_like(rows, -1))

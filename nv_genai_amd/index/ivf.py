@@ -6,8 +6,11 @@ configuration.py:38-47, utils.py:198-203).
   (``topk`` kernel) against the centroids, centroid update is a scatter-add;
 * storage: vectors re-ordered by list into one contiguous bf16 slab with per-list offsets,
   so a probe scans contiguous HBM;
-* search: coarse top-nprobe over centroids (batched over queries), then per query a
-  gather-free scan of its probed list ranges with the same score + top-k kernels.
+* search: coarse top-nprobe over centroids (batched over queries), then ONE launch of the
+  fused score + top-k kernel over (list, query-chunk) work items: the (query, probe) pairs
+  are grouped by list on the device, each probed list is streamed in place (no gather, no
+  per-query loop, no host sync) once for every query probing it, and a final k-merge picks
+  each query's top-k from its nprobe lists' candidates (``ops.ivf_search_topk``).
 
 Flat search of a batch of queries reads the whole index once for the batch; IVF reads
 nprobe/nlist of it per query — so IVF wins for small batches / latency, flat for big batches.
@@ -64,9 +67,18 @@ class IVFFlatIndex:
         self.bias = torch.zeros(0, dtype=torch.float32, device=self.device)
         self.offsets = torch.zeros(nlist + 1, dtype=torch.int64)
         self._pending = []  # vectors added before training
+        self._n_live = 0    # live (non-tombstoned) rows of the slab, kept on the host
+        self._ranges = None  # device (list_beg, list_end) of the slab, rebuilt after adds
 
     def __len__(self):
-        return int(torch.isfinite(self.bias).sum().item()) + sum(v.shape[0] for v, _ in self._pending)
+        return self._n_live + sum(v.shape[0] for v, _ in self._pending)
+
+    def _list_ranges(self):
+        if self._ranges is None:
+            off = self.offsets.to(self.device)
+            self._ranges = (off[:-1].contiguous(), off[1:].contiguous(),
+                            int((self.offsets[1:] - self.offsets[:-1]).max().item()) if self.nlist else 0)
+        return self._ranges
 
     def _prep(self, v: torch.Tensor) -> torch.Tensor:
         v = v.to(self.device, torch.float32)
@@ -107,6 +119,8 @@ class IVFFlatIndex:
         self.X, self.ids, self.bias = allX[order].contiguous(), allI[order], allB[order]
         cnt = torch.bincount(lists, minlength=self.nlist).cpu()
         self.offsets = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(cnt, 0)])
+        self._n_live += X.shape[0]
+        self._ranges = None
 
     def _ensure_trained(self):
         """Train on whatever was added so far (k-means wants ~39 points per list, so adds
@@ -120,7 +134,9 @@ class IVFFlatIndex:
         ids_t = torch.as_tensor(list(ids) if not torch.is_tensor(ids) else ids, dtype=torch.int64, device=self.device)
         hit = torch.isin(self.ids, ids_t) & torch.isfinite(self.bias)
         self.bias[hit] = float("-inf")
-        return int(hit.sum().item())
+        n = int(hit.sum().item())
+        self._n_live -= n
+        return n
 
     @torch.inference_mode()
     def search(self, q: torch.Tensor, k: int, nprobe: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -133,26 +149,24 @@ class IVFFlatIndex:
             return (torch.empty(nq, 0, device=self.device), torch.empty(nq, 0, dtype=torch.int64, device=self.device))
         nprobe = min(nprobe or self.nprobe, self.nlist)
         qb = q.to(self.dtype).contiguous()
+        if self.X.shape[0] == 0 or k <= 0:
+            return (torch.full((nq, max(k, 0)), float("-inf"), device=self.device),
+                    torch.full((nq, max(k, 0)), -1, dtype=torch.int64, device=self.device))
+        # coarse quantiser: top-nprobe centroids per query (MFMA score + top-k kernels)
         cS = ops.score(qb, self.centroids.to(self.dtype).contiguous(), None, 1.0)
         _, probes = ops.topk(cS, nprobe)
-        probes = probes.cpu()
-        off = self.offsets
-        vals = torch.full((nq, k), float("-inf"), device=self.device)
-        out_ids = torch.full((nq, k), -1, dtype=torch.int64, device=self.device)
-        for i in range(nq):
-            rng = [(int(off[p]), int(off[p + 1])) for p in probes[i].tolist() if off[p + 1] > off[p]]
-            if not rng:
-                continue
-            rows = torch.cat([torch.arange(a, b) for a, b in rng]).to(self.device)
-            Xs = self.X.index_select(0, rows)
-            scale = 2.0 if self.metric == "l2" else 1.0
-            S = ops.score(qb[i:i + 1], Xs, self.bias.index_select(0, rows), scale)
-            kk = min(k, rows.numel())
-            v, r = ops.topk(S, kk)
-            if self.metric == "l2":
-                v = v - q[i].pow(2).sum()
-            vals[i, :kk] = v[0]
-            out_ids[i, :kk] = torch.where(torch.isfinite(v[0]), self.ids[rows[r[0]]], torch.full_like(r[0], -1))
+        beg, end, max_rows = self._list_ranges()
+        scale = 2.0 if self.metric == "l2" else 1.0
+        kmax = 64 if not ops._gpu(self.X) else ops.kernels().score_topk_kmax(min(nq, 64))
+        if k <= kmax:
+            vals, rows = ops.ivf_search_topk(qb, self.X, self.bias, scale, probes, beg, end, max_rows, k)
+        else:   # beyond the fused kernel's register lists: per-query reference scan
+            from ..ops import reference
+            vals, rows = reference.ivf_search_topk(qb, self.X, self.bias, scale, probes, beg, end, k)
+        if self.metric == "l2":
+            vals = vals - q.float().pow(2).sum(-1, keepdim=True)
+        ok = torch.isfinite(vals) & (rows >= 0)
+        out_ids = torch.where(ok, self.ids[rows.clamp_min(0)], torch.full_like(rows, -1))
         return vals, out_ids
 
     def save(self, path: str):
@@ -180,6 +194,7 @@ class IVFFlatIndex:
         idx = cls(m["dim"], m["nlist"], m["nprobe"], m["metric"], device)
         idx.X, idx.ids, idx.bias = t["X"].to(idx.device), t["ids"].to(idx.device), t["bias"].to(idx.device)
         idx.offsets = t["offsets"]
+        idx._n_live = int(torch.isfinite(t["bias"]).sum())
         if "centroids" in t:
             idx.centroids = t["centroids"].to(idx.device)
         return idx

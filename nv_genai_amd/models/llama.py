@@ -84,6 +84,7 @@ class LlamaModel:
         self.ffn = cfg.ffn // ffn_tp
         self.n_experts = (cfg.num_experts // tp if self.expert_parallel else cfg.num_experts)
         self.expert0 = self.p.tp_rank * self.n_experts if self.expert_parallel else 0
+        self.moe_ws = None    # ops.MoEWorkspace owned by the serving engine (GPU MoE)
         self.window = int(cfg.sliding_window or 0)
         self.vocab_local = cfg.vocab_size // tp
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
@@ -438,12 +439,12 @@ class LlamaModel:
         cfg = self.cfg
         if cfg.is_moe:
             return ops.moe_ffn(x, L["router"], L["w13"], L["w2"], cfg.experts_per_tok,
-                               expert0=self.expert0, act=cfg.act)
+                               expert0=self.expert0, act=cfg.act, ws=self.moe_ws)
         if cfg.gated_mlp:
             gu = self._lin(x, L, "wgu")
             if cfg.act == "silu":
                 return self._lin(gu, L, "wd", swiglu=True)
-            return ops.gelu_tanh_mul(gu) @ L["wd"].t()
+            return self._lin(ops.gelu_tanh_mul(gu), L, "wd")
         h = x @ L["wgu"].t()
         ops.bias_gelu_(h, L.get("bgu"), approximate=cfg.act == "gelu_tanh")
         return self._bias_rank0(h @ L["wd"].t(), L.get("bd"))

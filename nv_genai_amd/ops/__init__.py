@@ -236,11 +236,16 @@ MOE_BN = 128       # weight rows per grouped-GEMM tile
 
 
 class MoEWorkspace:
-    """Routing / permutation buffers of the grouped MoE GEMMs for up to ``rows`` tokens,
-    cached per (device, top-k, local experts) and grown on demand (never inside a hipGraph
-    capture: the engine's warm-up forward sizes it for the largest step first)."""
+    """Routing / permutation buffers of the grouped MoE GEMMs for up to ``rows`` tokens.
+
+    A serving model owns one, sized once for its largest step before any hipGraph capture
+    (``LlamaModel.moe_ws``, set by the engine) and passed to :func:`moe_ffn`, so two engines
+    in one process never share routing buffers. Callers without one (benchmarks, tests) use
+    the per-(device, top-k, experts) cache of :meth:`get`; a workspace it outgrows is retired,
+    not freed, because a graph captured earlier may still write to its buffers."""
 
     _cache = {}
+    _retired = []
 
     @classmethod
     def get(cls, rows: int, k: int, E: int, device):
@@ -249,6 +254,8 @@ class MoEWorkspace:
         if ws is None or ws.rows < rows:
             if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("MoE workspace must be sized before graph capture")
+            if ws is not None:
+                cls._retired.append(ws)
             ws = cls(max(rows, 64), k, E, device)
             cls._cache[key] = ws
         return ws
@@ -267,7 +274,7 @@ class MoEWorkspace:
 
 
 def moe_ffn(x: torch.Tensor, router: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, k: int,
-            expert0: int = 0, act: str = "silu") -> torch.Tensor:
+            expert0: int = 0, act: str = "silu", ws: Optional["MoEWorkspace"] = None) -> torch.Tensor:
     """Sparse MoE MLP on rows x [T, H] -> [T, H] (a TP partial sum when the experts or their
     FFN dims are split over ranks). ``w13`` [E, 2F, H] = [gate | up] rows per local expert,
     ``w2`` [E, H, F]; the router [num_experts, H] scores every expert.
@@ -286,7 +293,11 @@ def moe_ffn(x: torch.Tensor, router: torch.Tensor, w13: torch.Tensor, w2: torch.
     out = torch.empty(T, H, dtype=x.dtype, device=x.device)
     if T == 0:
         return out
-    ws = MoEWorkspace.get(T, k, E, x.device)
+    if ws is None:
+        ws = MoEWorkspace.get(T, k, E, x.device)
+    elif ws.rows < T or ws.k != k or ws.E != E:
+        raise ValueError(f"MoE workspace for {ws.rows} rows / top-{ws.k} / {ws.E} experts cannot "
+                         f"take {T} rows / top-{k} / {E} experts")
     M = T * k
     # 64-row M tiles while the experts average <= 4 of them (decode), 128 beyond (prefill)
     bm = 64 if M <= 256 * E else 128
@@ -391,6 +402,85 @@ def topk(S: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
     i2 = torch.empty(rows, k, dtype=torch.int64, device=S.device)
     C.topk(v1, i1, nseg * k, k, v2, i2)
     return v2, i2
+
+
+def score_topk_blocks(nrows: int, rows_per_item: int, n_active_items: int, q_per_item: int) -> int:
+    """Blocks per work item of the fused score + top-k kernel: ~1024 resident blocks over the
+    chip (512 for 64-query items, whose 8-wave blocks hold 128 KiB of query tile each), no
+    more than the item's row tiles."""
+    rows_per_tile = 256 if q_per_item > 32 else 128
+    tiles = max(1, -(-rows_per_item // rows_per_tile))
+    target = (512 if q_per_item > 32 else 1024) // max(1, n_active_items)
+    return int(max(1, min(tiles, max(4, target), 65535)))
+
+
+def search_topk(Q: torch.Tensor, X: torch.Tensor, row_bias=None, dot_scale: float = 1.0, k: int = 4):
+    """Exact top-k rows of X [N, D] for every query of Q [nq, D] by S = dot_scale Q.X^T +
+    row_bias, without materialising S: the fused MFMA score + per-block top-k kernel writes
+    [nq, blocks, k] candidates and one ``topk`` pass merges them (K13: per-tile top-k fused
+    into scoring, then the k-merge). Returns (scores [nq, k], rows [nq, k]; -inf / -1 where X
+    has fewer than k live rows). Falls back to the score matrix + ``topk`` when k exceeds the
+    kernel's register lists."""
+    k = int(min(k, X.shape[0]))
+    nq = Q.shape[0]
+    if not _gpu(X):
+        return ref.topk(ref.score(Q, X, row_bias, dot_scale), k)
+    C = kernels()
+    qpi = min(nq, 64)
+    if k > C.score_topk_kmax(qpi) or nq == 0:
+        return topk(score(Q, X, row_bias, dot_scale), k)
+    items = -(-nq // 64)
+    nblk = score_topk_blocks(X.shape[0], X.shape[0], items, qpi)
+    cv = torch.empty(items * 64, nblk, k, dtype=torch.float32, device=X.device)
+    cr = torch.empty(items * 64, nblk, k, dtype=torch.int64, device=X.device)
+    C.score_topk(Q, X, row_bias, float(dot_scale), None, None, None, None, items, qpi, nblk, k, cv, cr)
+    cv, cr = cv[:nq].view(nq, nblk * k), cr[:nq].view(nq, nblk * k)
+    if nblk == 1:
+        return cv, cr
+    v = torch.empty(nq, k, dtype=torch.float32, device=X.device)
+    r = torch.empty(nq, k, dtype=torch.int64, device=X.device)
+    C.topk(cv, cr, nblk * k, k, v, r)
+    return v, r
+
+
+def ivf_search_topk(Q: torch.Tensor, X: torch.Tensor, row_bias, dot_scale: float, probes: torch.Tensor,
+                    list_beg: torch.Tensor, list_end: torch.Tensor, max_list_rows: int, k: int):
+    """IVF list scan (K14) for a batch of queries in one launch: the (query, probe) pairs are
+    grouped by list on the device (no host sync), every probed list is streamed once for all
+    the queries that probe it by the fused score + top-k kernel, and each query's nprobe x
+    blocks x k candidates are merged by one ``topk`` pass. ``probes`` [nq, nprobe] int64 list
+    ids; ``list_beg`` / ``list_end`` [nlist] int64 row ranges of the list-sorted slab X.
+    Returns (scores [nq, k], slab rows [nq, k]). Launches: plan (1 block), scan, k-merge."""
+    nq, nprobe = probes.shape
+    nlist = list_beg.numel()
+    dev = X.device
+    if not _gpu(X):
+        return ref.ivf_search_topk(Q, X, row_bias, dot_scale, probes, list_beg, list_end, k)
+    C = kernels()
+    qpi = min(nq, 64)
+    if nlist > 16384:    # the plan kernel's LDS list counters (IVF_PLAN_MAX_LISTS)
+        return ref.ivf_search_topk(Q, X, row_bias, dot_scale, probes, list_beg, list_end, k)
+    if k > C.score_topk_kmax(qpi):
+        raise ValueError(f"IVF search: k={k} above the fused kernel's limit {C.score_topk_kmax(qpi)}")
+    chunks = -(-nq // 64)
+    n_items = nlist * chunks
+    probes = probes.to(torch.int64).contiguous()
+    # one block groups the pairs by list: slot -> query, slot -> pair (candidate row)
+    qtab = torch.empty(n_items * 64, dtype=torch.int32, device=dev)
+    slot_rows = torch.empty(n_items * 64, dtype=torch.int32, device=dev)
+    C.ivf_plan(probes, nlist, qtab, slot_rows)
+    rb = list_beg if chunks == 1 else list_beg.repeat_interleave(chunks)
+    re = list_end if chunks == 1 else list_end.repeat_interleave(chunks)
+    nblk = score_topk_blocks(X.shape[0], max_list_rows, min(nlist, nq * nprobe), qpi)
+    # candidates in (query, probe) order: [nq, nprobe * nblk * k] with no gather
+    gv = torch.empty(nq * nprobe, nblk, k, dtype=torch.float32, device=dev)
+    gr = torch.empty(nq * nprobe, nblk, k, dtype=torch.int64, device=dev)
+    C.score_topk(Q, X, row_bias, float(dot_scale), rb, re, qtab, slot_rows, n_items, qpi, nblk, k, gv, gr)
+    gv, gr = gv.view(nq, nprobe * nblk * k), gr.view(nq, nprobe * nblk * k)
+    v = torch.empty(nq, k, dtype=torch.float32, device=dev)
+    r = torch.empty(nq, k, dtype=torch.int64, device=dev)
+    C.topk(gv, gr, gv.shape[1], k, v, r)
+    return v, r
 
 
 def pool_l2norm(hidden, cu, mode: int = 0, normalize: bool = True, out=None):

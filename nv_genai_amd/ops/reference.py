@@ -307,6 +307,26 @@ def topk(S: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
     return v, i
 
 
+def ivf_search_topk(Q, X, row_bias, dot_scale, probes, list_beg, list_end, k):
+    """Per query: exact top-k over the rows of its probed lists (slab rows; -inf / -1 pads)."""
+    nq = Q.shape[0]
+    vals = torch.full((nq, k), float("-inf"), device=X.device)
+    rows = torch.full((nq, k), -1, dtype=torch.int64, device=X.device)
+    beg, end = list_beg.tolist(), list_end.tolist()
+    for i in range(nq):
+        rr = [torch.arange(beg[p], end[p]) for p in probes[i].tolist() if end[p] > beg[p]]
+        if not rr:
+            continue
+        r = torch.cat(rr).to(X.device)
+        s = score(Q[i:i + 1], X.index_select(0, r), None if row_bias is None else row_bias.index_select(0, r),
+                  dot_scale)[0]
+        kk = min(k, r.numel())
+        v, j = torch.topk(s, kk)
+        vals[i, :kk] = v
+        rows[i, :kk] = r[j]
+    return vals, rows
+
+
 def pool_l2norm(hidden, cu, mode: int, normalize: bool):
     B = cu.numel() - 1
     out = torch.zeros(B, hidden.shape[1], dtype=torch.float32, device=hidden.device)

@@ -69,6 +69,9 @@ class LLMTokenizer:
     """Text <-> ids plus the Llama-3 chat template."""
 
     def __init__(self, tok: Optional[Tokenizer] = None):
+        # the bundled synthetic vocabulary (random-init benchmarks): its id space may exceed
+        # a small model's vocabulary, and the engine folds such ids instead of refusing them
+        self.synthetic = tok is None
         if tok is None:
             p = ASSETS / "llm_tokenizer.json"
             with _LOCK:

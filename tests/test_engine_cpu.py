@@ -185,22 +185,24 @@ def test_json_grammar_mask_semantics():
     assert [i for i in range(101) if m[i]] == [100]         # complete: only the stop token
 
 
-def test_fp8_w8a8_model_close_to_bf16():
+@pytest.mark.parametrize("model", ["llama-tiny", "gemma-tiny"])
+def test_fp8_w8a8_model_close_to_bf16(model):
     """W8A8 mode (LlamaModel.quantize_fp8): per-channel FP8 weights, per-row FP8 activations;
-    the forward stays close to the bf16 model and the engine serves it."""
+    the forward stays close to the bf16 model and the engine serves it (SwiGLU and Gemma's
+    GeGLU down projection both go through the FP8 GEMM)."""
     from nv_genai_amd.models.config import llama_config
     from nv_genai_amd.models.llama import LlamaModel
     from nv_genai_amd.parallel.dist import ParallelContext
     from nv_genai_amd.training.functional import llama_hidden  # noqa: F401  (bf16 path import)
 
-    cfg = llama_config("llama-tiny")
+    cfg = llama_config(model)
     sd = LlamaModel(cfg, "cpu", pctx=ParallelContext(), seed=4).state_dict()
     outs = {}
     for fp8 in (False, True):
         m = LlamaModel(cfg, "cpu", pctx=ParallelContext(), weights=sd, fp8=fp8)
         assert m.fp8 == fp8 and ("wqkv" in m.layers[0]) != fp8
-        e = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=4, max_batched_tokens=256, max_model_len=512,
-                                   kv_cache_blocks=32), device="cpu", model=m)
+        e = LLMEngine(EngineConfig(model=model, max_num_seqs=4, max_batched_tokens=256, max_model_len=512,
+                                   kv_cache_blocks=32), device="cpu", model=m, model_cfg=cfg)
         cap = {}
         orig = e._sample
 

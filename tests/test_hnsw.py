@@ -84,3 +84,37 @@ def test_reference_index_conf_mapping():
                                                       "hnsw_ef_construction": 64}
     assert store_kwargs(vcfg, "gpu") == {"metric": "ip", "index_type": "ivf_flat", "nlist": 64}
     assert store_kwargs(vcfg, "plain") == {} and store_kwargs({}, "x") == {}
+
+
+def test_load_rejects_corrupt_graph(tmp_path):
+    """A graph file whose neighbour ids, link counts or entry point do not fit the index is
+    refused at load (search trusts the loaded graph without bounds checks)."""
+    import shutil
+    import struct
+
+    rng = np.random.default_rng(2)
+    n, d, M = 300, 8, 8
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    idx = HNSWIndex(d, "l2", M=M, ef_construction=32, ef=32, threads=2)
+    idx.add(X, np.arange(n))
+    good = tmp_path / "good"
+    idx.save(str(good))
+    raw = (good / "graph.hnsw").read_bytes()
+    l0 = 8 + 28 + 8 + n * d * 4 + n * 8 + n + n * 4      # start of the level-0 link lists
+    hdr_entry = 8 + 5 * 4
+
+    def corrupt(name, off, value):
+        dst = tmp_path / name
+        shutil.copytree(good, dst)
+        b = bytearray(raw)
+        b[off:off + 4] = struct.pack("<i", value)
+        (dst / "graph.hnsw").write_bytes(bytes(b))
+        return str(dst)
+
+    for path in (corrupt("nbr", l0 + 4, 10 ** 6),            # node 0's first neighbour id
+                 corrupt("cnt", l0, 2 * M + 5),               # node 0's level-0 link count
+                 corrupt("entry", hdr_entry, n + 3)):          # entry point past the end
+        with pytest.raises(Exception, match="corrupt"):
+            HNSWIndex.load(path)
+    s, i = HNSWIndex.load(str(good)).search(X[:4], 3)
+    assert i.numpy()[:, 0].tolist() == [0, 1, 2, 3]
