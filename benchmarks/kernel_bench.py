@@ -113,20 +113,26 @@ def main():
         if args.only == "search":
             print(json.dumps(out))
             return
-    for name, lens in (("prefill_1x1196", [1196]), ("prefill_6x1200", [1200] * 6),
-                       ("prefill_27x1200", [1200] * 27), ("prefill_4x4096", [4096] * 4)):
+    for name, lens, qls in (("prefill_1x1196", [1196], None), ("prefill_2x1200", [1200] * 2, None),
+                            ("prefill_3x1200", [1200] * 3, None), ("prefill_6x1200", [1200] * 6, None),
+                            ("prefill_27x1200", [1200] * 27, None), ("prefill_4x4096", [4096] * 4, None),
+                            ("prefill_chunk_940_of_1200", [1200], [940]),
+                            ("prefill_chunk_1024_of_8192", [8192], [1024])):
         if args.only and args.only != "prefill":
             break
+        qls = qls or lens
         kc, vc, bt = paged_setup(lens)
-        T = sum(lens)
+        T = sum(qls)
         q = torch.randn(T, Hq * D, device=dev, dtype=torch.bfloat16)
-        cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0).tolist()), dtype=torch.int32, device=dev)
+        cu = torch.tensor([0] + list(torch.tensor(qls).cumsum(0).tolist()), dtype=torch.int32, device=dev)
         ctx = torch.tensor(lens, dtype=torch.int32, device=dev)
-        flops = sum(2 * 2 * l * (l + 1) / 2 * D * Hq for l in lens)
+        # causal FLOPs: query i of a ql-row chunk ending at ctx sees ctx - ql + i + 1 keys
+        flops = sum(2 * 2 * (ql * (c - ql) + ql * (ql + 1) / 2) * D * Hq for c, ql in zip(lens, qls))
         out[name] = {}
-        for impl, tag in ((0, "auto"), (1, "mfma16"), (2, "mfma32")):
-            us = timeit(lambda: ops.prefill_attention_paged(q, kc, vc, bt, cu, ctx, Hq, Hkv, D, max(lens),
-                                                            D ** -0.5, impl=impl))
+        for impl, tag, mc in ((0, "auto", max(lens)), (0, "auto_nosplit", 0), (1, "mfma16", 0),
+                              (2, "mfma32", 0), (2, "mfma32_split", max(lens))):
+            us = timeit(lambda: ops.prefill_attention_paged(q, kc, vc, bt, cu, ctx, Hq, Hkv, D, max(qls),
+                                                            D ** -0.5, impl=impl, max_ctx=mc))
             out[name][tag] = {"us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1)}
     B, L = 256, 1400
     if args.only == "prefill":

@@ -77,9 +77,12 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
   if (L >= P.total) return;
   const int G = P.Hq / P.Hkv;
   const int ngrp = G / HPW;
-  const int qb = P.ntiles - 1 - L % P.ntiles;
-  const int hg = (L / P.ntiles) % (P.Hkv * ngrp);
-  const int b = L / (P.ntiles * P.Hkv * ngrp);
+  // split-K: the chunk index runs fastest, so a row block's chunks sit side by side on one XCD
+  const int chunk = L % P.nchunks;
+  const int Lb = L / P.nchunks;
+  const int qb = P.ntiles - 1 - Lb % P.ntiles;
+  const int hg = (Lb / P.ntiles) % (P.Hkv * ngrp);
+  const int b = Lb / (P.ntiles * P.Hkv * ngrp);
   const int q0 = P.cu_q[b], qlen = P.cu_q[b + 1] - q0;
   if (qb * RW >= qlen) return;
   const int ctx = P.ctx_lens[b];
@@ -112,8 +115,13 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
   const int wq_lo = ctx - qlen + qb * RW;
   const int wq_hi = ctx - qlen + min(qlen - 1, qb * RW + RW - 1);
   const int last_key = CAUSAL ? wq_hi : ctx - 1;
-  const int n_tiles = last_key / KT + 1;
-  const int t_first = W > 0 ? max(0, wq_lo - W + 1) / KT : 0;
+  const int n_tiles_all = last_key / KT + 1;
+  const int t_first_all = W > 0 ? max(0, wq_lo - W + 1) / KT : 0;
+  // this workgroup's chunk of the row block's tiles (all of them without split-K)
+  const int nchunk_valid = P.nchunks > 1 ? (n_tiles_all - t_first_all + P.split_ch - 1) / P.split_ch : 1;
+  if (chunk >= nchunk_valid) return;
+  const int t_first = P.nchunks > 1 ? t_first_all + chunk * P.split_ch : t_first_all;
+  const int n_tiles = P.nchunks > 1 ? min(n_tiles_all, t_first + P.split_ch) : n_tiles_all;
   const int nt = n_tiles - t_first;
 
   // per-lane DMA source offsets (fixed over tiles): wave instruction i fills LDS chunk
@@ -307,6 +315,23 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
 
   // epilogue: o[dt][j] = O^T[d = 32 dt + (j & 3) + 8 (j >> 2) + 4h][q = r32]
   l += __shfl_xor(l, 32, 64);
+  if (nchunk_valid > 1) {
+    // split row block: unnormalised partials for the combine kernel (coalesced over rows)
+    float* po = P.part_o + ((int64_t)L * 4 + w) * (D * 32);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int d = 32 * dt + (j & 3) + 8 * (j >> 2) + 4 * h;
+        po[d * 32 + r32] = o[dt][j];
+      }
+    if (h == 0) {
+      float* pm = P.part_ml + (((int64_t)L * 4 + w) * 32 + r32) * 2;
+      pm[0] = m;
+      pm[1] = l;
+    }
+    return;
+  }
   if (row_ok) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
     uint16_t* op = P.out + (int64_t)(q0 + qr) * P.out_stride + (int64_t)hq * D + 4 * h;
@@ -322,22 +347,115 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
   }
 }
 
-bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q_len, int D,
-                                 bool paged, bool causal, hipStream_t stream) {
+// Combine of split row blocks: one workgroup per (sequence, head group, row block); wave w
+// and lane (r32, h) own row r32 of wave w's head over d in [64h, 64h + 64). O = sum_c
+// 2^(m_c - M) O_c / sum_c 2^(m_c - M) l_c over the row block's non-empty chunks.
+template <bool CAUSAL, int HPW>
+__global__ void __launch_bounds__(256) prefill_v2_combine_kernel(PrefillParams P) {
+  constexpr int D = 128, KT = 64, RB = 4 / HPW, RW = 32 * RB;
+  const int Lb = blockIdx.x;
+  const int G = P.Hq / P.Hkv;
+  const int ngrp = G / HPW;
+  const int qb = P.ntiles - 1 - Lb % P.ntiles;
+  const int hg = (Lb / P.ntiles) % (P.Hkv * ngrp);
+  const int b = Lb / (P.ntiles * P.Hkv * ngrp);
+  const int q0 = P.cu_q[b], qlen = P.cu_q[b + 1] - q0;
+  if (qb * RW >= qlen) return;
+  const int ctx = P.ctx_lens[b];
+  const int W = CAUSAL ? P.window : 0;
+  const int wq_lo = ctx - qlen + qb * RW;
+  const int wq_hi = ctx - qlen + min(qlen - 1, qb * RW + RW - 1);
+  const int last_key = CAUSAL ? wq_hi : ctx - 1;
+  const int n_tiles_all = last_key / KT + 1;
+  const int t_first_all = W > 0 ? max(0, wq_lo - W + 1) / KT : 0;
+  const int nc = (n_tiles_all - t_first_all + P.split_ch - 1) / P.split_ch;
+  if (nc <= 1) return;   // the attention kernel wrote this row block itself
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int kvh = hg / ngrp;
+  const int hq = kvh * G + (hg % ngrp) * HPW + w % HPW;
+  const int qr = qb * RW + (w / HPW) * 32 + r32;
+  const int64_t L0 = (int64_t)Lb * P.nchunks;
+  float M = -INFINITY;
+  for (int c = 0; c < nc; ++c) M = fmaxf(M, P.part_ml[(((L0 + c) * 4 + w) * 32 + r32) * 2]);
+  const float mo = M == -INFINITY ? 0.f : M;
+  float acc[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) acc[i] = 0.f;
+  float lsum = 0.f;
+  for (int c = 0; c < nc; ++c) {
+    const float* pm = P.part_ml + (((L0 + c) * 4 + w) * 32 + r32) * 2;
+    const float f = __builtin_amdgcn_exp2f(pm[0] - mo);
+    lsum += f * pm[1];
+    const float* po = P.part_o + ((L0 + c) * 4 + w) * (D * 32) + (64 * h) * 32 + r32;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) acc[i] += f * po[i * 32];
+  }
+  if (qr >= qlen) return;
+  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+  uint16_t* op = P.out + (int64_t)(q0 + qr) * P.out_stride + (int64_t)hq * D + 64 * h;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    u16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = f2bf(acc[8 * g + j] * inv);
+    *reinterpret_cast<u16x8*>(op + 8 * g) = v;
+  }
+}
+
+namespace {
+bool v2_takes(const PrefillParams& p, int D, bool paged) {
   static const bool disabled = [] {
     const char* e = getenv("NGA_PREFILL_V1");
     return e && atoi(e) != 0;
   }();
-  if (p.impl == 1 || (p.impl == 0 && disabled) || D != 128 || !paged || p.kv_fp8 ||
-      p.max_blocks > V2_MAX_TILES)
-    return false;
+  return !(p.impl == 1 || (p.impl == 0 && disabled) || D != 128 || !paged || p.kv_fp8 ||
+           p.max_blocks > V2_MAX_TILES);
+}
+}  // namespace
+
+PrefillSplitPlan prefill_v2_split_plan(const PrefillParams& p, int num_seqs, int max_q_len, int max_ctx, int D,
+                                       bool paged, bool causal) {
+  PrefillSplitPlan sp{1, 0, 0, 0};
+  static const int mode = [] {   // NGA_PREFILL_SPLIT=0 disables split-K (A/B runs)
+    const char* e = getenv("NGA_PREFILL_SPLIT");
+    return e ? atoi(e) : 1;
+  }();
+  if (!mode || !v2_takes(p, D, paged) || num_seqs == 0 || max_q_len == 0 || max_ctx <= 0) return sp;
+  const int G = p.Hq / p.Hkv;
+  const int hpw = G % 4 == 0 ? 4 : G % 2 == 0 ? 2 : 1;
+  const int rw = 32 * (4 / hpw);
+  const int64_t base = (int64_t)((max_q_len + rw - 1) / rw) * (p.Hq / hpw) * num_seqs;
+  // the GPU holds 2 of these workgroups per CU (512): below ~2 rounds of row blocks the
+  // longest causal row blocks set the time, so cut them into chunks
+  if (base >= 1024) return sp;
+  const int max_tiles = (max_ctx + 63) / 64;
+  int c = (int)((1536 + base - 1) / base);
+  c = c < 1 ? 1 : c > 8 ? 8 : c;
+  int ch = (max_tiles + c - 1) / c;
+  if (ch < 2) ch = 2;
+  c = (max_tiles + ch - 1) / ch;
+  if (c <= 1) return sp;
+  sp.nchunks = c;
+  sp.split_ch = ch;
+  const int64_t items = base * c;
+  sp.part_o_floats = items * 4 * 128 * 32;
+  sp.part_ml_floats = items * 4 * 32 * 2;
+  return sp;
+}
+
+bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q_len, int D,
+                                 bool paged, bool causal, hipStream_t stream) {
+  if (!v2_takes(p, D, paged)) return false;
   if (num_seqs == 0 || max_q_len == 0) return true;
   const int G = p.Hq / p.Hkv;
   const int hpw = G % 4 == 0 ? 4 : G % 2 == 0 ? 2 : 1;
   const int rw = 32 * (4 / hpw);
   PrefillParams pp = p;
+  if (pp.nchunks < 1) pp.nchunks = 1;
   pp.ntiles = (max_q_len + rw - 1) / rw;
-  const int64_t total = (int64_t)pp.ntiles * (p.Hq / hpw) * num_seqs;
+  const int64_t base = (int64_t)pp.ntiles * (p.Hq / hpw) * num_seqs;
+  const int64_t total = base * pp.nchunks;
   // Size rule: this kernel needs about two of its workgroups per CU (two waves per SIMD) to
   // overlap one wave's softmax with the other's MFMAs. A single ~1K-token prompt is ~300
   // workgroups of 128 (row, head) pairs — one wave per SIMD, measured no faster than the
@@ -345,6 +463,7 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
   // shares the chip with the decode attention of a mixed step (benchmarks/kernel_bench.py
   // and scripts/gpu_r2_attn_ab.sh). From ~6 such prompts (or long ones) up it is 15-25% faster.
   if (p.impl == 0 && total < 2 * 256 * 2) return false;
+  if (pp.nchunks > 1 && (!pp.part_o || !pp.part_ml)) return false;
   pp.total = (int)total;
   pp.per_xcd = (int)((total + 7) / 8);
   dim3 grid(8 * pp.per_xcd);
@@ -367,6 +486,16 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
     if (hpw == 4) NGA_PF2(false, 4); else if (hpw == 2) NGA_PF2(false, 2); else NGA_PF2(false, 1);
   }
 #undef NGA_PF2
+  if (pp.nchunks > 1) {
+    dim3 cgrid((unsigned)base);
+#define NGA_PFC(CS, HP) prefill_v2_combine_kernel<CS, HP><<<cgrid, 256, 0, stream>>>(pp)
+    if (causal) {
+      if (hpw == 4) NGA_PFC(true, 4); else if (hpw == 2) NGA_PFC(true, 2); else NGA_PFC(true, 1);
+    } else {
+      if (hpw == 4) NGA_PFC(false, 4); else if (hpw == 2) NGA_PFC(false, 2); else NGA_PFC(false, 1);
+    }
+#undef NGA_PFC
+  }
   return true;
 }
 

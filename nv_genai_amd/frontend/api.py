@@ -3,8 +3,15 @@ pages/kb.py). Gradio is not available here, so the two pages (Converse, Knowledg
 self-contained HTML/JS page served by FastAPI, talking to same-origin ``/api/*`` routes that
 proxy the chain server through :class:`ChatClient` (trace context propagated).
 
-Speech (Riva streaming ASR / TTS, asr_utils.py / tts_utils.py) needs a Riva endpoint: the
-routes answer 501 unless ``RIVA_API_URI`` is configured, and the UI hides the mic/speaker.
+Speech (the reference's Riva streaming ASR / TTS, frontend/frontend/asr_utils.py:106-155,
+tts_utils.py:77-127): ``SPEECH_API_URI`` (or ``RIVA_API_URI``) names a speech server with the
+OpenAI-style ``/v1/audio/transcriptions`` and ``/v1/audio/speech`` routes; the playground's
+``/api/asr`` streams a recorded clip's transcripts back segment by segment (the reference's
+running / finalized transcript updates) through :class:`dsp.asr.HTTPTranscriptionASR`, and
+``/api/tts`` streams the answer's PCM16 chunks as they are synthesised (the reference's
+``text_to_speech`` generator, with its 300-character segmentation) through
+:class:`dsp.tts.HTTPSpeechTTS`. Without an endpoint both routes answer 501 and the UI hides
+the speech controls.
 """
 from __future__ import annotations
 
@@ -28,6 +35,8 @@ white-space:pre-wrap}.u{color:#8cf}.a{color:#cfc}input[type=text]{width:70%}.hid
 <main><section id="converse"><div id="log"></div><p><input id="q" type="text" placeholder="Ask a question">
 <button onclick="send()">Submit</button> <label><input id="kb" type="checkbox"> Use knowledge base</label>
 <button onclick="document.getElementById('log').innerHTML=''">Clear</button></p>
+<p id="speech" class="hide"><label>Transcribe audio <input id="audio" type="file" accept="audio/wav"
+onchange="asr()"></label> <button onclick="speak()">Read answer aloud</button></p>
 <details><summary>Show context</summary><pre id="ctx"></pre></details></section>
 <section id="kb" class="hide"><p><input id="file" type="file" multiple> <button onclick="upload()">Upload</button></p>
 <ul id="docs"></ul></section></main>
@@ -47,13 +56,51 @@ for(const f of d.documents){const li=document.createElement('li');li.textContent
 b.onclick=async()=>{await fetch('/api/documents?filename='+encodeURIComponent(f),{method:'DELETE'});docs();};li.appendChild(b);ul.appendChild(li);}}
 async function upload(){const fs=document.getElementById('file').files;for(const f of fs){const fd=new FormData();fd.append('file',f);
 await fetch('/api/documents',{method:'POST',body:fd});}docs();}
-fetch('/api/config').then(r=>r.json()).then(c=>document.getElementById('model').textContent=c.model_name);
+async function asr(){const f=document.getElementById('audio').files[0];if(!f)return;
+const r=await fetch('/api/asr',{method:'POST',body:await f.arrayBuffer(),headers:{'Content-Type':'audio/wav'}});
+const q=document.getElementById('q');q.value='';for(const line of (await r.text()).split('\n'))if(line)q.value+=(q.value?' ':'')+JSON.parse(line).text;}
+async function speak(){const as=document.querySelectorAll('#log .a');if(!as.length)return;
+const r=await fetch('/api/tts?format=wav',{method:'POST',headers:{'Content-Type':'application/json'},body:JSON.stringify({text:as[as.length-1].textContent})});
+new Audio(URL.createObjectURL(await r.blob())).play();}
+fetch('/api/config').then(r=>r.json()).then(c=>{document.getElementById('model').textContent=c.model_name;
+document.getElementById('speech').classList.toggle('hide',!c.speech);});
 </script></body></html>"""
 
 
-def create_frontend(client: ChatClient) -> FastAPI:
+def speech_url() -> Optional[str]:
+    return os.environ.get("SPEECH_API_URI") or os.environ.get("RIVA_API_URI") or None
+
+
+def _pcm_of(body: bytes, rate: int):
+    """(PCM16 bytes, sample rate) of an uploaded clip: a WAV file, or raw PCM16 at ``rate``."""
+    import io
+    import wave
+
+    if body[:4] == b"RIFF":
+        with wave.open(io.BytesIO(body)) as w:
+            if w.getsampwidth() != 2 or w.getnchannels() != 1:
+                raise ValueError("speech input must be mono 16-bit PCM")
+            return w.readframes(w.getnframes()), w.getframerate()
+    return body, rate
+
+
+def create_frontend(client: ChatClient, asr=None, tts=None) -> FastAPI:
+    """``asr`` / ``tts``: speech backends (``dsp.asr.ASRBackend`` with a ``rate``, and an object
+    with ``synthesize(text, voice)`` yielding (rate, int16 array) chunks); by default built
+    from ``SPEECH_API_URI`` / ``RIVA_API_URI`` when set."""
     app = FastAPI(title="RAG playground")
     app.state.client = client
+    url = speech_url()
+    if url and asr is None:
+        from ..dsp.asr import HTTPTranscriptionASR
+
+        asr = HTTPTranscriptionASR(url, model=os.environ.get("SPEECH_ASR_MODEL", "asr"),
+                                   segment_s=float(os.environ.get("SPEECH_ASR_SEGMENT_S", "5")))
+    if url and tts is None:
+        from ..dsp.tts import HTTPSpeechTTS
+
+        tts = HTTPSpeechTTS(url, model=os.environ.get("SPEECH_TTS_MODEL", "tts"),
+                            voice=os.environ.get("SPEECH_TTS_VOICE", "default"))
 
     @app.get("/", response_class=HTMLResponse)
     @app.get("/content/converse", response_class=HTMLResponse)
@@ -64,7 +111,7 @@ def create_frontend(client: ChatClient) -> FastAPI:
     @app.get("/api/config")
     def config():
         return {"model_name": client.model_name, "server_url": client.server_url,
-                "speech": bool(os.environ.get("RIVA_API_URI"))}
+                "speech": asr is not None and tts is not None}
 
     @app.post("/api/generate")
     async def generate(request: Request):
@@ -108,10 +155,66 @@ def create_frontend(client: ChatClient) -> FastAPI:
         return {"message": "File uploaded successfully"}
 
     @app.post("/api/asr")
+    async def transcribe(request: Request, rate: int = 16000, chunk_ms: int = 100):
+        """Recorded clip (WAV, or raw PCM16 at ``rate``) -> NDJSON transcripts, one line per
+        recognised segment ({"text", "final"}), streamed as the recogniser produces them."""
+        if asr is None:
+            return JSONResponse({"message": "speech requires a speech endpoint (SPEECH_API_URI)"},
+                                status_code=501)
+        try:
+            pcm, sr = _pcm_of(await request.body(), rate)
+        except (ValueError, EOFError) as e:
+            return JSONResponse({"message": str(e)}, status_code=400)
+        if getattr(asr, "rate", sr) != sr:
+            return JSONResponse({"message": f"the recogniser takes {asr.rate} Hz audio, got {sr} Hz"},
+                                status_code=400)
+        step = max(2, int(sr * chunk_ms / 1000) * 2)
+        chunks = (pcm[i:i + step] for i in range(0, len(pcm), step))
+
+        def lines():
+            for text, final in asr.stream(chunks):
+                yield json.dumps({"text": text, "final": bool(final)}) + "\n"
+
+        return StreamingResponse(lines(), media_type="application/x-ndjson")
+
     @app.post("/api/tts")
-    def speech():
-        if not os.environ.get("RIVA_API_URI"):
-            return JSONResponse({"message": "speech requires a Riva endpoint (RIVA_API_URI)"}, status_code=501)
-        return JSONResponse({"message": "Riva client library not installed on this image"}, status_code=501)
+    async def speak(request: Request, format: str = "pcm"):
+        """{"text", "voice"?} -> the synthesised answer: raw PCM16 chunks streamed as they
+        arrive (``X-Sample-Rate`` header; first audio before the whole answer is rendered),
+        or one WAV file with ``?format=wav``."""
+        if tts is None:
+            return JSONResponse({"message": "speech requires a speech endpoint (SPEECH_API_URI)"},
+                                status_code=501)
+        body = await request.json()
+        text = str(body.get("text", "")).strip()
+        if not text:
+            return JSONResponse({"message": "no text to synthesise"}, status_code=400)
+        gen = tts.synthesize(text, body.get("voice"))
+        first = next(gen, None)
+        if first is None:
+            return JSONResponse({"message": "the speech server returned no audio"}, status_code=502)
+        rate = int(first[0])
+        if format == "wav":
+            import io
+            import wave
+
+            buf = io.BytesIO()
+            with wave.open(buf, "wb") as w:
+                w.setnchannels(1)
+                w.setsampwidth(2)
+                w.setframerate(rate)
+                w.writeframes(first[1].astype("<i2").tobytes())
+                for _, pcm in gen:
+                    w.writeframes(pcm.astype("<i2").tobytes())
+            return StreamingResponse(iter([buf.getvalue()]), media_type="audio/wav")
+
+        def chunks():
+            yield first[1].astype("<i2").tobytes()
+            for _, pcm in gen:
+                if len(pcm):
+                    yield pcm.astype("<i2").tobytes()
+
+        return StreamingResponse(chunks(), media_type=f"audio/L16;rate={rate}",
+                                 headers={"X-Sample-Rate": str(rate)})
 
     return app

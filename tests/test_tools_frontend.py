@@ -100,7 +100,81 @@ def test_frontend_pages_and_api():
     assert up.json()["message"] == "File uploaded successfully"
     assert c.get("/api/documents").json()["documents"] == ["facts.txt"]
     assert c.delete("/api/documents", params={"filename": "facts.txt"}).json()["message"] == "Deleted facts.txt"
-    assert c.post("/api/tts").status_code == 501        # Riva is an optional remote service
+    assert c.post("/api/tts", json={"text": "x"}).status_code == 501   # speech is an optional remote service
+    assert c.post("/api/asr", content=b"\0\0").status_code == 501
+
+
+def test_frontend_speech_against_a_fake_speech_server(monkeypatch):
+    """/api/asr and /api/tts through the real HTTP speech clients (dsp/asr.py, dsp/tts.py) to
+    a local fake server with the OpenAI-style audio routes: a clip's segments come back as
+    NDJSON transcripts, an answer comes back as streamed PCM16 (and as one WAV), segmented
+    for the 300-character limit (reference tts_utils.py:105-108)."""
+    import io
+    import socket
+    import threading
+    import time
+    import wave
+
+    import numpy as np
+    import uvicorn
+    from fastapi import FastAPI, Request
+
+    from nv_genai_amd.dsp.asr import pcm_to_wav
+    from nv_genai_amd.frontend.api import create_frontend
+
+    fake = FastAPI()
+    seen = {"asr": [], "tts": []}
+
+    @fake.post("/v1/audio/transcriptions")
+    async def transcriptions(request: Request):
+        from nv_genai_amd.chain_server.multipart import parse_multipart
+
+        _, data = parse_multipart(await request.body(), request.headers.get("content-type", ""))["file"]
+        with wave.open(io.BytesIO(data)) as w:
+            n = w.getnframes()
+        seen["asr"].append(n)
+        return {"text": f"segment of {n} samples"}
+
+    @fake.post("/v1/audio/speech")
+    async def speech(request: Request):
+        body = await request.json()
+        seen["tts"].append(body["input"])
+        pcm = (np.arange(len(body["input"]) * 100) % 200 - 100).astype("<i2").tobytes()
+        return __import__("fastapi").Response(pcm_to_wav(pcm, 22050), media_type="audio/wav")
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    srv = uvicorn.Server(uvicorn.Config(fake, host="127.0.0.1", port=port, log_level="error"))
+    t = threading.Thread(target=srv.run, daemon=True)
+    t.start()
+    try:
+        for _ in range(200):
+            if srv.started:
+                break
+            time.sleep(0.05)
+        monkeypatch.setenv("SPEECH_API_URI", f"http://127.0.0.1:{port}")
+        monkeypatch.setenv("SPEECH_ASR_SEGMENT_S", "1")
+        c = TestClient(create_frontend(FakeChainClient()))
+        assert c.get("/api/config").json()["speech"] is True
+        clip = pcm_to_wav(np.zeros(16000 * 2 + 4000, dtype="<i2").tobytes(), 16000)   # 2.25 s
+        lines = [json.loads(x) for x in c.post("/api/asr", content=clip).text.splitlines()]
+        assert [x["text"] for x in lines] == ["segment of 16000 samples"] * 2 + ["segment of 4000 samples"]
+        assert all(x["final"] for x in lines) and seen["asr"] == [16000, 16000, 4000]
+        assert c.post("/api/asr?rate=8000", content=b"\0\0" * 10).status_code == 400   # wrong rate
+        answer = "word " * 130                                                           # 650 characters
+        r = c.post("/api/tts", json={"text": answer})
+        assert r.status_code == 200 and r.headers["x-sample-rate"] == "22050"
+        assert seen["tts"][-1].count(" . ") == 3                                        # segmented
+        assert len(r.content) == 2 * 100 * len(seen["tts"][-1])
+        w = c.post("/api/tts?format=wav", json={"text": "short answer"})
+        with wave.open(io.BytesIO(w.content)) as wf:
+            assert wf.getframerate() == 22050 and wf.getnframes() == 100 * len(seen["tts"][-1])
+        assert c.post("/api/tts", json={"text": "  "}).status_code == 400
+    finally:
+        srv.should_exit = True
+        t.join(timeout=5)
 
 
 def test_five_minute_rag_offline_and_reuse(tmp_path, capsys):
