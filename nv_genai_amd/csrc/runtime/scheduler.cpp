@@ -610,6 +610,7 @@ void register_bm25(py::module_& m);
 void register_text(py::module_& m);
 void register_json(py::module_& m);
 void register_hnsw(py::module_& m);
+void register_idmap(py::module_& m);
 
 PYBIND11_MODULE(_rt, m) {
   m.doc() = "nv_genai_amd native host runtime";
@@ -660,4 +661,5 @@ PYBIND11_MODULE(_rt, m) {
   register_text(m);
   register_json(m);
   register_hnsw(m);
+  register_idmap(m);
 }

@@ -9,6 +9,10 @@ HBM (1M x 1024 = 2 GB; a 288 GB MI355X holds >100M at this width), scored by the
   added back on the host so returned scores are true negative squared distances);
 * deletes: bias = -inf tombstones (no re-packing on delete; compaction is lazy).
 
+Bookkeeping is batched: the id -> row map is the native runtime's ``IdMap`` (an open-
+addressing table fed numpy batches), and tombstones are one device scatter per call, so
+ingesting or deleting millions of chunks never loops over ids in Python or syncs per row.
+
 Search is one fused kernel (``ops.search_topk``): the MFMA scoring stream keeps a per-lane
 register top-k, so only [queries, blocks, k] candidates reach HBM before the final k-merge.
 
@@ -25,6 +29,7 @@ from typing import Optional, Tuple
 import torch
 
 from .. import ops
+from .._native import rt
 from ..observability.markers import gpu_range
 
 
@@ -38,7 +43,7 @@ class FlatIndex:
         self.n = 0
         self.n_deleted = 0
         self._alloc(max(capacity, 1))
-        self._id2row = {}
+        self._map = rt.IdMap()
 
     def _alloc(self, cap: int):
         X = torch.zeros(cap, self.dim, dtype=self.dtype, device=self.device)
@@ -64,9 +69,11 @@ class FlatIndex:
         vecs = self._prep(vecs)
         m = vecs.shape[0]
         if ids is None:
-            start = max(self._id2row.keys(), default=-1) + 1
+            start = self._map.max_id() + 1
             ids = torch.arange(start, start + m, dtype=torch.int64)
-        ids = ids.to(torch.int64).cpu()
+        ids = torch.as_tensor(ids).to(torch.int64).cpu()
+        if ids.numel() != m:
+            raise ValueError(f"{m} vectors but {ids.numel()} ids")
         if self.n + m > self.capacity:
             cap = self.capacity
             while cap < self.n + m:
@@ -79,10 +86,8 @@ class FlatIndex:
         else:
             self.bias[r0:r0 + m] = 0.0
         self.ids[r0:r0 + m] = ids.to(self.device)
-        for j, i in enumerate(ids.tolist()):
-            if i in self._id2row:
-                self._delete_row(self._id2row[i])
-            self._id2row[i] = r0 + j
+        # re-added ids replace their old rows: tombstone those in one scatter
+        self._tombstone(self._map.add(ids.numpy(), r0))
         self.n += m
         return ids
 
@@ -92,7 +97,7 @@ class FlatIndex:
         are ``first_id + id_stride * i`` (a sharded index strides its global ids)."""
         g = torch.Generator(device=self.device)
         g.manual_seed(seed)
-        start = max(self._id2row.keys(), default=-1) + 1 if first_id is None else first_id
+        start = self._map.max_id() + 1 if first_id is None else first_id
         if self.n + n > self.capacity:
             self._alloc(self.n + n)
         for c in range(0, n, chunk):
@@ -105,23 +110,23 @@ class FlatIndex:
             self.ids[r0:r0 + m] = start + id_stride * torch.arange(c, c + m, device=self.device)
             self.n += m
         base = self.n - n
-        self._id2row.update(zip(range(start, start + id_stride * n, id_stride), range(base, base + n)))
+        self._map.add_range(start, id_stride, n, base)
 
-    def _delete_row(self, r: int):
-        if self.bias[r].item() != float("-inf"):
-            self.bias[r] = float("-inf")
-            self.n_deleted += 1
+    def _tombstone(self, rows) -> None:
+        """-inf bias on live rows (the map only ever returns rows it held live)."""
+        if len(rows) == 0:
+            return
+        r = torch.from_numpy(rows).to(self.device)
+        self.bias.index_fill_(0, r, float("-inf"))
+        self.n_deleted += len(rows)
 
     def remove(self, ids) -> int:
-        cnt = 0
-        for i in (ids.tolist() if torch.is_tensor(ids) else list(ids)):
-            r = self._id2row.pop(int(i), None)
-            if r is not None:
-                self._delete_row(r)
-                cnt += 1
+        ids = torch.as_tensor(ids if not isinstance(ids, (list, tuple)) else list(ids), dtype=torch.int64)
+        rows = self._map.remove(ids.reshape(-1).cpu().numpy())
+        self._tombstone(rows)
         if self.n_deleted > max(1024, self.n // 4):
             self.compact()
-        return cnt
+        return len(rows)
 
     def compact(self):
         keep = torch.nonzero(self.bias[: self.n] != float("-inf")).flatten()
@@ -132,7 +137,7 @@ class FlatIndex:
         self.bias[m: self.n] = float("-inf")
         self.ids[m: self.n] = -1
         self.n, self.n_deleted = m, 0
-        self._id2row = {int(i): r for r, i in enumerate(self.ids[:m].tolist())}
+        self._map.rebuild(self.ids[:m].cpu().numpy(), torch.ones(m, dtype=torch.uint8).numpy())
 
     @torch.inference_mode()
     def search(self, q: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -183,6 +188,7 @@ class FlatIndex:
         idx.bias[:n] = t["bias"].to(idx.device)
         idx.ids[:n] = t["ids"].to(idx.device)
         idx.n = n
-        idx.n_deleted = int((t["bias"] == float("-inf")).sum())
-        idx._id2row = {int(i): r for r, i in enumerate(t["ids"].tolist()) if t["bias"][r] != float("-inf")}
+        live = t["bias"] != float("-inf")
+        idx.n_deleted = int((~live).sum())
+        idx._map.rebuild(t["ids"].numpy(), live.to(torch.uint8).numpy())
         return idx

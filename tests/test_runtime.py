@@ -102,3 +102,73 @@ def test_token_windows_and_char_split():
     long = " ".join(f"w{i}" for i in range(200))
     cs = rt.char_split(long, 100, 20)
     assert all(len(c) <= 100 for c in cs) and len(cs) > 5
+
+
+def test_idmap_matches_dict_under_random_ops():
+    """Native id -> row map (csrc/runtime/idmap.cpp) against a Python dict through random
+    batched adds (with re-adds and in-batch duplicates), removes, lookups and rebuilds."""
+    import numpy as np
+
+    from nv_genai_amd._native import rt
+
+    rng = np.random.default_rng(0)
+    m, ref = rt.IdMap(), {}
+    row = 0
+    for step in range(300):
+        op = rng.integers(0, 3)
+        if op == 0:
+            ids = rng.integers(-50, 5000, size=int(rng.integers(1, 200)))
+            disp = m.add(ids, row)
+            want = []
+            for j, i in enumerate(ids.tolist()):
+                if i in ref:
+                    want.append(ref[i])
+                ref[i] = row + j
+            row += len(ids)
+            assert sorted(disp.tolist()) == sorted(want)
+        elif op == 1:
+            ids = rng.integers(-50, 5000, size=int(rng.integers(1, 300)))
+            got = m.remove(ids)
+            want = []
+            for i in ids.tolist():
+                if i in ref:
+                    want.append(ref.pop(i))
+            assert sorted(got.tolist()) == sorted(want)
+        else:
+            q = rng.integers(-60, 5100, size=100)
+            assert m.rows(q).tolist() == [ref.get(i, -1) for i in q.tolist()]
+        assert len(m) == len(ref)
+    keys = np.array(sorted(ref), dtype=np.int64)
+    live = (rng.random(len(keys)) < 0.7).astype(np.uint8)
+    m.rebuild(keys, live)
+    assert len(m) == int(live.sum())
+    assert m.rows(keys).tolist() == [j if live[j] else -1 for j in range(len(keys))]
+    m.add_range(100_000, 8, 1000, 7)
+    assert m.rows(np.array([100_000, 100_008, 107_992, 100_001])).tolist() == [7, 8, 1006, -1]
+    assert m.max_id() == 107_992
+
+
+def test_flat_index_batched_bookkeeping():
+    """FlatIndex add / re-add / remove / compact / save-load keep ids and live counts right
+    with the native map (no per-id Python loop, one tombstone scatter per call)."""
+    import torch
+
+    from nv_genai_amd.index.flat import FlatIndex
+
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(3000, 32, generator=g)
+    idx = FlatIndex(32, "cosine", "cpu", capacity=16)
+    idx.add(X[:2000], torch.arange(2000) * 2)
+    assert len(idx) == 2000
+    idx.add(X[2000:2100], torch.arange(100) * 2)           # re-add 100 ids: old rows tombstoned
+    assert len(idx) == 2000 and idx.n_deleted == 100
+    s, i = idx.search(X[2000:2005], 1)
+    assert i[:, 0].tolist() == [0, 2, 4, 6, 8]               # the new vectors answer for the ids
+    assert idx.remove(torch.arange(0, 400, 2)) == 200 and len(idx) == 1800
+    assert idx.remove([0, 2, 123456]) == 0
+    auto = idx.add(X[2100:2110])                              # fresh ids continue after the max id
+    assert auto.tolist() == list(range(3999, 3999 + 10))
+    idx.compact()
+    assert idx.n == len(idx) == 1810 and idx.n_deleted == 0
+    s2, i2 = idx.search(X[2100:2103], 1)
+    assert i2[:, 0].tolist() == [3999, 4000, 4001]
