@@ -285,9 +285,9 @@ void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optio
                        c10::optional<Tensor> block_tables, Tensor cu_q,
                        c10::optional<Tensor> ctx_lens, int64_t Hq, int64_t Hkv, int64_t D,
                        int64_t max_q_len, double scale, bool causal, int64_t window,
-                       int64_t impl, double k_scale, double v_scale, int64_t max_ctx) {
+                       int64_t impl, double k_scale, double v_scale) {
   CHECK_BF16(out); CHECK_BF16(q);
-  TORCH_CHECK(impl >= 0 && impl <= 2, "prefill_attention: impl is 0 (auto), 1 or 2");
+  TORCH_CHECK(impl >= 0 && impl <= 3, "prefill_attention: impl is 0 (auto), 1, 2 or 3");
   CHECK_DEV(cu_q); CHECK_DT(cu_q, at::kInt); CHECK_CONTIG(cu_q);
   TORCH_CHECK(D == 64 || D == 128 || (D == 32 && !kc.has_value()) || (D == 256 && kc.has_value()),
               "prefill_attention: head_dim must be 64 or 128 (32: packed only, 256: paged only)");
@@ -335,21 +335,6 @@ void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optio
     p.kv_stride = k->stride(0);
   }
   p.impl = (int)impl;
-  p.nchunks = 1;
-  // split-K for few long prompts (32x32 kernel): fp32 partials from the caching allocator,
-  // released to it (stream-ordered) when this call returns
-  at::Tensor ws;
-  if (paged && max_ctx > 0) {
-    const nga::PrefillSplitPlan sp =
-        nga::prefill_v2_split_plan(p, (int)B, (int)max_q_len, (int)max_ctx, (int)D, paged, causal);
-    if (sp.nchunks > 1) {
-      ws = at::empty({sp.part_o_floats + sp.part_ml_floats}, q.options().dtype(at::kFloat));
-      p.nchunks = sp.nchunks;
-      p.split_ch = sp.split_ch;
-      p.part_o = ws.data_ptr<float>();
-      p.part_ml = p.part_o + sp.part_o_floats;
-    }
-  }
   nga::launch_prefill_attention(p, (int)B, (int)max_q_len, (int)D, paged, causal, cur_stream(q));
 }
 

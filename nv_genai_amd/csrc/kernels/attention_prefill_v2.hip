@@ -55,20 +55,32 @@ __device__ __forceinline__ int vswz(int row) { return (row >> 1) & 7; }
 
 // ABL (diagnostic builds with NGA_DIAG_BUILD=1, picked by NGA_PV2_ABLATE; results are wrong):
 // 1 = no DMA inside the loop, 2 = no compute, 4 = no DMA and no barrier inside the loop
-template <bool CAUSAL, int HPW, int ABL = 0>
-__global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P) {
+//
+// KS = 2 (split-key, few prompts): 8 waves = two groups of the 4-wave layout above, group g
+// walking key tiles t_first + 2i + g of the same row block with its own double buffers
+// (128 KiB of LDS: one workgroup per CU, two waves per SIMD). A single ~1.2K-token prompt
+// is only ~300 row-block workgroups — about one per CU — so the longest causal row block
+// sets the time; two groups halve that critical path, and the second wave per SIMD
+// overlaps one group's softmax with the other's MFMAs. Both groups run the same number of
+// iterations (the odd last tile of group 1 is a fully masked ghost: no DMA) so the
+// workgroup-wide barriers line up; at the end group 1 hands (m, l, O) to group 0 through
+// LDS and group 0 writes the merged rows.
+template <bool CAUSAL, int HPW, int ABL = 0, int KS = 1>
+__global__ void __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) prefill_attn_v2_kernel(PrefillParams P) {
   constexpr int D = 128, KT = 64;
   constexpr int TILE = KT * D;          // elements of one K (or V^T) tile: 16 KiB
   constexpr int RB = 4 / HPW;           // 32-row query blocks per workgroup
   constexpr int RW = 32 * RB;           // query rows per workgroup
-  // ONE LDS object: [K buffer 0 | K buffer 1 | V^T buffer 0 | V^T buffer 1 | block ids].
-  // (With several LDS variables the compiler gives their accesses alias scopes and then waits
-  // vmcnt(0) before fragment reads of a buffer whose earlier DMA it cannot see retired —
-  // serialising the prefetch; a VMEM block-table load inside the loop did the same.)
-  __shared__ __attribute__((aligned(16))) uint16_t smem[4 * TILE + 2 * V2_MAX_TILES];
-  int32_t* sbt = reinterpret_cast<int32_t*>(smem + 4 * TILE);
-  uint16_t* const kbuf = smem;
-  uint16_t* const vbuf = smem + 2 * TILE;
+  // ONE LDS object: [K buffer 0 | K buffer 1 | V^T buffer 0 | V^T buffer 1 | block ids] per
+  // wave group (the block ids once). (With several LDS variables the compiler gives their
+  // accesses alias scopes and then waits vmcnt(0) before fragment reads of a buffer whose
+  // earlier DMA it cannot see retired — serialising the prefetch; a VMEM block-table load
+  // inside the loop did the same.)
+  __shared__ __attribute__((aligned(16))) uint16_t smem[KS * 4 * TILE + 2 * V2_MAX_TILES];
+  int32_t* sbt = reinterpret_cast<int32_t*>(smem + KS * 4 * TILE);
+  const int grp = KS == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
+  uint16_t* const kbuf = smem + grp * 4 * TILE;
+  uint16_t* const vbuf = kbuf + 2 * TILE;
 
   // XCD-aware order (as the 16x16 kernel): each XCD gets a contiguous range of
   // (sequence, kv head, head group, query block), longest causal blocks first.
@@ -77,18 +89,15 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
   if (L >= P.total) return;
   const int G = P.Hq / P.Hkv;
   const int ngrp = G / HPW;
-  // split-K: the chunk index runs fastest, so a row block's chunks sit side by side on one XCD
-  const int chunk = L % P.nchunks;
-  const int Lb = L / P.nchunks;
-  const int qb = P.ntiles - 1 - Lb % P.ntiles;
-  const int hg = (Lb / P.ntiles) % (P.Hkv * ngrp);
-  const int b = Lb / (P.ntiles * P.Hkv * ngrp);
+  const int qb = P.ntiles - 1 - L % P.ntiles;
+  const int hg = (L / P.ntiles) % (P.Hkv * ngrp);
+  const int b = L / (P.ntiles * P.Hkv * ngrp);
   const int q0 = P.cu_q[b], qlen = P.cu_q[b + 1] - q0;
   if (qb * RW >= qlen) return;
   const int ctx = P.ctx_lens[b];
   const int kvh = hg / ngrp;
 
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x & 255, lane = tid & 63;   // position within the wave group
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hq = kvh * G + (hg % ngrp) * HPW + w % HPW;
   const int rb = w / HPW;
@@ -115,14 +124,12 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
   const int wq_lo = ctx - qlen + qb * RW;
   const int wq_hi = ctx - qlen + min(qlen - 1, qb * RW + RW - 1);
   const int last_key = CAUSAL ? wq_hi : ctx - 1;
-  const int n_tiles_all = last_key / KT + 1;
-  const int t_first_all = W > 0 ? max(0, wq_lo - W + 1) / KT : 0;
-  // this workgroup's chunk of the row block's tiles (all of them without split-K)
-  const int nchunk_valid = P.nchunks > 1 ? (n_tiles_all - t_first_all + P.split_ch - 1) / P.split_ch : 1;
-  if (chunk >= nchunk_valid) return;
-  const int t_first = P.nchunks > 1 ? t_first_all + chunk * P.split_ch : t_first_all;
-  const int n_tiles = P.nchunks > 1 ? min(n_tiles_all, t_first + P.split_ch) : n_tiles_all;
-  const int nt = n_tiles - t_first;
+  const int n_tiles = last_key / KT + 1;
+  const int t_first = W > 0 ? max(0, wq_lo - W + 1) / KT : 0;
+  // iterations of each wave group: group g takes tiles t_first + KS i + g (a tile index past
+  // n_tiles is a ghost: no DMA, fully masked)
+  const int nt = (n_tiles - t_first + KS - 1) / KS;
+  auto tile_of = [&](int i) { return t_first + KS * i + grp; };
 
   // per-lane DMA source offsets (fixed over tiles): wave instruction i fills LDS chunk
   // positions [64 (4w + i), +64) of the K tile (16 chunks per row) and of the V^T tile
@@ -139,17 +146,19 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
   }
   {
     const int32_t* btab = P.block_tables + (int64_t)b * P.max_blocks;
-    for (int i = t_first + tid; i < n_tiles; i += 256) sbt[i] = btab[i];
+    for (int i = t_first + (int)threadIdx.x; i < n_tiles; i += 256 * KS) sbt[i] = btab[i];
     __syncthreads();
   }
   auto page = [&](int t) { return ((int64_t)sbt[t] * P.Hkv + kvh) * (int64_t)TILE; };
   auto issue_k = [&](int t, uint16_t* dst) {
+    if (KS > 1 && t >= n_tiles) return;   // ghost tile
     const char* src = reinterpret_cast<const char*>(P.kc + page(t));
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       glds16(reinterpret_cast<const uint16_t*>(src + koff[i]), dst + (4 * w + i) * 512);
   };
   auto issue_v = [&](int t, uint16_t* dst) {
+    if (KS > 1 && t >= n_tiles) return;   // ghost tile
     const char* src = reinterpret_cast<const char*>(P.vc + page(t));
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -189,6 +198,11 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
   };
   auto mask = [&](f32x16& S, int t, int h2) {
     const int kbase = t * KT + 32 * h2;
+    if (KS > 1 && t >= n_tiles) {   // ghost tile: stale LDS, nothing visible
+#pragma unroll
+      for (int j = 0; j < 16; ++j) S[j] = -INFINITY;
+      return;
+    }
     const bool need = CAUSAL ? (kbase + 31 > wq_lo || (W > 0 && kbase <= wq_hi - W))
                              : (kbase + 32 > ctx);
     if (need) {   // raw scores; the scale is folded into the exp
@@ -279,11 +293,11 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
   // whose last reader was stage A).
   f32x16 Sa, Sb;
   auto iter = [&](int i, int par, bool first) {
-    const int t = t_first + i;
+    const int t = tile_of(i);
     const uint16_t* kc_ = kbuf + par * TILE;
     sync_tiles();   // K(i), V(i) landed; every wave is done with iteration i-1
     if constexpr (ABL != 1 && ABL != 4)
-      if (i + 1 < nt) issue_k(t + 1, kbuf + (par ^ 1) * TILE);
+      if (i + 1 < nt) issue_k(t + KS, kbuf + (par ^ 1) * TILE);
     if constexpr (ABL != 2) {
       if (first) {
         qk(Sa, kc_, 0);
@@ -294,12 +308,12 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
     }
     if constexpr (ABL != 4) __builtin_amdgcn_s_barrier();   // V(i-1) is free
     if constexpr (ABL != 1 && ABL != 4)
-      if (i + 1 < nt) issue_v(t + 1, vbuf + (par ^ 1) * TILE);
+      if (i + 1 < nt) issue_v(t + KS, vbuf + (par ^ 1) * TILE);
     if constexpr (ABL != 2) stage(Sa, vbuf + par * TILE, 0, Sb, kc_, 1, t);
   };
 
-  issue_k(t_first, kbuf);
-  issue_v(t_first, vbuf);
+  issue_k(tile_of(0), kbuf);
+  issue_v(tile_of(0), vbuf);
   iter(0, 0, true);
   for (int i = 1; i < nt; i += 2) {
     iter(i, 1, false);
@@ -315,22 +329,30 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
 
   // epilogue: o[dt][j] = O^T[d = 32 dt + (j & 3) + 8 (j >> 2) + 4h][q = r32]
   l += __shfl_xor(l, 32, 64);
-  if (nchunk_valid > 1) {
-    // split row block: unnormalised partials for the combine kernel (coalesced over rows)
-    float* po = P.part_o + ((int64_t)L * 4 + w) * (D * 32);
+  if constexpr (KS > 1) {
+    // group 1 -> LDS (the tile buffers are free: every wave waited for its own DMA above and
+    // the barrier below orders the hand-off); group 0 merges: O = 2^(m0-M) O0 + 2^(m1-M) O1
+    __syncthreads();
+    float* xo = reinterpret_cast<float*>(smem) + (w * 64 + lane) * 66;
+    if (grp == 1) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) xo[16 * dt + j] = o[dt][j];
+      xo[64] = m;
+      xo[65] = l;
+    }
+    __syncthreads();
+    if (grp == 1) return;
+    const float m1 = xo[64], l1 = xo[65];
+    const float M = fmaxf(m, m1);
+    const float f0 = M == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m - M);
+    const float f1 = M == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m1 - M);
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int d = 32 * dt + (j & 3) + 8 * (j >> 2) + 4 * h;
-        po[d * 32 + r32] = o[dt][j];
-      }
-    if (h == 0) {
-      float* pm = P.part_ml + (((int64_t)L * 4 + w) * 32 + r32) * 2;
-      pm[0] = m;
-      pm[1] = l;
-    }
-    return;
+      for (int j = 0; j < 16; ++j) o[dt][j] = o[dt][j] * f0 + xo[16 * dt + j] * f1;
+    l = l * f0 + l1 * f1;
   }
   if (row_ok) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
@@ -347,127 +369,44 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_v2_kernel(PrefillParams P
   }
 }
 
-// Combine of split row blocks: one workgroup per (sequence, head group, row block); wave w
-// and lane (r32, h) own row r32 of wave w's head over d in [64h, 64h + 64). O = sum_c
-// 2^(m_c - M) O_c / sum_c 2^(m_c - M) l_c over the row block's non-empty chunks.
-template <bool CAUSAL, int HPW>
-__global__ void __launch_bounds__(256) prefill_v2_combine_kernel(PrefillParams P) {
-  constexpr int D = 128, KT = 64, RB = 4 / HPW, RW = 32 * RB;
-  const int Lb = blockIdx.x;
-  const int G = P.Hq / P.Hkv;
-  const int ngrp = G / HPW;
-  const int qb = P.ntiles - 1 - Lb % P.ntiles;
-  const int hg = (Lb / P.ntiles) % (P.Hkv * ngrp);
-  const int b = Lb / (P.ntiles * P.Hkv * ngrp);
-  const int q0 = P.cu_q[b], qlen = P.cu_q[b + 1] - q0;
-  if (qb * RW >= qlen) return;
-  const int ctx = P.ctx_lens[b];
-  const int W = CAUSAL ? P.window : 0;
-  const int wq_lo = ctx - qlen + qb * RW;
-  const int wq_hi = ctx - qlen + min(qlen - 1, qb * RW + RW - 1);
-  const int last_key = CAUSAL ? wq_hi : ctx - 1;
-  const int n_tiles_all = last_key / KT + 1;
-  const int t_first_all = W > 0 ? max(0, wq_lo - W + 1) / KT : 0;
-  const int nc = (n_tiles_all - t_first_all + P.split_ch - 1) / P.split_ch;
-  if (nc <= 1) return;   // the attention kernel wrote this row block itself
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r32 = lane & 31, h = lane >> 5;
-  const int kvh = hg / ngrp;
-  const int hq = kvh * G + (hg % ngrp) * HPW + w % HPW;
-  const int qr = qb * RW + (w / HPW) * 32 + r32;
-  const int64_t L0 = (int64_t)Lb * P.nchunks;
-  float M = -INFINITY;
-  for (int c = 0; c < nc; ++c) M = fmaxf(M, P.part_ml[(((L0 + c) * 4 + w) * 32 + r32) * 2]);
-  const float mo = M == -INFINITY ? 0.f : M;
-  float acc[64];
-#pragma unroll
-  for (int i = 0; i < 64; ++i) acc[i] = 0.f;
-  float lsum = 0.f;
-  for (int c = 0; c < nc; ++c) {
-    const float* pm = P.part_ml + (((L0 + c) * 4 + w) * 32 + r32) * 2;
-    const float f = __builtin_amdgcn_exp2f(pm[0] - mo);
-    lsum += f * pm[1];
-    const float* po = P.part_o + ((L0 + c) * 4 + w) * (D * 32) + (64 * h) * 32 + r32;
-#pragma unroll
-    for (int i = 0; i < 64; ++i) acc[i] += f * po[i * 32];
-  }
-  if (qr >= qlen) return;
-  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-  uint16_t* op = P.out + (int64_t)(q0 + qr) * P.out_stride + (int64_t)hq * D + 64 * h;
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    u16x8 v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = f2bf(acc[8 * g + j] * inv);
-    *reinterpret_cast<u16x8*>(op + 8 * g) = v;
-  }
-}
-
-namespace {
-bool v2_takes(const PrefillParams& p, int D, bool paged) {
+bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q_len, int D,
+                                 bool paged, bool causal, hipStream_t stream) {
   static const bool disabled = [] {
     const char* e = getenv("NGA_PREFILL_V1");
     return e && atoi(e) != 0;
   }();
-  return !(p.impl == 1 || (p.impl == 0 && disabled) || D != 128 || !paged || p.kv_fp8 ||
-           p.max_blocks > V2_MAX_TILES);
-}
-}  // namespace
-
-PrefillSplitPlan prefill_v2_split_plan(const PrefillParams& p, int num_seqs, int max_q_len, int max_ctx, int D,
-                                       bool paged, bool causal) {
-  PrefillSplitPlan sp{1, 0, 0, 0};
-  static const int mode = [] {   // NGA_PREFILL_SPLIT=0 disables split-K (A/B runs)
-    const char* e = getenv("NGA_PREFILL_SPLIT");
-    return e ? atoi(e) : 1;
+  if (p.impl == 1 || (p.impl == 0 && disabled) || D != 128 || !paged || p.kv_fp8 ||
+      p.max_blocks > V2_MAX_TILES)
+    return false;
+  static const int ks_env = [] {   // NGA_PREFILL_KS=1|2 forces the wave-group count (A/B)
+    const char* e = getenv("NGA_PREFILL_KS");
+    return e ? atoi(e) : 0;
   }();
-  if (!mode || !v2_takes(p, D, paged) || num_seqs == 0 || max_q_len == 0 || max_ctx <= 0) return sp;
-  const int G = p.Hq / p.Hkv;
-  const int hpw = G % 4 == 0 ? 4 : G % 2 == 0 ? 2 : 1;
-  const int rw = 32 * (4 / hpw);
-  const int64_t base = (int64_t)((max_q_len + rw - 1) / rw) * (p.Hq / hpw) * num_seqs;
-  // the GPU holds 2 of these workgroups per CU (512): below ~2 rounds of row blocks the
-  // longest causal row blocks set the time, so cut them into chunks
-  if (base >= 1024) return sp;
-  const int max_tiles = (max_ctx + 63) / 64;
-  int c = (int)((1536 + base - 1) / base);
-  c = c < 1 ? 1 : c > 8 ? 8 : c;
-  int ch = (max_tiles + c - 1) / c;
-  if (ch < 2) ch = 2;
-  c = (max_tiles + ch - 1) / ch;
-  if (c <= 1) return sp;
-  sp.nchunks = c;
-  sp.split_ch = ch;
-  const int64_t items = base * c;
-  sp.part_o_floats = items * 4 * 128 * 32;
-  sp.part_ml_floats = items * 4 * 32 * 2;
-  return sp;
-}
-
-bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q_len, int D,
-                                 bool paged, bool causal, hipStream_t stream) {
-  if (!v2_takes(p, D, paged)) return false;
   if (num_seqs == 0 || max_q_len == 0) return true;
   const int G = p.Hq / p.Hkv;
   const int hpw = G % 4 == 0 ? 4 : G % 2 == 0 ? 2 : 1;
   const int rw = 32 * (4 / hpw);
   PrefillParams pp = p;
-  if (pp.nchunks < 1) pp.nchunks = 1;
   pp.ntiles = (max_q_len + rw - 1) / rw;
-  const int64_t base = (int64_t)pp.ntiles * (p.Hq / hpw) * num_seqs;
-  const int64_t total = base * pp.nchunks;
+  const int64_t total = (int64_t)pp.ntiles * (p.Hq / hpw) * num_seqs;
   // Size rule: this kernel needs about two of its workgroups per CU (two waves per SIMD) to
   // overlap one wave's softmax with the other's MFMAs. A single ~1K-token prompt is ~300
   // workgroups of 128 (row, head) pairs — one wave per SIMD, measured no faster than the
   // 16x16 kernel's ~500 half-size workgroups standalone and 1.6% slower end to end when it
   // shares the chip with the decode attention of a mixed step (benchmarks/kernel_bench.py
   // and scripts/gpu_r2_attn_ab.sh). From ~6 such prompts (or long ones) up it is 15-25% faster.
-  if (p.impl == 0 && total < 2 * 256 * 2) return false;
-  if (pp.nchunks > 1 && (!pp.part_o || !pp.part_ml)) return false;
+  // Few row blocks (~one per CU, e.g. one ~1.2K-token prompt): the 8-wave split-key form.
+  int ks = p.impl == 3 ? 2 : p.impl == 2 ? 1 : (total <= 320 ? 2 : 1);
+  if (ks_env == 1 || ks_env == 2) ks = ks_env;
+  if (p.impl == 0 && ks == 1 && total < 2 * 256 * 2) return false;
   pp.total = (int)total;
   pp.per_xcd = (int)((total + 7) / 8);
   dim3 grid(8 * pp.per_xcd);
-#define NGA_PF2(CS, HP) prefill_attn_v2_kernel<CS, HP><<<grid, 256, 0, stream>>>(pp)
+#define NGA_PF2(CS, HP)                                                                   \
+  do {                                                                                      \
+    if (ks == 2) prefill_attn_v2_kernel<CS, HP, 0, 2><<<grid, 512, 0, stream>>>(pp);        \
+    else prefill_attn_v2_kernel<CS, HP><<<grid, 256, 0, stream>>>(pp);                      \
+  } while (0)
 #ifdef NGA_DIAG_ABLATION  // diagnostic builds only (NGA_DIAG_BUILD=1): results are wrong
   static const int abl = [] {
     const char* e = getenv("NGA_PV2_ABLATE");
@@ -486,16 +425,6 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
     if (hpw == 4) NGA_PF2(false, 4); else if (hpw == 2) NGA_PF2(false, 2); else NGA_PF2(false, 1);
   }
 #undef NGA_PF2
-  if (pp.nchunks > 1) {
-    dim3 cgrid((unsigned)base);
-#define NGA_PFC(CS, HP) prefill_v2_combine_kernel<CS, HP><<<cgrid, 256, 0, stream>>>(pp)
-    if (causal) {
-      if (hpw == 4) NGA_PFC(true, 4); else if (hpw == 2) NGA_PFC(true, 2); else NGA_PFC(true, 1);
-    } else {
-      if (hpw == 4) NGA_PFC(false, 4); else if (hpw == 2) NGA_PFC(false, 2); else NGA_PFC(false, 1);
-    }
-#undef NGA_PFC
-  }
   return true;
 }
 

@@ -65,24 +65,7 @@ struct PrefillParams {
   int impl;    // 0: pick by size, 1: the 16x16 kernel, 2: the 32x32 kernel where it applies
   int kv_fp8;      // paged caches hold fp8 e4m3fn (k / k_scale, v / v_scale); 16x16 kernel only
   float v_scale;   // output multiplier (fp8 caches; `scale` already includes k_scale)
-  // split-K (32x32 kernel, few prompts): each row block's key tiles are cut into chunks of
-  // split_ch tiles, nchunks per row block; a row block with more than one non-empty chunk
-  // leaves per-chunk partials (unnormalised O, running max, sum) for the combine kernel
-  int nchunks;     // 1 = no split
-  int split_ch;
-  float* part_o;   // [items][4 waves][128 d][32 rows] fp32
-  float* part_ml;  // [items][4 waves][32 rows][2] fp32 (m in the exp2 domain, l)
 };
-// split plan of the 32x32 kernel for this call (nchunks = 1: no split); the caller provides
-// ws_floats of fp32 workspace in part_o / part_ml when nchunks > 1
-struct PrefillSplitPlan {
-  int nchunks;
-  int split_ch;
-  int64_t part_o_floats;
-  int64_t part_ml_floats;
-};
-PrefillSplitPlan prefill_v2_split_plan(const PrefillParams& p, int num_seqs, int max_q_len, int max_ctx, int D,
-                                       bool paged, bool causal);
 void launch_prefill_attention(const PrefillParams& p, int num_seqs, int max_q_len, int D,
                               bool paged, bool causal, hipStream_t stream);
 // 32x32-MFMA prefill (paged, head_dim 128); returns false when it does not take the call

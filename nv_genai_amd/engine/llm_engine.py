@@ -840,12 +840,10 @@ class LLMEngine:
         m = AttnMeta(kind=kind, slots=self.d_slots[:ntok], cu_q=self.d_cu[: n + 1],
                      ctx_lens=self.d_ctx[:n], block_tables=self.d_bt[:n], max_q_len=max_q,
                      max_ctx=max_ctx, decode_ws=self.decode_ws)
-        m.max_ctx_prefill = max_ctx
         if nd:
             # mixed step: rows [0, nd) decode, the rest prefill with its own cu_seqlens
             m.kind, m.n_decode, m.max_ctx = "mixed", nd, self.cfg.max_model_len
             m.cu_q_prefill = self.d_cu[nd: n + 1] - nd
-            m.max_ctx_prefill = int(self._np[4][nd:n].max()) if n > nd else 0
         return m
 
     def _upload(self, n, ntok):

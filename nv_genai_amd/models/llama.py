@@ -58,7 +58,6 @@ class AttnMeta:
     decode_ws: Optional[ops.DecodeWorkspace] = None
     n_decode: int = 0                          # mixed steps: rows [0, n_decode) are decode rows
     cu_q_prefill: Optional[torch.Tensor] = None  # mixed steps: cu_seqlens of the prefill rows
-    max_ctx_prefill: int = 0                   # longest context among the prefill rows (0: unknown)
 
 
 class LlamaModel:
@@ -468,7 +467,7 @@ class LlamaModel:
                                             meta.block_tables[nd:], meta.cu_q_prefill,
                                             meta.ctx_lens[nd:], hq, hkv, D, meta.max_q_len,
                                             self.scale, out=attn[nd:], window=W,
-                                            kv_scales=self.kv_scales, max_ctx=meta.max_ctx_prefill)
+                                            kv_scales=self.kv_scales)
 
             side = None
             if self.concurrent_attention and qkv.is_cuda and not torch.cuda.is_current_stream_capturing():
@@ -491,8 +490,7 @@ class LlamaModel:
         return ops.prefill_attention_paged(q, self.k_cache[li], self.v_cache[li],
                                            meta.block_tables, meta.cu_q, meta.ctx_lens,
                                            hq, hkv, D, meta.max_q_len, self.scale, window=W,
-                                           kv_scales=self.kv_scales,
-                                           max_ctx=meta.max_ctx_prefill or meta.max_ctx)
+                                           kv_scales=self.kv_scales)
 
     def _reduce_add_norm(self, partial, resid, w, b=None):
         """resid += all_reduce_TP(partial); returns norm(resid). A small TP message goes
@@ -676,8 +674,7 @@ class LlamaModel:
                       max_q_len=1, max_ctx=meta.max_ctx, decode_ws=meta.decode_ws)
         mp = AttnMeta(kind="prefill", slots=meta.slots[nd:], cu_q=meta.cu_q_prefill,
                       ctx_lens=meta.ctx_lens[nd:], block_tables=meta.block_tables[nd:],
-                      max_q_len=meta.max_q_len, max_ctx=meta.max_ctx,
-                      max_ctx_prefill=meta.max_ctx_prefill)
+                      max_q_len=meta.max_q_len, max_ctx=meta.max_ctx)
         aux.wait_stream(main)
         with torch.cuda.stream(aux):
             hd = self._stack(resid[:nd], pos[:nd], md, None)

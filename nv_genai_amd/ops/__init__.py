@@ -201,13 +201,12 @@ def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, max_ctx, scale,
 
 def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D, max_q_len,
                             scale, out=None, causal=True, window: int = 0, impl: int = 0,
-                            kv_scales=(1.0, 1.0), max_ctx: int = 0):
+                            kv_scales=(1.0, 1.0)):
     """Paged prefill attention. ``impl``: 0 picks the kernel by problem size, 1 forces the
-    16x16-MFMA kernel, 2 the 32x32-MFMA kernel (head_dim 128, bf16 caches) — for tests and
-    A/B runs. fp8 e4m3fn caches (``kv_scales``) run the 16x16 kernel. ``max_ctx`` (the
-    longest context of the call, known to the host scheduler) enables split-K of the 32x32
-    kernel when a few prompts would leave most CUs idle: the longest causal row blocks' key
-    ranges are cut into chunks that run in parallel and a combine kernel merges them."""
+    16x16-MFMA kernel, 2 the 32x32-MFMA kernel (head_dim 128, bf16 caches), 3 its 8-wave
+    split-key form (few prompts: two wave groups walk alternate key tiles of the same row
+    block and merge in LDS) — for tests and A/B runs. fp8 e4m3fn caches (``kv_scales``) run
+    the 16x16 kernel."""
     if not _gpu(q):
         r = ref.prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
                                         scale, causal, window, kv_scales)
@@ -219,7 +218,7 @@ def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
         out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
     kernels().prefill_attention(out, q, None, None, kc, vc, block_tables, cu_q, ctx_lens, Hq,
                                 Hkv, D, int(max_q_len), float(scale), bool(causal), int(window),
-                                int(impl), float(kv_scales[0]), float(kv_scales[1]), int(max_ctx))
+                                int(impl), float(kv_scales[0]), float(kv_scales[1]))
     return out
 
 
@@ -230,7 +229,7 @@ def varlen_attention(q, k, v, cu, Hq, Hkv, D, max_len, scale, causal=False, out=
     if out is None:
         out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
     kernels().prefill_attention(out, q, k, v, None, None, None, cu, None, Hq, Hkv, D,
-                                int(max_len), float(scale), bool(causal), 0, 0, 1.0, 1.0, 0)
+                                int(max_len), float(scale), bool(causal), 0, 0, 1.0, 1.0)
     return out
 
 

@@ -188,13 +188,13 @@ def test_prefill_attention_v2_layouts(gpu, Hkv, G, window, causal):
     ctx_t = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
     scale = 1 / math.sqrt(D)
     o_ref = ref.prefill_attention_paged(q.float(), kc, vc, bt, cu_t, ctx_t, Hq, Hkv, D, scale, causal, window)
-    for max_ctx in (0, max(ctxs)):      # without / with split-K
+    for impl in (2, 3):      # 4-wave, and 8-wave split-key
         out = ops.prefill_attention_paged(q, kc, vc, bt, cu_t, ctx_t, Hq, Hkv, D, max(qls), scale,
-                                          causal=causal, window=window, impl=2, max_ctx=max_ctx)
+                                          causal=causal, window=window, impl=impl)
         _close_rows(out, o_ref, width=D)
 
 
-@pytest.mark.parametrize("impl", [0, 1, 2])
+@pytest.mark.parametrize("impl", [0, 1, 2, 3])
 @pytest.mark.parametrize("ctxs,qls,window", [
     ([1200], [940], 0),            # one prompt after a 260-token prefix hit
     ([1200] * 6, [1200] * 6, 0),   # six prompts (the size rule picks the 32x32 kernel)
@@ -217,12 +217,9 @@ def test_prefill_attention_kernel_choice(gpu, ctxs, qls, window, impl):
     ctx_t = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
     scale = 1 / math.sqrt(D)
     o_ref = ref.prefill_attention_paged(q.float(), kc, vc, bt, cu_t, ctx_t, Hq, Hkv, D, scale, True, window)
-    # max_ctx = 0: no split-K; max(ctxs): the 32x32 kernel may cut long row blocks into
-    # key chunks merged by the combine kernel (few prompts)
-    for max_ctx in (0, max(ctxs)):
-        out = ops.prefill_attention_paged(q, kc, vc, bt, cu_t, ctx_t, Hq, Hkv, D, max(qls), scale,
-                                          window=window, impl=impl, max_ctx=max_ctx)
-        _close_rows(out, o_ref, width=D)
+    out = ops.prefill_attention_paged(q, kc, vc, bt, cu_t, ctx_t, Hq, Hkv, D, max(qls), scale,
+                                      window=window, impl=impl)
+    _close_rows(out, o_ref, width=D)
 
 
 @pytest.mark.parametrize("D,scales", [(128, (1.0, 1.0)), (128, (3.0, 0.5)), (256, (2.0, 2.0))])
