@@ -243,7 +243,7 @@ int64_t decode_pages_per_part(int64_t num_seqs, int64_t Hkv, int64_t max_ctx) {
 void decode_attention(Tensor out, Tensor q, Tensor kc, Tensor vc, Tensor block_tables,
                       Tensor ctx_lens, int64_t Hq, int64_t Hkv, int64_t max_ctx, double scale,
                       int64_t pages_per_part, Tensor part_ml, Tensor part_o, int64_t window,
-                      double k_scale, double v_scale) {
+                      double k_scale, double v_scale, bool skip_empty) {
   CHECK_BF16(out); CHECK_BF16(q);
   const bool fp8 = kv_is_fp8(kc, vc);
   CHECK_CONTIG(kc); CHECK_CONTIG(vc);
@@ -277,7 +277,56 @@ void decode_attention(Tensor out, Tensor q, Tensor kc, Tensor vc, Tensor block_t
                                (int)pages_per_part,
                                nparts > 1 ? part_ml.data_ptr<float>() : nullptr,
                                nparts > 1 ? part_o.data_ptr<float>() : nullptr, (int)window, fp8,
-                               (float)k_scale, (float)v_scale, cur_stream(q));
+                               (float)k_scale, (float)v_scale, cur_stream(q), skip_empty);
+}
+
+// Work-list prefill (32x32 kernel): q / out rows are absolute token rows of the step (the
+// cu_q offsets of ALL its sequences); items [n, 2] int32 (sequence, row block) pairs, n_items
+// a 1-element device int32 (read by the kernel, so a captured graph replays any step's list)
+void prefill_attention_worklist(Tensor out, Tensor q, Tensor kc, Tensor vc, Tensor block_tables,
+                                Tensor cu_q, Tensor ctx_lens, int64_t Hq, int64_t Hkv, double scale,
+                                bool causal, int64_t window, Tensor items, Tensor n_items, int64_t grid,
+                                int64_t ks) {
+  CHECK_BF16(out); CHECK_BF16(q); CHECK_BF16(kc); CHECK_BF16(vc);
+  CHECK_CONTIG(kc); CHECK_CONTIG(vc);
+  TORCH_CHECK(Hq % Hkv == 0, "prefill_attention_worklist: Hq % Hkv");
+  TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(2) == 64 && kc.size(3) == 128,
+              "prefill_attention_worklist: bf16 k cache [nb, Hkv, 64, 128]");
+  TORCH_CHECK(vc.sizes() == at::IntArrayRef({kc.size(0), Hkv, 128, 64}), "v cache must be [nb, Hkv, 128, 64]");
+  TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1 && q.size(1) >= Hq * 128 && q.stride(0) % 8 == 0);
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) >= Hq * 128 && out.size(0) == q.size(0));
+  CHECK_DEV(block_tables); CHECK_DT(block_tables, at::kInt); CHECK_CONTIG(block_tables);
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(1) <= 1024,
+              "prefill_attention_worklist: at most 1024 pages per sequence");
+  CHECK_DEV(cu_q); CHECK_DT(cu_q, at::kInt); CHECK_CONTIG(cu_q);
+  CHECK_DEV(ctx_lens); CHECK_DT(ctx_lens, at::kInt); CHECK_CONTIG(ctx_lens);
+  TORCH_CHECK(cu_q.numel() == ctx_lens.numel() + 1 && block_tables.size(0) >= ctx_lens.numel(),
+              "prefill_attention_worklist: cu_q [B+1], ctx_lens [B], block_tables [>=B, pages]");
+  CHECK_DEV(items); CHECK_DT(items, at::kInt); CHECK_CONTIG(items);
+  CHECK_DEV(n_items); CHECK_DT(n_items, at::kInt);
+  TORCH_CHECK(items.dim() == 2 && items.size(1) == 2 && n_items.numel() == 1,
+              "prefill_attention_worklist: items [n, 2], n_items [1]");
+  TORCH_CHECK(window >= 0 && (window == 0 || causal));
+  TORCH_CHECK(grid >= 1 && grid <= 65535 && (ks == 1 || ks == 2), "prefill_attention_worklist: grid / ks");
+  nga::PrefillParams p{};
+  p.out = bfp(out);
+  p.out_stride = out.stride(0);
+  p.q = bfp(q);
+  p.q_stride = q.stride(0);
+  p.cu_q = cu_q.data_ptr<int32_t>();
+  p.Hq = (int)Hq;
+  p.Hkv = (int)Hkv;
+  p.scale = (float)scale;
+  p.window = (int)window;
+  p.kc = bfp(kc);
+  p.vc = bfp(vc);
+  p.block_tables = block_tables.data_ptr<int32_t>();
+  p.max_blocks = (int)block_tables.size(1);
+  p.ctx_lens = ctx_lens.data_ptr<int32_t>();
+  p.v_scale = 1.f;
+  p.items = items.data_ptr<int32_t>();
+  p.n_items = n_items.data_ptr<int32_t>();
+  nga::launch_prefill_attention_v2_worklist(p, (int)grid, (int)ks, causal, cur_stream(q));
 }
 
 void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optional<Tensor> v,
@@ -643,6 +692,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("decode_pages_per_part", &decode_pages_per_part);
   m.def("decode_attention", checked("decode_attention", &decode_attention));
   m.def("prefill_attention", checked("prefill_attention", &prefill_attention));
+  m.def("prefill_attention_worklist", checked("prefill_attention_worklist", &prefill_attention_worklist));
   m.def("moe_route", checked("moe_route", &moe_route));
   m.def("moe_align", checked("moe_align", &moe_align));
   m.def("moe_gemm", checked("moe_gemm", &moe_gemm));

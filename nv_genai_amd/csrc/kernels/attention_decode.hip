@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     int64_t q_stride, const CT* __restrict__ kc, const CT* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int max_blocks,
     const int32_t* __restrict__ ctx_lens, int Hq, int Hkv, float scale, int pages_per_part,
-    float* __restrict__ part_ml, float* __restrict__ part_o, int window, float v_scale) {
+    float* __restrict__ part_ml, float* __restrict__ part_o, int window, float v_scale, int skip_empty) {
   // fp8 pages at head_dim 128: 16-byte loads (half as many load instructions as 8-byte ones).
   // Each lane's 16 K bytes cover two d-steps (Q is loaded with the same d order, the dot
   // product does not care) and its 16 Vt bytes cover 16 consecutive keys of both key
@@ -77,7 +77,10 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   __shared__ float m_s[NW][16], l_s[NW][16];
 
   if (p_begin >= p_end) {
-    // empty partition (or an empty padding sequence, ctx = 0)
+    // empty partition (or an empty padding sequence, ctx = 0). skip_empty: a ctx-0 row is not
+    // this launch's row at all (a mixed-step graph covers a bucket of rows, the ones past the
+    // step's decode rows belong to its prefill tokens) and is left untouched
+    if (skip_empty && ctx == 0) return;
     if (nparts == 1) {
       for (int i = threadIdx.x; i < G * D; i += blockDim.x)
         out[(int64_t)b * out_stride + (int64_t)(kvh * G) * D + i] = 0;
@@ -275,8 +278,10 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 template <int D>
 __global__ void decode_attn_reduce_kernel(uint16_t* __restrict__ out, int64_t out_stride,
                                           const float* __restrict__ part_ml,
-                                          const float* __restrict__ part_o, int Hq, int nparts) {
+                                          const float* __restrict__ part_o, int Hq, int nparts,
+                                          const int32_t* __restrict__ ctx_lens, int skip_empty) {
   const int b = blockIdx.x, hq = blockIdx.y;
+  if (skip_empty && ctx_lens[b] == 0) return;
   const int64_t base = ((int64_t)b * Hq + hq) * nparts;
   float M = -INFINITY;
   for (int p = 0; p < nparts; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
@@ -309,7 +314,8 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
                              const int32_t* block_tables, int max_blocks, const int32_t* ctx_lens,
                              int num_seqs, int Hq, int Hkv, int D, int max_ctx, float scale,
                              int pages_per_part, float* part_ml, float* part_o, int window,
-                             bool kv_fp8, float k_scale, float v_scale, hipStream_t stream) {
+                             bool kv_fp8, float k_scale, float v_scale, hipStream_t stream,
+                             bool skip_empty) {
   if (num_seqs == 0) return;
   int pages = (max_ctx + BS - 1) / BS;
   if (window > 0) pages = min(pages, (window + BS - 1) / BS + 1);  // visible pages at most
@@ -322,15 +328,17 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
   decode_attn_kernel<DD, CT><<<grid, 256, 0, stream>>>(                                        \
       out, out_stride, q, q_stride, static_cast<const CT*>(kc), static_cast<const CT*>(vc),   \
       block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, pages_per_part, part_ml, part_o, window, \
-      v_scale)
+      v_scale, skip_empty ? 1 : 0)
   if (D == 256) {
     if (kv_fp8) NGA_DEC(256, uint8_t); else NGA_DEC(256, uint16_t);
     if (nparts > 1)
-      decode_attn_reduce_kernel<256><<<g2, 256, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts);
+      decode_attn_reduce_kernel<256><<<g2, 256, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts,
+                                                             ctx_lens, skip_empty ? 1 : 0);
   } else {
     if (kv_fp8) NGA_DEC(128, uint8_t); else NGA_DEC(128, uint16_t);
     if (nparts > 1)
-      decode_attn_reduce_kernel<128><<<g2, 128, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts);
+      decode_attn_reduce_kernel<128><<<g2, 128, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts,
+                                                             ctx_lens, skip_empty ? 1 : 0);
   }
 #undef NGA_DEC
 }

@@ -65,33 +65,22 @@ __device__ __forceinline__ int vswz(int row) { return (row >> 1) & 7; }
 // iterations (the odd last tile of group 1 is a fully masked ghost: no DMA) so the
 // workgroup-wide barriers line up; at the end group 1 hands (m, l, O) to group 0 through
 // LDS and group 0 writes the merged rows.
-template <bool CAUSAL, int HPW, int ABL = 0, int KS = 1>
-__global__ void __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) prefill_attn_v2_kernel(PrefillParams P) {
+constexpr int V2_TILE = 64 * 128;       // elements of one K (or V^T) tile: 16 KiB
+
+// One row block: query rows [RW qb, RW qb + RW) of sequence b, head group hg (its HPW heads
+// share each K / V^T tile), over the row block's whole causal key range.
+template <bool CAUSAL, int HPW, int ABL, int KS>
+__device__ __forceinline__ void v2_row_block(const PrefillParams& P, uint16_t* smem, int b, int hg, int qb) {
   constexpr int D = 128, KT = 64;
-  constexpr int TILE = KT * D;          // elements of one K (or V^T) tile: 16 KiB
+  constexpr int TILE = V2_TILE;
   constexpr int RB = 4 / HPW;           // 32-row query blocks per workgroup
   constexpr int RW = 32 * RB;           // query rows per workgroup
-  // ONE LDS object: [K buffer 0 | K buffer 1 | V^T buffer 0 | V^T buffer 1 | block ids] per
-  // wave group (the block ids once). (With several LDS variables the compiler gives their
-  // accesses alias scopes and then waits vmcnt(0) before fragment reads of a buffer whose
-  // earlier DMA it cannot see retired — serialising the prefetch; a VMEM block-table load
-  // inside the loop did the same.)
-  __shared__ __attribute__((aligned(16))) uint16_t smem[KS * 4 * TILE + 2 * V2_MAX_TILES];
   int32_t* sbt = reinterpret_cast<int32_t*>(smem + KS * 4 * TILE);
   const int grp = KS == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
   uint16_t* const kbuf = smem + grp * 4 * TILE;
   uint16_t* const vbuf = kbuf + 2 * TILE;
-
-  // XCD-aware order (as the 16x16 kernel): each XCD gets a contiguous range of
-  // (sequence, kv head, head group, query block), longest causal blocks first.
-  const int pblk = blockIdx.x;
-  const int L = (pblk & 7) * P.per_xcd + (pblk >> 3);
-  if (L >= P.total) return;
   const int G = P.Hq / P.Hkv;
   const int ngrp = G / HPW;
-  const int qb = P.ntiles - 1 - L % P.ntiles;
-  const int hg = (L / P.ntiles) % (P.Hkv * ngrp);
-  const int b = L / (P.ntiles * P.Hkv * ngrp);
   const int q0 = P.cu_q[b], qlen = P.cu_q[b + 1] - q0;
   if (qb * RW >= qlen) return;
   const int ctx = P.ctx_lens[b];
@@ -263,8 +252,10 @@ __global__ void __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) prefill_attn_v2_ker
   };
   // one pipeline stage: softmax + P.V of the previous half (S, V^T buffer vs, half vh2); the
   // softmax VALU is interleaved with the next half's S^T MFMAs (Sn, K buffer ks, half kh2)
+  // skip_pv: S came from a ghost tile (KS = 2: its V^T buffer may hold whatever the LDS held
+  // before this workgroup — a NaN pattern times P = 0 is still NaN)
   auto stage = [&](const f32x16& S, const uint16_t* vs, int vh2, f32x16& Sn, const uint16_t* ks,
-                   int kh2, int t_next) {
+                   int kh2, int t_next, bool skip_pv) {
     bf16x8 pf[2];
     float alpha;
     qk(Sn, ks, kh2);
@@ -280,7 +271,7 @@ __global__ void __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) prefill_attn_v2_ker
     // out of the region the MFMAs above cover
     asm volatile("" ::"v"(pf[0]), "v"(pf[1]), "v"(l));
     rescale(grow, alpha);
-    pv(pf, vs, vh2);
+    if (!skip_pv) pv(pf, vs, vh2);
     mask(Sn, t_next, kh2);
   };
 
@@ -303,13 +294,13 @@ __global__ void __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) prefill_attn_v2_ker
         qk(Sa, kc_, 0);
         mask(Sa, t, 0);
       } else {
-        stage(Sb, vbuf + (par ^ 1) * TILE, 1, Sa, kc_, 0, t);
+        stage(Sb, vbuf + (par ^ 1) * TILE, 1, Sa, kc_, 0, t, false);
       }
     }
     if constexpr (ABL != 4) __builtin_amdgcn_s_barrier();   // V(i-1) is free
     if constexpr (ABL != 1 && ABL != 4)
       if (i + 1 < nt) issue_v(t + KS, vbuf + (par ^ 1) * TILE);
-    if constexpr (ABL != 2) stage(Sa, vbuf + par * TILE, 0, Sb, kc_, 1, t);
+    if constexpr (ABL != 2) stage(Sa, vbuf + par * TILE, 0, Sb, kc_, 1, t, KS > 1 && t >= n_tiles);
   };
 
   issue_k(tile_of(0), kbuf);
@@ -323,7 +314,7 @@ __global__ void __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) prefill_attn_v2_ker
     bf16x8 pf[2];
     float alpha;
     rescale(softmax(Sb, pf, alpha), alpha);
-    pv(pf, vbuf + ((nt - 1) & 1) * TILE, 1);
+    if (!(KS > 1 && tile_of(nt - 1) >= n_tiles)) pv(pf, vbuf + ((nt - 1) & 1) * TILE, 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may outlive the workgroup
 
@@ -367,6 +358,45 @@ __global__ void __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) prefill_attn_v2_ker
         *reinterpret_cast<u16x4*>(op + 32 * dt + 8 * g) = v;
       }
   }
+}
+
+// ONE LDS object per workgroup: [K buffer 0 | K buffer 1 | V^T buffer 0 | V^T buffer 1] per
+// wave group, then the block ids. (With several LDS variables the compiler gives their
+// accesses alias scopes and then waits vmcnt(0) before fragment reads of a buffer whose
+// earlier DMA it cannot see retired — serialising the prefetch; a VMEM block-table load
+// inside the loop did the same.)
+//
+// Grid modes:
+// * enumerated (P.items == nullptr): workgroup -> (sequence, head group, row block) in the
+//   XCD-aware order below, longest causal blocks first;
+// * work list (P.items: host-planned (sequence, row block) pairs, longest first, and
+//   P.n_items on the device): a fixed grid walks items it = blockIdx.x + k gridDim.x with
+//   head group it % NG. The grid does not depend on the step, so a hipGraph captures it once
+//   and each replay reads that step's list (engine mixed-step graphs).
+template <bool CAUSAL, int HPW, int ABL = 0, int KS = 1>
+__global__ void __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) prefill_attn_v2_kernel(PrefillParams P) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[KS * 4 * V2_TILE + 2 * V2_MAX_TILES];
+  const int G = P.Hq / P.Hkv;
+  const int ngrp = G / HPW;
+  const int NG = P.Hkv * ngrp;
+  if (P.items) {
+    const int total = *P.n_items * NG;
+    for (int it = blockIdx.x; it < total; it += gridDim.x) {
+      __syncthreads();   // the previous item's waves are done with the block-id table
+      const int k = it / NG;
+      v2_row_block<CAUSAL, HPW, ABL, KS>(P, smem, P.items[2 * k], it % NG, P.items[2 * k + 1]);
+    }
+    return;
+  }
+  // XCD-aware order (as the 16x16 kernel): each XCD gets a contiguous range of
+  // (sequence, kv head, head group, query block), longest causal blocks first.
+  const int pblk = blockIdx.x;
+  const int L = (pblk & 7) * P.per_xcd + (pblk >> 3);
+  if (L >= P.total) return;
+  const int qb = P.ntiles - 1 - L % P.ntiles;
+  const int hg = (L / P.ntiles) % NG;
+  const int b = L / (P.ntiles * NG);
+  v2_row_block<CAUSAL, HPW, ABL, KS>(P, smem, b, hg, qb);
 }
 
 bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q_len, int D,
@@ -426,6 +456,24 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
   }
 #undef NGA_PF2
   return true;
+}
+
+void launch_prefill_attention_v2_worklist(const PrefillParams& p, int grid, int ks, bool causal,
+                                          hipStream_t stream) {
+  const int G = p.Hq / p.Hkv;
+  const int hpw = G % 4 == 0 ? 4 : G % 2 == 0 ? 2 : 1;
+  dim3 g(grid);
+#define NGA_PFW(CS, HP)                                                                   \
+  do {                                                                                    \
+    if (ks == 2) prefill_attn_v2_kernel<CS, HP, 0, 2><<<g, 512, 0, stream>>>(p);          \
+    else prefill_attn_v2_kernel<CS, HP><<<g, 256, 0, stream>>>(p);                        \
+  } while (0)
+  if (causal) {
+    if (hpw == 4) NGA_PFW(true, 4); else if (hpw == 2) NGA_PFW(true, 2); else NGA_PFW(true, 1);
+  } else {
+    if (hpw == 4) NGA_PFW(false, 4); else if (hpw == 2) NGA_PFW(false, 2); else NGA_PFW(false, 1);
+  }
+#undef NGA_PFW
 }
 
 }  // namespace nga

@@ -38,7 +38,8 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
                              const int32_t* block_tables, int max_blocks, const int32_t* ctx_lens,
                              int num_seqs, int Hq, int Hkv, int D, int max_ctx, float scale,
                              int pages_per_part, float* part_ml, float* part_o, int window,
-                             bool kv_fp8, float k_scale, float v_scale, hipStream_t stream);
+                             bool kv_fp8, float k_scale, float v_scale, hipStream_t stream,
+                             bool skip_empty = false);
 
 // attention_prefill.hip
 struct PrefillParams {
@@ -65,12 +66,20 @@ struct PrefillParams {
   int impl;    // 0: pick by size, 1: the 16x16 kernel, 2: the 32x32 kernel where it applies
   int kv_fp8;      // paged caches hold fp8 e4m3fn (k / k_scale, v / v_scale); 16x16 kernel only
   float v_scale;   // output multiplier (fp8 caches; `scale` already includes k_scale)
+  // work-list mode of the 32x32 kernel (nullptr: enumerated grid): [n, 2] (sequence, row
+  // block) pairs, and the device count n
+  const int32_t* items;
+  const int32_t* n_items;
 };
 void launch_prefill_attention(const PrefillParams& p, int num_seqs, int max_q_len, int D,
                               bool paged, bool causal, hipStream_t stream);
 // 32x32-MFMA prefill (paged, head_dim 128); returns false when it does not take the call
 bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q_len, int D,
                                  bool paged, bool causal, hipStream_t stream);
+// work-list launch (p.items / p.n_items set): a fixed grid of `grid` workgroups; ks = wave
+// groups (1 or 2). Rows per row block: 32 * 4 / hpw with hpw = 4, 2, 1 for Hq/Hkv % 4, % 2, else.
+void launch_prefill_attention_v2_worklist(const PrefillParams& p, int grid, int ks, bool causal,
+                                          hipStream_t stream);
 
 // sampling.hip
 void launch_sample(float* logits, int B, int V, const float* temperature, const int32_t* top_k,

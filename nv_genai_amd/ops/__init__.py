@@ -176,15 +176,21 @@ class DecodeWorkspace:
 
 def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, max_ctx, scale,
                      out=None, ws: Optional[DecodeWorkspace] = None, window: int = 0,
-                     kv_scales=(1.0, 1.0)):
+                     kv_scales=(1.0, 1.0), skip_empty: bool = False):
     """Paged GQA decode attention (head_dim 128 or 256); ``window`` > 0: sliding window;
-    bf16 or fp8 e4m3fn caches (``kv_scales`` = the fp8 caches' K / V scales)."""
+    bf16 or fp8 e4m3fn caches (``kv_scales`` = the fp8 caches' K / V scales). ``skip_empty``:
+    rows with ctx_len 0 are left untouched (not zeroed) — a graph-captured launch over a
+    bucket of rows of which only the first few are this step's decode rows."""
     D = kc.shape[3]
     if not _gpu(q):
         r = ref.decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, scale, D=D,
                                  window=window, kv_scales=kv_scales)
         if out is not None:
-            out[: r.shape[0], : r.shape[1]].copy_(r)
+            if skip_empty:
+                live = ctx_lens[: r.shape[0]] > 0
+                out[: r.shape[0], : r.shape[1]][live] = r[live].to(out.dtype)
+            else:
+                out[: r.shape[0], : r.shape[1]].copy_(r)
             return out
         return r
     B = ctx_lens.numel()
@@ -195,7 +201,7 @@ def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, max_ctx, scale,
     assert max_ctx <= ws.max_ctx and ws.D == D
     kernels().decode_attention(out, q, kc, vc, block_tables, ctx_lens, Hq, Hkv, int(max_ctx),
                                float(scale), ws.pages_per_part(B, max_ctx), ws.ml, ws.o,
-                               int(window), float(kv_scales[0]), float(kv_scales[1]))
+                               int(window), float(kv_scales[0]), float(kv_scales[1]), bool(skip_empty))
     return out
 
 
@@ -219,6 +225,63 @@ def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
     kernels().prefill_attention(out, q, None, None, kc, vc, block_tables, cu_q, ctx_lens, Hq,
                                 Hkv, D, int(max_q_len), float(scale), bool(causal), int(window),
                                 int(impl), float(kv_scales[0]), float(kv_scales[1]))
+    return out
+
+
+def prefill_rows_per_block(Hq: int, Hkv: int) -> int:
+    """Query rows of one row block of the 32x32 prefill kernel (4 waves = 4 heads x 32 rows,
+    2 heads x 2 x 32, or 1 head x 4 x 32 by the GQA group size)."""
+    G = Hq // Hkv
+    hpw = 4 if G % 4 == 0 else 2 if G % 2 == 0 else 1
+    return 32 * (4 // hpw)
+
+
+def plan_prefill_items(cu, ctx, first: int, n: int, Hq: int, Hkv: int, window: int = 0,
+                       out: Optional["np.ndarray"] = None):
+    """Host work list of the work-list prefill kernel for sequences [first, n) of a step
+    (numpy ``cu`` [n+1] token offsets, ``ctx`` [n] context lengths): one (sequence, row
+    block) pair per row block, longest causal key range first (so the fixed grid's
+    workgroups take the long blocks first). Returns an int32 [k, 2] array (written into
+    ``out`` when given)."""
+    import numpy as np
+
+    rw = prefill_rows_per_block(Hq, Hkv)
+    cu = np.asarray(cu[first: n + 1], dtype=np.int64)
+    ql = cu[1:] - cu[:-1]
+    cx = np.asarray(ctx[first:n], dtype=np.int64)
+    nb = (ql + rw - 1) // rw
+    seq = np.repeat(np.arange(first, n, dtype=np.int64), nb)
+    starts = np.repeat(np.cumsum(nb) - nb, nb)
+    qb = np.arange(int(nb.sum()), dtype=np.int64) - starts
+    qls, cxs = ql[seq - first], cx[seq - first]
+    last = cxs - qls + np.minimum(qls - 1, qb * rw + rw - 1)      # last visible key of the block
+    first_key = np.maximum(0, cxs - qls + qb * rw - window + 1) if window > 0 else np.zeros_like(last)
+    tiles = last // 64 + 1 - first_key // 64
+    order = np.argsort(-tiles, kind="stable")
+    k = len(order)
+    res = out[:k] if out is not None else np.empty((k, 2), dtype=np.int32)
+    res[:, 0] = seq[order]
+    res[:, 1] = qb[order]
+    return res
+
+
+def prefill_attention_worklist(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, scale,
+                               items, n_items, grid: int = 512, ks: int = 1, out=None,
+                               causal: bool = True, window: int = 0):
+    """Paged prefill attention driven by a device work list (``plan_prefill_items``): rows
+    are absolute token rows of the step, ``items`` [>=n, 2] int32 and ``n_items`` a
+    1-element int32 tensor on the device. The launch shape (``grid`` workgroups x ``ks``
+    wave groups) is fixed, so one hipGraph capture serves every step's list. Rows no item
+    covers are left untouched."""
+    if not _gpu(q):
+        return ref.prefill_attention_worklist(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, scale,
+                                              items, n_items, out, causal, window,
+                                              prefill_rows_per_block(Hq, Hkv))
+    if out is None:
+        out = torch.zeros(q.shape[0], Hq * 128, dtype=q.dtype, device=q.device)
+    kernels().prefill_attention_worklist(out, q, kc, vc, block_tables, cu_q, ctx_lens, int(Hq), int(Hkv),
+                                         float(scale), bool(causal), int(window), items, n_items,
+                                         int(grid), int(ks))
     return out
 
 

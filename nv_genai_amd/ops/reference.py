@@ -177,6 +177,35 @@ def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
     return out
 
 
+def prefill_attention_worklist(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, scale, items, n_items,
+                               out=None, causal=True, window=0, rw=128, D=128):
+    """The work-list kernel's semantics: every listed (sequence, row block) pair writes its
+    RW query rows (absolute token rows cu_q[b] + RW qb ...) of every head; other rows of
+    ``out`` are left as they are."""
+    G = Hq // Hkv
+    if out is None:
+        out = torch.zeros(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
+    n = int(n_items.reshape(-1)[0])
+    for b, qb in items[:n].tolist():
+        s0, s1 = int(cu_q[b]), int(cu_q[b + 1])
+        ql, ctx = s1 - s0, int(ctx_lens[b])
+        r0, r1 = qb * rw, min(ql, qb * rw + rw)
+        if r0 >= r1:
+            continue
+        qpos = torch.arange(ctx - ql + r0, ctx - ql + r1, device=q.device)
+        kpos = torch.arange(ctx, device=q.device)
+        mask = kpos[None, :] <= qpos[:, None] if causal else torch.ones(r1 - r0, ctx, dtype=torch.bool,
+                                                                        device=q.device)
+        if window > 0:
+            mask = mask & (kpos[None, :] > qpos[:, None] - window)
+        for hq in range(Hq):
+            k, v = _gather_kv(kc, vc, block_tables[b], ctx, hq // G)
+            qs = q[s0 + r0:s0 + r1, hq * D:(hq + 1) * D].float()
+            sc = ((qs @ k.T) * scale).masked_fill(~mask, float("-inf"))
+            out[s0 + r0:s0 + r1, hq * D:(hq + 1) * D] = (torch.softmax(sc, -1) @ v).to(out.dtype)
+    return out
+
+
 def varlen_attention(q, k, v, cu, Hq, Hkv, D, scale, causal=False):
     G = Hq // Hkv
     T = q.shape[0]

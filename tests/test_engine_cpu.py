@@ -215,3 +215,42 @@ def test_fp8_w8a8_model_close_to_bf16(model):
     a, b = outs[False][0], outs[True][0]
     assert float((a - b).norm() / a.norm()) < 0.15
     assert len(outs[True][1]) == 4
+
+
+def test_prefill_worklist_plan_covers_every_row_once():
+    """plan_prefill_items + the work-list semantics (reference) reproduce paged prefill
+    attention on the prefill sequences of a mixed step and leave the decode rows alone;
+    items are ordered longest key range first."""
+    import numpy as np
+
+    from nv_genai_amd import ops
+    from nv_genai_amd.ops import reference as ref
+
+    torch.manual_seed(0)
+    Hq, Hkv, D = 8, 2, 128
+    nd = 3
+    ctxs = [50, 7, 130] + [200, 65, 1, 129]
+    qls = [1] * nd + [200, 30, 1, 129]
+    pages = [(c + 63) // 64 for c in ctxs]
+    nb = sum(pages)
+    kc = torch.randn(nb, Hkv, 64, D)
+    vc = torch.randn(nb, Hkv, D, 64)
+    bt = torch.zeros(len(ctxs), max(pages), dtype=torch.int32)
+    k = 0
+    for i, p in enumerate(pages):
+        bt[i, :p] = torch.arange(k, k + p)
+        k += p
+    cu = np.concatenate([[0], np.cumsum(qls)]).astype(np.int32)
+    q = torch.randn(int(cu[-1]), Hq * D)
+    items = ops.plan_prefill_items(cu, np.array(ctxs), nd, len(ctxs), Hq, Hkv)
+    rw = ops.prefill_rows_per_block(Hq, Hkv)
+    assert rw == 32 and len(items) == 7 + 1 + 1 + 5     # 32-row blocks of 200, 30, 1, 129 rows
+    out = torch.full((int(cu[-1]), Hq * D), 5.0)
+    ref.prefill_attention_worklist(q, kc, vc, bt, torch.from_numpy(cu), torch.tensor(ctxs), Hq, Hkv, D ** -0.5,
+                                   torch.from_numpy(items), torch.tensor([len(items)]), out=out, rw=rw)
+    want = ref.prefill_attention_paged(q[nd:], kc, vc, bt[nd:], torch.from_numpy(cu[nd:] - cu[nd]),
+                                       torch.tensor(ctxs[nd:]), Hq, Hkv, D, D ** -0.5)
+    assert torch.allclose(out[nd:], want, atol=1e-5)
+    assert bool((out[:nd] == 5.0).all())
+    tiles = [(ctxs[b] - qls[b] + min(qls[b] - 1, qb * rw + rw - 1)) // 64 + 1 for b, qb in items.tolist()]
+    assert tiles == sorted(tiles, reverse=True)

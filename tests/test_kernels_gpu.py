@@ -535,3 +535,56 @@ def test_fp8_linear_matches_dequantised_matmul(gpu):
     _close(y, y_ref, 0.05, 0.01)
     exact = x.float() @ w.float().t()
     assert float((y.float() - exact).norm() / exact.norm()) < 0.06
+
+
+@pytest.mark.parametrize("Hkv,G,window,ks,grid", [(8, 4, 0, 1, 512), (8, 4, 0, 2, 7), (2, 8, 0, 1, 13),
+                                                  (4, 1, 0, 2, 64), (2, 4, 200, 1, 512)])
+def test_prefill_attention_worklist(gpu, Hkv, G, window, ks, grid):
+    """Work-list mode of the 32x32 prefill kernel (the engine's mixed-step graphs): a step
+    whose first rows are decode rows (left untouched) and whose prefill sequences are covered
+    by the host-planned (sequence, row block) list, with a fixed grid smaller than the list
+    (the persistent loop), against the fp32 reference."""
+    D = 128
+    Hq = Hkv * G
+    nd = 5                                   # decode rows: one token each, not in the list
+    ctxs = [300, 64, 1, 900, 33] + [1200, 700, 64, 1, 1500, 33]
+    qls = [1] * nd + [940, 300, 64, 1, 1500, 1]
+    kc, vc, bt = _paged_setup(ctxs, Hkv, D, gpu, seed=17)
+    cu = [0]
+    for ql in qls:
+        cu.append(cu[-1] + ql)
+    q = _bf(cu[-1], Hq * D, dev=gpu)
+    cu_t = torch.tensor(cu, dtype=torch.int32, device=gpu)
+    ctx_t = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
+    scale = 1 / math.sqrt(D)
+    import numpy as np
+
+    items = ops.plan_prefill_items(np.array(cu), np.array(ctxs), nd, len(ctxs), Hq, Hkv, window)
+    it_d = torch.zeros(len(items) + 9, 2, dtype=torch.int32, device=gpu)   # capacity > count
+    it_d[: len(items)] = torch.from_numpy(items).to(gpu)
+    n_d = torch.tensor([len(items)], dtype=torch.int32, device=gpu)
+    out = torch.full((cu[-1], Hq * D), 7.0, dtype=torch.bfloat16, device=gpu)
+    ops.prefill_attention_worklist(q, kc, vc, bt, cu_t, ctx_t, Hq, Hkv, scale, it_d, n_d, grid=grid, ks=ks,
+                                   out=out, window=window)
+    o_ref = ref.prefill_attention_paged(q[nd:].float(), kc, vc, bt[nd:], cu_t[nd:] - nd, ctx_t[nd:], Hq, Hkv, D,
+                                        scale, True, window)
+    _close_rows(out[nd:], o_ref, width=D)
+    assert bool((out[:nd] == 7.0).all())     # decode rows untouched
+
+
+def test_decode_attention_skip_empty_rows(gpu):
+    """skip_empty: rows with ctx 0 are not written (the mixed-step graph's decode launch
+    covers a bucket of rows whose tail belongs to the prefill tokens)."""
+    Hkv, G, D = 8, 4, 128
+    Hq = Hkv * G
+    ctxs = [100, 0, 700, 0]
+    kc, vc, bt = _paged_setup([max(c, 1) for c in ctxs], Hkv, D, gpu)
+    ctx = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
+    q = _bf(4, Hq * D, dev=gpu)
+    for ppp in (None, 1):
+        ws = ops.DecodeWorkspace(4, Hq, Hkv, 700, gpu, ppp)
+        out = torch.full((4, Hq * D), 3.0, dtype=torch.bfloat16, device=gpu)
+        ops.decode_attention(q, kc, vc, bt, ctx, Hq, Hkv, 700, 1 / math.sqrt(D), out=out, ws=ws, skip_empty=True)
+        assert bool((out[1] == 3.0).all()) and bool((out[3] == 3.0).all())
+        o_ref = ref.decode_attention(q.float(), kc, vc, bt, ctx, Hq, Hkv, 1 / math.sqrt(D))
+        _close_rows(out[[0, 2]], o_ref[[0, 2]], width=D)
