@@ -120,6 +120,14 @@ class EngineConfig:
     kv_cache_dtype: str = "auto"   # "fp8": e4m3fn KV pages (2x the cached tokens, half the KV reads)
     kv_scales: Tuple[float, float] = (1.0, 1.0)   # fp8 KV: the per-tensor K / V scales
     sp_min_tokens: int = 512
+    # prefill / mixed steps as hipGraphs, one per (token bucket, decode-row bucket), captured
+    # on first use: the whole step (embedding, every layer, LM head, sampling) is one launch,
+    # with the step's layout in device buffers (work-list prefill attention, decode rows
+    # past the step's own skipped); graph_eager runs the same body without capture (tests)
+    mixed_graphs: bool = True
+    graph_eager: bool = False
+    graph_token_step: int = 256
+    max_graph_tokens: int = 0     # 0: mixed_prefill_tokens + max_num_seqs, rounded up
 
 
 _INERT = Request(id=-1, prompt_ids=[0], params=SamplingParams(temperature=0.0))
@@ -257,6 +265,21 @@ class LLMEngine:
             if self.p.pp_size > 1:
                 over["use_graphs"] = False
             self.cfg = cfg = type(cfg)(**{**cfg.__dict__, **over})
+        # ---- prefill / mixed step graphs (step layout in device buffers)
+        self.mgraphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._graph_pool = None
+        self._cap_stream = None
+        self._mg_ok = self._mixed_graphs_eligible()
+        if self._mg_ok:
+            step = max(1, cfg.graph_token_step)
+            mx = cfg.max_graph_tokens or (cfg.mixed_prefill_tokens + cfg.max_num_seqs)
+            self._mg_max_tokens = min(-(-mx // step) * step, T // step * step)
+            self._nd_buckets = sorted({b for b in (8, 16, 32, 64, 128, 256, 512) if b < S} | {S})
+            cap = self._mg_max_tokens // 32 + S + 16
+            self.h_ctxd, self.d_ctxd = hbuf(S), dbuf(S)
+            self.h_sidx, self.d_sidx = hbuf(S, dtype=torch.int64), dbuf(S, dtype=torch.int64)
+            self.h_items, self.d_items = hbuf(cap, 2), dbuf(cap, 2)
+            self.h_nitems, self.d_nitems = hbuf(1), dbuf(1)
         if self.gpu and cfg.use_graphs:
             self._capture_graphs()
 
@@ -520,12 +543,17 @@ class LLMEngine:
             cu = self._np[3][: n + 1]
             max_q = int((cu[1:] - cu[:-1]).max())
             max_ctx = int(self._np[4][:n].max())
-            with gpu_range(f"{'mixed' if nd else 'prefill'} n={n} tok={ntok} dec={nd}"):
-                self._sync_step(kind, n, ntok, max_q, max_ctx, 0, nd)
-                self._upload(n, ntok)
-                self._gather_ids(src)
-                logits = self._prefill_forward(n, ntok, max_q, max_ctx, nd)
-                self._sample(logits, n)
+            key = self._graph_key(n, ntok, nd)
+            with gpu_range(f"{'mixed' if nd else 'prefill'} n={n} tok={ntok} dec={nd}"
+                           + (" graph" if key is not None else "")):
+                if key is not None:
+                    self._graph_step(key, kind, n, ntok, max_q, max_ctx, nd, src)
+                else:
+                    self._sync_step(kind, n, ntok, max_q, max_ctx, 0, nd)
+                    self._upload(n, ntok)
+                    self._gather_ids(src)
+                    logits = self._prefill_forward(n, ntok, max_q, max_ctx, nd)
+                    self._sample(logits, n)
         buf = self._tok_host[self._tok_flip]
         self._tok_flip ^= 1
         buf[0][:n].copy_(self.d_tok[:n], non_blocking=self.gpu)
@@ -658,26 +686,30 @@ class LLMEngine:
         dist.broadcast(x, src=self._tp_src(), group=self.p.mp_group)
         return x
 
-    def _sync_step(self, kind: int, n: int, ntok: int, max_q: int, max_ctx: int, bs: int, nd: int = 0) -> None:
-        """Driver: publish the step (header + packed int buffers) to the replica's ranks."""
+    def _sync_step(self, kind: int, n: int, ntok: int, max_q: int, max_ctx: int, bs: int, nd: int = 0,
+                   gb: int = 0) -> None:
+        """Driver: publish the step (header + packed int buffers) to the replica's ranks.
+        ``gb``: token bucket of a graph-captured prefill / mixed step (its padded token rows
+        travel too, so followers replay the same graph on the same inputs)."""
         if self.p.mp_size == 1:
             return
-        hdr = torch.tensor([kind, n, ntok, max_q, max_ctx, bs, nd, 0], dtype=torch.int64)
+        hdr = torch.tensor([kind, n, ntok, max_q, max_ctx, bs, nd, gb], dtype=torch.int64)
         self._bcast(hdr)
         if kind < 0:
             return
         rows = max(n, bs)
-        toks = max(ntok, bs)
+        toks = max(ntok, bs, gb)
         payload = torch.cat([self.h_ids[:toks], self.h_pos[:toks], self.h_slots[:toks],
                              self.h_cu[: rows + 1], self.h_ctx[:rows], self.h_bt[:rows].reshape(-1)])
         self._bcast(payload)
 
     def _recv_step(self):
         hdr = self._bcast(torch.zeros(8, dtype=torch.int64)).cpu().tolist()
-        kind, n, ntok, max_q, max_ctx, bs, nd = hdr[:7]
+        kind, n, ntok, max_q, max_ctx, bs, nd, gb = hdr
+        self._recv_gb = gb
         if kind < 0:
             return kind, n, 0, 0, 0, 0, 0
-        rows, toks = max(n, bs), max(ntok, bs)
+        rows, toks = max(n, bs), max(ntok, bs, gb)
         size = 3 * toks + (rows + 1) + rows + rows * self.max_blocks
         payload = self._bcast(torch.zeros(size, dtype=torch.int32)).cpu()
         if self._up_ev is not None:
@@ -709,7 +741,12 @@ class LLMEngine:
                 continue
             if kind < 0:
                 return
-            if kind in (1, 3):
+            if kind in (1, 3) and self._recv_gb:
+                key = self._graph_key(n, ntok, nd)
+                if key is None or key[0] != self._recv_gb:
+                    raise RuntimeError(f"follower cannot replay the driver's step graph {self._recv_gb}")
+                self._graph_step(key, kind, n, ntok, max_q, max_ctx, nd, None, follower=True)
+            elif kind in (1, 3):
                 self._upload(n, ntok)
                 self._prefill_forward(n, ntok, max_q, max_ctx, nd)
             elif bs:
@@ -846,7 +883,10 @@ class LLMEngine:
             m.cu_q_prefill = self.d_cu[nd: n + 1] - nd
         return m
 
-    def _upload(self, n, ntok):
+    def _upload(self, n, ntok, nparam: Optional[int] = None, extra=()):
+        """Step buffers host -> device (pinned, async): ``ntok`` token rows, ``n`` sequence
+        rows, ``nparam`` (default n) sampling-parameter rows, plus ``extra`` (host, device,
+        rows) triples; one event marks the whole upload."""
         nb = non_blocking = self.gpu
         self.d_ids[:ntok].copy_(self.h_ids[:ntok], non_blocking=nb)
         self.d_pos[:ntok].copy_(self.h_pos[:ntok], non_blocking=nb)
@@ -854,9 +894,12 @@ class LLMEngine:
         self.d_cu[: n + 1].copy_(self.h_cu[: n + 1], non_blocking=nb)
         self.d_ctx[:n].copy_(self.h_ctx[:n], non_blocking=nb)
         self.d_bt[:n].copy_(self.h_bt[:n], non_blocking=nb)
+        npr = n if nparam is None else nparam
         for h, d in ((self.h_temp, self.d_temp), (self.h_topk, self.d_topk), (self.h_topp, self.d_topp),
                      (self.h_seed, self.d_seed), (self.h_step, self.d_step), (self.h_pen, self.d_pen)):
-            d[:n].copy_(h[:n], non_blocking=non_blocking)
+            d[:npr].copy_(h[:npr], non_blocking=non_blocking)
+        for h, d, rows in extra:
+            d[:rows].copy_(h[:rows], non_blocking=non_blocking)
         if self.gpu:
             self._up_ev = torch.cuda.Event()
             self._up_ev.record()
@@ -935,6 +978,10 @@ class LLMEngine:
         cu = self._np[3][: n + 1]
         max_q = int((cu[nd + 1:] - cu[nd:-1]).max())
         max_ctx = int(self._np[4][:n].max())
+        key = None if (self._beam_rows or self._needs_penalty(n)) else self._graph_key(n, ntok, nd)
+        if key is not None:
+            self._graph_step(key, 3 if nd else 1, n, ntok, max_q, max_ctx, nd, None)
+            return self.d_tok[:n].cpu(), self.d_lp[:n].cpu()
         self._sync_step(3 if nd else 1, n, ntok, max_q, max_ctx, 0, nd)
         self._upload(n, ntok)
         logits = self._prefill_forward(n, ntok, max_q, max_ctx, nd)
@@ -999,6 +1046,129 @@ class LLMEngine:
                    self.d_seed[:bs], self.d_step[:bs], None, None,
                    out_tok=self.d_tok[:bs], out_lp=self.d_lp[:bs])
 
+    # ------------------------------------------------------------------ prefill / mixed step graphs
+    def _mixed_graphs_eligible(self) -> bool:
+        """Graph-captured prefill / mixed steps need the work-list prefill kernel (head_dim
+        128, bf16 KV pages, <= 1024 pages per sequence), one pipeline stage and the plain
+        stacked forward (no sequence-parallel prefill, no split mixed steps, no MoE)."""
+        c, m = self.cfg, self.model
+        if not c.mixed_graphs or not (self.gpu and c.use_graphs or c.graph_eager):
+            return False
+        return (self.p.pp_size == 1 and not c.sequence_parallel and not m.split_mixed and m.D == 128
+                and m.kv_dtype == "auto" and not self.mcfg.is_moe and self.max_blocks <= 1024)
+
+    def _graph_key(self, n: int, ntok: int, nd: int):
+        """(token bucket, decode-row bucket) of a prefill / mixed step, or None (eager)."""
+        if not self._mg_ok or self._has_mm or n > self.cfg.max_num_seqs:
+            return None
+        step = self.cfg.graph_token_step
+        tb = -(-ntok // step) * step
+        if tb > self._mg_max_tokens:
+            return None
+        ndb = 0 if nd == 0 else next(b for b in self._nd_buckets if b >= nd)
+        return (tb, ndb)
+
+    def _graph_meta(self, key) -> AttnMeta:
+        tb, ndb = key
+        rw = ops.prefill_rows_per_block(self.model.hq, self.model.hkv)
+        G = self.model.hq // self.model.hkv
+        hpw = 4 if G % 4 == 0 else 2 if G % 2 == 0 else 1
+        ng = self.model.hkv * (G // hpw)
+        # few row blocks (one short prompt): the 8-wave split-key form, one workgroup per CU
+        ks = 2 if (tb - ndb) // rw * ng <= 320 else 1
+        S = self.cfg.max_num_seqs
+        return AttnMeta(kind="graph", slots=self.d_slots[:tb], cu_q=self.d_cu[: S + 1], ctx_lens=self.d_ctx[:S],
+                        block_tables=self.d_bt[:S], max_q_len=0, max_ctx=self.cfg.max_model_len,
+                        decode_ws=self.decode_ws, n_decode=ndb, decode_ctx=self.d_ctxd[:max(ndb, 1)],
+                        items=self.d_items, n_items=self.d_nitems, pf_grid=256 if ks == 2 else 512, pf_ks=ks)
+
+    def _graph_body(self, key) -> None:
+        """One prefill / mixed step over the bucket: forward of tb token rows, logits of the
+        S = max_num_seqs sampling rows (d_sidx), sampling into d_tok / d_lp."""
+        tb, _ = key
+        S = self.cfg.max_num_seqs
+        h = self.model.forward(self.d_ids[:tb], self.d_pos[:tb], self._graph_meta(key), self.d_sidx[:S])
+        logits = self.model.logits(h)
+        tok, lp = ops.sample(logits, self.d_temp[:S], self.d_topk[:S], self.d_topp[:S], self.d_seed[:S],
+                             self.d_step[:S], None, None, out_tok=self.d_tok[:S], out_lp=self.d_lp[:S])
+        if tok.data_ptr() != self.d_tok.data_ptr():   # reference path returns fresh tensors
+            self.d_tok[:S].copy_(tok[:S])
+            self.d_lp[:S].copy_(lp[:S])
+
+    def _capture_step_graph(self, key) -> "torch.cuda.CUDAGraph":
+        """Capture the step graph of ``key`` (first use). The device is drained first; the
+        warm-up and capture run on inert inputs (no KV writes or reads: slots -1, no decode
+        rows, an empty work list) and the sampled tokens of the step in flight are kept."""
+        tb, ndb = key
+        dev = self.device
+        torch.cuda.synchronize(dev)
+        keep = (self.d_tok.clone(), self.d_lp.clone())
+        self.d_ids[:tb].zero_()
+        self.d_pos[:tb].zero_()
+        self.d_slots[:tb].fill_(-1)
+        self.d_ctxd.zero_()
+        self.d_nitems.zero_()
+        self.d_sidx.zero_()
+        if self._cap_stream is None:
+            self._cap_stream = torch.cuda.Stream(dev)
+        stream = self._cap_stream
+        stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(stream):
+            self._graph_body(key)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self._graph_pool, stream=stream, capture_error_mode="thread_local"):
+                self._graph_body(key)
+        torch.cuda.current_stream(dev).wait_stream(stream)
+        torch.cuda.synchronize(dev)
+        self._graph_pool = g.pool()
+        self.d_tok.copy_(keep[0])
+        self.d_lp.copy_(keep[1])
+        self.mgraphs[key] = g
+        return g
+
+    def _graph_step(self, key, kind, n, ntok, max_q, max_ctx, nd, src, follower: bool = False) -> None:
+        """Launch a prefill / mixed step through its graph: pad the token rows to the bucket,
+        fill the step's device layout (decode-row contexts, prefill work list, sampling rows
+        and parameters), upload, gather pipelined ids, replay."""
+        tb, ndb = key
+        S = self.cfg.max_num_seqs
+        g = self.mgraphs.get(key)
+        if g is None and self.gpu and not self.cfg.graph_eager:
+            g = self._capture_step_graph(key)
+        if not follower:
+            self.h_ids[ntok:tb] = 0
+            self.h_pos[ntok:tb] = 0
+            self.h_slots[ntok:tb] = -1
+        cu, ctx = self._np[3], self._np[4]
+        self.h_ctxd[:nd] = self.h_ctx[:nd]
+        self.h_ctxd[nd:max(ndb, nd)] = 0
+        items = ops.plan_prefill_items(cu, ctx, nd, n, self.model.hq, self.model.hkv, self.model.window,
+                                       out=self.h_items.numpy())
+        self.h_nitems[0] = len(items)
+        sidx = self.h_sidx.numpy()
+        sidx[:n] = cu[1:n + 1] - 1
+        sidx[n:S] = 0
+        self._pad_params(n, S)
+        if not follower:
+            self._sync_step(kind, n, ntok, max_q, max_ctx, 0, nd, gb=tb)
+        self._upload(n, tb, nparam=S, extra=((self.h_ctxd, self.d_ctxd, max(ndb, 1)),
+                                             (self.h_items, self.d_items, max(len(items), 1)),
+                                             (self.h_nitems, self.d_nitems, 1), (self.h_sidx, self.d_sidx, S)))
+        self._gather_ids(src)
+        if g is not None:
+            g.replay()
+        else:
+            self._graph_body(key)
+
+    def _pad_params(self, n: int, rows: int) -> None:
+        """Sampling-parameter rows [n, rows) of a padded launch: greedy, no penalty."""
+        self.h_temp[n:rows] = 0.0
+        self.h_topk[n:rows] = 0
+        self.h_topp[n:rows] = 1.0
+        self.h_seed[n:rows] = 0
+        self.h_step[n:rows] = 0
+        self.h_pen[n:rows] = 1.0
+
     def _capture_graphs(self):
         sizes = [b for b in self.cfg.graph_batch_sizes if b <= self.cfg.max_num_seqs]
         # inert inputs for capture: no cache writes, empty contexts
@@ -1020,6 +1190,7 @@ class LLMEngine:
                     self._decode_body(bs)
                 pool = g.pool()
                 self.graphs[bs] = g
+        self._graph_pool = pool     # step graphs captured later share the pool
         torch.cuda.current_stream(self.device).wait_stream(stream)
         torch.cuda.synchronize(self.device)
 

@@ -30,6 +30,7 @@ a partial sum that joins the dense path's all-reduce.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from dataclasses import dataclass
@@ -58,6 +59,16 @@ class AttnMeta:
     decode_ws: Optional[ops.DecodeWorkspace] = None
     n_decode: int = 0                          # mixed steps: rows [0, n_decode) are decode rows
     cu_q_prefill: Optional[torch.Tensor] = None  # mixed steps: cu_seqlens of the prefill rows
+    # kind "graph" (a hipGraph-captured prefill / mixed step over a bucket of rows; every
+    # step-dependent quantity lives in device buffers): decode rows [0, n_decode) read
+    # decode_ctx (0 past the step's real decode rows: skipped), the prefill rows are covered
+    # by the work list (items [k, 2], n_items [1]) over absolute token rows (cu_q / ctx_lens
+    # of all the step's sequences); launch shape of the work-list kernel: (grid, ks)
+    decode_ctx: Optional[torch.Tensor] = None
+    items: Optional[torch.Tensor] = None
+    n_items: Optional[torch.Tensor] = None
+    pf_grid: int = 512
+    pf_ks: int = 1
 
 
 class LlamaModel:
@@ -458,6 +469,8 @@ class LlamaModel:
                                         meta.block_tables, meta.ctx_lens, hq, hkv,
                                         meta.max_ctx, self.scale, ws=meta.decode_ws, window=W,
                                         kv_scales=self.kv_scales)
+        if meta.kind == "graph":
+            return self._attention_graph(q, qkv, li, meta, T)
         if meta.kind == "mixed":
             nd = meta.n_decode
             attn = torch.empty(T, qdim, dtype=qkv.dtype, device=qkv.device)
@@ -491,6 +504,34 @@ class LlamaModel:
                                            meta.block_tables, meta.cu_q, meta.ctx_lens,
                                            hq, hkv, D, meta.max_q_len, self.scale, window=W,
                                            kv_scales=self.kv_scales)
+
+    def _attention_graph(self, q, qkv, li, meta: AttnMeta, T: int):
+        """Attention of a graph-captured step: the decode launch over the bucket's first
+        n_decode rows (rows whose decode_ctx is 0 are not this step's and stay untouched) on
+        the current stream and the work-list prefill kernel on the side stream, writing
+        disjoint rows of one output (rows no one covers are bucket padding)."""
+        hq, hkv, D = self.hq, self.hkv, self.D
+        W = self.window
+        attn = torch.empty(T, hq * D, dtype=qkv.dtype, device=qkv.device)
+        gpu = qkv.is_cuda
+        if gpu:
+            if self._attn_stream is None:
+                self._attn_stream = torch.cuda.Stream(qkv.device)
+            side = self._attn_stream
+            main = torch.cuda.current_stream(qkv.device)
+            side.wait_stream(main)
+        with (torch.cuda.stream(side) if gpu else contextlib.nullcontext()):
+            ops.prefill_attention_worklist(q, self.k_cache[li], self.v_cache[li], meta.block_tables, meta.cu_q,
+                                           meta.ctx_lens, hq, hkv, self.scale, meta.items, meta.n_items,
+                                           grid=meta.pf_grid, ks=meta.pf_ks, out=attn, window=W)
+        nd = meta.n_decode
+        if nd:
+            ops.decode_attention(q[:nd], self.k_cache[li], self.v_cache[li], meta.block_tables[:nd],
+                                 meta.decode_ctx[:nd], hq, hkv, meta.max_ctx, self.scale, out=attn[:nd],
+                                 ws=meta.decode_ws, window=W, kv_scales=self.kv_scales, skip_empty=True)
+        if gpu:
+            main.wait_stream(side)
+        return attn
 
     def _reduce_add_norm(self, partial, resid, w, b=None):
         """resid += all_reduce_TP(partial); returns norm(resid). A small TP message goes

@@ -16,7 +16,7 @@ def _free_port():
     return p
 
 
-def _tp_worker(rank, world, port, q, tp=2, pp=1, sp=False, model="llama-tiny", over=None):
+def _tp_worker(rank, world, port, q, tp=2, pp=1, sp=False, model="llama-tiny", over=None, ekw=None):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
@@ -29,7 +29,7 @@ def _tp_worker(rank, world, port, q, tp=2, pp=1, sp=False, model="llama-tiny", o
     cfg = llama_config(model, **(over or {}))
     full = LlamaModel(cfg, "cpu", pctx=single, seed=7).state_dict()
     ecfg = EngineConfig(model=model, max_num_seqs=4, max_batched_tokens=256, max_model_len=512,
-                        kv_cache_blocks=32, sequence_parallel=sp, sp_min_tokens=16)
+                        kv_cache_blocks=32, sequence_parallel=sp, sp_min_tokens=16, **(ekw or {}))
     prompts = [[5, 6, 7, 8] * 20, [9, 10, 11] * 11]
     params = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
     # fp32: a TP shard sums its partial products in a different order than one device, and
@@ -96,6 +96,25 @@ def test_tensor_parallel_families_match_single(model, over, sp):
     q = ctx.Queue()
     procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q, 2, 1, sp, model, over))
              for r in range(world)]
+    for p in procs:
+        p.start()
+    out, ref, _, _, _ = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out == ref
+
+
+def test_tensor_parallel_graph_steps_match_single():
+    """TP=2 with graph-layout prefill steps (run uncaptured on CPU: graph_eager): the
+    followers rebuild the step's device layout from the broadcast payload (padded token
+    rows included) and stay in lock-step with the driver's collectives."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ekw = {"mixed_graphs": True, "graph_eager": True, "graph_token_step": 32}
+    procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q, 2, 1, False, "llama-tiny",
+                                                  {"head_dim": 128}, ekw)) for r in range(world)]
     for p in procs:
         p.start()
     out, ref, _, _, _ = q.get(timeout=300)

@@ -254,3 +254,41 @@ def test_prefill_worklist_plan_covers_every_row_once():
     assert bool((out[:nd] == 5.0).all())
     tiles = [(ctxs[b] - qls[b] + min(qls[b] - 1, qb * rw + rw - 1)) // 64 + 1 for b, qb in items.tolist()]
     assert tiles == sorted(tiles, reverse=True)
+
+
+@pytest.mark.parametrize("async_", [True, False])
+def test_graph_step_layout_matches_eager(async_):
+    """The graph-captured prefill / mixed step body (engine mixed_graphs, run without capture
+    on CPU: graph_eager) — token rows padded to the bucket, decode rows past the step's own
+    skipped, prefill attention from the host work list over absolute rows, S sampling rows —
+    generates exactly the eager steps' tokens and log-probabilities."""
+    from nv_genai_amd.models.config import llama_config
+    from nv_genai_amd.models.llama import LlamaModel
+    from nv_genai_amd.parallel.dist import ParallelContext
+
+    cfg = llama_config("llama-tiny", head_dim=128)        # the work-list kernel's head_dim
+    m = LlamaModel(cfg, "cpu", dtype=torch.float32, pctx=ParallelContext(), seed=5)
+    prompts = [[3, 4, 5, 6] * 25, [7, 8] * 40, [9] * 5, [11, 12, 13] * 30, [2] * 70]
+    p = SamplingParams(temperature=0.0, max_tokens=7, ignore_eos=True, logprobs=True)
+    outs = {}
+    for graphs in (False, True):
+        e = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=8, max_batched_tokens=160, max_model_len=512,
+                                   kv_cache_blocks=64, mixed_prefill_tokens=64, token_alignment=32,
+                                   async_decode=async_, mixed_graphs=graphs, graph_eager=graphs,
+                                   graph_token_step=32), device="cpu", model=m, model_cfg=cfg)
+        assert e._mg_ok == graphs
+        calls = []
+        if graphs:
+            orig = e._graph_step
+            e._graph_step = lambda key, *a, **k: (calls.append(key), orig(key, *a, **k))[1]
+        reqs = [e.add_request(pr, p) for pr in prompts[:3]]
+        e.step()
+        reqs += [e.add_request(pr, p) for pr in prompts[3:]]   # arrive while the first ones decode
+        e.run_until_done(reqs)
+        outs[graphs] = [(r.output_ids, r.logprobs) for r in reqs]
+        if graphs:
+            assert calls and any(k[1] > 0 for k in calls)       # mixed steps went through the body
+            assert all(k[0] % 32 == 0 for k in calls)
+    for (a, la), (b, lb) in zip(outs[False], outs[True]):
+        assert a == b
+        assert torch.allclose(torch.tensor(la), torch.tensor(lb), atol=1e-4)

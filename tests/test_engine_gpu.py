@@ -262,3 +262,29 @@ def test_fp8_kv_cache_engine_gpu(gpu, weights):
     g = [r.output_ids for r in _engine(weights, "cuda", kv_cache_dtype="fp8").generate(PROMPTS, p)]
     e = [r.output_ids for r in _engine(weights, "cuda", kv_cache_dtype="fp8", use_graphs=False).generate(PROMPTS, p)]
     assert g == e
+
+
+def test_step_graphs_equal_eager_steps(gpu, weights):
+    """Prefill / mixed steps captured as hipGraphs (one per token / decode-row bucket, work-
+    list prefill attention, decode rows past the step's own skipped) generate the eager
+    steps' tokens, with requests arriving while others decode (mixed steps)."""
+    from nv_genai_amd.engine.llm_engine import SamplingParams
+
+    p = SamplingParams(temperature=0.0, max_tokens=20, ignore_eos=True, logprobs=True)
+    outs = {}
+    for graphs in (True, False):
+        e = _engine(weights, "cuda", use_graphs=True, mixed_graphs=graphs, mixed_prefill_tokens=512,
+                    max_graph_tokens=1536)
+        reqs = [e.add_request(pr, p) for pr in PROMPTS[:2]]
+        for _ in range(3):
+            e.step()
+        reqs += [e.add_request(pr, p) for pr in PROMPTS[2:]]
+        e.run_until_done(reqs)
+        outs[graphs] = [(r.output_ids, r.logprobs) for r in reqs]
+        if graphs:
+            assert e.mgraphs and any(nd > 0 for _, nd in e.mgraphs)   # mixed steps were graphed
+        else:
+            assert not e.mgraphs
+    for (a, la), (b, lb) in zip(outs[True], outs[False]):
+        assert a == b
+        assert max(abs(x - y) for x, y in zip(la, lb)) < 0.05
