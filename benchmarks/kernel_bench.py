@@ -74,6 +74,19 @@ def main():
         if args.only == "rope":
             print(json.dumps(out))
             return
+    if args.only in ("", "bw"):
+        # HBM read ceiling of this box for the bandwidth-bound kernels: a 2 GiB bf16 slab
+        # reduced by PyTorch (read-only stream) and copied device to device (read + write)
+        X = torch.empty(1 << 30, dtype=torch.bfloat16, device=dev).normal_()
+        Y = torch.empty_like(X)
+        us_sum = timeit(lambda: X.sum(dtype=torch.float32))
+        us_cp = timeit(lambda: Y.copy_(X))
+        out["hbm_read_sum_2GiB"] = {"us": round(us_sum, 1), "TBps": round(X.numel() * 2 / us_sum / 1e6, 2)}
+        out["hbm_copy_2GiB"] = {"us": round(us_cp, 1), "TBps_read_plus_write": round(2 * X.numel() * 2 / us_cp / 1e6, 2)}
+        del X, Y
+        if args.only == "bw":
+            print(json.dumps(out))
+            return
     if args.only in ("", "search"):
         N, Dx = 1_000_000, 1024
         X = torch.nn.functional.normalize(torch.randn(N, Dx, device=dev), dim=1).to(torch.bfloat16)
@@ -83,7 +96,11 @@ def main():
             us = timeit(lambda: ops.score(Q, X, None, 1.0))
             us_all = timeit(lambda: ops.topk(ops.score(Q, X, None, 1.0), 4))
             us_f = timeit(lambda: ops.search_topk(Q, X, bias, 1.0, 4))
-            out[f"search_1Mx1024_q{nq}"] = {"score_us": round(us, 1), "score_TBps": round(N * Dx * 2 / us / 1e6, 2),
+            os.environ["NGA_SEARCH_NT"] = "1"
+            us_nt = timeit(lambda: ops.search_topk(Q, X, bias, 1.0, 4))
+            os.environ.pop("NGA_SEARCH_NT")
+            out[f"search_1Mx1024_q{nq}"] = {"fused_nt_us": round(us_nt, 1),
+                                             "fused_nt_TBps": round(N * Dx * 2 / us_nt / 1e6, 2),"score_us": round(us, 1), "score_TBps": round(N * Dx * 2 / us / 1e6, 2),
                                              "score_topk_us": round(us_all, 1),
                                              "fused_us": round(us_f, 1),
                                              "fused_TBps": round(N * Dx * 2 / us_f / 1e6, 2),
@@ -168,6 +185,15 @@ def main():
             us = timeit(lambda: ops.decode_attention(q2, kc2, vc2, bt2, ctx2, Hq, Hkv, 8192, D ** -0.5, ws=ws))
             out[f"decode_{Bs}x1400_auto"] = {"us": round(us, 1), "parts": ws.nparts(Bs),
                                              "TBps": round(Bs * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
+        # Llama-3-70B at TP=8: 8 q heads and 1 KV head per rank (the agent config's decode)
+        for Bs in (4, 32):
+            kc3, vc3, bt3 = paged_setup([L] * Bs, Hkv=1, width=8192 // 64)
+            q3 = torch.randn(Bs, 8 * D, device=dev, dtype=torch.bfloat16)
+            ctx3 = torch.full((Bs,), L, dtype=torch.int32, device=dev)
+            ws = ops.DecodeWorkspace(Bs, 8, 1, 8192, torch.device(dev))
+            us = timeit(lambda: ops.decode_attention(q3, kc3, vc3, bt3, ctx3, 8, 1, 8192, D ** -0.5, ws=ws))
+            out[f"decode_70b_tp8_{Bs}x1400"] = {"us": round(us, 1), "parts": ws.nparts(Bs),
+                                                "TBps": round(Bs * L * D * 2 * 2 / us / 1e6, 2)}
         if args.only == "decode":
             print(json.dumps(out))
             return

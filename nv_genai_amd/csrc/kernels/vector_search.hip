@@ -8,6 +8,8 @@
 // topk_select_kernel: exact per-segment top-k by a 3-level radix descent on order-preserving
 //   float keys (counts in LDS), then a bitonic sort of the <= k survivors. Used twice: per
 //   4096-score segment, then once more over the per-segment candidates (the k-merge).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -352,7 +354,12 @@ __global__ void __launch_bounds__(64 * W) score_topk_kernel(
     const uint16_t* __restrict__ Q, int nq, const uint16_t* __restrict__ X, int64_t N, int D,
     const float* __restrict__ row_bias, float dot_scale, const int64_t* __restrict__ row_beg,
     const int64_t* __restrict__ row_end, const int32_t* __restrict__ qtab,
-    const int32_t* __restrict__ slot_rows, int k, float* __restrict__ out_v, int64_t* __restrict__ out_r) {
+    const int32_t* __restrict__ slot_rows, int k, float* __restrict__ out_v, int64_t* __restrict__ out_r,
+    int nt_loads) {
+  // X is streamed exactly once: nt_loads marks its loads non-temporal (A/B: NGA_SEARCH_NT)
+  auto xload = [&](const uint16_t* p) -> u16x8 {
+    return nt_loads ? __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(p)) : load8(p);
+  };
   extern __shared__ __attribute__((aligned(16))) uint16_t q_s[];
   __shared__ int s_nql;
   constexpr int ROWS = 32 * W;
@@ -433,8 +440,8 @@ __global__ void __launch_bounds__(64 * W) score_topk_kernel(
 #pragma unroll
     for (int j = 0; j < SC_KB; ++j) {
       if (j < nsteps) {
-        a0[j] = load8(x0 + 32 * j);
-        a1[j] = load8(x1 + 32 * j);
+        a0[j] = xload(x0 + 32 * j);
+        a1[j] = xload(x1 + 32 * j);
       }
     }
     for (int s0 = 0; s0 < nsteps; s0 += SC_KB) {
@@ -443,8 +450,8 @@ __global__ void __launch_bounds__(64 * W) score_topk_kernel(
 #pragma unroll
       for (int j = 0; j < SC_KB; ++j) {
         if (more && s0 + SC_KB + j < nsteps) {
-          b0[j] = load8(x0 + 32 * (s0 + SC_KB + j));
-          b1[j] = load8(x1 + 32 * (s0 + SC_KB + j));
+          b0[j] = xload(x0 + 32 * (s0 + SC_KB + j));
+          b1[j] = xload(x1 + 32 * (s0 + SC_KB + j));
         }
       }
 #pragma unroll
@@ -570,6 +577,8 @@ void launch_score_topk(const uint16_t* Q, int nq, const uint16_t* X, int64_t N, 
   const size_t mg = (size_t)64 * W * KR * 8;
   const size_t lds = qs > mg ? qs : mg;
   dim3 grid((unsigned)nblk, (unsigned)n_items);
+  const char* nte = getenv("NGA_SEARCH_NT");
+  const int nt = nte && atoi(nte) ? 1 : 0;
 #define NGA_STK(NG_, W_, K_)                                                                    \
   do {                                                                                           \
     static bool attr_ = false;                                                                   \
@@ -583,7 +592,7 @@ void launch_score_topk(const uint16_t* Q, int nq, const uint16_t* X, int64_t N, 
     score_topk_kernel<NG_, W_, K_><<<grid, 64 * W_, lds, stream>>>(Q, nq, X, N, D, row_bias,     \
                                                                    dot_scale, row_beg, row_end,  \
                                                                    qtab, slot_rows, k, out_v,    \
-                                                                   out_r);                       \
+                                                                   out_r, nt);                   \
   } while (0)
   if (ng == 1) {
     if (KR == 4) NGA_STK(1, 4, 4); else if (KR == 8) NGA_STK(1, 4, 8); else NGA_STK(1, 4, 16);

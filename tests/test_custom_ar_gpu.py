@@ -44,11 +44,71 @@ def _inp(rank, ci, n, dtype):
     return torch.randn(n, generator=g).to(dtype)
 
 
-def _expect(ci, n, dtype):
+def _expect(ci, n, dtype, world=WORLD):
     acc = torch.zeros(n, dtype=torch.float32)
-    for r in range(WORLD):
+    for r in range(world):
         acc = acc + _inp(r, ci, n, dtype).float()
     return acc.to(dtype)
+
+
+CASES4 = [  # 4 ranks: the auto choice (one-shot small, two-shot above 512 KiB) and forced two-shot
+    (8192, torch.bfloat16, 0),
+    (3 * 1024 * 1024, torch.bfloat16, 0),
+    (8192 * 256 + 8, torch.bfloat16, 2),
+    (1 << 20, torch.float32, 0),
+]
+
+
+def _worker4(rank, port, q, world=4):
+    """Four ranks on the one GPU: exact sums and the algorithm the Python routing picked."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from nv_genai_amd.parallel.custom_ar import CustomAllReduce
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = {"rank": rank}
+    try:
+        car = CustomAllReduce(None, capacity_mb=16, timeout_s=10.0)
+        res["self_test"] = car.enabled
+        bad = []
+        for ci, (n, dt, algo) in enumerate(CASES4):
+            x = _inp(rank, ci, n, dt).cuda()
+            out = car.all_reduce(x, out=torch.empty_like(x), algo=algo)
+            torch.cuda.synchronize()
+            if not torch.equal(out.cpu(), _expect(ci, n, dt, world)):
+                bad.append(ci)
+        res["bad"] = bad
+        res["algo_counts"] = dict(car.algo_counts)
+        res["error"] = car.error()
+    except Exception as e:  # noqa: BLE001
+        res["exc"] = repr(e)
+    q.put(res)
+    dist.destroy_process_group()
+
+
+def test_custom_all_reduce_four_ranks_two_shot_auto():
+    """W = 4 takes the two-shot path for messages above 512 KiB (choose_algo, resolved in
+    Python) and the sums stay bit-exact in rank order."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker4, args=(r, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert "exc" not in r, r
+        assert r["self_test"] and r["bad"] == [] and r["error"] == 0, r
+        # self-test: one-shot + two-shot + auto(1 MiB -> two-shot); cases: auto small -> one,
+        # auto 6 MiB -> two, forced two, auto 4 MiB fp32 -> two
+        assert r["algo_counts"] == {1: 2, 2: 5}, r["algo_counts"]
 
 
 def _worker(rank, port, q):
