@@ -292,18 +292,23 @@ void decode_attention(Tensor out, Tensor q, Tensor kc, Tensor vc, Tensor block_t
 void prefill_attention_worklist(Tensor out, Tensor q, Tensor kc, Tensor vc, Tensor block_tables,
                                 Tensor cu_q, Tensor ctx_lens, int64_t Hq, int64_t Hkv, double scale,
                                 bool causal, int64_t window, Tensor items, Tensor n_items, int64_t grid,
-                                int64_t ks) {
-  CHECK_BF16(out); CHECK_BF16(q); CHECK_BF16(kc); CHECK_BF16(vc);
+                                int64_t ks, int64_t impl, double k_scale, double v_scale) {
+  CHECK_BF16(out); CHECK_BF16(q);
   CHECK_CONTIG(kc); CHECK_CONTIG(vc);
+  TORCH_CHECK(impl == 1 || impl == 2, "prefill_attention_worklist: impl 1 (16x16) or 2 (32x32)");
   TORCH_CHECK(Hq % Hkv == 0, "prefill_attention_worklist: Hq % Hkv");
-  TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(2) == 64 && kc.size(3) == 128,
-              "prefill_attention_worklist: bf16 k cache [nb, Hkv, 64, 128]");
-  TORCH_CHECK(vc.sizes() == at::IntArrayRef({kc.size(0), Hkv, 128, 64}), "v cache must be [nb, Hkv, 128, 64]");
-  TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1 && q.size(1) >= Hq * 128 && q.stride(0) % 8 == 0);
-  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) >= Hq * 128 && out.size(0) == q.size(0));
+  const bool fp8 = kv_is_fp8(kc, vc);
+  TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(2) == 64, "k cache must be [nb, Hkv, 64, D]");
+  const int64_t D = kc.size(3);
+  TORCH_CHECK(impl == 2 ? (D == 128 && !fp8) : (D == 64 || D == 128 || D == 256),
+              "prefill_attention_worklist: the 32x32 kernel takes bf16 head_dim 128 pages, the 16x16 one "
+              "head_dim 64 / 128 / 256");
+  TORCH_CHECK(vc.sizes() == at::IntArrayRef({kc.size(0), Hkv, D, 64}), "v cache must be [nb, Hkv, D, 64]");
+  TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1 && q.size(1) >= Hq * D && q.stride(0) % 8 == 0);
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) >= Hq * D && out.size(0) == q.size(0));
   CHECK_DEV(block_tables); CHECK_DT(block_tables, at::kInt); CHECK_CONTIG(block_tables);
-  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(1) <= 1024,
-              "prefill_attention_worklist: at most 1024 pages per sequence");
+  TORCH_CHECK(block_tables.dim() == 2 && (impl == 1 || block_tables.size(1) <= 1024),
+              "prefill_attention_worklist: at most 1024 pages per sequence (32x32 kernel)");
   CHECK_DEV(cu_q); CHECK_DT(cu_q, at::kInt); CHECK_CONTIG(cu_q);
   CHECK_DEV(ctx_lens); CHECK_DT(ctx_lens, at::kInt); CHECK_CONTIG(ctx_lens);
   TORCH_CHECK(cu_q.numel() == ctx_lens.numel() + 1 && block_tables.size(0) >= ctx_lens.numel(),
@@ -324,15 +329,21 @@ void prefill_attention_worklist(Tensor out, Tensor q, Tensor kc, Tensor vc, Tens
   p.Hkv = (int)Hkv;
   p.scale = (float)scale;
   p.window = (int)window;
-  p.kc = bfp(kc);
-  p.vc = bfp(vc);
+  p.kc = static_cast<const uint16_t*>(kc.data_ptr());
+  p.vc = static_cast<const uint16_t*>(vc.data_ptr());
   p.block_tables = block_tables.data_ptr<int32_t>();
   p.max_blocks = (int)block_tables.size(1);
   p.ctx_lens = ctx_lens.data_ptr<int32_t>();
   p.v_scale = 1.f;
+  p.kv_fp8 = fp8 ? 1 : 0;
+  if (fp8) {
+    p.scale = (float)(scale * k_scale);
+    p.v_scale = (float)v_scale;
+  }
   p.items = items.data_ptr<int32_t>();
   p.n_items = n_items.data_ptr<int32_t>();
-  nga::launch_prefill_attention_v2_worklist(p, (int)grid, (int)ks, causal, cur_stream(q));
+  if (impl == 2) nga::launch_prefill_attention_v2_worklist(p, (int)grid, (int)ks, causal, cur_stream(q));
+  else nga::launch_prefill_attention_v1_worklist(p, (int)grid, (int)D, causal, cur_stream(q));
 }
 
 void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optional<Tensor> v,

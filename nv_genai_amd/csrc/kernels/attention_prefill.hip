@@ -37,7 +37,8 @@ __device__ __forceinline__ int row_swz(int row) {  // 4-bit key: distinct over a
 }  // namespace
 
 template <int D, bool PAGED, bool CAUSAL, int NCG>
-__global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
+__device__ __forceinline__ void v1_tile(const PrefillParams& P, uint16_t* k_s, uint16_t* v_s, int b, int hq,
+                                        int tile) {
   // NCG query column-groups (16 rows each) per wave: the K and V^T fragments read from LDS
   // for one key tile feed NCG MFMAs each, and the tile's staging + barriers are amortised
   // over a 64*NCG-row query tile.
@@ -49,23 +50,9 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
   constexpr int PER_T = K_CHUNKS / 256;  // chunks per thread per operand
   constexpr int QT = 64 * NCG;           // query rows per workgroup
 
-  __shared__ __attribute__((aligned(16))) uint16_t k_s[KT * D];
-  __shared__ __attribute__((aligned(16))) uint16_t v_s[D * KT];
-
-  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so physical block p
-  // runs on XCD p % 8. Logical work item L = (p % 8) * per_xcd + p / 8 gives every XCD one
-  // contiguous range of the (sequence, kv head, q head, tile) order: the G query heads that
-  // share a KV head — and every query tile of them — read their K/V pages through the same
-  // 4 MB L2. Within a (sequence, head) the longest causal tiles go first.
   // K-row swizzle: XOR the 16-B chunk index with up to 4 bits of the row (fewer for short
   // rows: the XOR value must stay below the chunk count)
   constexpr int SWS = NCH_K >= 16 ? 0 : NCH_K == 8 ? 1 : 2;
-  const int pblk = blockIdx.x;
-  const int L = (pblk & 7) * P.per_xcd + (pblk >> 3);
-  if (L >= P.total) return;
-  const int tile = P.ntiles - 1 - L % P.ntiles;
-  const int hq = (L / P.ntiles) % P.Hq;
-  const int b = L / (P.ntiles * P.Hq);
   const int q0 = P.cu_q[b], qlen = P.cu_q[b + 1] - q0;
   if (tile * QT >= qlen) return;
   const int ctx = PAGED ? P.ctx_lens[b] : qlen;
@@ -302,6 +289,50 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
         *reinterpret_cast<u16x4*>(op + 16 * dt + 4 * h) = v;
       }
     }
+  }
+}
+
+// Grid modes (as attention_prefill_v2.hip): enumerated — workgroups dealt round-robin over
+// the 8 XCDs, physical block p runs on XCD p % 8 and logical item L = (p % 8) * per_xcd + p / 8
+// gives every XCD one contiguous range of the (sequence, kv head, q head, tile) order (the G
+// query heads sharing a KV head read its pages through the same L2; longest causal tiles
+// first) — or a host-planned work list of (sequence, 64-row tile) pairs walked by a fixed
+// grid with q head it % Hq (graph-captured steps with fp8 KV pages or head_dim != 128).
+template <int D, bool PAGED, bool CAUSAL, int NCG>
+__global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams P) {
+  constexpr int KT = 64;
+  __shared__ __attribute__((aligned(16))) uint16_t k_s[KT * D];
+  __shared__ __attribute__((aligned(16))) uint16_t v_s[D * KT];
+  if (P.items) {
+    const int total = *P.n_items * P.Hq;
+    for (int it = blockIdx.x; it < total; it += gridDim.x) {
+      __syncthreads();
+      const int k = it / P.Hq;
+      v1_tile<D, PAGED, CAUSAL, NCG>(P, k_s, v_s, P.items[2 * k], it % P.Hq, P.items[2 * k + 1]);
+    }
+    return;
+  }
+  const int pblk = blockIdx.x;
+  const int L = (pblk & 7) * P.per_xcd + (pblk >> 3);
+  if (L >= P.total) return;
+  const int tile = P.ntiles - 1 - L % P.ntiles;
+  const int hq = (L / P.ntiles) % P.Hq;
+  const int b = L / (P.ntiles * P.Hq);
+  v1_tile<D, PAGED, CAUSAL, NCG>(P, k_s, v_s, b, hq, tile);
+}
+
+void launch_prefill_attention_v1_worklist(const PrefillParams& p, int grid, int D, bool causal,
+                                          hipStream_t stream) {
+  dim3 g(grid);
+  if (D == 256) {
+    if (causal) prefill_attn_kernel<256, true, true, 1><<<g, 256, 0, stream>>>(p);
+    else prefill_attn_kernel<256, true, false, 1><<<g, 256, 0, stream>>>(p);
+  } else if (D == 128) {
+    if (causal) prefill_attn_kernel<128, true, true, 1><<<g, 256, 0, stream>>>(p);
+    else prefill_attn_kernel<128, true, false, 1><<<g, 256, 0, stream>>>(p);
+  } else {
+    if (causal) prefill_attn_kernel<64, true, true, 1><<<g, 256, 0, stream>>>(p);
+    else prefill_attn_kernel<64, true, false, 1><<<g, 256, 0, stream>>>(p);
   }
 }
 

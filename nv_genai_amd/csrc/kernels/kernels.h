@@ -80,6 +80,10 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
 // groups (1 or 2). Rows per row block: 32 * 4 / hpw with hpw = 4, 2, 1 for Hq/Hkv % 4, % 2, else.
 void launch_prefill_attention_v2_worklist(const PrefillParams& p, int grid, int ks, bool causal,
                                           hipStream_t stream);
+// work-list launch of the 16x16 kernel (paged, head_dim 64 / 128 / 256, bf16 or fp8 pages):
+// items are (sequence, 64-row tile) pairs, q head = item index % Hq
+void launch_prefill_attention_v1_worklist(const PrefillParams& p, int grid, int D, bool causal,
+                                          hipStream_t stream);
 
 // sampling.hip
 void launch_sample(float* logits, int B, int V, const float* temperature, const int32_t* top_k,

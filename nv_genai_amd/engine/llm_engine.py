@@ -275,7 +275,7 @@ class LLMEngine:
             mx = cfg.max_graph_tokens or (cfg.mixed_prefill_tokens + cfg.max_num_seqs)
             self._mg_max_tokens = min(-(-mx // step) * step, T // step * step)
             self._nd_buckets = sorted({b for b in (8, 16, 32, 64, 128, 256, 512) if b < S} | {S})
-            cap = self._mg_max_tokens // 32 + S + 16
+            cap = self._mg_max_tokens // 32 + S + 16     # >= row blocks of any step in a bucket
             self.h_ctxd, self.d_ctxd = hbuf(S), dbuf(S)
             self.h_sidx, self.d_sidx = hbuf(S, dtype=torch.int64), dbuf(S, dtype=torch.int64)
             self.h_items, self.d_items = hbuf(cap, 2), dbuf(cap, 2)
@@ -1048,14 +1048,16 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ prefill / mixed step graphs
     def _mixed_graphs_eligible(self) -> bool:
-        """Graph-captured prefill / mixed steps need the work-list prefill kernel (head_dim
-        128, bf16 KV pages, <= 1024 pages per sequence), one pipeline stage and the plain
-        stacked forward (no sequence-parallel prefill, no split mixed steps, no MoE)."""
+        """Graph-captured prefill / mixed steps need a work-list prefill kernel (the 32x32
+        one for bf16 head_dim-128 pages with <= 1024 pages per sequence, else the 16x16 one
+        for head_dim 64 / 128 / 256 and fp8 pages), one pipeline stage and the plain stacked
+        forward (no sequence-parallel prefill, no split mixed steps, no MoE)."""
         c, m = self.cfg, self.model
         if not c.mixed_graphs or not (self.gpu and c.use_graphs or c.graph_eager):
             return False
-        return (self.p.pp_size == 1 and not c.sequence_parallel and not m.split_mixed and m.D == 128
-                and m.kv_dtype == "auto" and not self.mcfg.is_moe and self.max_blocks <= 1024)
+        self._pf_impl = 2 if (m.D == 128 and m.kv_dtype == "auto" and self.max_blocks <= 1024) else 1
+        return (self.p.pp_size == 1 and not c.sequence_parallel and not m.split_mixed and m.D in (64, 128, 256)
+                and not self.mcfg.is_moe)
 
     def _graph_key(self, n: int, ntok: int, nd: int):
         """(token bucket, decode-row bucket) of a prefill / mixed step, or None (eager)."""
@@ -1070,17 +1072,19 @@ class LLMEngine:
 
     def _graph_meta(self, key) -> AttnMeta:
         tb, ndb = key
-        rw = ops.prefill_rows_per_block(self.model.hq, self.model.hkv)
+        impl = self._pf_impl
+        rw = ops.worklist_rows(impl, self.model.hq, self.model.hkv)
         G = self.model.hq // self.model.hkv
         hpw = 4 if G % 4 == 0 else 2 if G % 2 == 0 else 1
         ng = self.model.hkv * (G // hpw)
         # few row blocks (one short prompt): the 8-wave split-key form, one workgroup per CU
-        ks = 2 if (tb - ndb) // rw * ng <= 320 else 1
+        ks = 2 if impl == 2 and (tb - ndb) // rw * ng <= 320 else 1
         S = self.cfg.max_num_seqs
         return AttnMeta(kind="graph", slots=self.d_slots[:tb], cu_q=self.d_cu[: S + 1], ctx_lens=self.d_ctx[:S],
                         block_tables=self.d_bt[:S], max_q_len=0, max_ctx=self.cfg.max_model_len,
                         decode_ws=self.decode_ws, n_decode=ndb, decode_ctx=self.d_ctxd[:max(ndb, 1)],
-                        items=self.d_items, n_items=self.d_nitems, pf_grid=256 if ks == 2 else 512, pf_ks=ks)
+                        items=self.d_items, n_items=self.d_nitems, pf_grid=256 if ks == 2 else 512, pf_ks=ks,
+                        pf_impl=impl)
 
     def _graph_body(self, key) -> None:
         """One prefill / mixed step over the bucket: forward of tb token rows, logits of the
@@ -1143,7 +1147,8 @@ class LLMEngine:
         self.h_ctxd[:nd] = self.h_ctx[:nd]
         self.h_ctxd[nd:max(ndb, nd)] = 0
         items = ops.plan_prefill_items(cu, ctx, nd, n, self.model.hq, self.model.hkv, self.model.window,
-                                       out=self.h_items.numpy())
+                                       out=self.h_items.numpy(),
+                                       rw=ops.worklist_rows(self._pf_impl, self.model.hq, self.model.hkv))
         self.h_nitems[0] = len(items)
         sidx = self.h_sidx.numpy()
         sidx[:n] = cu[1:n + 1] - 1

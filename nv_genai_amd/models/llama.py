@@ -69,6 +69,7 @@ class AttnMeta:
     n_items: Optional[torch.Tensor] = None
     pf_grid: int = 512
     pf_ks: int = 1
+    pf_impl: int = 2    # 2: 32x32 kernel (bf16 head_dim-128 pages), 1: 16x16 kernel
 
 
 class LlamaModel:
@@ -523,7 +524,8 @@ class LlamaModel:
         with (torch.cuda.stream(side) if gpu else contextlib.nullcontext()):
             ops.prefill_attention_worklist(q, self.k_cache[li], self.v_cache[li], meta.block_tables, meta.cu_q,
                                            meta.ctx_lens, hq, hkv, self.scale, meta.items, meta.n_items,
-                                           grid=meta.pf_grid, ks=meta.pf_ks, out=attn, window=W)
+                                           grid=meta.pf_grid, ks=meta.pf_ks, out=attn, window=W,
+                                           impl=meta.pf_impl, kv_scales=self.kv_scales)
         nd = meta.n_decode
         if nd:
             ops.decode_attention(q[:nd], self.k_cache[li], self.v_cache[li], meta.block_tables[:nd],

@@ -241,15 +241,16 @@ def prefill_rows_per_block(Hq: int, Hkv: int) -> int:
 
 
 def plan_prefill_items(cu, ctx, first: int, n: int, Hq: int, Hkv: int, window: int = 0,
-                       out: Optional["np.ndarray"] = None):
+                       out: Optional["np.ndarray"] = None, rw: Optional[int] = None):
     """Host work list of the work-list prefill kernel for sequences [first, n) of a step
     (numpy ``cu`` [n+1] token offsets, ``ctx`` [n] context lengths): one (sequence, row
     block) pair per row block, longest causal key range first (so the fixed grid's
     workgroups take the long blocks first). Returns an int32 [k, 2] array (written into
-    ``out`` when given)."""
+    ``out`` when given). ``rw``: rows per block (default: the 32x32 kernel's; 64 for the
+    16x16 kernel's tiles)."""
     import numpy as np
 
-    rw = prefill_rows_per_block(Hq, Hkv)
+    rw = rw or prefill_rows_per_block(Hq, Hkv)
     cu = np.asarray(cu[first: n + 1], dtype=np.int64)
     ql = cu[1:] - cu[:-1]
     cx = np.asarray(ctx[first:n], dtype=np.int64)
@@ -269,23 +270,34 @@ def plan_prefill_items(cu, ctx, first: int, n: int, Hq: int, Hkv: int, window: i
     return res
 
 
+def worklist_rows(impl: int, Hq: int, Hkv: int) -> int:
+    """Query rows per work item: the 32x32 kernel's row block (impl 2) or the 16x16
+    kernel's 64-row tile (impl 1)."""
+    return prefill_rows_per_block(Hq, Hkv) if impl == 2 else 64
+
+
 def prefill_attention_worklist(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, scale,
                                items, n_items, grid: int = 512, ks: int = 1, out=None,
-                               causal: bool = True, window: int = 0):
-    """Paged prefill attention driven by a device work list (``plan_prefill_items``): rows
-    are absolute token rows of the step, ``items`` [>=n, 2] int32 and ``n_items`` a
-    1-element int32 tensor on the device. The launch shape (``grid`` workgroups x ``ks``
-    wave groups) is fixed, so one hipGraph capture serves every step's list. Rows no item
-    covers are left untouched."""
+                               causal: bool = True, window: int = 0, impl: int = 2,
+                               kv_scales=(1.0, 1.0)):
+    """Paged prefill attention driven by a device work list (``plan_prefill_items`` with
+    ``rw = worklist_rows(impl, ...)``): rows are absolute token rows of the step, ``items``
+    [>=n, 2] int32 and ``n_items`` a 1-element int32 tensor on the device. The launch shape
+    (``grid`` workgroups x ``ks`` wave groups) is fixed, so one hipGraph capture serves
+    every step's list. Rows no item covers are left untouched. ``impl`` 2: the 32x32 kernel
+    (bf16 head_dim-128 pages), 1: the 16x16 kernel (head_dim 64 / 128 / 256, bf16 or fp8
+    pages with ``kv_scales``)."""
+    D = kc.shape[3]
     if not _gpu(q):
         return ref.prefill_attention_worklist(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, scale,
                                               items, n_items, out, causal, window,
-                                              prefill_rows_per_block(Hq, Hkv))
+                                              worklist_rows(impl, Hq, Hkv), D, kv_scales)
     if out is None:
-        out = torch.zeros(q.shape[0], Hq * 128, dtype=q.dtype, device=q.device)
+        out = torch.zeros(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
     kernels().prefill_attention_worklist(out, q, kc, vc, block_tables, cu_q, ctx_lens, int(Hq), int(Hkv),
                                          float(scale), bool(causal), int(window), items, n_items,
-                                         int(grid), int(ks))
+                                         int(grid), int(ks), int(impl), float(kv_scales[0]),
+                                         float(kv_scales[1]))
     return out
 
 

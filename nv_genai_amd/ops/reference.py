@@ -178,7 +178,7 @@ def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
 
 
 def prefill_attention_worklist(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, scale, items, n_items,
-                               out=None, causal=True, window=0, rw=128, D=128):
+                               out=None, causal=True, window=0, rw=128, D=128, kv_scales=(1.0, 1.0)):
     """The work-list kernel's semantics: every listed (sequence, row block) pair writes its
     RW query rows (absolute token rows cu_q[b] + RW qb ...) of every head; other rows of
     ``out`` are left as they are."""
@@ -199,7 +199,7 @@ def prefill_attention_worklist(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv,
         if window > 0:
             mask = mask & (kpos[None, :] > qpos[:, None] - window)
         for hq in range(Hq):
-            k, v = _gather_kv(kc, vc, block_tables[b], ctx, hq // G)
+            k, v = _gather_kv(kc, vc, block_tables[b], ctx, hq // G, kv_scales)
             qs = q[s0 + r0:s0 + r1, hq * D:(hq + 1) * D].float()
             sc = ((qs @ k.T) * scale).masked_fill(~mask, float("-inf"))
             out[s0 + r0:s0 + r1, hq * D:(hq + 1) * D] = (torch.softmax(sc, -1) @ v).to(out.dtype)

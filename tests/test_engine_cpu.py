@@ -256,8 +256,8 @@ def test_prefill_worklist_plan_covers_every_row_once():
     assert tiles == sorted(tiles, reverse=True)
 
 
-@pytest.mark.parametrize("async_", [True, False])
-def test_graph_step_layout_matches_eager(async_):
+@pytest.mark.parametrize("async_,head_dim", [(True, 128), (False, 128), (True, 64)])
+def test_graph_step_layout_matches_eager(async_, head_dim):
     """The graph-captured prefill / mixed step body (engine mixed_graphs, run without capture
     on CPU: graph_eager) — token rows padded to the bucket, decode rows past the step's own
     skipped, prefill attention from the host work list over absolute rows, S sampling rows —
@@ -266,7 +266,7 @@ def test_graph_step_layout_matches_eager(async_):
     from nv_genai_amd.models.llama import LlamaModel
     from nv_genai_amd.parallel.dist import ParallelContext
 
-    cfg = llama_config("llama-tiny", head_dim=128)        # the work-list kernel's head_dim
+    cfg = llama_config("llama-tiny", head_dim=head_dim)   # 128: 32x32 work-list kernel, 64: 16x16
     m = LlamaModel(cfg, "cpu", dtype=torch.float32, pctx=ParallelContext(), seed=5)
     prompts = [[3, 4, 5, 6] * 25, [7, 8] * 40, [9] * 5, [11, 12, 13] * 30, [2] * 70]
     p = SamplingParams(temperature=0.0, max_tokens=7, ignore_eos=True, logprobs=True)
@@ -277,6 +277,8 @@ def test_graph_step_layout_matches_eager(async_):
                                    async_decode=async_, mixed_graphs=graphs, graph_eager=graphs,
                                    graph_token_step=32), device="cpu", model=m, model_cfg=cfg)
         assert e._mg_ok == graphs
+        if graphs:
+            assert e._pf_impl == (2 if head_dim == 128 else 1)
         calls = []
         if graphs:
             orig = e._graph_step

@@ -537,9 +537,11 @@ def test_fp8_linear_matches_dequantised_matmul(gpu):
     assert float((y.float() - exact).norm() / exact.norm()) < 0.06
 
 
-@pytest.mark.parametrize("Hkv,G,window,ks,grid", [(8, 4, 0, 1, 512), (8, 4, 0, 2, 7), (2, 8, 0, 1, 13),
-                                                  (4, 1, 0, 2, 64), (2, 4, 200, 1, 512)])
-def test_prefill_attention_worklist(gpu, Hkv, G, window, ks, grid):
+@pytest.mark.parametrize("Hkv,G,window,ks,grid,impl", [(8, 4, 0, 1, 512, 2), (8, 4, 0, 2, 7, 2),
+                                                       (2, 8, 0, 1, 13, 2), (4, 1, 0, 2, 64, 2),
+                                                       (2, 4, 200, 1, 512, 2), (8, 4, 0, 1, 512, 1),
+                                                       (2, 4, 200, 1, 9, 1)])
+def test_prefill_attention_worklist(gpu, Hkv, G, window, ks, grid, impl):
     """Work-list mode of the 32x32 prefill kernel (the engine's mixed-step graphs): a step
     whose first rows are decode rows (left untouched) and whose prefill sequences are covered
     by the host-planned (sequence, row block) list, with a fixed grid smaller than the list
@@ -559,17 +561,47 @@ def test_prefill_attention_worklist(gpu, Hkv, G, window, ks, grid):
     scale = 1 / math.sqrt(D)
     import numpy as np
 
-    items = ops.plan_prefill_items(np.array(cu), np.array(ctxs), nd, len(ctxs), Hq, Hkv, window)
+    items = ops.plan_prefill_items(np.array(cu), np.array(ctxs), nd, len(ctxs), Hq, Hkv, window,
+                                   rw=ops.worklist_rows(impl, Hq, Hkv))
     it_d = torch.zeros(len(items) + 9, 2, dtype=torch.int32, device=gpu)   # capacity > count
     it_d[: len(items)] = torch.from_numpy(items).to(gpu)
     n_d = torch.tensor([len(items)], dtype=torch.int32, device=gpu)
     out = torch.full((cu[-1], Hq * D), 7.0, dtype=torch.bfloat16, device=gpu)
     ops.prefill_attention_worklist(q, kc, vc, bt, cu_t, ctx_t, Hq, Hkv, scale, it_d, n_d, grid=grid, ks=ks,
-                                   out=out, window=window)
+                                   out=out, window=window, impl=impl)
     o_ref = ref.prefill_attention_paged(q[nd:].float(), kc, vc, bt[nd:], cu_t[nd:] - nd, ctx_t[nd:], Hq, Hkv, D,
                                         scale, True, window)
     _close_rows(out[nd:], o_ref, width=D)
     assert bool((out[:nd] == 7.0).all())     # decode rows untouched
+
+
+def test_prefill_attention_worklist_fp8_and_d256(gpu):
+    """The 16x16 kernel's work-list mode over fp8 e4m3fn pages (scales) and head_dim 256."""
+    import numpy as np
+
+    for D, fp8 in ((128, True), (256, False)):
+        Hkv, G = 2, 4
+        Hq = Hkv * G
+        ctxs, qls = [9, 700, 130], [1, 300, 130]
+        kc, vc, bt = _paged_setup(ctxs, Hkv, D, gpu, seed=23)
+        scales = (2.0, 0.5) if fp8 else (1.0, 1.0)
+        if fp8:
+            kc, vc = (kc.float() / scales[0]).to(torch.float8_e4m3fn), (vc.float() / scales[1]).to(torch.float8_e4m3fn)
+        cu = [0]
+        for ql in qls:
+            cu.append(cu[-1] + ql)
+        q = _bf(cu[-1], Hq * D, dev=gpu)
+        cu_t = torch.tensor(cu, dtype=torch.int32, device=gpu)
+        ctx_t = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
+        items = ops.plan_prefill_items(np.array(cu), np.array(ctxs), 1, 3, Hq, Hkv, rw=64)
+        it_d = torch.from_numpy(items).to(gpu)
+        n_d = torch.tensor([len(items)], dtype=torch.int32, device=gpu)
+        out = torch.zeros(cu[-1], Hq * D, dtype=torch.bfloat16, device=gpu)
+        ops.prefill_attention_worklist(q, kc, vc, bt, cu_t, ctx_t, Hq, Hkv, D ** -0.5, it_d, n_d, grid=33,
+                                       out=out, impl=1, kv_scales=scales)
+        o_ref = ref.prefill_attention_paged(q[1:].float().cpu(), kc.cpu(), vc.cpu(), bt[1:].cpu(), cu_t[1:].cpu() - 1,
+                                            ctx_t[1:].cpu(), Hq, Hkv, D, D ** -0.5, kv_scales=scales)
+        _close_rows(out[1:], o_ref, width=D, rel=2e-2 if fp8 else 1e-2, peak=3e-2)
 
 
 def test_decode_attention_skip_empty_rows(gpu):
