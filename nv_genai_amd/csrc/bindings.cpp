@@ -432,6 +432,17 @@ void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p,
                      out_logprob.data_ptr<float>(), cur_stream(logits));
 }
 
+// ------------------------------------------------------------------ embedding gather
+void embedding(Tensor out, Tensor table, Tensor ids, int64_t vocab_lo, double scale) {
+  CHECK_BF16(out); CHECK_BF16(table); CHECK_CONTIG(out); CHECK_CONTIG(table);
+  CHECK_DEV(ids); CHECK_DT(ids, at::kInt); CHECK_CONTIG(ids);
+  TORCH_CHECK(table.dim() == 2 && table.size(1) % 8 == 0, "embedding: table [rows, H], H % 8 == 0");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == ids.numel() && out.size(1) == table.size(1),
+              "embedding: out [T, H] for T ids");
+  nga::launch_embedding(bfp(out), bfp(table), ids.data_ptr<int32_t>(), (int)ids.numel(), (int)table.size(1),
+                        vocab_lo, table.size(0), (float)scale, cur_stream(ids));
+}
+
 // ------------------------------------------------------------------ vector search
 void score(Tensor Q, Tensor X, c10::optional<Tensor> row_bias, Tensor S, double dot_scale) {
   CHECK_BF16(Q); CHECK_BF16(X); CHECK_CONTIG(Q); CHECK_CONTIG(X);
@@ -715,6 +726,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_gemm", checked("moe_gemm", &moe_gemm));
   m.def("moe_combine", checked("moe_combine", &moe_combine));
   m.def("sample", checked("sample", &sample));
+  m.def("embedding", checked("embedding", &embedding));
   m.def("score", checked("score", &score));
   m.def("topk", checked("topk", &topk));
   m.def("score_topk", checked("score_topk", &score_topk));

@@ -107,6 +107,11 @@ void launch_ivf_plan(const int64_t* probes, int nq, int nprobe, int nlist, int32
 void launch_topk(const float* in, const int64_t* in_idx, int64_t rows, int64_t row_len,
                  int64_t seg_len, int k, float* out_v, int64_t* out_i, hipStream_t stream);
 
+// embedding.hip: rows of this rank's vocabulary shard [vocab_lo, vocab_lo + rows), zeros
+// for ids outside it; H % 8 == 0
+void launch_embedding(uint16_t* out, const uint16_t* table, const int32_t* ids, int T, int H, int64_t vocab_lo,
+                      int64_t rows, float scale, hipStream_t stream);
+
 // pool.hip
 void launch_pool_l2norm(const uint16_t* hidden, const int32_t* cu, int B, int H, int mode,
                         int normalize, float* out, hipStream_t stream);

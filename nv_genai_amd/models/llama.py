@@ -39,6 +39,7 @@ from typing import Dict, List, Optional
 import torch
 
 from .. import ops
+from ..ops import reference as ref
 from ..parallel.comm import custom_all_reduce_for
 from ..parallel.dist import (ParallelContext, get_context, tp_all_gather, tp_all_gather_rows,
                              tp_all_reduce, tp_reduce_scatter_rows)
@@ -409,18 +410,16 @@ class LlamaModel:
 
     # ------------------------------------------------------------------ forward
     def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
-        if self.p.tp_size == 1:
-            h = torch.nn.functional.embedding(ids.long(), self.embed)
-        else:
-            lo = self.p.tp_rank * self.vocab_local
-            local = ids.long() - lo
-            ok = (local >= 0) & (local < self.vocab_local)
-            h = torch.nn.functional.embedding(local.clamp(0, self.vocab_local - 1), self.embed)
-            h = h * ok.unsqueeze(-1).to(h.dtype)
+        """Vocab-parallel embedding (K8, CC3): each rank gathers the rows of its vocabulary
+        shard (zeros elsewhere) and the TP all-reduce sums them. Gemma's embedding scale is
+        a bf16 constant (HF multiplies by it in the model dtype); the gather applies it."""
+        lo = self.p.tp_rank * self.vocab_local if self.p.tp_size > 1 else 0
+        if self.embed.dtype == torch.bfloat16 or not ids.is_cuda:
+            h = ops.embedding(ids, self.embed, lo, self.cfg.embed_scale)
+        else:   # fp32 tables (CPU-reference models moved to the GPU)
+            h = ref.embedding(ids, self.embed, lo, self.cfg.embed_scale)
+        if self.p.tp_size > 1:
             h = tp_all_reduce(h, self.p)
-        if self.cfg.embed_scale != 1.0:
-            # Gemma: the scale is a bf16 constant (HF multiplies by it in the model dtype)
-            h = h * torch.tensor(self.cfg.embed_scale, dtype=h.dtype)
         return h
 
     # norms: RMSNorm (Llama/Mistral/Mixtral/Gemma) or LayerNorm with bias (StarCoder2)

@@ -564,6 +564,18 @@ def ivf_search_topk(Q: torch.Tensor, X: torch.Tensor, row_bias, dot_scale: float
     return v, r
 
 
+def embedding(ids: torch.Tensor, table: torch.Tensor, vocab_lo: int = 0, scale: float = 1.0, out=None):
+    """Token rows of ``table`` (this rank's vocabulary shard starting at ``vocab_lo``; ids
+    outside it give zero rows), times ``scale`` in bf16 (K8). GPU: the embedding.hip gather."""
+    if not _gpu(table):
+        return ref.embedding(ids, table, vocab_lo, scale)
+    ids = ids.to(torch.int32).contiguous()
+    if out is None:
+        out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=table.device)
+    kernels().embedding(out, table, ids, int(vocab_lo), float(scale))
+    return out
+
+
 def pool_l2norm(hidden, cu, mode: int = 0, normalize: bool = True, out=None):
     if not _gpu(hidden):
         return ref.pool_l2norm(hidden, cu, mode, normalize)

@@ -356,6 +356,16 @@ def ivf_search_topk(Q, X, row_bias, dot_scale, probes, list_beg, list_end, k):
     return vals, rows
 
 
+def embedding(ids, table, vocab_lo=0, scale=1.0):
+    local = ids.long() - vocab_lo
+    ok = (local >= 0) & (local < table.shape[0])
+    h = torch.nn.functional.embedding(local.clamp(0, table.shape[0] - 1), table)
+    h = h * ok.unsqueeze(-1).to(h.dtype)
+    if scale != 1.0:
+        h = h * torch.tensor(scale, dtype=h.dtype)
+    return h
+
+
 def pool_l2norm(hidden, cu, mode: int, normalize: bool):
     B = cu.numel() - 1
     out = torch.zeros(B, hidden.shape[1], dtype=torch.float32, device=hidden.device)

@@ -620,3 +620,14 @@ def test_decode_attention_skip_empty_rows(gpu):
         assert bool((out[1] == 3.0).all()) and bool((out[3] == 3.0).all())
         o_ref = ref.decode_attention(q.float(), kc, vc, bt, ctx, Hq, Hkv, 1 / math.sqrt(D))
         _close_rows(out[[0, 2]], o_ref[[0, 2]], width=D)
+
+
+def test_embedding_gather(gpu):
+    """embedding.hip: rows of the local vocabulary shard, zeros outside it, bf16 scale."""
+    torch.manual_seed(12)
+    table = _bf(1000, 4096, dev=gpu)
+    ids = torch.tensor([0, 999, 5, 1000, 1500, 2999, 2000, 7], dtype=torch.int32, device=gpu)
+    for lo, scale in ((0, 1.0), (1000, 1.0), (2000, 64.0)):
+        got = ops.embedding(ids, table, lo, scale)
+        want = ref.embedding(ids.cpu(), table.cpu(), lo, scale)
+        assert torch.equal(got.cpu(), want)
