@@ -20,6 +20,8 @@
 // when seqs*kv_heads is too small to fill 256 CUs) combine in a second small kernel. A
 // sequence's pages are divided evenly over the partitions at run time (pages_per_part only
 // sizes the grid), so the split adapts to each sequence's real context length.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -47,7 +49,7 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     const int32_t* __restrict__ block_tables, int max_blocks,
     const int32_t* __restrict__ ctx_lens, int Hq, int Hkv, float scale, int pages_per_part,
     float* __restrict__ part_ml, float* __restrict__ part_o, int window, float v_scale, int skip_empty,
-    int* __restrict__ tickets) {
+    int* __restrict__ tickets, int nt_loads) {
   // fp8 pages at head_dim 128: 16-byte loads (half as many load instructions as 8-byte ones).
   // Each lane's 16 K bytes cover two d-steps (Q is loaded with the same d order, the dot
   // product does not care) and its 16 Vt bytes cover 16 consecutive keys of both key
@@ -190,7 +192,8 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
           for (int s = 0; s < DS; ++s) {
             const CT* src = kp + key * D + 32 * s + 8 * h;
             if constexpr (F8) kw[ti][s] = *reinterpret_cast<const uint2*>(src);
-            else kf[ti][s] = load8(src);
+            else kf[ti][s] = nt_loads ? __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(src))
+                                      : load8(src);
           }
         }
 #pragma unroll
@@ -200,7 +203,8 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
           for (int dt = 0; dt < DT; ++dt) {
             const CT* src = vp + (16 * dt + col) * BS + 32 * g + 8 * h;
             if constexpr (F8) vw[gi][dt] = *reinterpret_cast<const uint2*>(src);
-            else vf[gi][dt] = load8(src);
+            else vf[gi][dt] = nt_loads ? __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(src))
+                                       : load8(src);
           }
         }
       }
@@ -358,12 +362,17 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
   dim3 grid(num_seqs, Hkv, nparts);
   dim3 g2(num_seqs, Hq);
   if (!kv_fp8) k_scale = v_scale = 1.f;
+  // A/B knob: non-temporal KV loads (each page is streamed once per step)
+  static const int nt = [] {
+    const char* e = getenv("NGA_DECODE_NT");
+    return e && atoi(e) ? 1 : 0;
+  }();
   const float sc = scale * k_scale;
 #define NGA_DEC(DD, CT)                                                                        \
   decode_attn_kernel<DD, CT><<<grid, 256, 0, stream>>>(                                        \
       out, out_stride, q, q_stride, static_cast<const CT*>(kc), static_cast<const CT*>(vc),   \
       block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, pages_per_part, part_ml, part_o, window, \
-      v_scale, skip_empty ? 1 : 0, tickets)
+      v_scale, skip_empty ? 1 : 0, tickets, nt)
   if (D == 256) {
     if (kv_fp8) NGA_DEC(256, uint8_t); else NGA_DEC(256, uint16_t);
     if (nparts > 1 && !tickets)

@@ -11,5 +11,6 @@ timeout -k 10 300 python -u -m pytest tests/test_custom_ar_gpu.py -x -v --timeou
 timeout -k 10 200 python benchmarks/kernel_bench.py --only bw > "$OUT/kb_bw.json" 2> "$OUT/kb_bw.err" &&
 timeout -k 10 300 python benchmarks/kernel_bench.py --only prefill > "$OUT/kb_prefill.json" 2> "$OUT/kb_prefill.err" &&
 timeout -k 10 300 python benchmarks/kernel_bench.py --only decode > "$OUT/kb_decode.json" 2> "$OUT/kb_decode.err" &&
+NGA_DECODE_NT=1 timeout -k 10 300 python benchmarks/kernel_bench.py --only decode > "$OUT/kb_decode_nt.json" 2> "$OUT/kb_decode_nt.err" &&
 timeout -k 10 300 python benchmarks/kernel_bench.py --only search > "$OUT/kb_search.json" 2> "$OUT/kb_search.err" &&
 timeout -k 10 500 python bench.py --steps 5 --warmup 2 > "$OUT/bench.json" 2> "$OUT/bench.err"
