@@ -89,10 +89,15 @@ class LlamaModel:
         # divides; otherwise every expert's FFN is sharded like a dense MLP
         self.expert_parallel = cfg.is_moe and tp > 1 and cfg.num_experts % tp == 0
         ffn_tp = 1 if self.expert_parallel else tp
-        if cfg.heads % tp or cfg.kv_heads % tp or cfg.ffn % ffn_tp or cfg.vocab_size % tp:
+        # KV heads: split over the ranks, or — with more ranks than KV heads (Gemma-2B's one
+        # KV head at TP=2, Llama-3-70B at TP=16) — replicated: each group of tp / kv_heads
+        # ranks holds one KV head, exactly the one its query heads attend to
+        kv_ok = cfg.kv_heads % tp == 0 or tp % cfg.kv_heads == 0
+        if cfg.heads % tp or not kv_ok or cfg.ffn % ffn_tp or cfg.vocab_size % tp:
             raise ValueError(f"{cfg.name}: dims not divisible by tp={tp}")
         self.hq = cfg.heads // tp
-        self.hkv = cfg.kv_heads // tp
+        self.hkv = max(1, cfg.kv_heads // tp)
+        self.kv_replicas = max(1, tp // cfg.kv_heads)
         self.D = cfg.head_dim
         self.ffn = cfg.ffn // ffn_tp
         self.n_experts = (cfg.num_experts // tp if self.expert_parallel else cfg.num_experts)
@@ -241,6 +246,12 @@ class LlamaModel:
             c = t.shape[1] // tp
             return t[:, r * c:(r + 1) * c]
 
+        def kv_rows(t):  # K / V projection rows: this rank's KV heads (split or replicated)
+            if self.kv_replicas == 1:
+                return rows(t)
+            h = r // self.kv_replicas
+            return t[h * cfg.head_dim:(h + 1) * cfg.head_dim]
+
         def get(name):
             return w[name].to(dev, dt)
 
@@ -256,7 +267,7 @@ class LlamaModel:
             q, k, v = get(a + "q_proj.weight"), get(a + "k_proj.weight"), get(a + "v_proj.weight")
             L = {
                 "attn_norm": norm(p + "input_layernorm.weight"),
-                "wqkv": torch.cat([rows(q), rows(k), rows(v)]).contiguous(),
+                "wqkv": torch.cat([rows(q), kv_rows(k), kv_rows(v)]).contiguous(),
                 "wo": cols(get(a + "o_proj.weight")).contiguous(),
                 "mlp_norm": norm(p + "post_attention_layernorm.weight"),
             }
@@ -264,8 +275,8 @@ class LlamaModel:
                 L["attn_norm_b"] = get(p + "input_layernorm.bias")
                 L["mlp_norm_b"] = get(p + "post_attention_layernorm.bias")
             if cfg.attn_bias:
-                L["bqkv"] = torch.cat([rows(get(a + "q_proj.bias")), rows(get(a + "k_proj.bias")),
-                                       rows(get(a + "v_proj.bias"))]).contiguous()
+                L["bqkv"] = torch.cat([rows(get(a + "q_proj.bias")), kv_rows(get(a + "k_proj.bias")),
+                                       kv_rows(get(a + "v_proj.bias"))]).contiguous()
                 L["bo"] = get(a + "o_proj.bias")
             if cfg.is_moe:
                 L.update(self._load_experts(w, p, get, rows))

@@ -87,6 +87,7 @@ def test_sequence_parallel_tp_matches_single():
     ("mixtral-tiny", {"num_experts": 3}, False),       # 3 experts: each expert's FFN split
     ("starcoder2-tiny", None, True),                   # biases on rank 0, LayerNorm, window
     ("gemma-tiny", {"heads": 4, "kv_heads": 2}, False),
+    ("gemma-tiny", {"heads": 4, "kv_heads": 1}, False),   # one KV head, replicated on both ranks
 ])
 def test_tensor_parallel_families_match_single(model, over, sp):
     """Every decoder family at TP=2 generates the TP=1 tokens (Mixtral in both MoE sharding

@@ -103,6 +103,13 @@ def test_tp8_70b_head_ratio_matches_single():
     assert [(hq, hkv) for _, _, _, hq, hkv in gens] == [(8, 1)]
 
 
+def test_tp8_with_two_kv_heads_replicates_them():
+    """TP=8 over a model with 2 KV heads: each KV head lives on 4 ranks (those whose query
+    heads attend to it); tokens and log-probs still match one process."""
+    gens = _check(_run(8, 8, 1, {"heads": 8, "kv_heads": 2, "head_dim": 32}, 1))
+    assert [(hq, hkv) for _, _, _, hq, hkv in gens] == [(1, 1)]
+
+
 def test_tp4_matches_single():
     gens = _check(_run(4, 4, 1, TINY_8Q4KV, 1))
     assert [(hq, hkv) for _, _, _, hq, hkv in gens] == [(2, 1)]
