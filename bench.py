@@ -103,6 +103,8 @@ def parse(argv=None):
     ap.add_argument("--workload", choices=("rag", "agent"), default="rag",
                     help="agent: query-decomposition agent, one TP=N replica + N-way sharded index")
     ap.add_argument("--kv-cache-fraction", type=float, default=None)
+    ap.add_argument("--no-step-graphs", action="store_true",
+                    help="prefill / mixed steps eagerly (A/B of the step hipGraphs)")
     return ap.parse_args(argv)
 
 
@@ -268,7 +270,8 @@ def main(argv=None):
                         kv_cache_blocks=None if gpu else 512,
                         mixed_prefill_tokens=args.mixed_prefill_tokens,
                         mixed_min_tokens=args.mixed_min_tokens, mixed_max_wait=args.mixed_max_wait,
-                        fp8=args.fp8, kv_cache_dtype="fp8" if args.kv_fp8 else "auto")
+                        fp8=args.fp8, kv_cache_dtype="fp8" if args.kv_fp8 else "auto",
+                        mixed_graphs=not args.no_step_graphs)
     llm = LLMEngine(ecfg, device=dev, pctx=pctx)
     from nv_genai_amd.models.config import encoder_config
 
@@ -473,6 +476,10 @@ def main(argv=None):
         "world_size": world,
         "backend": pctx.backend,
         "per_replica_qps": [x for x in per_replica if x is not None],
+        "step_graphs": {"timed_graph_steps": llm.stats["graph_steps"],
+                        "captured_total": len(llm.mgraphs),
+                        "captured_in_timed_region": llm.stats["graph_captures"],
+                        "capture_s_in_timed_region": round(llm.stats["graph_capture_s"], 3)},
         "prefix_cache_hit_blocks": int(llm.sched.prefix_hits()),
         "distinct_docs_retrieved": len({d for r in results for d in r.doc_ids}),
     }

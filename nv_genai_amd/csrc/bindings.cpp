@@ -243,7 +243,7 @@ int64_t decode_pages_per_part(int64_t num_seqs, int64_t Hkv, int64_t max_ctx) {
 void decode_attention(Tensor out, Tensor q, Tensor kc, Tensor vc, Tensor block_tables,
                       Tensor ctx_lens, int64_t Hq, int64_t Hkv, int64_t max_ctx, double scale,
                       int64_t pages_per_part, Tensor part_ml, Tensor part_o, int64_t window,
-                      double k_scale, double v_scale, bool skip_empty, c10::optional<Tensor> tickets) {
+                      double k_scale, double v_scale, bool skip_empty) {
   CHECK_BF16(out); CHECK_BF16(q);
   const bool fp8 = kv_is_fp8(kc, vc);
   CHECK_CONTIG(kc); CHECK_CONTIG(vc);
@@ -265,16 +265,10 @@ void decode_attention(Tensor out, Tensor q, Tensor kc, Tensor vc, Tensor block_t
   TORCH_CHECK(pages_per_part >= 1);
   const int64_t pages = (max_ctx + 63) / 64;
   const int64_t nparts = (pages + pages_per_part - 1) / pages_per_part;
-  int* tk = nullptr;
   if (nparts > 1) {
     CHECK_DEV(part_ml); CHECK_DEV(part_o);
     TORCH_CHECK(part_ml.numel() >= B * Hq * nparts * 2 && part_o.numel() >= B * Hq * nparts * D,
                 "decode_attention: partition workspace too small");
-    if (tickets.has_value()) {   // zero-initialised [>= B * Hkv] int32, kept zero by the kernel
-      CHECK_DEV(*tickets); CHECK_DT(*tickets, at::kInt); CHECK_CONTIG(*tickets);
-      TORCH_CHECK(tickets->numel() >= B * Hkv, "decode_attention: tickets must hold B * Hkv counters");
-      tk = tickets->data_ptr<int32_t>();
-    }
   }
   nga::launch_decode_attention(bfp(out), out.stride(0), bfp(q), q.stride(0), kc.data_ptr(),
                                vc.data_ptr(), block_tables.data_ptr<int32_t>(),
@@ -283,7 +277,7 @@ void decode_attention(Tensor out, Tensor q, Tensor kc, Tensor vc, Tensor block_t
                                (int)pages_per_part,
                                nparts > 1 ? part_ml.data_ptr<float>() : nullptr,
                                nparts > 1 ? part_o.data_ptr<float>() : nullptr, (int)window, fp8,
-                               (float)k_scale, (float)v_scale, cur_stream(q), skip_empty, tk);
+                               (float)k_scale, (float)v_scale, cur_stream(q), skip_empty);
 }
 
 // Work-list prefill (32x32 kernel): q / out rows are absolute token rows of the step (the

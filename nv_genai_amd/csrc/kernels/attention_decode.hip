@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     const int32_t* __restrict__ block_tables, int max_blocks,
     const int32_t* __restrict__ ctx_lens, int Hq, int Hkv, float scale, int pages_per_part,
     float* __restrict__ part_ml, float* __restrict__ part_o, int window, float v_scale, int skip_empty,
-    int* __restrict__ tickets, int nt_loads) {
+    int nt_loads) {
   // fp8 pages at head_dim 128: 16-byte loads (half as many load instructions as 8-byte ones).
   // Each lane's 16 K bytes cover two d-steps (Q is loaded with the same d order, the dot
   // product does not care) and its 16 Vt bytes cover 16 consecutive keys of both key
@@ -80,37 +80,6 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 
   __shared__ float o_s[NW][16][D + 4];
   __shared__ float m_s[NW][16], l_s[NW][16];
-  __shared__ int s_last;
-
-  // split-K epilogue: the partition that finishes last for its (sequence, kv head) merges
-  // every partition's partial (a device-scope ticket per pair, reset by that last one, so
-  // the counters are zero again for the next launch or graph replay) — no second kernel
-  auto finish_split = [&]() {
-    __threadfence();                       // this partition's partials, visible device-wide
-    __syncthreads();
-    if (threadIdx.x == 0)
-      s_last = atomicAdd(&tickets[b * Hkv + kvh], 1) == nparts - 1;
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    for (int i = threadIdx.x; i < G * D; i += blockDim.x) {
-      const int qi = i / D, d = i % D;
-      const int64_t base = ((int64_t)b * Hq + kvh * G + qi) * nparts;
-      float M = -INFINITY;
-      for (int pp = 0; pp < nparts; ++pp) M = fmaxf(M, part_ml[2 * (base + pp)]);
-      float L = 0.f, acc = 0.f;
-      for (int pp = 0; pp < nparts; ++pp) {
-        const float mp = part_ml[2 * (base + pp)];
-        if (mp == -INFINITY) continue;
-        const float f = exp2f(mp - M);
-        L += f * part_ml[2 * (base + pp) + 1];
-        acc += f * part_o[(base + pp) * D + d];
-      }
-      out[(int64_t)b * out_stride + (int64_t)(kvh * G + qi) * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
-    }
-    if (threadIdx.x == 0) tickets[b * Hkv + kvh] = 0;
-  };
-
   if (p_begin >= p_end) {
     // empty partition (or an empty padding sequence, ctx = 0). skip_empty: a ctx-0 row is not
     // this launch's row at all (a mixed-step graph covers a bucket of rows, the ones past the
@@ -125,7 +94,6 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
         part_ml[2 * idx] = -INFINITY;
         part_ml[2 * idx + 1] = 0.f;
       }
-      if (tickets) finish_split();
     }
     return;
   }
@@ -311,7 +279,6 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
       }
     }
   }
-  if (nparts > 1 && tickets) finish_split();
 }
 
 template <int D>
@@ -354,7 +321,7 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
                              int num_seqs, int Hq, int Hkv, int D, int max_ctx, float scale,
                              int pages_per_part, float* part_ml, float* part_o, int window,
                              bool kv_fp8, float k_scale, float v_scale, hipStream_t stream,
-                             bool skip_empty, int* tickets) {
+                             bool skip_empty) {
   if (num_seqs == 0) return;
   int pages = (max_ctx + BS - 1) / BS;
   if (window > 0) pages = min(pages, (window + BS - 1) / BS + 1);  // visible pages at most
@@ -372,15 +339,15 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
   decode_attn_kernel<DD, CT><<<grid, 256, 0, stream>>>(                                        \
       out, out_stride, q, q_stride, static_cast<const CT*>(kc), static_cast<const CT*>(vc),   \
       block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, pages_per_part, part_ml, part_o, window, \
-      v_scale, skip_empty ? 1 : 0, tickets, nt)
+      v_scale, skip_empty ? 1 : 0, nt)
   if (D == 256) {
     if (kv_fp8) NGA_DEC(256, uint8_t); else NGA_DEC(256, uint16_t);
-    if (nparts > 1 && !tickets)
+    if (nparts > 1)
       decode_attn_reduce_kernel<256><<<g2, 256, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts,
                                                              ctx_lens, skip_empty ? 1 : 0);
   } else {
     if (kv_fp8) NGA_DEC(128, uint8_t); else NGA_DEC(128, uint16_t);
-    if (nparts > 1 && !tickets)
+    if (nparts > 1)
       decode_attn_reduce_kernel<128><<<g2, 128, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts,
                                                              ctx_lens, skip_empty ? 1 : 0);
   }

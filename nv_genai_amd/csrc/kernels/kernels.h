@@ -39,7 +39,7 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
                              int num_seqs, int Hq, int Hkv, int D, int max_ctx, float scale,
                              int pages_per_part, float* part_ml, float* part_o, int window,
                              bool kv_fp8, float k_scale, float v_scale, hipStream_t stream,
-                             bool skip_empty = false, int* tickets = nullptr);
+                             bool skip_empty = false);
 
 // attention_prefill.hip
 struct PrefillParams {

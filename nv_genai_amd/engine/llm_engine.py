@@ -230,7 +230,8 @@ class LLMEngine:
         self.stats = {"prefill_steps": 0, "decode_steps": 0, "mixed_steps": 0, "prefill_tokens": 0,
                       "decode_tokens": 0, "prefill_time": 0.0, "decode_time": 0.0, "unpipelined_steps": 0,
                       "host_sched_s": 0.0, "host_launch_s": 0.0, "host_between_s": 0.0,
-                      "host_wait_s": 0.0, "host_finalize_s": 0.0}
+                      "host_wait_s": 0.0, "host_finalize_s": 0.0, "graph_steps": 0, "graph_captures": 0,
+                      "graph_capture_s": 0.0}
         self.lock = threading.RLock()
         self._pending: Optional[dict] = None
         self._tok_flip = 0
@@ -1105,6 +1106,7 @@ class LLMEngine:
         rows, an empty work list) and the sampled tokens of the step in flight are kept."""
         tb, ndb = key
         dev = self.device
+        t0 = time.perf_counter()
         torch.cuda.synchronize(dev)
         keep = (self.d_tok.clone(), self.d_lp.clone())
         self.d_ids[:tb].zero_()
@@ -1128,6 +1130,8 @@ class LLMEngine:
         self.d_tok.copy_(keep[0])
         self.d_lp.copy_(keep[1])
         self.mgraphs[key] = g
+        self.stats["graph_captures"] += 1
+        self.stats["graph_capture_s"] += time.perf_counter() - t0
         return g
 
     def _graph_step(self, key, kind, n, ntok, max_q, max_ctx, nd, src, follower: bool = False) -> None:
@@ -1160,6 +1164,7 @@ class LLMEngine:
                                              (self.h_items, self.d_items, max(len(items), 1)),
                                              (self.h_nitems, self.d_nitems, 1), (self.h_sidx, self.d_sidx, S)))
         self._gather_ids(src)
+        self.stats["graph_steps"] += 1
         if g is not None:
             g.replay()
         else:

@@ -158,9 +158,6 @@ class DecodeWorkspace:
         need = max(b * self.nparts(b) for b in range(1, max_seqs + 1))
         self.ml = torch.empty(need * Hq * 2, dtype=torch.float32, device=device)
         self.o = torch.empty(need * Hq * D, dtype=torch.float32, device=device)
-        # split-K merge tickets, one per (sequence, kv head): the last partition of a pair
-        # merges in the attention kernel itself and resets its ticket to zero
-        self.tickets = torch.zeros(max_seqs * Hkv, dtype=torch.int32, device=device)
         self.D = D
 
     def nparts(self, B: int) -> int:
@@ -204,8 +201,7 @@ def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, max_ctx, scale,
     assert max_ctx <= ws.max_ctx and ws.D == D
     kernels().decode_attention(out, q, kc, vc, block_tables, ctx_lens, Hq, Hkv, int(max_ctx),
                                float(scale), ws.pages_per_part(B, max_ctx), ws.ml, ws.o,
-                               int(window), float(kv_scales[0]), float(kv_scales[1]), bool(skip_empty),
-                               ws.tickets if B <= ws.tickets.numel() // Hkv else None)
+                               int(window), float(kv_scales[0]), float(kv_scales[1]), bool(skip_empty))
     return out
 
 
