@@ -276,7 +276,7 @@ class LLMEngine:
             mx = cfg.max_graph_tokens or (cfg.mixed_prefill_tokens + cfg.max_num_seqs)
             self._mg_max_tokens = min(-(-mx // step) * step, T // step * step)
             self._nd_buckets = sorted({b for b in (8, 16, 32, 64, 128, 256, 512) if b < S} | {S})
-            cap = self._mg_max_tokens // 32 + S + 16     # >= row blocks of any step in a bucket
+            cap = self._mg_max_tokens // 32 + S + 16     # >= row blocks (32 or 64 rows) of any step
             self.h_ctxd, self.d_ctxd = hbuf(S), dbuf(S)
             self.h_sidx, self.d_sidx = hbuf(S, dtype=torch.int64), dbuf(S, dtype=torch.int64)
             self.h_items, self.d_items = hbuf(cap, 2), dbuf(cap, 2)
@@ -1071,15 +1071,27 @@ class LLMEngine:
         ndb = 0 if nd == 0 else next(b for b in self._nd_buckets if b >= nd)
         return (tb, ndb)
 
-    def _graph_meta(self, key) -> AttnMeta:
+    def _graph_kernel(self, key):
+        """(impl, ks) of the work-list prefill kernel in the step graph of ``key``, by the
+        eager size rule: the 32x32 kernel from ~1,024 row-block workgroups up (two per CU),
+        else the 16x16 one — whose small LDS footprint also lets the decode attention of a
+        mixed step share the CUs (the 32x32 kernel's 64-128 KiB per workgroup crowds it out).
+        The 8-wave split-key form only for a lone prompt with no decode rows beside it."""
         tb, ndb = key
-        impl = self._pf_impl
-        rw = ops.worklist_rows(impl, self.model.hq, self.model.hkv)
+        if self._pf_impl != 2:
+            return 1, 1
         G = self.model.hq // self.model.hkv
         hpw = 4 if G % 4 == 0 else 2 if G % 2 == 0 else 1
-        ng = self.model.hkv * (G // hpw)
-        # few row blocks (one short prompt): the 8-wave split-key form, one workgroup per CU
-        ks = 2 if impl == 2 and (tb - ndb) // rw * ng <= 320 else 1
+        items = (tb - ndb) // ops.prefill_rows_per_block(self.model.hq, self.model.hkv) * self.model.hkv * (G // hpw)
+        if items >= 1024:
+            return 2, 1
+        if ndb == 0 and items <= 320:
+            return 2, 2
+        return 1, 1
+
+    def _graph_meta(self, key) -> AttnMeta:
+        tb, ndb = key
+        impl, ks = self._graph_kernel(key)
         S = self.cfg.max_num_seqs
         return AttnMeta(kind="graph", slots=self.d_slots[:tb], cu_q=self.d_cu[: S + 1], ctx_lens=self.d_ctx[:S],
                         block_tables=self.d_bt[:S], max_q_len=0, max_ctx=self.cfg.max_model_len,
@@ -1152,7 +1164,8 @@ class LLMEngine:
         self.h_ctxd[nd:max(ndb, nd)] = 0
         items = ops.plan_prefill_items(cu, ctx, nd, n, self.model.hq, self.model.hkv, self.model.window,
                                        out=self.h_items.numpy(),
-                                       rw=ops.worklist_rows(self._pf_impl, self.model.hq, self.model.hkv))
+                                       rw=ops.worklist_rows(self._graph_kernel(key)[0], self.model.hq,
+                                                            self.model.hkv))
         self.h_nitems[0] = len(items)
         sidx = self.h_sidx.numpy()
         sidx[:n] = cu[1:n + 1] - 1
