@@ -105,6 +105,8 @@ def parse(argv=None):
     ap.add_argument("--kv-cache-fraction", type=float, default=None)
     ap.add_argument("--no-step-graphs", action="store_true",
                     help="prefill / mixed steps eagerly (A/B of the step hipGraphs)")
+    ap.add_argument("--graph-token-step", type=int, default=None,
+                    help="token-count bucket of the prefill / mixed step graphs (engine default)")
     return ap.parse_args(argv)
 
 
@@ -271,7 +273,8 @@ def main(argv=None):
                         mixed_prefill_tokens=args.mixed_prefill_tokens,
                         mixed_min_tokens=args.mixed_min_tokens, mixed_max_wait=args.mixed_max_wait,
                         fp8=args.fp8, kv_cache_dtype="fp8" if args.kv_fp8 else "auto",
-                        mixed_graphs=not args.no_step_graphs)
+                        mixed_graphs=not args.no_step_graphs,
+                        **({"graph_token_step": args.graph_token_step} if args.graph_token_step else {}))
     llm = LLMEngine(ecfg, device=dev, pctx=pctx)
     from nv_genai_amd.models.config import encoder_config
 

@@ -347,7 +347,7 @@ void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optio
                        int64_t max_q_len, double scale, bool causal, int64_t window,
                        int64_t impl, double k_scale, double v_scale) {
   CHECK_BF16(out); CHECK_BF16(q);
-  TORCH_CHECK(impl >= 0 && impl <= 3, "prefill_attention: impl is 0 (auto), 1, 2 or 3");
+  TORCH_CHECK(impl >= 0 && impl <= 4, "prefill_attention: impl is 0 (auto), 1, 2, 3 or 4 (auto, alone)");
   CHECK_DEV(cu_q); CHECK_DT(cu_q, at::kInt); CHECK_CONTIG(cu_q);
   TORCH_CHECK(D == 64 || D == 128 || (D == 32 && !kc.has_value()) || (D == 256 && kc.has_value()),
               "prefill_attention: head_dim must be 64 or 128 (32: packed only, 256: paged only)");

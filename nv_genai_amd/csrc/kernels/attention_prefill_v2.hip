@@ -405,7 +405,7 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
     const char* e = getenv("NGA_PREFILL_V1");
     return e && atoi(e) != 0;
   }();
-  if (p.impl == 1 || (p.impl == 0 && disabled) || D != 128 || !paged || p.kv_fp8 ||
+  if (p.impl == 1 || ((p.impl == 0 || p.impl == 4) && disabled) || D != 128 || !paged || p.kv_fp8 ||
       p.max_blocks > V2_MAX_TILES)
     return false;
   static const int ks_env = [] {   // NGA_PREFILL_KS=1|2 forces the wave-group count (A/B)
@@ -426,6 +426,9 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
   // shares the chip with the decode attention of a mixed step (benchmarks/kernel_bench.py
   // and scripts/gpu_r2_attn_ab.sh). From ~6 such prompts (or long ones) up it is 15-25% faster.
   // Few row blocks (~one per CU, e.g. one ~1.2K-token prompt): the 8-wave split-key form.
+  // impl 4 ("alone": a prefill with no decode attention beside it, e.g. a prefill-only step)
+  // drops the sharing concern: standalone this kernel wins from one prompt up — 2 x 1,200
+  // tokens 47.6 vs 75.9 us, 3 x 1,200 59.6 vs 97.6 us (profiles/r3_kernels/kb_prefill.json).
   int ks = p.impl == 3 ? 2 : p.impl == 2 ? 1 : (total <= 320 ? 2 : 1);
   if (ks_env == 1 || ks_env == 2) ks = ks_env;
   if (p.impl == 0 && ks == 1 && total < 2 * 256 * 2) return false;

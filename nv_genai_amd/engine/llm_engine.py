@@ -1069,6 +1069,11 @@ class LLMEngine:
         if tb > self._mg_max_tokens:
             return None
         ndb = 0 if nd == 0 else next(b for b in self._nd_buckets if b >= nd)
+        # the decode launch covers the first ndb rows of the bucket (fine token steps: a
+        # mostly-decode step can round to fewer tokens than its decode-row bucket)
+        tb = max(tb, -(-ndb // step) * step)
+        if tb > self._mg_max_tokens:
+            return None
         return (tb, ndb)
 
     def _graph_kernel(self, key):
@@ -1085,8 +1090,8 @@ class LLMEngine:
         items = (tb - ndb) // ops.prefill_rows_per_block(self.model.hq, self.model.hkv) * self.model.hkv * (G // hpw)
         if items >= 1024:
             return 2, 1
-        if ndb == 0 and items <= 320:
-            return 2, 2
+        if ndb == 0:   # no decode attention beside it: the standalone size rule (impl 4)
+            return (2, 2) if items <= 320 else (2, 1)
         return 1, 1
 
     def _graph_meta(self, key) -> AttnMeta:

@@ -511,10 +511,11 @@ class LlamaModel:
             else:
                 prefill()
             return attn
+        # a prefill-only step: no decode attention shares the chip (impl 4)
         return ops.prefill_attention_paged(q, self.k_cache[li], self.v_cache[li],
                                            meta.block_tables, meta.cu_q, meta.ctx_lens,
                                            hq, hkv, D, meta.max_q_len, self.scale, window=W,
-                                           kv_scales=self.kv_scales)
+                                           kv_scales=self.kv_scales, impl=4)
 
     def _attention_graph(self, q, qkv, li, meta: AttnMeta, T: int):
         """Attention of a graph-captured step: the decode launch over the bucket's first

@@ -211,8 +211,10 @@ def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
     """Paged prefill attention. ``impl``: 0 picks the kernel by problem size, 1 forces the
     16x16-MFMA kernel, 2 the 32x32-MFMA kernel (head_dim 128, bf16 caches), 3 its 8-wave
     split-key form (few prompts: two wave groups walk alternate key tiles of the same row
-    block and merge in LDS) — for tests and A/B runs. fp8 e4m3fn caches (``kv_scales``) run
-    the 16x16 kernel."""
+    block and merge in LDS) — for tests and A/B runs; 4 picks by size for a prefill that
+    runs alone (no decode attention beside it: the 32x32 kernel from one prompt up, the
+    split-key form for ~one row block per CU). fp8 e4m3fn caches (``kv_scales``) run the
+    16x16 kernel."""
     if not _gpu(q):
         r = ref.prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
                                         scale, causal, window, kv_scales)

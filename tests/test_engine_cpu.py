@@ -294,3 +294,15 @@ def test_graph_step_layout_matches_eager(async_, head_dim):
     for (a, la), (b, lb) in zip(outs[False], outs[True]):
         assert a == b
         assert torch.allclose(torch.tensor(la), torch.tensor(lb), atol=1e-4)
+
+
+def test_graph_key_token_bucket_covers_decode_bucket():
+    """Fine token buckets: a mostly-decode step may round to fewer tokens than its decode-row
+    bucket; the key's token bucket is raised so the captured decode launch's rows exist."""
+    e = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=64, max_batched_tokens=512, max_model_len=512,
+                               kv_cache_blocks=64, mixed_prefill_tokens=256, mixed_graphs=True, graph_eager=True,
+                               graph_token_step=32), device="cpu")
+    assert e._mg_ok
+    tb, ndb = e._graph_key(40, 40, 39)     # 39 decode rows + 1 prompt token
+    assert ndb == 64 and tb >= ndb and tb % 32 == 0
+    assert e._graph_key(10, 100, 0) == (128, 0)
