@@ -24,6 +24,27 @@ def timeit(fn, iters=20):
     return a.elapsed_time(b) / iters * 1e3  # us
 
 
+def timeit_graph(fn, iters=20):
+    """Per-call time of ``iters`` calls captured in one hipGraph and replayed: the form the
+    engine runs decode in (no per-launch host overhead between the kernels)."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(3):
+        g.replay()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / (3 * iters) * 1e3  # us
+
+
 def paged_setup(lens, Hkv=8, D=128, dev="cuda", width=None):
     nb = sum((l + 63) // 64 for l in lens)
     kc = torch.randn(nb, Hkv, 64, D, device=dev, dtype=torch.bfloat16)
@@ -182,17 +203,23 @@ def main():
             q2 = torch.randn(Bs, Hq * D, device=dev, dtype=torch.bfloat16)
             ctx2 = torch.full((Bs,), L, dtype=torch.int32, device=dev)
             ws = ops.DecodeWorkspace(Bs, Hq, Hkv, 8192, torch.device(dev))
-            us = timeit(lambda: ops.decode_attention(q2, kc2, vc2, bt2, ctx2, Hq, Hkv, 8192, D ** -0.5, ws=ws))
+            fn = lambda: ops.decode_attention(q2, kc2, vc2, bt2, ctx2, Hq, Hkv, 8192, D ** -0.5, ws=ws)  # noqa: E731
+            us = timeit(fn)
+            ug = timeit_graph(fn)
             out[f"decode_{Bs}x1400_auto"] = {"us": round(us, 1), "parts": ws.nparts(Bs),
-                                             "TBps": round(Bs * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
+                                             "TBps": round(Bs * L * Hkv * D * 2 * 2 / us / 1e6, 2),
+                                             "graph_us": round(ug, 1),
+                                             "graph_TBps": round(Bs * L * Hkv * D * 2 * 2 / ug / 1e6, 2)}
         # Llama-3-70B at TP=8: 8 q heads and 1 KV head per rank (the agent config's decode)
         for Bs in (4, 32):
             kc3, vc3, bt3 = paged_setup([L] * Bs, Hkv=1, width=8192 // 64)
             q3 = torch.randn(Bs, 8 * D, device=dev, dtype=torch.bfloat16)
             ctx3 = torch.full((Bs,), L, dtype=torch.int32, device=dev)
             ws = ops.DecodeWorkspace(Bs, 8, 1, 8192, torch.device(dev))
-            us = timeit(lambda: ops.decode_attention(q3, kc3, vc3, bt3, ctx3, 8, 1, 8192, D ** -0.5, ws=ws))
-            out[f"decode_70b_tp8_{Bs}x1400"] = {"us": round(us, 1), "parts": ws.nparts(Bs),
+            fn = lambda: ops.decode_attention(q3, kc3, vc3, bt3, ctx3, 8, 1, 8192, D ** -0.5, ws=ws)  # noqa: E731
+            us = timeit(fn)
+            ug = timeit_graph(fn)
+            out[f"decode_70b_tp8_{Bs}x1400"] = {"us": round(us, 1), "parts": ws.nparts(Bs), "graph_us": round(ug, 1),
                                                 "TBps": round(Bs * L * D * 2 * 2 / us / 1e6, 2)}
         if args.only == "decode":
             print(json.dumps(out))

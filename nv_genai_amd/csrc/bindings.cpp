@@ -266,6 +266,7 @@ void decode_attention(Tensor out, Tensor q, Tensor kc, Tensor vc, Tensor block_t
   const int64_t pages = (max_ctx + 63) / 64;
   const int64_t nparts = (pages + pages_per_part - 1) / pages_per_part;
   if (nparts > 1) {
+    TORCH_CHECK(nparts <= 256, "decode_attention: at most 256 key partitions");
     CHECK_DEV(part_ml); CHECK_DEV(part_o);
     TORCH_CHECK(part_ml.numel() >= B * Hq * nparts * 2 && part_o.numel() >= B * Hq * nparts * D,
                 "decode_attention: partition workspace too small");

@@ -281,27 +281,55 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   }
 }
 
+// Combine of the split-K partitions, one workgroup per (sequence, query head), one thread per
+// output dimension. Wave 0 turns the partitions' (m, l) into normalised weights in LDS (all
+// (m, l) loads in flight at once); then every thread sums its d over the partitions with the
+// O loads issued 8 at a time. (The first version walked the partitions with one dependent
+// load chain per thread: ~6 us per call at 16 x 1,400, profiles/r3_pmc/decode_fetch.txt.)
+constexpr int REDUCE_MAX_PARTS = 256;
 template <int D>
-__global__ void decode_attn_reduce_kernel(uint16_t* __restrict__ out, int64_t out_stride,
-                                          const float* __restrict__ part_ml,
-                                          const float* __restrict__ part_o, int Hq, int nparts,
-                                          const int32_t* __restrict__ ctx_lens, int skip_empty) {
+__global__ void __launch_bounds__(D) decode_attn_reduce_kernel(
+    uint16_t* __restrict__ out, int64_t out_stride, const float* __restrict__ part_ml,
+    const float* __restrict__ part_o, int Hq, int nparts, const int32_t* __restrict__ ctx_lens,
+    int skip_empty) {
+  __shared__ float w_s[REDUCE_MAX_PARTS];
+  __shared__ float inv_s;
   const int b = blockIdx.x, hq = blockIdx.y;
   if (skip_empty && ctx_lens[b] == 0) return;
   const int64_t base = ((int64_t)b * Hq + hq) * nparts;
-  float M = -INFINITY;
-  for (int p = 0; p < nparts; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    float L = 0.f, acc = 0.f;
-    for (int p = 0; p < nparts; ++p) {
+  if (threadIdx.x < 64) {
+    float M = -INFINITY;
+    for (int p = threadIdx.x; p < nparts; p += 64) M = fmaxf(M, part_ml[2 * (base + p)]);
+    M = wave_max(M);
+    float L = 0.f;
+    for (int p = threadIdx.x; p < nparts; p += 64) {
       const float mp = part_ml[2 * (base + p)];
-      if (mp == -INFINITY) continue;
-      const float f = exp2f(mp - M);
+      const float f = mp == -INFINITY ? 0.f : exp2f(mp - M);   // empty partition: weight 0
       L += f * part_ml[2 * (base + p) + 1];
-      acc += f * part_o[(base + p) * D + d];
+      w_s[p] = f;
     }
-    out[(int64_t)b * out_stride + (int64_t)hq * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
+    L = wave_sum(L);
+    if (threadIdx.x == 0) inv_s = L > 0.f ? 1.f / L : 0.f;
   }
+  __syncthreads();
+  const int d = threadIdx.x;
+  const float* po = part_o + base * D + d;
+  float acc = 0.f;
+  int p = 0;
+  // unconditional loads (an empty partition's O slot holds stale bytes: the select, not the
+  // multiply, drops it — 0 x NaN would not)
+  for (; p + 8 <= nparts; p += 8) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = po[(int64_t)(p + j) * D];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += w_s[p + j] != 0.f ? w_s[p + j] * v[j] : 0.f;
+  }
+  for (; p < nparts; ++p) {
+    const float v = po[(int64_t)p * D];
+    acc += w_s[p] != 0.f ? w_s[p] * v : 0.f;
+  }
+  out[(int64_t)b * out_stride + (int64_t)hq * D + d] = f2bf(acc * inv_s);
 }
 
 int decode_attn_pages_per_part(int num_seqs, int Hkv, int max_ctx) {
