@@ -281,6 +281,223 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   }
 }
 
+// LDS-DMA form for bf16 head_dim-128 pages (the serving shape). The register form above
+// loads each MFMA fragment straight from HBM: one wave instruction reads 16 rows x 64 B, half
+// of each 128-B line, and a page-shaped stream in that order tops out near 6.0 TB/s, while
+// lane-linear 1-KiB instructions reach 6.9 TB/s with non-temporal loads and LDS-DMA 6.5-6.8
+// (scripts/dev/read_bw_probe.hip, profiles/r3_bw/read_bw.json). Here each wave streams its
+// page's K and V^T (32 KiB) by non-temporal LDS-DMA, one contiguous 1 KiB per instruction,
+// into its own LDS slot, XOR-swizzled through the source address (the prefill kernels'
+// swizzles, bank-conflict-free fragment reads); reads the fragments with ds_read_b128; and
+// issues the next page's DMA before computing this one. A wave only touches its own slot, so
+// the page loop has no barrier. 128 KiB of LDS: one workgroup (4 waves) per CU.
+namespace {
+constexpr int DSLOT = 2 * BS * 128;   // elements of one wave's slot: K page + V^T page
+constexpr int DMA_MAX_PAGES = 1024;   // block ids of a workgroup's partition staged in LDS
+__device__ __forceinline__ int dkswz(int row) { return (row & 3) | (((row >> 3) & 3) << 2); }
+__device__ __forceinline__ int dvswz(int row) { return (row >> 1) & 7; }
+}  // namespace
+
+__global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
+    uint16_t* __restrict__ out, int64_t out_stride, const uint16_t* __restrict__ q,
+    int64_t q_stride, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const int32_t* __restrict__ block_tables, int max_blocks,
+    const int32_t* __restrict__ ctx_lens, int Hq, int Hkv, float scale,
+    float* __restrict__ part_ml, float* __restrict__ part_o, int window, int skip_empty) {
+  constexpr int D = 128, DS = 4, DT = 8;
+  // ONE LDS object (a second one makes the compiler drain the DMA before fragment reads):
+  // the waves' page slots, reused by the wave combine after the loop
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NW * DSLOT + 2 * DMA_MAX_PAGES];
+  const int b = blockIdx.x, kvh = blockIdx.y, part = blockIdx.z, nparts = gridDim.z;
+  const int G = Hq / Hkv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, h = lane >> 4;
+  const int ctx = ctx_lens[b];
+  const int n_pages = (ctx + BS - 1) / BS;
+  const int key_lo = window > 0 ? max(0, ctx - window) : 0;
+  const int p_lo = key_lo / BS;
+  const int ppp = max(NW, (n_pages - p_lo + nparts - 1) / nparts);
+  const int p_begin = p_lo + part * ppp;
+  const int p_end = min(n_pages, p_begin + ppp);
+  if (p_begin >= p_end) {   // as decode_attn_kernel
+    if (skip_empty && ctx == 0) return;
+    if (nparts == 1) {
+      for (int i = threadIdx.x; i < G * D; i += blockDim.x)
+        out[(int64_t)b * out_stride + (int64_t)(kvh * G) * D + i] = 0;
+    } else {
+      for (int i = threadIdx.x; i < G; i += blockDim.x) {
+        const int64_t idx = ((int64_t)b * Hq + kvh * G + i) * nparts + part;
+        part_ml[2 * idx] = -INFINITY;
+        part_ml[2 * idx + 1] = 0.f;
+      }
+    }
+    return;
+  }
+
+  uint16_t* const ks = smem + w * DSLOT;
+  uint16_t* const vs = ks + BS * D;
+  const int32_t* bt = block_tables + (int64_t)b * max_blocks;
+  // DMA instruction i fills slot bytes [1 KiB i, +1 KiB): K keys 4i .. 4i+3 (lane: key
+  // 4i + (l >> 4), 16-B position l & 15 holding logical chunk (l & 15) ^ kswz(key)); V^T rows
+  // 8i .. 8i+7 (lane: row 8i + (l >> 3), position l & 7 holding chunk (l & 7) ^ vswz(row))
+  auto issue = [&](int64_t blk) {
+    const char* kp = reinterpret_cast<const char*>(kc + (blk * Hkv + kvh) * (int64_t)(BS * D));
+    const char* vp = reinterpret_cast<const char*>(vc + (blk * Hkv + kvh) * (int64_t)(D * BS));
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = 4 * i + (lane >> 4);
+      __builtin_amdgcn_global_load_lds((gptr_t)(kp + key * 256 + (((lane & 15) ^ dkswz(key)) << 4)),
+                                       (lptr_t)(ks + i * 512), 16, 0, 2);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = 8 * i + (lane >> 3);
+      __builtin_amdgcn_global_load_lds((gptr_t)(vp + row * 128 + (((lane & 7) ^ dvswz(row)) << 4)),
+                                       (lptr_t)(vs + i * 512), 16, 0, 2);
+    }
+  };
+
+  const float sl2 = scale * LOG2E;
+  float m = -INFINITY, l = 0.f;
+  f32x4 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x4)(0.f);
+
+  // the partition's block ids in LDS: a VMEM block-id load in the loop would be sunk past the
+  // page wait by the compiler and then waited for on its own before every next-page DMA
+  int32_t* const sbt = reinterpret_cast<int32_t*>(smem + NW * DSLOT);
+  for (int i = threadIdx.x; i < p_end - p_begin; i += blockDim.x) sbt[i] = bt[p_begin + i];
+  __syncthreads();
+  int p = p_begin + w;
+  if (p < p_end) issue(sbt[p - p_begin]);
+  // Q after the first DMA: its wait is the first page's anyway
+  bf16x8 qf[DS];
+  {
+    const bool qv = col < G;
+    const uint16_t* qp = q + (int64_t)b * q_stride + (int64_t)(kvh * G + (qv ? col : 0)) * D;
+#pragma unroll
+    for (int s = 0; s < DS; ++s) {
+      u16x8 v = load8(qp + 32 * s + 8 * h);
+      if (!qv) v = (u16x8)(0);
+      qf[s] = as_bf16x8(v);
+    }
+  }
+  for (; p < p_end; p += NW) {
+    const int pn = p + NW;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    u16x8 kf[4][DS], vf[2][DT];
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti) {
+      const int key = 32 * (ti >> 1) + 8 * (col >> 2) + 4 * (ti & 1) + (col & 3);
+#pragma unroll
+      for (int s = 0; s < DS; ++s)
+        kf[ti][s] = *reinterpret_cast<const u16x8*>(ks + key * D + (((4 * s + h) ^ dkswz(key)) << 3));
+    }
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int row = 16 * dt + col;
+        vf[g][dt] = *reinterpret_cast<const u16x8*>(vs + row * BS + (((4 * g + h) ^ dvswz(row)) << 3));
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot is free: next page's DMA
+    if (pn < p_end) issue(sbt[pn - p_begin]);
+
+    const int kbase = p * BS;
+    const bool full = kbase + BS <= ctx && kbase >= key_lo;
+    f32x4 sacc[4];
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti) {
+      sacc[ti] = (f32x4)(0.f);
+#pragma unroll
+      for (int s = 0; s < DS; ++s) sacc[ti] = mfma16(as_bf16x8(kf[ti][s]), qf[s], sacc[ti]);
+    }
+    float mloc = -INFINITY;
+    if (full) {
+#pragma unroll
+      for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mloc = fmaxf(mloc, sacc[ti][r]);
+    } else {
+#pragma unroll
+      for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kbase + 32 * (ti >> 1) + 8 * h + 4 * (ti & 1) + r;
+          const float sv = (key < ctx && key >= key_lo) ? sacc[ti][r] : -INFINITY;
+          sacc[ti][r] = sv;
+          mloc = fmaxf(mloc, sv);
+        }
+    }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    mloc *= sl2;
+    if (mloc > m + RESCALE_LOG2) {   // lazy rescale, as decode_attn_kernel
+      const float alpha = __builtin_amdgcn_exp2f(m - mloc);
+      m = mloc;
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+    }
+    const float mo = m == -INFINITY ? 0.f : -m;
+    bf16x8 pf[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[2 * g + (j >> 2)][j & 3], sl2, mo));
+        l += pv;
+        pf[g][j] = (__bf16)pv;
+      }
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16(as_bf16x8(vf[g][dt]), pf[g], o[dt]);
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+
+  // wave partials -> LDS (the page slots are free: every wave waited for its last DMA)
+  __syncthreads();
+  float* o_s = reinterpret_cast<float*>(smem);              // [NW][16][D + 4]
+  float* m_s = o_s + NW * 16 * (D + 4);                     // [NW][16]
+  float* l_s = m_s + NW * 16;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o_s[(w * 16 + col) * (D + 4) + 16 * dt + 4 * h + r] = o[dt][r];
+  if (h == 0) {
+    m_s[w * 16 + col] = m;
+    l_s[w * 16 + col] = l;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < G * D; i += blockDim.x) {
+    const int qi = i / D, d = i % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, m_s[ww * 16 + qi]);
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) {
+      const float mw = m_s[ww * 16 + qi];
+      const float f = mw == -INFINITY ? 0.f : exp2f(mw - M);
+      L += f * l_s[ww * 16 + qi];
+      acc += f * o_s[(ww * 16 + qi) * (D + 4) + d];
+    }
+    const int hq = kvh * G + qi;
+    if (nparts == 1) {
+      out[(int64_t)b * out_stride + (int64_t)hq * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
+    } else {
+      const int64_t idx = ((int64_t)b * Hq + hq) * nparts + part;
+      part_o[idx * D + d] = acc;
+      if (d == 0) {
+        part_ml[2 * idx] = M;
+        part_ml[2 * idx + 1] = L;
+      }
+    }
+  }
+}
+
 // Combine of the split-K partitions, one workgroup per (sequence, query head), one thread per
 // output dimension. Wave 0 turns the partitions' (m, l) into normalised weights in LDS (all
 // (m, l) loads in flight at once); then every thread sums its d over the partitions with the
@@ -374,7 +591,22 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
       decode_attn_reduce_kernel<256><<<g2, 256, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts,
                                                              ctx_lens, skip_empty ? 1 : 0);
   } else {
-    if (kv_fp8) NGA_DEC(128, uint8_t); else NGA_DEC(128, uint16_t);
+    // The LDS-DMA kernel holds one workgroup per CU, so it needs the batch itself to give
+    // plenty of (sequence, kv head) workgroups: from 512 up it is faster (256 x 1,400:
+    // 257 -> 224 us, 64 x 1,400: 82 -> 75 us), below it the 4-per-CU register kernel wins
+    // (16 x 1,400: 22.4 vs 26.5 us; profiles/r3_dma). A/B knob: NGA_DECODE_DMA=0 / 1 forces
+    // the register / DMA kernel.
+    static const int dma_env = [] {
+      const char* e = getenv("NGA_DECODE_DMA");
+      return e ? atoi(e) : -1;
+    }();
+    const bool dma = dma_env >= 0 ? dma_env != 0 : num_seqs * Hkv >= 512;
+    if (kv_fp8) NGA_DEC(128, uint8_t);
+    else if (dma && (pages + nparts - 1) / nparts <= DMA_MAX_PAGES)
+      decode_attn_dma_kernel<<<grid, 256, 0, stream>>>(
+          out, out_stride, q, q_stride, static_cast<const uint16_t*>(kc), static_cast<const uint16_t*>(vc),
+          block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, part_ml, part_o, window, skip_empty ? 1 : 0);
+    else NGA_DEC(128, uint16_t);
     if (nparts > 1)
       decode_attn_reduce_kernel<128><<<g2, 128, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts,
                                                              ctx_lens, skip_empty ? 1 : 0);
