@@ -91,6 +91,18 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
     global _CTX
     world, rank, local = env_world()
     use_gpu = torch.cuda.is_available() if device is None else device.startswith("cuda")
+    ngpu = torch.cuda.device_count() if use_gpu else 0
+    oversubscribed = use_gpu and world > ngpu
+    if oversubscribed:
+        # more local ranks than GPUs (a multi-rank rehearsal on a 1-GPU box): ranks share
+        # devices round-robin and the host-side groups go over gloo, since RCCL refuses two
+        # ranks of one communicator on the same device. An 8-GPU node never takes this path.
+        local = local % max(1, ngpu)
+        if backend is None:
+            backend = "gloo"
+        if rank == 0:
+            print(f"[nga] {world} ranks on {ngpu} GPU(s): ranks share devices, {backend} backend",
+                  flush=True)
     if backend is None:
         backend = "nccl" if use_gpu else "gloo"
     dev = torch.device(f"cuda:{local}") if use_gpu else torch.device("cpu")

@@ -13,5 +13,6 @@ timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ra
 s=$?
 grep '^{' "$O/bench.log" | tail -1 > "$O/bench.json"
 python3 "$R/scripts/summarize_prof.py" "$O/raw" > "$O/kernels.txt" 2>&1
+python3 "$R/scripts/attn_overlap.py" "$O/raw" > "$O/attn_overlap.json" 2>&1
 rm -rf "$O/raw"
 exit $s
