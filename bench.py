@@ -400,6 +400,8 @@ def main(argv=None):
     llm.step_timing = args.step_timing
     for v in hostprof.values():
         v.clear()
+    for k in getattr(rag, "submit_host_s", {}):
+        rag.submit_host_s[k] = 0.0
     t0 = time.perf_counter()
     results = []
     if args.mode == "wave":
@@ -469,6 +471,7 @@ def main(argv=None):
         "steps_prefill_decode_mixed": [llm.stats["prefill_steps"] - llm.stats["mixed_steps"],
                                        llm.stats["decode_steps"], llm.stats["mixed_steps"]],
         "unpipelined_steps": llm.stats["unpipelined_steps"],
+        "submit_host_ms": {k: round(1e3 * v, 1) for k, v in getattr(rag, "submit_host_s", {}).items()},
         "host_work_ms": {k: [len(v), round(1e3 * sum(v), 1), round(1e3 * max(v), 2) if v else 0.0,
                              sum(1 for x in v if x > 4e-3)] for k, v in hostprof.items()},
         "host_s": {k[5:-2]: round(llm.stats[k], 3) for k in ("host_sched_s", "host_launch_s", "host_between_s",

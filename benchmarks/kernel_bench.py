@@ -63,7 +63,7 @@ def main():
     import argparse
 
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="", help="rope | prefill | decode | sample | search (default: all)")
+    ap.add_argument("--only", default="", help="rope | prefill | decode | decode_small | sample | search (default: all)")
     ap.add_argument("--iters", type=int, default=20)
     args = ap.parse_args()
     global timeit
@@ -117,10 +117,15 @@ def main():
             us = timeit(lambda: ops.score(Q, X, None, 1.0))
             us_all = timeit(lambda: ops.topk(ops.score(Q, X, None, 1.0), 4))
             us_f = timeit(lambda: ops.search_topk(Q, X, bias, 1.0, 4))
+            os.environ["NGA_SEARCH_DMA"] = "0"    # the register-load form
+            us_reg = timeit(lambda: ops.search_topk(Q, X, bias, 1.0, 4))
             os.environ["NGA_SEARCH_NT"] = "1"
             us_nt = timeit(lambda: ops.search_topk(Q, X, bias, 1.0, 4))
             os.environ.pop("NGA_SEARCH_NT")
-            out[f"search_1Mx1024_q{nq}"] = {"fused_nt_us": round(us_nt, 1),
+            os.environ.pop("NGA_SEARCH_DMA")
+            out[f"search_1Mx1024_q{nq}"] = {"reg_us": round(us_reg, 1),
+                                             "reg_TBps": round(N * Dx * 2 / us_reg / 1e6, 2),
+                                             "fused_nt_us": round(us_nt, 1),
                                              "fused_nt_TBps": round(N * Dx * 2 / us_nt / 1e6, 2),"score_us": round(us, 1), "score_TBps": round(N * Dx * 2 / us / 1e6, 2),
                                              "score_topk_us": round(us_all, 1),
                                              "fused_us": round(us_f, 1),
@@ -133,7 +138,10 @@ def main():
         for nq in (8, 64):
             Q = torch.nn.functional.normalize(torch.randn(nq, Dx, device=dev), dim=1).to(torch.bfloat16)
             us_f = timeit(lambda: ops.search_topk(Q, Xs, bs, 1.0, 4))
-            out[f"search_shard1.25Mx1024_q{nq}"] = {"fused_us": round(us_f, 1),
+            os.environ["NGA_SEARCH_DMA"] = "0"
+            us_reg = timeit(lambda: ops.search_topk(Q, Xs, bs, 1.0, 4))
+            os.environ.pop("NGA_SEARCH_DMA")
+            out[f"search_shard1.25Mx1024_q{nq}"] = {"reg_us": round(us_reg, 1), "fused_us": round(us_f, 1),
                                                     "fused_TBps": round(Xs.numel() * 2 / us_f / 1e6, 2)}
         del Xs, bs
         # IVF-Flat, the reference's GPU_IVF_FLAT nlist 64 / nprobe 16 over 1M vectors
@@ -145,7 +153,10 @@ def main():
         for nq in (1, 8, 64):
             Q = torch.nn.functional.normalize(torch.randn(nq, Dx, device=dev), dim=1)
             us_i = timeit(lambda: ivf.search(Q, 4))
-            out[f"ivf_1Mx1024_nlist64_nprobe16_q{nq}"] = {"us": round(us_i, 1)}
+            os.environ["NGA_SEARCH_DMA"] = "0"
+            us_ir = timeit(lambda: ivf.search(Q, 4))
+            os.environ.pop("NGA_SEARCH_DMA")
+            out[f"ivf_1Mx1024_nlist64_nprobe16_q{nq}"] = {"us": round(us_i, 1), "reg_us": round(us_ir, 1)}
         del ivf
         del X
         if args.only == "search":
@@ -224,6 +235,27 @@ def main():
         if args.only == "decode":
             print(json.dumps(out))
             return
+    if args.only == "decode_small":
+        # small-batch sweep: register vs LDS-DMA kernel x pages per partition, graph replay
+        for name, Bs, Hq_, Hkv_ in (("16x1400", 16, Hq, Hkv), ("4x1400", 4, Hq, Hkv), ("64x1400", 64, Hq, Hkv),
+                                    ("70b_tp8_4x1400", 4, 8, 1), ("70b_tp8_32x1400", 32, 8, 1)):
+            kc3, vc3, bt3 = paged_setup([L] * Bs, Hkv=Hkv_, width=8192 // 64)
+            q3 = torch.randn(Bs, Hq_ * D, device=dev, dtype=torch.bfloat16)
+            ctx3 = torch.full((Bs,), L, dtype=torch.int32, device=dev)
+            res = {}
+            # ppp is in pages of max_ctx 8192 (128 pages): 32 / 43 / 64 / 128 -> 4 / 3 / 2 / 1 partitions
+            for ppp in (None, 32, 43, 64, 128):
+                ws = ops.DecodeWorkspace(Bs, Hq_, Hkv_, 8192, torch.device(dev), ppp)
+                fn = lambda: ops.decode_attention(q3, kc3, vc3, bt3, ctx3, Hq_, Hkv_, 8192, D ** -0.5, ws=ws)  # noqa: E731
+                for kern in ("0", "1"):
+                    os.environ["NGA_DECODE_DMA"] = kern
+                    res[f"{'dma' if kern == '1' else 'reg'}_ppp{ppp}"] = round(timeit_graph(fn), 1)
+                os.environ.pop("NGA_DECODE_DMA")
+            best = min(res, key=res.get)
+            out[f"decode_small_{name}"] = {"graph_us": res, "best": best,
+                                           "best_TBps": round(Bs * L * Hkv_ * D * 4 / res[best] / 1e6, 2)}
+        print(json.dumps(out))
+        return
     V = 128256
     logits = torch.randn(B, V, device=dev) * 3
     z = lambda v, dt=torch.float32: torch.full((B,), v, dtype=dt, device=dev)  # noqa: E731

@@ -464,7 +464,8 @@ void score_topk(Tensor Q, Tensor X, c10::optional<Tensor> row_bias, double dot_s
   CHECK_BF16(Q); CHECK_BF16(X); CHECK_CONTIG(Q); CHECK_CONTIG(X);
   TORCH_CHECK(Q.dim() == 2 && X.dim() == 2 && Q.size(1) == X.size(1));
   const int64_t D = X.size(1);
-  TORCH_CHECK(D % 32 == 0 && D <= 1216, "score_topk: D must be a multiple of 32 and <= 1216");
+  TORCH_CHECK(D % 32 == 0 && (D <= 1216 || nga::score_topk_dma_ok((int)D, (int)max_q_per_item)),
+              "score_topk: D must be a multiple of 32 and <= 1216 (<= 2048 for <= 16 queries per item)");
   TORCH_CHECK(max_q_per_item >= 1 && max_q_per_item <= 64, "score_topk: 1..64 queries per item");
   TORCH_CHECK(k >= 1 && k <= nga::score_topk_kmax((int)max_q_per_item), "score_topk: k too large");
   TORCH_CHECK(n_items >= 1 && nblk >= 1 && nblk <= 65535 && n_items <= 65535, "score_topk: bad grid");
@@ -727,6 +728,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("score_topk", checked("score_topk", &score_topk));
   m.def("ivf_plan", checked("ivf_plan", &ivf_plan));
   m.def("score_topk_kmax", [](int64_t q) { return (int64_t)nga::score_topk_kmax((int)q); });
+  m.def("score_topk_dma_ok", [](int64_t d, int64_t q) { return (bool)nga::score_topk_dma_ok((int)d, (int)q); });
   m.def("pool_l2norm", checked("pool_l2norm", &pool_l2norm));
   m.def("row_sqnorm", checked("row_sqnorm", &row_sqnorm));
   m.def("fir_c64", checked("fir_c64", &fir_c64));

@@ -596,10 +596,8 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
     // 257 -> 224 us, 64 x 1,400: 82 -> 75 us), below it the 4-per-CU register kernel wins
     // (16 x 1,400: 22.4 vs 26.5 us; profiles/r3_dma). A/B knob: NGA_DECODE_DMA=0 / 1 forces
     // the register / DMA kernel.
-    static const int dma_env = [] {
-      const char* e = getenv("NGA_DECODE_DMA");
-      return e ? atoi(e) : -1;
-    }();
+    const char* dma_e = getenv("NGA_DECODE_DMA");   // read per call (kernel_bench sweeps it)
+    const int dma_env = dma_e ? atoi(dma_e) : -1;
     const bool dma = dma_env >= 0 ? dma_env != 0 : num_seqs * Hkv >= 512;
     if (kv_fp8) NGA_DEC(128, uint8_t);
     else if (dma && (pages + nparts - 1) / nparts <= DMA_MAX_PAGES)

@@ -97,6 +97,8 @@ void launch_score(const uint16_t* Q, int nq, const uint16_t* X, int64_t N, int D
 // fused score + per-block top-k over work items (row range + <= 64 query slots); candidates
 // out [n_items * 64, nblk, k]; k <= score_topk_kmax(max_q_per_item)
 int score_topk_kmax(int nq_per_item);
+// 1 if launch_score_topk takes the LDS-DMA form (one workgroup per CU: size nblk to the CUs)
+int score_topk_dma_ok(int D, int max_q_per_item);
 void launch_score_topk(const uint16_t* Q, int nq, const uint16_t* X, int64_t N, int D,
                        const float* row_bias, float dot_scale, const int64_t* row_beg,
                        const int64_t* row_end, const int32_t* qtab, const int32_t* slot_rows, int n_items,

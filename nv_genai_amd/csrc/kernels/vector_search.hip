@@ -563,13 +563,254 @@ __global__ void __launch_bounds__(64 * W) score_topk_kernel(
   }
 }
 
+// LDS-DMA form for items of <= 16 queries (one query group) and D a multiple of CH. The
+// register form above loads its MFMA fragments straight from HBM: a wave instruction reads
+// 16 rows x 64 B, half of each 128-B line, an order that tops out near 5.9 TB/s (and whose
+// non-temporal variant re-fetches lines: 4.4 TB/s); lane-linear 1-KiB LDS-DMA reaches
+// 6.5-6.8 TB/s non-temporal (scripts/dev/read_bw_probe.hip, profiles/r3_bw/read_bw.json).
+// Here each wave owns a 32-row x CH-dim LDS slot. A unit of work is one CH-dim chunk of the
+// wave's 32 rows: the wave waits for its unit's DMA, reads every fragment of it into
+// registers, issues the next unit's DMA into the same slot, then runs the MFMAs against the
+// query tile (LDS) and, after a row tile's last chunk, the register top-k insert. A wave only
+// touches its own slot: no barrier in the loop. 4 x 32 KiB slots + the query tile fill the
+// CU's LDS: one workgroup per CU, so the launcher sizes the grid to the CU count.
+namespace {
+__device__ __forceinline__ int stk_swz(int row) { return row & 15; }
+}  // namespace
+
+template <int K, int CH>
+__global__ void __launch_bounds__(256, 1) score_topk_dma_kernel(
+    const uint16_t* __restrict__ Q, int nq, const uint16_t* __restrict__ X, int64_t N, int D,
+    const float* __restrict__ row_bias, float dot_scale, const int64_t* __restrict__ row_beg,
+    const int64_t* __restrict__ row_end, const int32_t* __restrict__ qtab,
+    const int32_t* __restrict__ slot_rows, int k, float* __restrict__ out_v, int64_t* __restrict__ out_r) {
+  constexpr int W = 4, ROWS = 32 * W;
+  constexpr int SLOT = 32 * CH;          // elements of one wave's slot
+  constexpr int NC = CH / 8;             // 16-B positions per row chunk (64 or 32)
+  constexpr int RPI = 64 / NC;           // rows per 1-KiB DMA instruction (1 or 2)
+  constexpr int NI = 32 / RPI;           // DMA instructions per unit
+  constexpr int NS = CH / 32;            // MFMA k-steps per unit
+  // ONE LDS object: [W] slots, then the query tile [16][D]; the block merge reuses it
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* const q_s = smem + W * SLOT;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int col = lane & 15, h = lane >> 4;
+  const int item = blockIdx.y;
+  const int64_t beg = row_beg ? row_beg[item] : 0;
+  const int64_t end = row_end ? row_end[item] : N;
+  const int nblk = gridDim.x;
+  const int nch = D / 8;
+  auto slot_q = [&](int s) -> int {
+    if (qtab) return qtab[item * 64 + s];
+    const int q = item * 64 + s;
+    return q < nq ? q : -1;
+  };
+  auto slot_row = [&](int s) -> int64_t {
+    return slot_rows ? (int64_t)slot_rows[item * 64 + s] : (int64_t)item * 64 + s;
+  };
+  // used query slots: every wave computes it from a ballot (no LDS scalar: the slots and the
+  // query tile take all 160 KiB)
+  const unsigned long long used = __ballot(slot_q(lane) >= 0);
+  const int nql = used ? 64 - __clzll((long long)used) : 0;
+  if (nql == 0 || end <= beg) {
+    for (int i = tid; i < 64 * k; i += 256) {
+      const int s = i / k, j = i % k;
+      const int64_t cr = slot_row(s);
+      if (cr < 0) continue;
+      const int64_t o = (cr * nblk + blockIdx.x) * k + j;
+      out_v[o] = -INFINITY;
+      out_r[o] = -1;
+    }
+    return;
+  }
+
+  uint16_t* const slot = smem + w * SLOT;
+  const int64_t ntiles = (end - beg + ROWS - 1) / ROWS;
+  const int nchx = D / CH;
+  float bnext[2][4], bcur[2][4];
+  // unit (tile, chunk) -> this wave's slot; DMA instruction i fills slot bytes [1 KiB i, +1 KiB):
+  // rows RPI i .. (lane: row RPI i + lane / NC, position lane % NC holding logical 16-B chunk
+  // (lane % NC) ^ swz(row)). With chunk 0 of a tile the tile's row biases are loaded too, so
+  // they are in registers long before its top-k (a bias load after the DMA would be waited
+  // for together with it).
+  auto issue = [&](int64_t tile, int c) {
+    const int64_t rbase = beg + tile * ROWS + w * 32;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int row = RPI * i + lane / NC;
+      int64_t gr = rbase + row;
+      if (gr >= end) gr = end - 1;
+      const uint16_t* src = X + gr * D + c * CH + (((lane % NC) ^ stk_swz(row)) << 3);
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(slot + i * 512), 16, 0, 2);
+    }
+    if (c == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int64_t r = rbase + 16 * i + 4 * h + rr;
+          bnext[i][rr] = (row_bias && r < end) ? row_bias[r] : 0.f;
+        }
+    }
+  };
+  int64_t t = blockIdx.x;
+  int c = 0;
+  if (t < ntiles) issue(t, 0);
+  // query tile after the first DMA (its wait is the first unit's anyway)
+  for (int i = tid; i < 16 * nch; i += 256) {
+    const int r = i / nch, ch = i % nch;
+    u16x8 v = (u16x8)(0);
+    const int q = r < nql ? slot_q(r) : -1;
+    if (q >= 0) v = load8(Q + (int64_t)q * D + ch * 8);
+    *reinterpret_cast<u16x8*>(&q_s[r * D + ((ch ^ (r & 15)) * 8)]) = v;
+  }
+  __syncthreads();
+
+  float tv[K];
+  int tr[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    tv[j] = -INFINITY;
+    tr[j] = -1;
+  }
+  f32x4 acc[2] = {(f32x4)(0.f), (f32x4)(0.f)};
+  while (t < ntiles) {
+    int c2 = c + 1;
+    int64_t t2 = t;
+    if (c2 == nchx) {
+      c2 = 0;
+      t2 = t + nblk;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (c == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) bcur[i][rr] = bnext[i][rr];
+    }
+    u16x8 a[2][NS];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        a[i][s] = *reinterpret_cast<const u16x8*>(slot + (16 * i + col) * CH + (((4 * s + h) ^ col) << 3));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot is free: next unit's DMA
+    if (t2 < ntiles) issue(t2, c2);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int ch = c * NC + 4 * s + h;
+      const bf16x8 bq = as_bf16x8(*reinterpret_cast<const u16x8*>(&q_s[col * D + ((ch ^ col) << 3)]));
+      acc[0] = mfma16(as_bf16x8(a[0][s]), bq, acc[0]);
+      acc[1] = mfma16(as_bf16x8(a[1][s]), bq, acc[1]);
+    }
+    if (c == nchx - 1) {
+      // acc[i][rr]: row tile_base + 16 i + 4 h + rr, query slot col
+      const int64_t rbase = beg + t * ROWS + w * 32;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int64_t rb = rbase + 16 * i + 4 * h;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const float sc = acc[i][rr] * dot_scale + bcur[i][rr];
+          if (rb + rr < end && sc > tv[K - 1]) tk_insert<K>(tv, tr, sc, (int)(rb + rr));
+        }
+        acc[i] = (f32x4)(0.f);
+      }
+    }
+    t = t2;
+    c = c2;
+  }
+
+  tk_merge_xor<K>(tv, tr, 16);
+  tk_merge_xor<K>(tv, tr, 32);
+  __syncthreads();   // every wave is past its last DMA wait and done with the query tile
+  float* mv = reinterpret_cast<float*>(smem);                 // [16 slots][W][K]
+  int* mr = reinterpret_cast<int*>(mv + 16 * W * K);
+  if (h == 0) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      mv[(col * W + w) * K + j] = tv[j];
+      mr[(col * W + w) * K + j] = tr[j];
+    }
+  }
+  __syncthreads();
+  if (tid < 64 && slot_row(tid) >= 0) {
+    const int sl = tid;
+    const int64_t o = (slot_row(sl) * nblk + blockIdx.x) * k;
+    if (sl >= nql || sl >= 16 || slot_q(sl) < 0) {
+      for (int j = 0; j < k; ++j) {
+        out_v[o + j] = -INFINITY;
+        out_r[o + j] = -1;
+      }
+    } else {
+      int head[W];
+#pragma unroll
+      for (int u = 0; u < W; ++u) head[u] = 0;
+      for (int j = 0; j < k; ++j) {
+        float best = -INFINITY;
+        int bu = -1;
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+          const float x = head[u] < K ? mv[(sl * W + u) * K + head[u]] : -INFINITY;
+          if (x > best) {
+            best = x;
+            bu = u;
+          }
+        }
+        int row = -1;
+        if (bu >= 0) {
+#pragma unroll
+          for (int u = 0; u < W; ++u)
+            if (u == bu) {
+              row = mr[(sl * W + u) * K + head[u]];
+              ++head[u];
+            }
+        }
+        out_v[o + j] = best;
+        out_r[o + j] = row;
+      }
+    }
+  }
+}
+
 int score_topk_kmax(int nq_per_item) { return nq_per_item <= 32 ? 16 : 8; }
+
+int score_topk_dma_ok(int D, int max_q_per_item) {
+  const char* e = getenv("NGA_SEARCH_DMA");   // A/B knob, read per call (kernel_bench)
+  return (e == nullptr || atoi(e) != 0) && max_q_per_item <= 16 && D % 256 == 0 && D >= 256 && D <= 2048;
+}
 
 void launch_score_topk(const uint16_t* Q, int nq, const uint16_t* X, int64_t N, int D,
                        const float* row_bias, float dot_scale, const int64_t* row_beg,
                        const int64_t* row_end, const int32_t* qtab, const int32_t* slot_rows, int n_items,
                        int max_q_per_item, int nblk, int k, float* out_v, int64_t* out_r, hipStream_t stream) {
   if (n_items == 0 || nblk == 0) return;
+  if (score_topk_dma_ok(D, max_q_per_item)) {
+    const int ch = (D % 512 == 0 && D <= 1024) ? 512 : 256;
+    const size_t lds = (size_t)(4 * 32 * ch + 16 * D) * sizeof(uint16_t);
+    const int KR = k <= 4 ? 4 : k <= 8 ? 8 : 16;
+    dim3 grid((unsigned)nblk, (unsigned)n_items);
+#define NGA_STKD(K_, CH_)                                                                       \
+  do {                                                                                           \
+    static bool attr_ = false;                                                                   \
+    if (!attr_) {                                                                                \
+      (void)hipFuncSetAttribute((const void*)score_topk_dma_kernel<K_, CH_>,                     \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);         \
+      (void)hipGetLastError();                                                                   \
+      attr_ = true;                                                                              \
+    }                                                                                            \
+    score_topk_dma_kernel<K_, CH_><<<grid, 256, lds, stream>>>(Q, nq, X, N, D, row_bias,         \
+                                                               dot_scale, row_beg, row_end,      \
+                                                               qtab, slot_rows, k, out_v, out_r); \
+  } while (0)
+    if (ch == 512) {
+      if (KR == 4) NGA_STKD(4, 512); else if (KR == 8) NGA_STKD(8, 512); else NGA_STKD(16, 512);
+    } else {
+      if (KR == 4) NGA_STKD(4, 256); else if (KR == 8) NGA_STKD(8, 256); else NGA_STKD(16, 256);
+    }
+#undef NGA_STKD
+    return;
+  }
   const int ng = max_q_per_item <= 16 ? 1 : max_q_per_item <= 32 ? 2 : 4;
   const int W = ng == 4 ? 8 : 4;
   const int KR = k <= 4 ? 4 : k <= 8 ? 8 : 16;

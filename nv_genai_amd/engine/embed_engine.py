@@ -106,15 +106,23 @@ class EmbeddingEngine:
                     batch.append(order[i])
                     tok += len(seqs[order[i]])
                     i += 1
+                # every host->device input goes through pinned memory: a pageable copy waits
+                # for the copy engine to drain this stream, i.e. for the previous batch's
+                # encoder forward, which under a concurrent LLM step can take a whole step
+                pin = self.device.type == "cuda"
                 ids = torch.tensor([t for b in batch for t in seqs[b]], dtype=torch.int32)
                 pos = torch.tensor([p for b in batch for p in range(len(seqs[b]))], dtype=torch.int32)
                 cu = [0]
                 for b in batch:
                     cu.append(cu[-1] + len(seqs[b]))
                 cu_t = torch.tensor(cu, dtype=torch.int32)
+                rows = torch.tensor(batch, dtype=torch.int64)
+                if pin:
+                    ids, pos, cu_t, rows = (t.pin_memory() for t in (ids, pos, cu_t, rows))
                 tt = None
                 if type_ids is not None:
-                    tt = torch.tensor([t for b in batch for t in type_ids[b]], dtype=torch.int32).to(self.device, non_blocking=True)
+                    tt = torch.tensor([t for b in batch for t in type_ids[b]], dtype=torch.int32)
+                    tt = (tt.pin_memory() if pin else tt).to(self.device, non_blocking=True)
                 with gpu_range(f"embed n={len(batch)} tok={tok}"):
                     res = self.model.forward(ids.to(self.device, non_blocking=True),
                                              pos.to(self.device, non_blocking=True),
@@ -125,7 +133,7 @@ class EmbeddingEngine:
                     if self.whiten is not None:
                         res = res @ self.whiten
                     res = res / res.norm(dim=-1, keepdim=True).clamp_min(1e-12)
-                out[torch.tensor(batch, device=self.device)] = res
+                out.index_copy_(0, rows.to(self.device, non_blocking=True), res.to(out.dtype))
                 self.stats["tokens"] += tok
             self.stats["calls"] += 1
             self.stats["texts"] += n

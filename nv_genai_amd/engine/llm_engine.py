@@ -263,7 +263,9 @@ class LLMEngine:
             # pipelined path is not replicated, so TP/PP steps run synchronously; pipeline
             # stages exchange activations with p2p sends, which stay out of hipGraphs
             over = {"async_decode": False}
-            if self.p.pp_size > 1:
+            if self.p.pp_size > 1 or (self.gpu and self.p.backend == "gloo"):
+                # gloo collectives (ranks sharing one GPU) go through host copies, which a
+                # graph capture cannot contain; RCCL's can be captured
                 over["use_graphs"] = False
             self.cfg = cfg = type(cfg)(**{**cfg.__dict__, **over})
         # ---- prefill / mixed step graphs (step layout in device buffers)

@@ -483,14 +483,29 @@ def topk(S: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
     return v2, i2
 
 
-def score_topk_blocks(nrows: int, rows_per_item: int, n_active_items: int, q_per_item: int) -> int:
+def score_topk_blocks(nrows: int, rows_per_item: int, n_active_items: int, q_per_item: int,
+                      dma: bool = False, cus: int = 256) -> int:
     """Blocks per work item of the fused score + top-k kernel: ~1024 resident blocks over the
     chip (512 for 64-query items, whose 8-wave blocks hold 128 KiB of query tile each), no
-    more than the item's row tiles."""
+    more than the item's row tiles. The LDS-DMA form (``dma``, <= 16 queries per item) fills
+    a CU's LDS with one block, so it gets one block per CU."""
     rows_per_tile = 256 if q_per_item > 32 else 128
     tiles = max(1, -(-rows_per_item // rows_per_tile))
-    target = (512 if q_per_item > 32 else 1024) // max(1, n_active_items)
+    if dma:
+        target = cus // max(1, n_active_items)
+    else:
+        target = (512 if q_per_item > 32 else 1024) // max(1, n_active_items)
     return int(max(1, min(tiles, max(4, target), 65535)))
+
+
+_CUS = {}
+
+
+def _cu_count(dev) -> int:
+    d = torch.device(dev)
+    if d not in _CUS:
+        _CUS[d] = torch.cuda.get_device_properties(d).multi_processor_count
+    return _CUS[d]
 
 
 def search_topk(Q: torch.Tensor, X: torch.Tensor, row_bias=None, dot_scale: float = 1.0, k: int = 4):
@@ -509,7 +524,8 @@ def search_topk(Q: torch.Tensor, X: torch.Tensor, row_bias=None, dot_scale: floa
     if k > C.score_topk_kmax(qpi) or nq == 0:
         return topk(score(Q, X, row_bias, dot_scale), k)
     items = -(-nq // 64)
-    nblk = score_topk_blocks(X.shape[0], X.shape[0], items, qpi)
+    dma = bool(C.score_topk_dma_ok(X.shape[1], qpi))
+    nblk = score_topk_blocks(X.shape[0], X.shape[0], items, qpi, dma, _cu_count(X.device) if dma else 256)
     cv = torch.empty(items * 64, nblk, k, dtype=torch.float32, device=X.device)
     cr = torch.empty(items * 64, nblk, k, dtype=torch.int64, device=X.device)
     C.score_topk(Q, X, row_bias, float(dot_scale), None, None, None, None, items, qpi, nblk, k, cv, cr)
@@ -550,7 +566,9 @@ def ivf_search_topk(Q: torch.Tensor, X: torch.Tensor, row_bias, dot_scale: float
     C.ivf_plan(probes, nlist, qtab, slot_rows)
     rb = list_beg if chunks == 1 else list_beg.repeat_interleave(chunks)
     re = list_end if chunks == 1 else list_end.repeat_interleave(chunks)
-    nblk = score_topk_blocks(X.shape[0], max_list_rows, min(nlist, nq * nprobe), qpi)
+    dma = bool(C.score_topk_dma_ok(X.shape[1], qpi))
+    nblk = score_topk_blocks(X.shape[0], max_list_rows, min(nlist, nq * nprobe), qpi, dma,
+                             _cu_count(dev) if dma else 256)
     # candidates in (query, probe) order: [nq, nprobe * nblk * k] with no gather
     gv = torch.empty(nq * nprobe, nblk, k, dtype=torch.float32, device=dev)
     gr = torch.empty(nq * nprobe, nblk, k, dtype=torch.int64, device=dev)

@@ -88,6 +88,8 @@ class RAGPipeline:
         # requests overlap the LLM step in flight instead of queueing behind it
         dev = getattr(embedder, "device", torch.device("cpu"))
         self.stream = torch.cuda.Stream(dev) if torch.device(dev).type == "cuda" else None
+        # host seconds spent in each part of submit_async (bench.py reports them)
+        self.submit_host_s = {"tokenize": 0.0, "embed": 0.0, "search": 0.0, "copy": 0.0}
 
     def set_template(self, template: str):
         tok = self.llm.tok
@@ -155,14 +157,23 @@ class RAGPipeline:
             scores, ids = self.retrieve(questions)
             return PendingRetrieval(list(questions), params, scores, ids, None, t0)
         with torch.cuda.stream(self.stream):
-            q = self.embedder.embed(questions, input_type="query")
+            seqs = self.embedder.tokenize(questions, "query")
+            t1 = time.perf_counter()
+            q = self.embedder.embed_ids(seqs)
+            t2 = time.perf_counter()
             scores, ids = self.index.search(q, self.top_k)
+            t3 = time.perf_counter()
             hs = torch.empty(scores.shape, dtype=scores.dtype, pin_memory=True)
             hi = torch.empty(ids.shape, dtype=ids.dtype, pin_memory=True)
             hs.copy_(scores, non_blocking=True)
             hi.copy_(ids, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.stream)
+        st = self.submit_host_s
+        st["tokenize"] += t1 - t0
+        st["embed"] += t2 - t1
+        st["search"] += t3 - t2
+        st["copy"] += time.perf_counter() - t3
         return PendingRetrieval(list(questions), params, hs, hi, ev, t0, keep=(scores, ids))
 
     def poll(self, pending: List["PendingRetrieval"], block: bool = False) -> List[RAGResult]:

@@ -23,7 +23,7 @@ def _run(extra):
     env = dict(os.environ, PYTHONPATH=ROOT)
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1",
-                        "--model", "llama-tiny", "--embed-model", "encoder-tiny", "--index-size", "20000",
+                        "--model", "llama-small", "--embed-model", "encoder-tiny", "--index-size", "20000",
                         "--concurrency", "8", "--max-tokens", "8", "--kv-cache-fraction", "0.02"] + extra,
                        cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stderr[-3000:]

@@ -37,7 +37,10 @@ def _check_topk(v, r, X, Q, bias, scale, k):
 
 @pytest.mark.parametrize("N,D,nq,k", [(1000, 128, 1, 4), (100_003, 1024, 1, 4), (100_003, 1024, 8, 8),
                                       (50_000, 384, 33, 16), (70_001, 1024, 64, 4), (70_001, 1024, 100, 8),
-                                      (3, 128, 5, 4), (20_000, 1024, 17, 1)])
+                                      (3, 128, 5, 4), (20_000, 1024, 17, 1),
+                                      # LDS-DMA form: 256- and 512-dim chunks, partial last tile
+                                      (30_011, 768, 16, 16), (20_000, 2048, 3, 4), (5_000, 256, 2, 4),
+                                      (777, 1024, 16, 8)])
 def test_search_topk_matches_reference(gpu, N, D, nq, k):
     X, Q = _data(N, D, nq, N + nq, gpu)
     bias = torch.zeros(N, device=gpu)
