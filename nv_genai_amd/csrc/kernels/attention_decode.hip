@@ -591,14 +591,14 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
       decode_attn_reduce_kernel<256><<<g2, 256, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts,
                                                              ctx_lens, skip_empty ? 1 : 0);
   } else {
-    // The LDS-DMA kernel holds one workgroup per CU, so it needs the batch itself to give
-    // plenty of (sequence, kv head) workgroups: from 512 up it is faster (256 x 1,400:
-    // 257 -> 224 us, 64 x 1,400: 82 -> 75 us), below it the 4-per-CU register kernel wins
-    // (16 x 1,400: 22.4 vs 26.5 us; profiles/r3_dma). A/B knob: NGA_DECODE_DMA=0 / 1 forces
-    // the register / DMA kernel.
-    const char* dma_e = getenv("NGA_DECODE_DMA");   // read per call (kernel_bench sweeps it)
-    const int dma_env = dma_e ? atoi(dma_e) : -1;
-    const bool dma = dma_env >= 0 ? dma_env != 0 : num_seqs * Hkv >= 512;
+    // bf16 pages run the LDS-DMA kernel at every batch size. It holds one workgroup per CU,
+    // so DecodeWorkspace sizes its split for ~256 busy workgroups (one per CU) rather than the
+    // register kernel's ~2,048 (graph replay, profiles/r3_search_dma/kb_decode_small_sweep.json):
+    // 16 x 1,400 22.1 -> 18.6 us (2 partitions), 64 x 1,400 81.5 -> 59.6 us (1 partition),
+    // 4 x 1,400 9.6 -> 8.1 us, the 70B TP=8 rank's 32 x 1,400 9.9 -> 8.8 us; 256 x 1,400
+    // 257 -> 224 us (profiles/r3_dma). A/B knob: NGA_DECODE_DMA=0 / 1 forces the register /
+    // DMA kernel.
+    const bool dma = dma_env != 0;
     if (kv_fp8) NGA_DEC(128, uint8_t);
     else if (dma && (pages + nparts - 1) / nparts <= DMA_MAX_PAGES)
       decode_attn_dma_kernel<<<grid, 256, 0, stream>>>(

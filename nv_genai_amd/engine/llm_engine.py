@@ -215,8 +215,8 @@ class LLMEngine:
         self.d_tok = dbuf(S)
         self.d_lp = dbuf(S, dtype=torch.float32)
         self.decode_ws = ops.DecodeWorkspace(S, self.model.hq, self.model.hkv, cfg.max_model_len,
-                                             dev, cfg.decode_pages_per_part,
-                                             D=self.model.D) if self.gpu else None
+                                             dev, cfg.decode_pages_per_part, D=self.model.D,
+                                             kv_fp8=cfg.kv_cache_dtype == "fp8") if self.gpu else None
         if self.gpu and self.mcfg.is_moe:
             # this engine's own routing buffers, sized for its largest step before any
             # hipGraph capture (graphs keep pointing at them for the engine's lifetime)

@@ -148,13 +148,15 @@ class DecodeWorkspace:
     TARGET_WGS = 2048
     FILL_WGS = 1024
     MAX_PARTS = 16
+    DMA_WGS = 256      # LDS-DMA kernel (bf16, head_dim 128): one workgroup per CU
 
     def __init__(self, max_seqs: int, Hq: int, Hkv: int, max_ctx: int, device,
-                 pages_per_part: Optional[int] = None, D: int = 128):
+                 pages_per_part: Optional[int] = None, D: int = 128, kv_fp8: bool = False):
         self.pages = (max_ctx + 63) // 64
         self.fixed = pages_per_part
         self.Hkv = Hkv
         self.max_ctx = max_ctx
+        self.dma = D == 128 and not kv_fp8
         need = max(b * self.nparts(b) for b in range(1, max_seqs + 1))
         self.ml = torch.empty(need * Hq * 2, dtype=torch.float32, device=device)
         self.o = torch.empty(need * Hq * D, dtype=torch.float32, device=device)
@@ -164,6 +166,10 @@ class DecodeWorkspace:
         if self.fixed:
             return -(-self.pages // max(1, self.fixed))
         items = B * self.Hkv
+        if self.dma:
+            # ~one busy workgroup per CU (the kernel gives every wave >= 1 page, so short
+            # contexts use fewer partitions than this; graph replay, kernel_bench decode_small)
+            return max(1, min(-(-self.DMA_WGS // items), self.MAX_PARTS))
         if items >= self.FILL_WGS:
             return 1
         return max(1, min(-(-self.TARGET_WGS // items), self.MAX_PARTS, max(1, self.pages // 4)))
@@ -197,7 +203,7 @@ def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, max_ctx, scale,
     if out is None:
         out = torch.empty(B, Hq * D, dtype=q.dtype, device=q.device)
     if ws is None:
-        ws = DecodeWorkspace(B, Hq, Hkv, max_ctx, q.device, D=D)
+        ws = DecodeWorkspace(B, Hq, Hkv, max_ctx, q.device, D=D, kv_fp8=kc.dtype != torch.bfloat16)
     assert max_ctx <= ws.max_ctx and ws.D == D
     kernels().decode_attention(out, q, kc, vc, block_tables, ctx_lens, Hq, Hkv, int(max_ctx),
                                float(scale), ws.pages_per_part(B, max_ctx), ws.ml, ws.o,
