@@ -63,7 +63,7 @@ def main():
     import argparse
 
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="", help="rope | prefill | decode | decode_small | sample | search (default: all)")
+    ap.add_argument("--only", default="", help="rope | norm | bw | prefill | decode | decode_small | sample | search (default: all)")
     ap.add_argument("--iters", type=int, default=20)
     args = ap.parse_args()
     global timeit
@@ -93,6 +93,24 @@ def main():
             out[f"rope_cache_T{T}_{kind}"] = {"us": round(us, 1), "TBps": round(moved / us / 1e6, 2)}
         del kc, vc
         if args.only == "rope":
+            print(json.dumps(out))
+            return
+    if args.only in ("", "norm"):
+        # residual add + RMSNorm at decode / mixed / full-budget step sizes (Llama-3-8B width):
+        # wave-per-row kernel vs the row-per-workgroup form
+        w = torch.randn(4096, device=dev).to(torch.bfloat16)
+        for T in (256, 1426, 4352):
+            r = torch.randn(T, 4096, device=dev).to(torch.bfloat16)
+            dlt = torch.randn(T, 4096, device=dev).to(torch.bfloat16)
+            o = torch.empty_like(r)
+            res = {}
+            for tag, env in (("wave", "1"), ("row_block", "0")):
+                os.environ["NGA_RMSNORM_WAVE"] = env
+                us = timeit(lambda: ops.add_rmsnorm(r, dlt, w, 1e-5, out=o))
+                res[tag] = {"us": round(us, 1), "TBps": round(4 * T * 4096 * 2 / us / 1e6, 2)}
+            os.environ.pop("NGA_RMSNORM_WAVE")
+            out[f"add_rmsnorm_{T}x4096"] = res
+        if args.only == "norm":
             print(json.dumps(out))
             return
     if args.only in ("", "bw"):

@@ -598,7 +598,8 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
     // 4 x 1,400 9.6 -> 8.1 us, the 70B TP=8 rank's 32 x 1,400 9.9 -> 8.8 us; 256 x 1,400
     // 257 -> 224 us (profiles/r3_dma). A/B knob: NGA_DECODE_DMA=0 / 1 forces the register /
     // DMA kernel.
-    const bool dma = dma_env != 0;
+    const char* dma_e = getenv("NGA_DECODE_DMA");   // read per call (kernel_bench sweeps it)
+    const bool dma = dma_e == nullptr || atoi(dma_e) != 0;
     if (kv_fp8) NGA_DEC(128, uint8_t);
     else if (dma && (pages + nparts - 1) / nparts <= DMA_MAX_PAGES)
       decode_attn_dma_kernel<<<grid, 256, 0, stream>>>(

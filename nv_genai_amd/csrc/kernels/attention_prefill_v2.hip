@@ -448,6 +448,12 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
     return e ? atoi(e) : 0;
   }();
   if (abl && causal && hpw == 4) {
+    if (ks == 2) {
+      if (abl == 1) prefill_attn_v2_kernel<true, 4, 1, 2><<<grid, 512, 0, stream>>>(pp);
+      else if (abl == 2) prefill_attn_v2_kernel<true, 4, 2, 2><<<grid, 512, 0, stream>>>(pp);
+      else prefill_attn_v2_kernel<true, 4, 4, 2><<<grid, 512, 0, stream>>>(pp);
+      return true;
+    }
     if (abl == 1) prefill_attn_v2_kernel<true, 4, 1><<<grid, 256, 0, stream>>>(pp);
     else if (abl == 2) prefill_attn_v2_kernel<true, 4, 2><<<grid, 256, 0, stream>>>(pp);
     else prefill_attn_v2_kernel<true, 4, 4><<<grid, 256, 0, stream>>>(pp);

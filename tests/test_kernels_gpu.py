@@ -42,7 +42,8 @@ def _close_rows(a, b, width=None, rel=1e-2, peak=2e-2):
     assert pk <= peak * b.abs().max().item() + 1e-6, f"max abs err {pk:.4g} > {peak} x max|ref|"
 
 
-@pytest.mark.parametrize("H", [1024, 4096, 8192])
+# 1024 / 768: one workgroup per row; 2048 .. 8192: the wave-per-row kernel (H = 512 NV)
+@pytest.mark.parametrize("H", [768, 1024, 2048, 3072, 4096, 5120, 6144, 8192])
 def test_rmsnorm(gpu, H):
     torch.manual_seed(0)
     x, w = _bf(37, H, dev=gpu), _bf(H, dev=gpu)
