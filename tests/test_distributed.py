@@ -4,6 +4,7 @@ import os
 import socket
 
 import pytest
+import numpy as np
 import torch
 import torch.multiprocessing as mp
 
@@ -163,7 +164,8 @@ def _shard_worker(rank, world, port, q):
         full = FlatIndex(64, "cosine", "cpu")
         full.add(X, ids)
         rv, ri = full.search(Q, 7)
-        q.put((vals, out_ids, rv, ri, len(sh.local)))
+        # numpy, not tensors: a tensor's shared-memory fd dies with the worker before the parent reads it
+        q.put((vals.numpy(), out_ids.numpy(), rv.numpy(), ri.numpy(), len(sh.local)))
     pd.destroy()
 
 
@@ -175,6 +177,7 @@ def test_sharded_index_matches_flat():
     for p in procs:
         p.start()
     vals, ids, rv, ri, nlocal = q.get(timeout=300)
+    vals, ids, rv, ri = (torch.from_numpy(a) for a in (vals, ids, rv, ri))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -205,7 +208,7 @@ def _shard_snapshot_worker(rank, world, port, path, mode, q):
     vals, ids = sh.search(Q if rank == 0 else torch.zeros(4, 32), 6)
     n = len(sh)
     if rank == 0:
-        q.put((vals, ids, n))
+        q.put((vals.numpy(), ids.numpy(), n))
     pd.destroy()
 
 
@@ -220,7 +223,7 @@ def _run_world(target, world, *args):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    return out
+    return tuple(torch.from_numpy(a) if isinstance(a, np.ndarray) else a for a in out)
 
 
 def test_sharded_index_snapshot_restore_and_restripe(tmp_path):

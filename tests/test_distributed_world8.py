@@ -148,7 +148,7 @@ def _shard8_worker(rank, world, port, q):
         full = FlatIndex(48, "cosine", "cpu")
         full.add(X, ids)
         rv, ri = full.search(Q, 10)
-        q.put((vals, out_ids, rv, ri, n, len(sh.local)))
+        q.put((vals.numpy(), out_ids.numpy(), rv.numpy(), ri.numpy(), n, len(sh.local)))
     pd.destroy()
 
 
@@ -160,6 +160,7 @@ def test_sharded_index_world8_matches_flat():
     for p in procs:
         p.start()
     vals, ids, rv, ri, n, nlocal = q.get(timeout=300)
+    vals, ids, rv, ri = (torch.from_numpy(a) for a in (vals, ids, rv, ri))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
