@@ -39,6 +39,8 @@ def main():
             t = e0.elapsed_time(e1) / a.iters / 1e3
             f = 2.0 * m * w.shape[0] * w.shape[1]
             row[k] = round(f / t / 1e15, 3)
+            row[k + "_us"] = round(t * 1e6, 1)
+            row[k + "_TBps"] = round((w.numel() + x.numel() + m * w.shape[0]) * 2 / t / 1e12, 2)
             tot_t += t
             tot_f += f
         row["layer_us"] = round(tot_t * 1e6, 1)

@@ -12,3 +12,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ra
 python3 "$R/scripts/summarize_prof.py" "$O/raw" > "$O/kernels.txt" 2>&1
 rm -rf "$O/raw"
 head -30 "$O/kernels.txt" | cut -c1-150
+timeout -k 10 200 python "$R/benchmarks/gemm_sweep.py" --tuned --ms 64,128,256,320,512,768 > "$O/gemm_small_m.log" 2>&1 || { tail -20 "$O/gemm_small_m.log"; exit 1; }
+cat "$O/gemm_small_m.log"
