@@ -108,7 +108,7 @@ def main():
                 os.environ["NGA_RMSNORM_WAVE"] = env
                 us = timeit(lambda: ops.add_rmsnorm(r, dlt, w, 1e-5, out=o))
                 res[tag] = {"us": round(us, 1), "TBps": round(4 * T * 4096 * 2 / us / 1e6, 2)}
-            os.environ.pop("NGA_RMSNORM_WAVE")
+            os.environ.pop("NGA_RMSNORM_WAVE")   # back to the default (row-per-block)
             out[f"add_rmsnorm_{T}x4096"] = res
         if args.only == "norm":
             print(json.dumps(out))

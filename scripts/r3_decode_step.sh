@@ -14,3 +14,5 @@ rm -rf "$O/raw"
 head -30 "$O/kernels.txt" | cut -c1-150
 timeout -k 10 200 python "$R/benchmarks/gemm_sweep.py" --tuned --ms 64,128,256,320,512,768 > "$O/gemm_small_m.log" 2>&1 || { tail -20 "$O/gemm_small_m.log"; exit 1; }
 cat "$O/gemm_small_m.log"
+timeout -k 10 200 python "$R/benchmarks/kernel_bench.py" --only norm > "$O/kb_norm.json" 2> "$O/kb_norm.err" || { tail -20 "$O/kb_norm.err"; exit 1; }
+cat "$O/kb_norm.json"

@@ -42,9 +42,12 @@ def _close_rows(a, b, width=None, rel=1e-2, peak=2e-2):
     assert pk <= peak * b.abs().max().item() + 1e-6, f"max abs err {pk:.4g} > {peak} x max|ref|"
 
 
-# 1024 / 768: one workgroup per row; 2048 .. 8192: the wave-per-row kernel (H = 512 NV)
+# default: one workgroup per row at every width; wave = "1": the opt-in wave-per-row kernel
+# (H = 512 NV; other widths fall back to the row form)
+@pytest.mark.parametrize("wave", ["0", "1"])
 @pytest.mark.parametrize("H", [768, 1024, 2048, 3072, 4096, 5120, 6144, 8192])
-def test_rmsnorm(gpu, H):
+def test_rmsnorm(gpu, H, wave, monkeypatch):
+    monkeypatch.setenv("NGA_RMSNORM_WAVE", wave)   # read by the launcher per call
     torch.manual_seed(0)
     x, w = _bf(37, H, dev=gpu), _bf(H, dev=gpu)
     _close_rows(ops.rmsnorm(x, w, 1e-5), ref.rmsnorm(x.cpu().float(), w.cpu().float(), 1e-5))
