@@ -212,6 +212,22 @@ def main():
             ws = ops.DecodeWorkspace(B, Hq, Hkv, 8192, torch.device(dev), ppp)
             us = timeit(lambda: ops.decode_attention(q, kc, vc, bt, ctx, Hq, Hkv, 8192, D ** -0.5, ws=ws))
             out[f"decode_256x1400_ppp{ppp}"] = {"us": round(us, 1), "TBps": round(B * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
+        # page placement: the same 256 x 1,400 rows with their pages spread over a serving-size
+        # cache (10,752 blocks per layer, as the headline's 30% KV fraction gives) — in order
+        # per sequence, and in a random permutation (what an LRU-recycled steady state gives)
+        nbig = 10752
+        kcb = torch.randn(nbig, Hkv, 64, D, device=dev, dtype=torch.bfloat16)
+        vcb = torch.randn(nbig, Hkv, D, 64, device=dev, dtype=torch.bfloat16)
+        npg = (L + 63) // 64
+        g = torch.Generator().manual_seed(3)
+        for tag, order in (("spread", torch.arange(B * npg) * (nbig // (B * npg))),
+                           ("random", torch.randperm(nbig, generator=g)[: B * npg])):
+            btb = torch.zeros(B, 8192 // 64, dtype=torch.int32, device=dev)
+            btb[:, :npg] = order.view(B, npg).to(torch.int32).to(dev)
+            ws = ops.DecodeWorkspace(B, Hq, Hkv, 8192, torch.device(dev))
+            us = timeit(lambda: ops.decode_attention(q, kcb, vcb, btb, ctx, Hq, Hkv, 8192, D ** -0.5, ws=ws))
+            out[f"decode_256x1400_pages_{tag}"] = {"us": round(us, 1), "TBps": round(B * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
+        del kcb, vcb
         # fp8 e4m3fn KV pages (half the bytes; TB/s counted on the bytes actually read)
         kc8, vc8 = kc.to(torch.float8_e4m3fn), vc.to(torch.float8_e4m3fn)
         ws = ops.DecodeWorkspace(B, Hq, Hkv, 8192, torch.device(dev))
