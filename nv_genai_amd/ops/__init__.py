@@ -100,6 +100,23 @@ def gelu_tanh_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None):
     return out
 
 
+def linear_rows_split(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
+                      split: int = 0) -> torch.Tensor:
+    """``x @ w^T`` (library GEMM) with the rows cut at ``split`` when ``x`` has more: the first
+    ``split`` rows, then the rest, into disjoint row ranges of one output. At N = 4,096 a
+    4,352-row GEMM is 272 output tiles of 256 x 256 — one full wave on 256 CUs plus a 16-tile
+    second wave — while 4,096 rows are exactly one wave and the 256-row remainder runs right
+    after on MALL-warm weights (benchmarks/row_split_gemm.py)."""
+    M = x.shape[0]
+    if out is None:
+        out = torch.empty(M, w.shape[0], dtype=x.dtype, device=x.device)
+    if split <= 0 or M <= split:
+        return torch.matmul(x, w.t(), out=out)
+    torch.matmul(x[:split], w.t(), out=out[:split])
+    torch.matmul(x[split:], w.t(), out=out[split:])
+    return out
+
+
 def silu_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None):
     if not _gpu(x):
         return ref.silu_mul(x)

@@ -306,3 +306,20 @@ def test_graph_key_token_bucket_covers_decode_bucket():
     tb, ndb = e._graph_key(40, 40, 39)     # 39 decode rows + 1 prompt token
     assert ndb == 64 and tb >= ndb and tb % 32 == 0
     assert e._graph_key(10, 100, 0) == (128, 0)
+
+
+def test_linear_rows_split_matches_matmul():
+    """ops.linear_rows_split (the o / down GEMM of full mixed steps, rows cut at a multiple of
+    4,096) writes the same rows as one x @ W^T."""
+    from nv_genai_amd import ops
+
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(48, 96, generator=g)
+    for m, split in ((300, 256), (256, 256), (100, 256), (513, 512), (70, 0)):
+        x = torch.randn(m, 96, generator=g)
+        out = ops.linear_rows_split(x, w, split=split)
+        assert out.shape == (m, 48)
+        assert torch.allclose(out, x @ w.t(), atol=1e-5)
+    buf = torch.empty(300, 48)
+    x = torch.randn(300, 96, generator=g)
+    assert ops.linear_rows_split(x, w, buf, 256).data_ptr() == buf.data_ptr()
