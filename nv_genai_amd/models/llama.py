@@ -132,9 +132,11 @@ class LlamaModel:
         self.sequence_parallel = False
         self.sp_min_tokens = 512
         self.sp_steps = 0
-        # o / down projections (N = 4,096) of full mixed steps (M = 4,096 + decode rows): the
-        # GEMM rows cut at the last multiple of 4,096 — at M = 4,352 o 134.8 -> 119.6 us and
-        # down 428 -> 373 us per layer (profiles/r3_rowsplit); NGA_ROW_SPLIT=0 turns it off
+        # o / down / gate-up projections of full mixed steps (M = 4,096 + decode rows) at
+        # hidden 4,096: the GEMM rows cut at the last multiple of 4,096 — at M = 4,352 o 134.8
+        # -> 119.6 us, down 428 -> 373 us, gate/up 694 -> 686 us per layer; headline +0.7-0.9%
+        # interleaved (profiles/r3_rowsplit). q/k/v loses (167 -> 184 us) and stays whole.
+        # NGA_ROW_SPLIT=0 turns it off
         self.row_split = os.environ.get("NGA_ROW_SPLIT", "1") != "0"
         self.fp8 = False
         if fp8:
@@ -168,7 +170,7 @@ class LlamaModel:
             a = ops.silu_mul(x) if swiglu else x
             w = L[name]
             M = a.shape[0]
-            if self.row_split and name in ("wo", "wd") and w.shape[0] == 4096 and M > 4096 and M % 4096:
+            if self.row_split and name in ("wo", "wd", "wgu") and self.cfg.hidden == 4096 and M > 4096 and M % 4096:
                 return ops.linear_rows_split(a, w, split=M // 4096 * 4096)
             return a @ w.t()
         x8, sx = ops.quant_fp8_rows(x, mode=1 if swiglu else 0)
