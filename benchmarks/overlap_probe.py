@@ -55,7 +55,13 @@ def main():
     ap.add_argument("--prefill", default="1168", help="comma-separated prompt lengths of the step")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--no-tuned", action="store_true")
+    ap.add_argument("--micro", action="store_true",
+                    help="decode-only step: the decode rows as ONE forward vs two half-batch forwards "
+                         "on two streams (HBM-bound attention of one half beside the latency-bound "
+                         "small-M GEMMs of the other)")
     args = ap.parse_args()
+    if args.micro:
+        return micro(args)
     dev = "cuda"
     tuned = False if args.no_tuned else use_tuned_gemms()
     H, I, Hq, Hkv, D, eps = 4096, 14336, 32, 8, 128, 1e-5
@@ -180,6 +186,95 @@ def main():
         del gr
     res["gain_conc_vs_fused"] = round(res["fused_ms"] / res["split_conc_ms"], 3)
     res["gain_graph_vs_fused_graph"] = round(res["fused_graph_ms"] / res["split_graph_ms"], 3)
+    print(json.dumps(res))
+
+
+def micro(args):
+    dev = "cuda"
+    tuned = False if args.no_tuned else use_tuned_gemms()
+    H, I, Hq, Hkv, D, eps = 4096, 14336, 32, 8, 128, 1e-5
+    QKV = (Hq + 2 * Hkv) * D
+    Md, hm = args.decode_rows, args.decode_rows // 2
+    g = torch.Generator(device=dev).manual_seed(0)
+
+    def w(n, k):
+        return (torch.randn(n, k, device=dev, dtype=torch.bfloat16, generator=g) * k ** -0.5)
+
+    Ws = [dict(qkv=w(QKV, H), o=w(H, Hq * D), gu=w(2 * I, H), d=w(H, I),
+               n1=torch.ones(H, device=dev, dtype=torch.bfloat16),
+               n2=torch.ones(H, device=dev, dtype=torch.bfloat16)) for _ in range(args.layers)]
+    kcd, vcd, btd = paged([args.decode_ctx] * Md, Hkv, D, dev, width=8192 // 64)
+    ctxd = torch.full((Md,), args.decode_ctx, dtype=torch.int32, device=dev)
+    scale = D ** -0.5
+    parts = {"all": (0, Md), "a": (0, hm), "b": (hm, Md)}
+    wss = {k: ops.DecodeWorkspace(hi - lo, Hq, Hkv, 8192, torch.device(dev)) for k, (lo, hi) in parts.items()}
+
+    def bufs(M):
+        return dict(x=torch.randn(M, H, device=dev, dtype=torch.bfloat16, generator=g) * 0.1,
+                    r=torch.zeros(M, H, device=dev, dtype=torch.bfloat16),
+                    a=torch.empty(M, Hq * D, device=dev, dtype=torch.bfloat16),
+                    h=torch.empty(M, I, device=dev, dtype=torch.bfloat16))
+
+    B = {k: bufs(hi - lo) for k, (lo, hi) in parts.items()}
+
+    def stack(k):
+        lo, hi = parts[k]
+        b = B[k]
+        x, r = b["x"], b["r"]
+        for W in Ws:
+            hn = ops.add_rmsnorm(r, x, W["n1"], eps)
+            qkv = F.linear(hn, W["qkv"])
+            ops.decode_attention(qkv[:, : Hq * D], kcd, vcd, btd[lo:hi], ctxd[lo:hi], Hq, Hkv, 8192, scale,
+                                 out=b["a"], ws=wss[k])
+            o = F.linear(b["a"], W["o"])
+            hn = ops.add_rmsnorm(r, o, W["n2"], eps)
+            gu = F.linear(hn, W["gu"])
+            ops.silu_mul(gu, out=b["h"])
+            x = F.linear(b["h"], W["d"])
+        return x
+
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def one():
+        stack("all")
+
+    def halves_ser():
+        stack("a")
+        stack("b")
+
+    def halves_conc():
+        cur = torch.cuda.current_stream()
+        sa.wait_stream(cur)
+        sb.wait_stream(cur)
+        with torch.cuda.stream(sa):
+            stack("a")
+        with torch.cuda.stream(sb):
+            stack("b")
+        cur.wait_stream(sa)
+        cur.wait_stream(sb)
+
+    def timeit(fn, iters):
+        fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(iters):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / iters
+
+    res = {"config": {"layers": args.layers, "decode_rows": Md, "decode_ctx": args.decode_ctx, "tuned_gemms": tuned}}
+    for name, fn in (("one_forward", one), ("halves_serial", halves_ser), ("halves_two_streams", halves_conc)):
+        gr = torch.cuda.CUDAGraph()
+        fn()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(gr):
+            fn()
+        res[name + "_graph_ms"] = round(timeit(gr.replay, args.iters), 3)
+        print(json.dumps({name: res[name + "_graph_ms"]}), flush=True)
+        del gr
+    res["gain_two_streams"] = round(res["one_forward_graph_ms"] / res["halves_two_streams_graph_ms"], 3)
     print(json.dumps(res))
 
 
