@@ -396,6 +396,8 @@ def main(argv=None):
         prof.__enter__()
     llm.stats.update({k: 0 if isinstance(v, int) else 0.0 for k, v in llm.stats.items()})
     llm._host_steps.clear()
+    llm.bucket_hist.clear()
+    llm.ntok_hist.clear()
     llm._step_events.clear()
     llm.step_timing = args.step_timing
     for v in hostprof.values():
@@ -485,7 +487,9 @@ def main(argv=None):
         "step_graphs": {"timed_graph_steps": llm.stats["graph_steps"],
                         "captured_total": len(llm.mgraphs),
                         "captured_in_timed_region": llm.stats["graph_captures"],
-                        "capture_s_in_timed_region": round(llm.stats["graph_capture_s"], 3)},
+                        "capture_s_in_timed_region": round(llm.stats["graph_capture_s"], 3),
+                        "launches_by_token_bucket": dict(sorted(llm.bucket_hist.items())),
+                        "launches_by_tokens_128": dict(sorted(llm.ntok_hist.items()))},
         "prefix_cache_hit_blocks": int(llm.sched.prefix_hits()),
         "distinct_docs_retrieved": len({d for r in results for d in r.doc_ids}),
     }

@@ -270,6 +270,10 @@ class LLMEngine:
             self.cfg = cfg = type(cfg)(**{**cfg.__dict__, **over})
         # ---- prefill / mixed step graphs (step layout in device buffers)
         self.mgraphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+        # step-graph launches by token bucket and by real token count (128-token bins):
+        # which GEMM sizes a workload actually runs (bench.py reports them)
+        self.bucket_hist: collections.Counter = collections.Counter()
+        self.ntok_hist: collections.Counter = collections.Counter()
         self._graph_pool = None
         self._cap_stream = None
         self._mg_ok = self._mixed_graphs_eligible()
@@ -1185,6 +1189,8 @@ class LLMEngine:
                                              (self.h_nitems, self.d_nitems, 1), (self.h_sidx, self.d_sidx, S)))
         self._gather_ids(src)
         self.stats["graph_steps"] += 1
+        self.bucket_hist[tb] += 1
+        self.ntok_hist[ntok // 128 * 128] += 1
         if g is not None:
             g.replay()
         else:

@@ -132,11 +132,11 @@ class LlamaModel:
         self.sequence_parallel = False
         self.sp_min_tokens = 512
         self.sp_steps = 0
-        # o / down / gate-up projections of full mixed steps (M = 4,096 + decode rows) at
-        # hidden 4,096: the GEMM rows cut at the last multiple of 4,096 — at M = 4,352 o 134.8
-        # -> 119.6 us, down 428 -> 373 us, gate/up 694 -> 686 us per layer; headline +0.7-0.9%
-        # interleaved (profiles/r3_rowsplit). q/k/v loses (167 -> 184 us) and stays whole.
-        # NGA_ROW_SPLIT=0 turns it off
+        # o / down / gate-up projections of steps above 4,096 rows at hidden 4,096 (prefill
+        # chunks or budgets past 4,096 tokens; the headline's steps stop at 4,096): the GEMM
+        # rows cut at the last multiple of 4,096 — at M = 4,352 o 134.8 -> 119.6 us, down
+        # 428 -> 373 us, gate/up 694 -> 686 us per layer (profiles/r3_rowsplit). q/k/v loses
+        # (167 -> 184 us) and stays whole. NGA_ROW_SPLIT=0 turns it off
         self.row_split = os.environ.get("NGA_ROW_SPLIT", "1") != "0"
         self.fp8 = False
         if fp8:
