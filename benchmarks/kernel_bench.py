@@ -212,6 +212,23 @@ def main():
             ws = ops.DecodeWorkspace(B, Hq, Hkv, 8192, torch.device(dev), ppp)
             us = timeit(lambda: ops.decode_attention(q, kc, vc, bt, ctx, Hq, Hkv, 8192, D ** -0.5, ws=ws))
             out[f"decode_256x1400_ppp{ppp}"] = {"us": round(us, 1), "TBps": round(B * L * Hkv * D * 2 * 2 / us / 1e6, 2)}
+        # DMA kernel forms (NGA_DECODE_DMA 1: whole page per wave slot, 2: half-page ring),
+        # interleaved 3 times at the headline's and smaller batch sizes
+        for Bs in (256, 64, 16):
+            kcx, vcx, btx = (kc, vc, bt) if Bs == B else paged_setup([L] * Bs, width=8192 // 64)
+            qx = q[:Bs].contiguous()
+            ctxx = torch.full((Bs,), L, dtype=torch.int32, device=dev)
+            wsx = ops.DecodeWorkspace(Bs, Hq, Hkv, 8192, torch.device(dev))
+            res = {"1": [], "2": []}
+            for _ in range(3):
+                for form in ("1", "2"):
+                    os.environ["NGA_DECODE_DMA"] = form
+                    res[form].append(round(timeit_graph(lambda: ops.decode_attention(
+                        qx, kcx, vcx, btx, ctxx, Hq, Hkv, 8192, D ** -0.5, ws=wsx)), 1))
+            os.environ.pop("NGA_DECODE_DMA")
+            out[f"decode_{Bs}x1400_dma_forms"] = {
+                "whole_page_us": res["1"], "ring_us": res["2"],
+                "TBps_whole_ring": [round(Bs * L * Hkv * D * 4 / min(res[f]) / 1e6, 2) for f in ("1", "2")]}
         # page placement: the same 256 x 1,400 rows with their pages spread over a serving-size
         # cache (10,752 blocks per layer, as the headline's 30% KV fraction gives) — in order
         # per sequence, and in a random permutation (what an LRU-recycled steady state gives)

@@ -298,6 +298,13 @@ __device__ __forceinline__ int dkswz(int row) { return (row & 3) | (((row >> 3) 
 __device__ __forceinline__ int dvswz(int row) { return (row >> 1) & 7; }
 }  // namespace
 
+// RING = true (NGA_DECODE_DMA=2): the wave's K and V^T buffers are refilled separately. With
+// one whole-page DMA the wave waits for K and V^T together, reads both and only then issues the
+// next page, so nothing of its own is in flight while it reads. In the ring form the next K
+// goes out once this K is in registers and the next V^T once this V^T is, so one 16-KiB DMA is
+// always in flight. (A half-page ring, 32-key units, read each V^T row's 128-B line in two
+// 64-B halves and ran at 4.7 TB/s against 6.7.)
+template <bool RING>
 __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
     uint16_t* __restrict__ out, int64_t out_stride, const uint16_t* __restrict__ q,
     int64_t q_stride, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
@@ -368,6 +375,128 @@ __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
   int32_t* const sbt = reinterpret_cast<int32_t*>(smem + NW * DSLOT);
   for (int i = threadIdx.x; i < p_end - p_begin; i += blockDim.x) sbt[i] = bt[p_begin + i];
   __syncthreads();
+  if constexpr (RING) {
+    // the slot as a ring of two 16-KiB DMA units, the wave's page k's K (buffer ks) and V^T
+    // (buffer vs): K(k+1) is issued as soon as K(k) is in registers, so it streams during page
+    // k's scores and softmax; V(k+1) as soon as V(k) is, during page k's P.V
+    const int my_pages = p_begin + w < p_end ? (p_end - 1 - (p_begin + w)) / NW + 1 : 0;
+    auto blk_of = [&](int k) { return (int64_t)sbt[w + NW * k]; };
+    auto issue_k = [&](int64_t blk) {
+      const char* kp = reinterpret_cast<const char*>(kc + (blk * Hkv + kvh) * (int64_t)(BS * D));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = 4 * i + (lane >> 4);
+        __builtin_amdgcn_global_load_lds((gptr_t)(kp + key * 256 + (((lane & 15) ^ dkswz(key)) << 4)),
+                                         (lptr_t)(ks + i * 512), 16, 0, 2);
+      }
+    };
+    auto issue_v = [&](int64_t blk) {
+      const char* vp = reinterpret_cast<const char*>(vc + (blk * Hkv + kvh) * (int64_t)(D * BS));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = 8 * i + (lane >> 3);
+        __builtin_amdgcn_global_load_lds((gptr_t)(vp + row * 128 + (((lane & 7) ^ dvswz(row)) << 4)),
+                                         (lptr_t)(vs + i * 512), 16, 0, 2);
+      }
+    };
+    if (my_pages > 0) {
+      issue_k(blk_of(0));
+      issue_v(blk_of(0));
+    }
+    bf16x8 qf[DS];
+    {
+      const bool qv = col < G;
+      const uint16_t* qp = q + (int64_t)b * q_stride + (int64_t)(kvh * G + (qv ? col : 0)) * D;
+#pragma unroll
+      for (int s = 0; s < DS; ++s) {
+        u16x8 v = load8(qp + 32 * s + 8 * h);
+        if (!qv) v = (u16x8)(0);
+        qf[s] = as_bf16x8(v);
+      }
+    }
+    // Q is consumed here, so the compiler's wait for it (a full vmcnt drain beside the DMAs)
+    // lands before the loop and not inside it
+#pragma unroll
+    for (int s = 0; s < DS; ++s) asm volatile("" ::"v"(qf[s]));
+    for (int k = 0; k < my_pages; ++k) {
+      const bool more = k + 1 < my_pages;
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // K(k) landed (V(k) may not have)
+      u16x8 kf[4][DS];
+#pragma unroll
+      for (int ti = 0; ti < 4; ++ti) {
+        const int key = 32 * (ti >> 1) + 8 * (col >> 2) + 4 * (ti & 1) + (col & 3);
+#pragma unroll
+        for (int s = 0; s < DS; ++s)
+          kf[ti][s] = *reinterpret_cast<const u16x8*>(ks + key * D + (((4 * s + h) ^ dkswz(key)) << 3));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // K buffer free
+      if (more) issue_k(blk_of(k + 1));
+
+      const int kbase = (p_begin + w + NW * k) * BS;
+      const bool full = kbase + BS <= ctx && kbase >= key_lo;
+      f32x4 sacc[4];
+#pragma unroll
+      for (int ti = 0; ti < 4; ++ti) {
+        sacc[ti] = (f32x4)(0.f);
+#pragma unroll
+        for (int s = 0; s < DS; ++s) sacc[ti] = mfma16(as_bf16x8(kf[ti][s]), qf[s], sacc[ti]);
+      }
+      float mloc = -INFINITY;
+      if (full) {
+#pragma unroll
+        for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mloc = fmaxf(mloc, sacc[ti][r]);
+      } else {
+#pragma unroll
+        for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kbase + 32 * (ti >> 1) + 8 * h + 4 * (ti & 1) + r;
+            const float sv = (key < ctx && key >= key_lo) ? sacc[ti][r] : -INFINITY;
+            sacc[ti][r] = sv;
+            mloc = fmaxf(mloc, sv);
+          }
+      }
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      mloc *= sl2;
+      if (mloc > m + RESCALE_LOG2) {
+        const float alpha = __builtin_amdgcn_exp2f(m - mloc);
+        m = mloc;
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      }
+      const float mo = m == -INFINITY ? 0.f : -m;
+      bf16x8 pf[2];
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[2 * g + (j >> 2)][j & 3], sl2, mo));
+          l += pv;
+          pf[g][j] = (__bf16)pv;
+        }
+      // V(k) landed: K(k+1), if issued, is the only younger DMA
+      if (more) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      u16x8 vf[2][DT];
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int row = 16 * dt + col;
+          vf[g][dt] = *reinterpret_cast<const u16x8*>(vs + row * BS + (((4 * g + h) ^ dvswz(row)) << 3));
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // V buffer free
+      if (more) issue_v(blk_of(k + 1));
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16(as_bf16x8(vf[g][dt]), pf[g], o[dt]);
+    }
+  } else {
   int p = p_begin + w;
   if (p < p_end) issue(sbt[p - p_begin]);
   // Q after the first DMA: its wait is the first page's anyway
@@ -454,6 +583,7 @@ __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16(as_bf16x8(vf[g][dt]), pf[g], o[dt]);
   }
+  }   // RING
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
 
@@ -598,14 +728,20 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
     // 4 x 1,400 9.6 -> 8.1 us, the 70B TP=8 rank's 32 x 1,400 9.9 -> 8.8 us; 256 x 1,400
     // 257 -> 224 us (profiles/r3_dma). A/B knob: NGA_DECODE_DMA=0 / 1 forces the register /
     // DMA kernel.
+    // NGA_DECODE_DMA=2: the half-page ring form of the DMA kernel.
     const char* dma_e = getenv("NGA_DECODE_DMA");   // read per call (kernel_bench sweeps it)
-    const bool dma = dma_e == nullptr || atoi(dma_e) != 0;
+    const int dma = dma_e == nullptr ? 1 : atoi(dma_e);
     if (kv_fp8) NGA_DEC(128, uint8_t);
-    else if (dma && (pages + nparts - 1) / nparts <= DMA_MAX_PAGES)
-      decode_attn_dma_kernel<<<grid, 256, 0, stream>>>(
-          out, out_stride, q, q_stride, static_cast<const uint16_t*>(kc), static_cast<const uint16_t*>(vc),
-          block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, part_ml, part_o, window, skip_empty ? 1 : 0);
-    else NGA_DEC(128, uint16_t);
+    else if (dma && (pages + nparts - 1) / nparts <= DMA_MAX_PAGES) {
+      if (dma == 2)
+        decode_attn_dma_kernel<true><<<grid, 256, 0, stream>>>(
+            out, out_stride, q, q_stride, static_cast<const uint16_t*>(kc), static_cast<const uint16_t*>(vc),
+            block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, part_ml, part_o, window, skip_empty ? 1 : 0);
+      else
+        decode_attn_dma_kernel<false><<<grid, 256, 0, stream>>>(
+            out, out_stride, q, q_stride, static_cast<const uint16_t*>(kc), static_cast<const uint16_t*>(vc),
+            block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, part_ml, part_o, window, skip_empty ? 1 : 0);
+    } else NGA_DEC(128, uint16_t);
     if (nparts > 1)
       decode_attn_reduce_kernel<128><<<g2, 128, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts,
                                                              ctx_lens, skip_empty ? 1 : 0);

@@ -115,12 +115,15 @@ def _paged_setup(ctxs, Hkv, D, dev, seed=0):
     return kc, vc, bt.to(dev)
 
 
+@pytest.mark.parametrize("dma", ["1", "2"])
 @pytest.mark.parametrize("G", [4, 8])
 @pytest.mark.parametrize("ppp", [None, 2, 3])
-def test_decode_attention(gpu, G, ppp):
-    """Short, page-edge, long (4096 / 8192) contexts and contexts one key either side of a
+def test_decode_attention(gpu, G, ppp, dma, monkeypatch):
+    """NGA_DECODE_DMA 1: the whole-page LDS-DMA kernel, 2: its half-page ring form.
+    Short, page-edge, long (4096 / 8192) contexts and contexts one key either side of a
     split-K partition boundary (ppp pages of 64 keys per partition), per-head relative error
     against the fp32 reference (computed on the GPU in fp32)."""
+    monkeypatch.setenv("NGA_DECODE_DMA", dma)
     Hkv, D = 8 if G == 4 else 1, 128
     Hq = Hkv * G
     part = 64 * (ppp or 2)
@@ -136,7 +139,9 @@ def test_decode_attention(gpu, G, ppp):
     _close_rows(out, o_ref, width=D)
 
 
-def test_decode_attention_empty_rows(gpu):
+@pytest.mark.parametrize("dma", ["1", "2"])
+def test_decode_attention_empty_rows(gpu, dma, monkeypatch):
+    monkeypatch.setenv("NGA_DECODE_DMA", dma)
     Hkv, G, D = 8, 4, 128
     Hq = Hkv * G
     kc, vc, bt = _paged_setup([100, 1], Hkv, D, gpu)
@@ -608,9 +613,11 @@ def test_prefill_attention_worklist_fp8_and_d256(gpu):
         _close_rows(out[1:], o_ref, width=D, rel=2e-2 if fp8 else 1e-2, peak=3e-2)
 
 
-def test_decode_attention_skip_empty_rows(gpu):
+@pytest.mark.parametrize("dma", ["1", "2"])
+def test_decode_attention_skip_empty_rows(gpu, dma, monkeypatch):
     """skip_empty: rows with ctx 0 are not written (the mixed-step graph's decode launch
     covers a bucket of rows whose tail belongs to the prefill tokens)."""
+    monkeypatch.setenv("NGA_DECODE_DMA", dma)
     Hkv, G, D = 8, 4, 128
     Hq = Hkv * G
     ctxs = [100, 0, 700, 0]
