@@ -43,7 +43,7 @@ def main(d):
         ov = [p for p in pre[j:j + 8] if p[0] < e + 50_000 and p[1] > s - 50_000]
         if ov:
             us, ue = min([s] + [p[0] for p in ov]), max([e] + [p[1] for p in ov])
-            mixed.append(((e - s) / 1e3, (ue - us) / 1e3))
+            mixed.append(((e - s) / 1e3, (ue - us) / 1e3, max((p[1] - p[0]) / 1e3 for p in ov)))
             for p in ov:
                 pre_d.append((p[1] - p[0]) / 1e3)
                 k = p[2].split("(")[0][:60]
@@ -60,6 +60,14 @@ def main(d):
         "prefill_us": med(pre_d), "decode_us_alone": med(alone),
         "union_minus_decode_us": med([m[1] - m[0] for m in mixed]),
         "prefill_kernels": pre_names,
+        # by the size of the prefill beside it (its kernel time): the few large prefills of
+        # full mixed steps are hidden in the median above
+        "by_prefill_us": {
+            name: {"n": len(b), "decode_us": med([m[0] for m in b]), "union_us": med([m[1] for m in b]),
+                   "union_minus_decode_us": med([m[1] - m[0] for m in b]),
+                   "union_minus_decode_total_ms": round(sum(m[1] - m[0] for m in b) / 1e3, 2)}
+            for name, lo_, hi_ in (("lt20", 0, 20), ("20_60", 20, 60), ("60_150", 60, 150), ("ge150", 150, 1e9))
+            for b in [[m for m in mixed if lo_ <= m[2] < hi_]] if b},
     }))
 
 
