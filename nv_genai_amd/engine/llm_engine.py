@@ -20,6 +20,7 @@ from __future__ import annotations
 import collections
 import itertools
 import logging
+import os
 import random
 import threading
 import time
@@ -1063,6 +1064,7 @@ class LLMEngine:
         if not c.mixed_graphs or not (self.gpu and c.use_graphs or c.graph_eager):
             return False
         self._pf_impl = 2 if (m.D == 128 and m.kv_dtype == "auto" and self.max_blocks <= 1024) else 1
+        self._pf_seq_min = int(os.environ.get("NGA_PF_SEQ_MIN", "384"))   # _graph_pf_seq; 0 = off
         return (self.p.pp_size == 1 and not c.sequence_parallel and not m.split_mixed and m.D in (64, 128, 256)
                 and not self.mcfg.is_moe)
 
@@ -1091,6 +1093,8 @@ class LLMEngine:
         tb, ndb = key
         if self._pf_impl != 2:
             return 1, 1
+        if self._graph_pf_seq(key):
+            return 2, 1
         G = self.model.hq // self.model.hkv
         hpw = 4 if G % 4 == 0 else 2 if G % 2 == 0 else 1
         items = (tb - ndb) // ops.prefill_rows_per_block(self.model.hq, self.model.hkv) * self.model.hkv * (G // hpw)
@@ -1100,6 +1104,19 @@ class LLMEngine:
             return (2, 2) if items <= 320 else (2, 1)
         return 1, 1
 
+    def _graph_pf_seq(self, key) -> bool:
+        """Mixed steps with a large prefill (NGA_PF_SEQ_MIN <= work items < 1,024, decode rows
+        beside it): the 32x32 prefill kernel after the decode attention instead of the 16x16
+        one concurrently. Beside a 60-150 us prefill the decode kernel stretches from 229 to
+        331 us (profiles/r3_prof_bins/attn_overlap.json)."""
+        tb, ndb = key
+        if self._pf_impl != 2 or ndb == 0 or self._pf_seq_min <= 0:
+            return False
+        G = self.model.hq // self.model.hkv
+        hpw = 4 if G % 4 == 0 else 2 if G % 2 == 0 else 1
+        items = (tb - ndb) // ops.prefill_rows_per_block(self.model.hq, self.model.hkv) * self.model.hkv * (G // hpw)
+        return self._pf_seq_min <= items < 1024
+
     def _graph_meta(self, key) -> AttnMeta:
         tb, ndb = key
         impl, ks = self._graph_kernel(key)
@@ -1108,7 +1125,7 @@ class LLMEngine:
                         block_tables=self.d_bt[:S], max_q_len=0, max_ctx=self.cfg.max_model_len,
                         decode_ws=self.decode_ws, n_decode=ndb, decode_ctx=self.d_ctxd[:max(ndb, 1)],
                         items=self.d_items, n_items=self.d_nitems, pf_grid=256 if ks == 2 else 512, pf_ks=ks,
-                        pf_impl=impl)
+                        pf_impl=impl, pf_seq=self._graph_pf_seq(key))
 
     def _graph_body(self, key) -> None:
         """One prefill / mixed step over the bucket: forward of tb token rows, logits of the

@@ -71,6 +71,7 @@ class AttnMeta:
     pf_grid: int = 512
     pf_ks: int = 1
     pf_impl: int = 2    # 2: 32x32 kernel (bf16 head_dim-128 pages), 1: 16x16 kernel
+    pf_seq: bool = False  # the work list after the decode attention on the main stream
 
 
 class LlamaModel:
@@ -536,6 +537,17 @@ class LlamaModel:
         hq, hkv, D = self.hq, self.hkv, self.D
         W = self.window
         attn = torch.empty(T, hq * D, dtype=qkv.dtype, device=qkv.device)
+        nd = meta.n_decode
+        if meta.pf_seq:   # back to back on the current stream: decode rows, then the work list
+            if nd:
+                ops.decode_attention(q[:nd], self.k_cache[li], self.v_cache[li], meta.block_tables[:nd],
+                                     meta.decode_ctx[:nd], hq, hkv, meta.max_ctx, self.scale, out=attn[:nd],
+                                     ws=meta.decode_ws, window=W, kv_scales=self.kv_scales, skip_empty=True)
+            ops.prefill_attention_worklist(q, self.k_cache[li], self.v_cache[li], meta.block_tables, meta.cu_q,
+                                           meta.ctx_lens, hq, hkv, self.scale, meta.items, meta.n_items,
+                                           grid=meta.pf_grid, ks=meta.pf_ks, out=attn, window=W,
+                                           impl=meta.pf_impl, kv_scales=self.kv_scales)
+            return attn
         gpu = qkv.is_cuda
         if gpu:
             if self._attn_stream is None:
@@ -548,7 +560,6 @@ class LlamaModel:
                                            meta.ctx_lens, hq, hkv, self.scale, meta.items, meta.n_items,
                                            grid=meta.pf_grid, ks=meta.pf_ks, out=attn, window=W,
                                            impl=meta.pf_impl, kv_scales=self.kv_scales)
-        nd = meta.n_decode
         if nd:
             ops.decode_attention(q[:nd], self.k_cache[li], self.v_cache[li], meta.block_tables[:nd],
                                  meta.decode_ctx[:nd], hq, hkv, meta.max_ctx, self.scale, out=attn[:nd],
