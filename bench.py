@@ -107,7 +107,54 @@ def parse(argv=None):
                     help="prefill / mixed steps eagerly (A/B of the step hipGraphs)")
     ap.add_argument("--graph-token-step", type=int, default=None,
                     help="token-count bucket of the prefill / mixed step graphs (engine default)")
+    ap.add_argument("--allow-shared-devices", action="store_true",
+                    help="let more ranks than GPUs share devices (a multi-rank rehearsal on a small box: "
+                         "gloo host groups, not a scaling record)")
     return ap.parse_args(argv)
+
+
+def check_devices(args, world: int) -> bool:
+    """Refuse a GPU job with more ranks on this node than GPUs unless --allow-shared-devices:
+    such a run shares devices and swaps RCCL for gloo, so its record must not pass for an
+    N-GPU scaling point. Counting devices does not initialise the GPU on this image. Returns
+    whether devices are shared."""
+    if world <= 1:
+        return False
+    ngpu = torch.cuda.device_count()
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    if ngpu == 0 or local_world <= ngpu:
+        return False
+    if not args.allow_shared_devices:
+        raise SystemExit(f"bench.py: {local_world} ranks on this node but only {ngpu} GPU(s); refusing to "
+                         "record a multi-GPU result on shared devices (pass --allow-shared-devices to rehearse)")
+    return True
+
+
+def rank_devices(pctx) -> dict:
+    """Run record of where the job ran: every rank's device index, name and PCI bus id, the
+    backend and the RCCL version, and (tensor parallel) the custom all-reduce outcome."""
+    from nv_genai_amd.parallel import dist as pd
+
+    me = {"rank": pctx.rank, "local_rank": pctx.local_rank, "device": str(pctx.device)}
+    if pctx.device.type == "cuda":
+        pr = torch.cuda.get_device_properties(pctx.device)
+        me.update(name=pr.name, pci_bus_id=getattr(pr, "pci_bus_id", None),
+                  pci_device_id=getattr(pr, "pci_device_id", None), pci_domain_id=getattr(pr, "pci_domain_id", None))
+    if pctx.tp_size > 1:
+        from nv_genai_amd.parallel.custom_ar import status
+
+        me["custom_all_reduce"] = status()
+    ranks = pd.all_gather_objects(me)
+    rec = {"ranks": ranks, "backend": pctx.backend,
+           "distinct_devices": len({(r.get("pci_domain_id"), r.get("pci_bus_id"), r.get("pci_device_id"), r["device"])
+                                    for r in ranks})}
+    if pctx.backend == "nccl":
+        try:
+            v = torch.cuda.nccl.version()
+            rec["rccl_version"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+        except Exception as e:  # noqa: BLE001
+            rec["rccl_version"] = f"unavailable ({e!r})"[:80]
+    return rec
 
 
 def _free_port() -> int:
@@ -178,7 +225,7 @@ class ReplicaSearch:
         return self.index.search(q, k, src=self.src)
 
 
-def run_agent(args, world: int) -> None:
+def run_agent(args, world: int, shared: bool = False) -> None:
     """``--workload agent``: benchmarks/agent_tp.py (one TP=world replica, world-way sharded
     index), ``--steps`` x ``--concurrency`` timed agent queries, reported in bench.py's shape."""
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -197,7 +244,7 @@ def run_agent(args, world: int) -> None:
         argv.append("--fp8")
     if args.kv_cache_fraction is not None:
         argv += ["--kv-cache-fraction", str(args.kv_cache_fraction)]
-    res = agent_tp.main(argv, emit=False)
+    res = agent_tp.main(argv, emit=False, record_devices=rank_devices if world > 1 else None)
     if res is None:          # follower rank
         return
     ms = 1000.0 * res["elapsed_s"] / max(1, args.steps)
@@ -214,7 +261,8 @@ def run_agent(args, world: int) -> None:
                    "workload": "agent"},
         **{k: res[k] for k in ("p50_latency_ms", "p95_latency_ms", "llm_calls_per_s", "searches_per_s",
                                "mean_prompt_tokens", "output_tokens_per_s", "setup_s")},
-        "world_size": world, "backend": res.get("backend"),
+        "world_size": world, "backend": res.get("backend"), "shared_devices": shared,
+        **({"devices": res["devices"]} if res.get("devices") else {}),
     }
     s = json.dumps(line)
     print(s, flush=True)
@@ -229,8 +277,9 @@ def main(argv=None):
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env} ranks were launched")
+    shared = check_devices(args, world_env)
     if args.workload == "agent":
-        run_agent(args, world_env)
+        run_agent(args, world_env, shared)
         return
     if world_env > 1:
         # one rank per GPU on a shared host: give each rank's tokenizer thread pool (Rust
@@ -252,6 +301,7 @@ def main(argv=None):
     world, rank = pctx.world_size, pctx.rank
     assert world == args.gpus, (world, args.gpus)
     replicas = world // tp
+    devices = rank_devices(pctx) if world > 1 else None
     dev = str(pctx.device)
     gpu = pctx.device.type == "cuda"
     if world > 1:
@@ -483,6 +533,8 @@ def main(argv=None):
         "setup_s": round(setup_s, 1),
         "world_size": world,
         "backend": pctx.backend,
+        "shared_devices": shared,
+        **({"devices": devices} if devices else {}),
         "per_replica_qps": [x for x in per_replica if x is not None],
         "step_graphs": {"timed_graph_steps": llm.stats["graph_steps"],
                         "captured_total": len(llm.mgraphs),

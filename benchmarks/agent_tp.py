@@ -64,9 +64,10 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def main(argv=None, emit: bool = True):
+def main(argv=None, emit: bool = True, record_devices=None):
     """Run the benchmark; the driver returns the result dict (and prints it when ``emit``),
-    follower ranks return None."""
+    follower ranks return None. ``record_devices(pctx)``: a collective run-record hook called
+    on every rank right after the process group exists (bench.py's per-rank device record)."""
     args = parse(argv)
     from nv_genai_amd.engine.llm_engine import EngineConfig, LLMEngine, SamplingParams
     from nv_genai_amd.examples.query_decomposition_rag.chains import EXTRACT_PROMPT, TEMPLATE, Ledger
@@ -74,6 +75,7 @@ def main(argv=None, emit: bool = True):
     from nv_genai_amd.parallel import dist as pd
 
     pctx = pd.init_distributed(tp_size=int(os.environ.get("WORLD_SIZE", "1")))
+    devices = record_devices(pctx) if record_devices is not None else None
     gpu = pctx.device.type == "cuda"
     dev = str(pctx.device)
     t0 = time.time()
@@ -182,7 +184,8 @@ def main(argv=None, emit: bool = True):
            "output_tokens_per_s": round(stats["output_tokens"] / elapsed, 1),
            "dtype": "fp8-w8a8" if args.fp8 else "bf16",
            "data": "synthetic: random-init weights, random unit-vector index, generated questions",
-           "setup_s": round(setup_s, 1), "backend": pctx.backend}
+           "setup_s": round(setup_s, 1), "backend": pctx.backend,
+           **({"devices": devices} if devices else {})}
     line = json.dumps(res)
     if emit:
         print(line, flush=True)

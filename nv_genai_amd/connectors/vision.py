@@ -43,6 +43,28 @@ def image_size(data: bytes):
     return "unknown", 0, 0
 
 
+def as_web_image(data: bytes, quality: int = 20):
+    """(bytes, "png" | "jpeg") a vision endpoint can take: PNG and JPEG pass through, any other
+    format PIL decodes (GIF, BMP, TIFF, WebP, ...) is re-encoded as JPEG at ``quality`` (the
+    reference sends JPEG q=20: multimodal_rag/vectorstore/custom_pdf_parser.py:29-34). Bytes
+    that are no image raise ValueError instead of going out mislabelled."""
+    fmt, _, _ = image_size(data)
+    if fmt in ("png", "jpeg"):
+        return data, fmt
+    import io
+
+    from PIL import Image, UnidentifiedImageError
+
+    try:
+        im = Image.open(io.BytesIO(data))
+        im.load()
+    except (UnidentifiedImageError, OSError) as e:
+        raise ValueError(f"not a decodable image ({len(data)} bytes)") from e
+    buf = io.BytesIO()
+    im.convert("RGB").save(buf, format="JPEG", quality=quality)
+    return buf.getvalue(), "jpeg"
+
+
 class VisionClient:
     def __init__(self, base_url: str, model: str = "ai-neva-22b", timeout: float = 120.0):
         from .http import _base
@@ -53,13 +75,13 @@ class VisionClient:
 
     def describe(self, image: bytes, prompt: str = "Describe this image in detail",
                  max_tokens: int = 1024, **steer) -> str:
-        fmt, _, _ = image_size(image)
+        image, fmt = as_web_image(image)
         b64 = base64.b64encode(image).decode()
         labels = ",".join(f"{k}:{v}" for k, v in steer.items())
         text = prompt + (f" [labels: {labels}]" if labels else "")
         body = {"model": self.model, "max_tokens": max_tokens, "messages": [{"role": "user", "content": [
             {"type": "text", "text": text},
-            {"type": "image_url", "image_url": {"url": f"data:image/{'jpeg' if fmt != 'png' else 'png'};base64,{b64}"}}]}]}
+            {"type": "image_url", "image_url": {"url": f"data:image/{fmt};base64,{b64}"}}]}]}
         r = requests.post(f"{self.base}/chat/completions", json=body, timeout=self.timeout)
         r.raise_for_status()
         return r.json()["choices"][0]["message"]["content"]

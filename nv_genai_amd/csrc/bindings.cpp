@@ -235,6 +235,85 @@ void moe_combine(Tensor y, Tensor inv, int64_t T, int64_t k, Tensor out) {
                           bfp(out), cur_stream(y));
 }
 
+// ------------------------------------------------------------------ decode-shape GEMM
+std::vector<int64_t> skinny_cfg(int64_t cfg) {
+  int info[4];
+  nga::skinny_gemm_cfg_info((int)cfg, info);
+  return {info[0], info[1], info[2], info[3]};
+}
+
+// epi 0: out [M, N] bf16 = x @ w^T; 1: out fp32 [split, M, N] partial slabs; 2: out [M, F] bf16 =
+// silu(x @ w[:F]^T) * (x @ w[F:]^T)
+void skinny_gemm(Tensor out, Tensor x, Tensor w, int64_t epi, int64_t split, int64_t cfg) {
+  CHECK_BF16(x); CHECK_BF16(w); CHECK_DEV(out);
+  CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() >= 2, "skinny_gemm: 2-D x / w");
+  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0, "skinny_gemm: x rows must be contiguous and 16-B aligned");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "skinny_gemm: x / w must be 16-B aligned");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(w.size(1) == K && K % 64 == 0 && K >= 64, "skinny_gemm: K must match and be a multiple of 64");
+  TORCH_CHECK(M >= 1 && M <= 65536, "skinny_gemm: 1 <= M <= 65536");
+  int info[4];
+  nga::skinny_gemm_cfg_info((int)cfg, info);
+  TORCH_CHECK(info[0] > 0, "skinny_gemm: unknown tile configuration ", cfg);
+  const int BN = info[0], BM = info[1];
+  TORCH_CHECK(epi >= 0 && epi <= 2, "skinny_gemm: epi 0, 1 or 2");
+  TORCH_CHECK(split >= 1 && split <= K / 64 && (epi == 1 || split == 1), "skinny_gemm: 1 <= split <= K / 64 (> 1 only for epi 1)");
+  nga::SkinnyGemmParams p{};
+  p.x = bfp(x);
+  p.ldx = x.stride(0);
+  p.w = bfp(w);
+  p.M = (int)M;
+  p.K = (int)K;
+  p.split = (int)split;
+  if (epi == 2) {
+    TORCH_CHECK(w.size(0) % 2 == 0, "skinny_gemm: SwiGLU weights are [gate | up] rows");
+    p.N = (int)(w.size(0) / 2);
+    TORCH_CHECK(p.N % (BN / 2) == 0, "skinny_gemm: F must be a multiple of BN / 2 = ", BN / 2);
+    p.nN = p.N / (BN / 2);
+  } else {
+    p.N = (int)w.size(0);
+    p.nN = (p.N + BN - 1) / BN;
+  }
+  TORCH_CHECK(p.N % 8 == 0, "skinny_gemm: N must be a multiple of 8");
+  p.nM = (int)((M + BM - 1) / BM);
+  TORCH_CHECK((int64_t)p.nN * p.nM * split < (1ll << 31));
+  if (epi == 1) {
+    CHECK_DT(out, at::kFloat); CHECK_CONTIG(out);
+    TORCH_CHECK(out.numel() >= split * M * p.N, "skinny_gemm: partial buffer needs split * M * N floats");
+    p.ldo = p.N;
+  } else {
+    CHECK_DT(out, at::kBFloat16);
+    TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == p.N && out.stride(1) == 1 &&
+                out.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 8 == 0,
+                "skinny_gemm: out must be [M, N] with 8-B aligned rows");
+    p.ldo = out.stride(0);
+  }
+  p.out = out.data_ptr();
+  nga::launch_skinny_gemm(p, (int)cfg, (int)epi, cur_stream(x));
+}
+
+void splitk_reduce(Tensor out, Tensor P, int64_t S) {
+  CHECK_DEV(P); CHECK_DT(P, at::kFloat); CHECK_CONTIG(P); CHECK_BF16(out);
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.stride(0) % 8 == 0, "splitk_reduce: out [M, N] rows 16-B aligned");
+  const int64_t M = out.size(0), N = out.size(1);
+  TORCH_CHECK(S >= 1 && N % 8 == 0 && P.numel() >= S * M * N, "splitk_reduce: P must hold S x M x N floats");
+  nga::launch_splitk_reduce(P.data_ptr<float>(), (int)S, (int)M, (int)N, bfp(out), out.stride(0), cur_stream(P));
+}
+
+// resid += sum of the S partial slabs; out = rmsnorm(resid) * w
+void splitk_add_rmsnorm(Tensor out, Tensor resid, Tensor P, int64_t S, Tensor w, double eps) {
+  CHECK_BF16(out); CHECK_BF16(resid); CHECK_BF16(w); CHECK_CONTIG(out); CHECK_CONTIG(resid);
+  CHECK_DEV(P); CHECK_DT(P, at::kFloat); CHECK_CONTIG(P);
+  TORCH_CHECK(resid.dim() == 2 && out.sizes() == resid.sizes());
+  const int64_t M = resid.size(0), H = resid.size(1);
+  TORCH_CHECK(H % 8 == 0 && H <= 8192 && w.numel() == H && w.is_contiguous());
+  TORCH_CHECK(S >= 1 && P.numel() >= S * M * H, "splitk_add_rmsnorm: P must hold S x M x H floats");
+  nga::launch_splitk_add_rmsnorm(P.data_ptr<float>(), (int)S, (int)M, bfp(resid), bfp(w), (float)eps, (int)H,
+                                 bfp(out), cur_stream(resid));
+}
+
 // ------------------------------------------------------------------ attention
 int64_t decode_pages_per_part(int64_t num_seqs, int64_t Hkv, int64_t max_ctx) {
   return nga::decode_attn_pages_per_part((int)num_seqs, (int)Hkv, (int)max_ctx);
@@ -721,6 +800,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_align", checked("moe_align", &moe_align));
   m.def("moe_gemm", checked("moe_gemm", &moe_gemm));
   m.def("moe_combine", checked("moe_combine", &moe_combine));
+  m.def("skinny_cfg", &skinny_cfg);
+  m.def("skinny_cfg_count", [] { return (int64_t)nga::skinny_gemm_cfg_count(); });
+  m.def("skinny_gemm", checked("skinny_gemm", &skinny_gemm));
+  m.def("splitk_reduce", checked("splitk_reduce", &splitk_reduce));
+  m.def("splitk_add_rmsnorm", checked("splitk_add_rmsnorm", &splitk_add_rmsnorm));
   m.def("sample", checked("sample", &sample));
   m.def("embedding", checked("embedding", &embedding));
   m.def("score", checked("score", &score));

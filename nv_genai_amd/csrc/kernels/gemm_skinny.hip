@@ -1,0 +1,354 @@
+// Decode-shape projection GEMM (K6 for the decode and small mixed buckets, M <= 512):
+//
+//   out[M, N] = x[M, K] . W[N, K]^T          (nn.Linear layout: both operands K-contiguous)
+//
+// Why not the library GEMM: at M = 256 the Llama-3-8B q/k/v, o and down projections make only
+// 24 / 16 / 16 output tiles of 256 x 256 for 256 CUs, and the tuned hipBLASLt solutions run
+// them at 1.3-2.4 TB/s of weight traffic (profiles/r3_decode_step/gemm_small_m.log) while the
+// weight stream alone bounds a layer at ~75 us. Every weight byte carries 256 FLOP at M = 256,
+// so the kernel has to keep all 256 CUs streaming AND multiplying: the grid is sized to the CUs
+// by an in-kernel K split (fp32 partial slabs, reduced by the consumer kernel), never by
+// shrinking the tile below the MFMA-bound ratio.
+//
+// Block tile: BN weight rows x BM token rows x K slice, 4 waves as WN (weight) x WM (token);
+// each wave owns (BN/WN) x (BM/WM) outputs as 16 x 16 MFMA tiles (mfma_f32_16x16x32_bf16).
+// Weight rows are the MFMA A operand and token rows the B operand, so a lane ends with 4
+// consecutive output features of one token (8-B bf16 / 16-B fp32 stores) and, for the fused
+// SwiGLU epilogue, the gate and up values of the same features in the same lane: the tile's
+// weight rows are ordered [gate f..f+15 | up f..f+15] per 32-row group, read from the standard
+// [gate rows | up rows] layout by index (no repacked weight copy; moe.hip does the same).
+//
+// Staging: both operands by LDS-DMA (global_load_lds, 16 B per lane, 1 KiB = 8 rows x 128 B per
+// wave instruction) into NSTAGE buffers of one __shared__ array; the XOR swizzle that keeps the
+// ds_read_b128 fragment reads conflict-free goes on each lane's global SOURCE chunk (the DMA
+// writes lane-linearly). One raw s_barrier per 64-deep K step after a counted vmcnt that
+// retires only this step's DMA (a __syncthreads would drain every DMA in flight).
+//
+// Grid: nN x nM x split blocks, remapped so each XCD gets a contiguous range with the token
+// tile fastest: the blocks that read the same weight tile share an L2.
+//
+// Epilogues: 0 = bf16 out, 1 = fp32 partial slab [split, M, N] (summed by splitk_reduce /
+// splitk_add_rmsnorm / the consumer), 2 = SwiGLU bf16 out [M, F] (N = F, gate rows [0, F),
+// up rows [F, 2F)).
+#include <cstdlib>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace nga {
+
+namespace {
+constexpr int SBK = 64;   // K per stage (one 128-B row of bf16)
+
+__device__ __forceinline__ int sk_swz(int row, int ch) {  // 16-B chunk position in a 128-B LDS row
+  return row * SBK + ((ch ^ ((row >> 1) & 7)) << 3);
+}
+
+// s_waitcnt vmcnt(N) alone (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[15:14];
+// expcnt 7 / lgkmcnt 15 = no wait on those counters)
+template <int N>
+__device__ __forceinline__ void sk_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+__device__ __forceinline__ float sk_silu(float x) { return x / (1.f + __expf(-x)); }
+}  // namespace
+
+template <int BN, int BM, int WN, int NSTAGE, int EPI>
+__global__ void __launch_bounds__(256) skinny_gemm_kernel(SkinnyGemmParams P) {
+  constexpr int WM = 4 / WN;
+  constexpr int RW = BN / WN;   // weight rows per wave
+  constexpr int CW = BM / WM;   // token rows per wave
+  constexpr int NTW = RW / 16, MTW = CW / 16;
+  static_assert(WN * WM == 4 && NTW >= 1 && MTW >= 1 && BN % 32 == 0 && BM % 32 == 0, "tile");
+  static_assert(EPI != 2 || NTW % 2 == 0, "SwiGLU pairs gate / up tiles inside a wave");
+  static_assert(NSTAGE >= 2 && NSTAGE <= 4, "stage count");
+  constexpr int W_GL = BN / 32, X_GL = BM / 32;   // DMA instructions per wave per stage
+  constexpr int NPS = W_GL + X_GL;
+  constexpr int STAGE = (BN + BM) * SBK;          // uint16 elements per stage
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NSTAGE * STAGE];
+
+  const int nblk = P.nN * P.nM * P.split;
+  const int pb = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, x8 = pb % 8;
+  const int L = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + pb / 8;
+  const int mi = L % P.nM;
+  const int ks = (L / P.nM) % P.split;
+  const int nb = L / (P.nM * P.split);
+  const int nk_all = P.K / SBK;
+  const int kb = ks * nk_all / P.split;
+  const int nk = (ks + 1) * nk_all / P.split - kb;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wn = wv % WN, wm = wv / WN;
+  const int col = lane & 15, h = lane >> 4;
+
+  // per-lane DMA sources (fixed over K): instruction i of wave wv fills LDS rows
+  // [8 (wv * N + i), +8) lane-linearly; lane l lands in row + l/8, physical chunk l%8, which
+  // holds logical chunk (l%8) ^ swizzle(row)
+  const uint16_t* wsrc[W_GL];
+#pragma unroll
+  for (int i = 0; i < W_GL; ++i) {
+    const int r = (wv * W_GL + i) * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((r >> 1) & 7);
+    int wrow;
+    if constexpr (EPI == 2) {
+      const int rr = r % RW;
+      const int f = nb * (BN / 2) + (r / RW) * (RW / 2) + (rr >> 5) * 16 + (rr & 15);
+      wrow = ((rr >> 4) & 1) ? P.N + f : f;
+    } else {
+      wrow = nb * BN + r;
+      if (wrow >= P.N) wrow = P.N - 1;   // ragged last block: any valid row (not stored)
+    }
+    wsrc[i] = P.w + (int64_t)wrow * P.K + (int64_t)kb * SBK + ch * 8;
+  }
+  const uint16_t* xsrc[X_GL];
+#pragma unroll
+  for (int i = 0; i < X_GL; ++i) {
+    const int r = (wv * X_GL + i) * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((r >> 1) & 7);
+    int t = mi * BM + r;
+    if (t >= P.M) t = P.M - 1;           // padding token rows: any valid row (not stored)
+    xsrc[i] = P.x + (int64_t)t * P.ldx + (int64_t)kb * SBK + ch * 8;
+  }
+  auto issue = [&](int kt, int buf) {
+    uint16_t* base = smem + buf * STAGE;
+    const int k0 = kt * SBK;
+#pragma unroll
+    for (int i = 0; i < W_GL; ++i) glds16(wsrc[i] + k0, base + (wv * W_GL + i) * 8 * SBK);
+#pragma unroll
+    for (int i = 0; i < X_GL; ++i) glds16(xsrc[i] + k0, base + BN * SBK + (wv * X_GL + i) * 8 * SBK);
+  };
+
+  f32x4 acc[NTW][MTW];
+#pragma unroll
+  for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt) acc[nt][mt] = (f32x4)(0.f);
+
+  bf16x8 af[2][NTW], bfr[2][MTW];
+  auto read_frags = [&](const uint16_t* ws, int s) {
+    const uint16_t* xs = ws + BN * SBK;
+    const int ch = 4 * s + h;
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt)
+      bfr[s][mt] = as_bf16x8(*reinterpret_cast<const u16x8*>(&xs[sk_swz(wm * CW + mt * 16 + col, ch)]));
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt)
+      af[s][nt] = as_bf16x8(*reinterpret_cast<const u16x8*>(&ws[sk_swz(wn * RW + nt * 16 + col, ch)]));
+  };
+  auto mfmas = [&](int s) {
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < MTW; ++mt) acc[nt][mt] = mfma16(af[s][nt], bfr[s][mt], acc[nt][mt]);
+  };
+  constexpr int NR = NTW + MTW, NM = NTW * MTW;   // reads / MFMAs per 32-deep k-step
+  constexpr int GR = NR >= 4 ? NR / 4 : 1, GM = NM >= 4 ? NM / 4 : 1;
+
+#pragma unroll
+  for (int st = 0; st < NSTAGE - 1; ++st)
+    if (st < nk) issue(st, st);
+  for (int kt = 0; kt < nk; ++kt) {
+    // retire stage kt (this wave's DMA); later stages stay in flight. The count is the DMA of
+    // the stages issued after kt: NSTAGE - 2 of them in the steady state, fewer at the tail.
+    const int after = min(nk - 1 - kt, NSTAGE - 2);
+    if (after >= 2) sk_wait_vm<2 * NPS>();
+    else if (after == 1) sk_wait_vm<NPS>();
+    else sk_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
+    const uint16_t* ws = smem + (kt % NSTAGE) * STAGE;
+    // k-step 0's fragments first; then its MFMAs with k-step 1's reads interleaved
+    read_frags(ws, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_frags(ws, 1);
+    mfmas(0);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, GM, 0);   // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, GR, 0);   // DS read
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(1);
+  }
+  sk_wait_vm<0>();   // no DMA may still target this CU's LDS when the workgroup ends
+
+  // epilogue: acc[nt][mt][r] = out[token (16-tile mt, col)][feature (16-tile nt, 4h + r)]
+  const int t_base = mi * BM + wm * CW;
+  const int n_base = nb * BN + wn * RW;
+#pragma unroll
+  for (int mt = 0; mt < MTW; ++mt) {
+    const int t = t_base + mt * 16 + col;
+    if (t >= P.M) continue;
+    if constexpr (EPI == 0) {
+      uint16_t* op = reinterpret_cast<uint16_t*>(P.out) + (int64_t)t * P.ldo;
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int n = n_base + nt * 16 + 4 * h;
+        if (n >= P.N) continue;
+        u16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = f2bf(acc[nt][mt][r]);
+        *reinterpret_cast<u16x4*>(op + n) = v;
+      }
+    } else if constexpr (EPI == 1) {
+      float* op = reinterpret_cast<float*>(P.out) + ((int64_t)ks * P.M + t) * P.N;
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int n = n_base + nt * 16 + 4 * h;
+        if (n >= P.N) continue;
+        *reinterpret_cast<f32x4*>(op + n) = acc[nt][mt];
+      }
+    } else {
+      uint16_t* op = reinterpret_cast<uint16_t*>(P.out) + (int64_t)t * P.ldo;
+#pragma unroll
+      for (int g = 0; g < NTW / 2; ++g) {
+        const int f = nb * (BN / 2) + wn * (RW / 2) + g * 16 + 4 * h;
+        u16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = f2bf(sk_silu(acc[2 * g][mt][r]) * acc[2 * g + 1][mt][r]);
+        *reinterpret_cast<u16x4*>(op + f) = v;
+      }
+    }
+  }
+}
+
+// out[m, n] = bf16(sum_s P[s, m, n]); 8 features per thread
+__global__ void splitk_reduce_kernel(const float* __restrict__ P, int S, int M, int N,
+                                     uint16_t* __restrict__ out, int64_t ldo) {
+  const int nv = N / 8;
+  const int64_t total = (int64_t)M * nv;
+  const int64_t slab = (int64_t)M * N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / nv;
+    const int c = (int)(i - m * nv) * 8;
+    const float* p = P + m * N + c;
+    f32x4 a0 = *reinterpret_cast<const f32x4*>(p), a1 = *reinterpret_cast<const f32x4*>(p + 4);
+    for (int s = 1; s < S; ++s) {
+      a0 += *reinterpret_cast<const f32x4*>(p + s * slab);
+      a1 += *reinterpret_cast<const f32x4*>(p + s * slab + 4);
+    }
+    u16x8 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      o[q] = f2bf(a0[q]);
+      o[4 + q] = f2bf(a1[q]);
+    }
+    store8(out + m * ldo + c, o);
+  }
+}
+
+// resid += sum_s P[s] (one rounding to the bf16 residual); out = rmsnorm(resid) * w.
+// One workgroup per row, 8 features per lane (the add_rmsnorm kernel with the split-K sum of
+// the producing GEMM folded into its load).
+__global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(const float* __restrict__ P, int S,
+                                                                  int M, uint16_t* __restrict__ resid,
+                                                                  const uint16_t* __restrict__ w,
+                                                                  float eps, int H,
+                                                                  uint16_t* __restrict__ out) {
+  __shared__ float red[16];
+  const int64_t row = blockIdx.x;
+  const int c = threadIdx.x * 8;
+  const bool active = c < H;
+  const int64_t slab = (int64_t)M * H;
+  float x[8];
+  float ss = 0.f;
+  if (active) {
+    const float* p = P + row * H + c;
+    f32x4 a0 = *reinterpret_cast<const f32x4*>(p), a1 = *reinterpret_cast<const f32x4*>(p + 4);
+    for (int s = 1; s < S; ++s) {
+      a0 += *reinterpret_cast<const f32x4*>(p + s * slab);
+      a1 += *reinterpret_cast<const f32x4*>(p + s * slab + 4);
+    }
+    const u16x8 v = load8(resid + row * H + c);
+    u16x8 st;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      st[i] = f2bf(bf2f(v[i]) + (i < 4 ? a0[i] : a1[i - 4]));
+      x[i] = bf2f(st[i]);   // normalise what is stored (bf16 residual stream)
+      ss += x[i] * x[i];
+    }
+    store8(resid + row * H + c, st);
+  }
+  ss = block_sum(ss, red);
+  const float r = rsqrtf(ss / (float)H + eps);
+  if (active) {
+    const u16x8 wv = load8(w + c);
+    u16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = f2bf(x[i] * r * bf2f(wv[i]));
+    store8(out + row * H + c, o);
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+// tile configurations: {BN, BM, WN, NSTAGE}
+#define NGA_SKINNY_CFGS(X) \
+  X(0, 256, 128, 2, 3)     \
+  X(1, 128, 128, 2, 3)     \
+  X(2, 128, 64, 2, 3)      \
+  X(3, 64, 64, 2, 4)       \
+  X(4, 128, 256, 2, 2)     \
+  X(5, 64, 256, 1, 3)      \
+  X(6, 256, 64, 4, 3)      \
+  X(7, 128, 32, 4, 4)      \
+  X(8, 256, 32, 4, 3)      \
+  X(9, 64, 128, 1, 3)
+
+int skinny_gemm_cfg_count() {
+  int n = 0;
+#define NGA_COUNT(ID, BN, BM, WN, NS) ++n;
+  NGA_SKINNY_CFGS(NGA_COUNT)
+#undef NGA_COUNT
+  return n;
+}
+
+// {BN, BM, WN, NSTAGE} of a configuration, or {0, 0, 0, 0}
+void skinny_gemm_cfg_info(int cfg, int* info) {
+  info[0] = info[1] = info[2] = info[3] = 0;
+#define NGA_INFO(ID, BN, BM, WN, NS) \
+  if (cfg == ID) {                   \
+    info[0] = BN;                    \
+    info[1] = BM;                    \
+    info[2] = WN;                    \
+    info[3] = NS;                    \
+  }
+  NGA_SKINNY_CFGS(NGA_INFO)
+#undef NGA_INFO
+}
+
+void launch_skinny_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t stream) {
+  const int nblk = p.nN * p.nM * p.split;
+  if (nblk == 0) return;
+  dim3 grid(nblk), block(256);
+#define NGA_LAUNCH(ID, BN, BM, WN, NS)                                                    \
+  if (cfg == ID) {                                                                        \
+    if (epi == 0) skinny_gemm_kernel<BN, BM, WN, NS, 0><<<grid, block, 0, stream>>>(p);   \
+    else if (epi == 1) skinny_gemm_kernel<BN, BM, WN, NS, 1><<<grid, block, 0, stream>>>(p); \
+    else skinny_gemm_kernel<BN, BM, WN, NS, 2><<<grid, block, 0, stream>>>(p);            \
+    return;                                                                               \
+  }
+  NGA_SKINNY_CFGS(NGA_LAUNCH)
+#undef NGA_LAUNCH
+}
+
+void launch_splitk_reduce(const float* P, int S, int M, int N, uint16_t* out, int64_t ldo,
+                          hipStream_t stream) {
+  if (M == 0) return;
+  int64_t g = ((int64_t)M * (N / 8) + 255) / 256;
+  if (g > 2048) g = 2048;
+  splitk_reduce_kernel<<<(unsigned)g, 256, 0, stream>>>(P, S, M, N, out, ldo);
+}
+
+void launch_splitk_add_rmsnorm(const float* P, int S, int M, uint16_t* resid, const uint16_t* w,
+                               float eps, int H, uint16_t* out, hipStream_t stream) {
+  if (M == 0) return;
+  int t = (H / 8 + 63) / 64 * 64;
+  if (t < 64) t = 64;
+  splitk_add_rmsnorm_kernel<<<M, t, 0, stream>>>(P, S, M, resid, w, eps, H, out);
+}
+
+}  // namespace nga

@@ -156,4 +156,23 @@ void launch_moe_gemm(const MoeGemmParams& p, int bm, int mode, hipStream_t strea
 void launch_moe_combine(const uint16_t* y, const int32_t* inv, int T, int k, int H, uint16_t* out,
                         hipStream_t stream);
 
+// gemm_skinny.hip (decode-shape projection GEMM, out = x . W^T)
+struct SkinnyGemmParams {
+  const uint16_t* x;   // [M, K] rows, stride ldx (16-B aligned)
+  int64_t ldx;
+  const uint16_t* w;   // [rows, K] contiguous (epi 2: [2N, K] = [gate | up])
+  int M, N, K;         // N: output features; K % 64 == 0
+  int split;           // K slices (epi 1 only may exceed 1)
+  void* out;           // epi 0 / 2: bf16 [M, ldo]; epi 1: fp32 [split, M, N]
+  int64_t ldo;
+  int nN, nM;          // weight-row blocks, token-row tiles (set by the caller from the cfg)
+};
+int skinny_gemm_cfg_count();
+void skinny_gemm_cfg_info(int cfg, int* info);   // {BN, BM, WN, NSTAGE}
+void launch_skinny_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t stream);
+void launch_splitk_reduce(const float* P, int S, int M, int N, uint16_t* out, int64_t ldo,
+                          hipStream_t stream);
+void launch_splitk_add_rmsnorm(const float* P, int S, int M, uint16_t* resid, const uint16_t* w,
+                               float eps, int H, uint16_t* out, hipStream_t stream);
+
 }  // namespace nga

@@ -1180,9 +1180,6 @@ class LLMEngine:
         and parameters), upload, gather pipelined ids, replay."""
         tb, ndb = key
         S = self.cfg.max_num_seqs
-        g = self.mgraphs.get(key)
-        if g is None and self.gpu and not self.cfg.graph_eager:
-            g = self._capture_step_graph(key)
         if not follower:
             self.h_ids[ntok:tb] = 0
             self.h_pos[ntok:tb] = 0
@@ -1201,6 +1198,13 @@ class LLMEngine:
         self._pad_params(n, S)
         if not follower:
             self._sync_step(kind, n, ntok, max_q, max_ctx, 0, nd, gb=tb)
+        # lazy capture only after the step header and payload went out: under TP the warm-up
+        # and captured forwards issue all-reduces, which the followers (blocked in _recv_step
+        # until the broadcast) must meet in the same order. The capture leaves the host-side
+        # step layout alone and the upload below refills every device input it zeroed.
+        g = self.mgraphs.get(key)
+        if g is None and self.gpu and not self.cfg.graph_eager:
+            g = self._capture_step_graph(key)
         self._upload(n, tb, nparam=S, extra=((self.h_ctxd, self.d_ctxd, max(ndb, 1)),
                                              (self.h_items, self.d_items, max(len(items), 1)),
                                              (self.h_nitems, self.d_nitems, 1), (self.h_sidx, self.d_sidx, S)))

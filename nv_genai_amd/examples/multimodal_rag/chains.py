@@ -2,11 +2,11 @@
 RetrievalAugmentedGeneration/examples/multimodal_rag/chains.py,
 vectorstore/custom_pdf_parser.py, custom_powerpoint_parser.py, vectorstore_updater.py).
 
-ingest (.pdf/.pptx only): page / slide text, plus every embedded image sent to the vision
-client — first "is it a graph/plot/chart?", and for charts a chart-to-table pass whose
-linearised table the LLM then explains in plain English (the Neva -> DePlot -> LLM path);
-all texts are split with a 1000/100 character splitter and stored with
-``{"filename", "page"|"slide", "type"}`` metadata.
+ingest (.pdf/.pptx only): :mod:`.parsers` turns every page / slide into text, table and image
+documents — header/footer crop, ruled tables through DePlot + the LLM, captioned images that
+NeVA calls a graph/plot/chart explained the same way, PPTX speaker notes (the Neva -> DePlot ->
+LLM path); all documents are split with a 1000/100 character splitter and stored with the
+parser's metadata plus ``filename``.
 rag: "Relevant documents:" + retrieved chunks + "\\n\\n[[QUESTION]]\\n\\n" + query with
 ``rag_template`` as the system prompt. The reference builds that string from a list, which
 raises and always lands in its fallback branch (plain top-k, no score threshold — SURVEY.md
@@ -15,45 +15,18 @@ raises and always lands in its fallback branch (plain top-k, no score threshold 
 from __future__ import annotations
 
 import logging
-import os
-import re
-import zipfile
-import zlib
 from typing import Any, Dict, Generator, List
 
 from ...chain_server import utils
 from ...chain_server.base import BaseExample
 from ...connectors.vision import get_vision_client
-from ...index.vectorstore import Document
-from ...rag.loaders import load_file
 from ...rag.splitters import RecursiveCharacterTextSplitter
 from ..common import NO_CONTEXT, NO_DOCS, TracedExample
+from .parsers import CHART_WORDS, get_pdf_documents, process_ppt_file
 
 logger = logging.getLogger(__name__)
 CHART_SYSTEM = ("Your responsibility is to explain charts. You are an expert in describing the responses of "
                 "linearized tables into plain English text for LLMs to use.")
-
-
-def pdf_images(data: bytes) -> List[bytes]:
-    out = []
-    for m in re.finditer(rb"obj(.*?)stream\r?\n(.*?)\r?\nendstream", data, re.S):
-        head, body = m.group(1), m.group(2)
-        if b"/Subtype /Image" not in head and b"/Subtype/Image" not in head:
-            continue
-        if b"/DCTDecode" in head:
-            out.append(body)  # JPEG bytes as stored
-        elif b"/FlateDecode" in head:
-            try:
-                zlib.decompress(body)
-                out.append(body)
-            except zlib.error:
-                pass
-    return out
-
-
-def pptx_images(path: str) -> List[bytes]:
-    with zipfile.ZipFile(path) as z:
-        return [z.read(n) for n in sorted(z.namelist()) if n.startswith("ppt/media/")]
 
 
 class MultimodalRAG(BaseExample, TracedExample):
@@ -61,35 +34,36 @@ class MultimodalRAG(BaseExample, TracedExample):
         TracedExample.__init__(self)
         self.splitter = RecursiveCharacterTextSplitter(1000, 100)
 
-    def _image_texts(self, images: List[bytes], filename: str) -> List[Document]:
-        neva = get_vision_client("ai-neva-22b")
-        deplot = get_vision_client("ai-google-deplot")
-        docs = []
-        for i, img in enumerate(images):
-            desc = neva.describe(img, "Describe this image in detail", creativity=0, quality=9,
-                                 complexity=0, verbosity=9)
-            if any(w in desc.lower() for w in ("graph", "plot", "chart")):
-                table = deplot.describe(img, "Generate underlying data table of the figure below:")
-                desc = self.invoke_llm([("system", CHART_SYSTEM),
-                                        ("user", "Explain the following linearized table. " + table)])
-            docs.append(Document(desc, {"filename": filename, "type": "image", "image": i}))
-        return docs
+    # the reference's is_graph / process_graph (custom_pdf_parser.py:40-70) on JPEG q=20 bytes
+    def is_graph(self, jpeg: bytes) -> bool:
+        res = get_vision_client("ai-neva-22b").describe(jpeg, "Describe this image in detail", creativity=0,
+                                                        quality=9, complexity=0, verbosity=9)
+        return any(w in res for w in CHART_WORDS)
+
+    def process_graph(self, jpeg: bytes) -> str:
+        table = get_vision_client("ai-google-deplot").describe(jpeg, "Generate underlying data table of the figure below:")
+        return self.invoke_llm([("system", CHART_SYSTEM), ("user", "Explain the following linearized table. " + table)])
+
+    def ocr(self, jpeg: bytes) -> str:
+        """Page transcription for PDF pages without a text layer (the reference runs tesseract,
+        custom_pdf_parser.py:142-165, not installed here: the vision model reads the page)."""
+        return get_vision_client("ai-neva-22b").describe(jpeg, "Transcribe all the text in this image", creativity=0,
+                                                         quality=9, complexity=0, verbosity=9)
 
     def ingest_docs(self, filepath: str, filename: str):
         if not filename.endswith((".pdf", ".pptx")):
             raise ValueError(f"{filename} is not a valid PDF/PPTX file. Only PDF/PPTX files are supported for "
                              "multimodal rag. The PDF/PPTX files can contain multimodal data.")
         try:
-            docs = load_file(filepath, filename)
-            for d in docs:
-                d.metadata.update({"filename": filename, "type": "text"})
             if filename.endswith(".pdf"):
-                with open(filepath, "rb") as f:
-                    images = pdf_images(f.read())
+                docs = [d for page in get_pdf_documents(filepath, self.is_graph, self.process_graph, ocr=self.ocr)
+                        for d in page]
             else:
-                images = pptx_images(filepath)
-            docs += self._image_texts(images, filename)
-            utils.get_vectorstore().add_documents(self.splitter.split_documents(docs))
+                docs = process_ppt_file(filepath, self.is_graph, self.process_graph)
+            docs = self.splitter.split_documents(docs)
+            for d in docs:
+                d.metadata["filename"] = filename
+            utils.get_vectorstore().add_documents(docs)
         except Exception as e:
             logger.error("Failed to ingest document due to exception %s", e)
             raise ValueError("Failed to upload document. Please upload an unstructured text document.")

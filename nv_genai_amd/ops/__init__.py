@@ -117,6 +117,59 @@ def linear_rows_split(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tens
     return out
 
 
+def skinny_gemm(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, epi: int = 0,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Decode-shape projection GEMM (gemm_skinny.hip) with an explicit tile configuration:
+    ``epi`` 0 -> bf16 ``x @ w^T``; 1 -> fp32 partial slabs [split, M, N] (K split ``split`` ways);
+    2 -> SwiGLU ``silu(x @ w[:F]^T) * (x @ w[F:]^T)`` [M, F]. CPU tensors: the fp32 reference."""
+    M = x.shape[0]
+    if not _gpu(x):
+        y = x.float() @ w.float().t()
+        if epi == 2:
+            F = w.shape[0] // 2
+            return (torch.nn.functional.silu(y[:, :F]) * y[:, F:]).to(x.dtype)
+        if epi == 1:   # one slab holding the whole sum, the rest zero
+            p = torch.zeros(split, M, w.shape[0])
+            p[0] = y
+            return p
+        return y.to(x.dtype)
+    N = w.shape[0] // 2 if epi == 2 else w.shape[0]
+    if out is None:
+        out = (torch.empty(split, M, N, dtype=torch.float32, device=x.device) if epi == 1
+               else torch.empty(M, N, dtype=x.dtype, device=x.device))
+    kernels().skinny_gemm(out, x, w, int(epi), int(split), int(cfg))
+    return out
+
+
+def splitk_reduce(P: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 sum of the K-split partial slabs P [S, M, N]."""
+    S, M, N = P.shape
+    if not _gpu(P):
+        return P.sum(0).to(torch.bfloat16)
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=P.device)
+    kernels().splitk_reduce(out, P, int(S))
+    return out
+
+
+def splitk_add_rmsnorm(resid: torch.Tensor, P: torch.Tensor, w: torch.Tensor, eps: float,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """resid += sum of the partial slabs P [S, M, H] (in place, one bf16 rounding); returns
+    rmsnorm(resid) * w."""
+    if not _gpu(resid):
+        s = (resid.float() + P.float().sum(0)).to(resid.dtype)
+        resid.copy_(s)
+        r = ref.rmsnorm(resid, w, eps)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    if out is None:
+        out = torch.empty_like(resid)
+    kernels().splitk_add_rmsnorm(out, resid, P, int(P.shape[0]), w, float(eps))
+    return out
+
+
 def silu_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None):
     if not _gpu(x):
         return ref.silu_mul(x)
@@ -561,6 +614,9 @@ def search_topk(Q: torch.Tensor, X: torch.Tensor, row_bias=None, dot_scale: floa
     return v, r
 
 
+IVF_MAX_ITEMS = 65535   # score_topk's work-item limit (grid dimension)
+
+
 def ivf_search_topk(Q: torch.Tensor, X: torch.Tensor, row_bias, dot_scale: float, probes: torch.Tensor,
                     list_beg: torch.Tensor, list_end: torch.Tensor, max_list_rows: int, k: int):
     """IVF list scan (K14) for a batch of queries in one launch: the (query, probe) pairs are
@@ -582,6 +638,13 @@ def ivf_search_topk(Q: torch.Tensor, X: torch.Tensor, row_bias, dot_scale: float
         raise ValueError(f"IVF search: k={k} above the fused kernel's limit {C.score_topk_kmax(qpi)}")
     chunks = -(-nq // 64)
     n_items = nlist * chunks
+    max_q = 64 * (IVF_MAX_ITEMS // nlist)
+    if n_items > IVF_MAX_ITEMS:
+        # the scan launch takes at most 65,535 (list, 64-query chunk) items: run the queries
+        # in sub-batches that fit (nlist 4,096: 1,024 queries per launch)
+        parts = [ivf_search_topk(Q[i:i + max_q], X, row_bias, dot_scale, probes[i:i + max_q], list_beg,
+                                 list_end, max_list_rows, k) for i in range(0, nq, max_q)]
+        return torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
     probes = probes.to(torch.int64).contiguous()
     # one block groups the pairs by list: slot -> query, slot -> pair (candidate row)
     qtab = torch.empty(n_items * 64, dtype=torch.int32, device=dev)

@@ -151,9 +151,27 @@ class CustomAllReduce:
         return ok
 
 
+_STATUS = {"state": "not requested"}
+_LAST = None
+
+
+def status() -> dict:
+    """Outcome of this process's last :func:`maybe_create` (for run records): ``state`` is
+    "not requested", "off" (world / device / NGA_CUSTOM_AR), "failed" (construction raised),
+    "self-test failed" (RCCL takes every all-reduce) or "enabled"; with the one-/two-shot call
+    counts of the Python entry point (calls recorded into a hipGraph count once, at capture)."""
+    s = dict(_STATUS)
+    if _LAST is not None:
+        s["algo_counts"] = {"one_shot": _LAST.algo_counts.get(ALGO_ONE_SHOT, 0),
+                            "two_shot": _LAST.algo_counts.get(ALGO_TWO_SHOT, 0)}
+    return s
+
+
 def maybe_create(group, world: int) -> Optional[CustomAllReduce]:
     """The TP group's custom all-reduce, or None when it does not apply (CPU, world 1 or
     > 8, ``NGA_CUSTOM_AR=0``). Collective: every rank of ``group`` must call it."""
+    global _STATUS, _LAST
+    _STATUS = {"state": "off", "world": world}
     if world <= 1 or world > 8 or not torch.cuda.is_available():
         return None
     if os.environ.get("NGA_CUSTOM_AR", "1") == "0":
@@ -162,5 +180,9 @@ def maybe_create(group, world: int) -> Optional[CustomAllReduce]:
         car = CustomAllReduce(group, capacity_mb=float(os.environ.get("NGA_CUSTOM_AR_MB", "64")))
     except Exception as e:  # noqa: BLE001
         log.warning("custom all-reduce unavailable (%r); TP all-reduces use RCCL", e)
+        _STATUS = {"state": "failed", "world": world, "error": repr(e)[:200]}
         return None
-    return car if car.enabled else None
+    _STATUS = {"state": "enabled" if car.enabled else "self-test failed", "world": world,
+               "self_test_passed": bool(car.enabled)}
+    _LAST = car if car.enabled else None
+    return _LAST

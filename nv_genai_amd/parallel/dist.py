@@ -92,7 +92,10 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
     world, rank, local = env_world()
     use_gpu = torch.cuda.is_available() if device is None else device.startswith("cuda")
     ngpu = torch.cuda.device_count() if use_gpu else 0
-    oversubscribed = use_gpu and world > ngpu
+    # ranks on THIS node against its GPUs (a multi-node job has world > device_count on
+    # every node and must stay on RCCL)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    oversubscribed = use_gpu and local_world > ngpu
     if oversubscribed:
         # more local ranks than GPUs (a multi-rank rehearsal on a 1-GPU box): ranks share
         # devices round-robin and the host-side groups go over gloo, since RCCL refuses two

@@ -5,6 +5,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 
 def test_multi_turn_benchmark_cpu(tmp_path):
     out = tmp_path / "mt.json"
@@ -76,3 +78,27 @@ def test_headline_bench_self_launches_for_gpus_n():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["world_size"] == 2 and res["config"]["parallelism"] == "dp2"
     assert len(res["per_replica_qps"]) == 2 and res["config"]["global_batch"] == 6
+    # the run record names each rank's device and the backend (CPU ranks here)
+    assert res["shared_devices"] is False and res["devices"]["backend"] == "gloo"
+    assert [r["rank"] for r in res["devices"]["ranks"]] == [0, 1]
+
+
+def test_bench_refuses_shared_devices_without_flag(monkeypatch):
+    """More ranks on the node than GPUs: refused unless --allow-shared-devices (then reported
+    as shared); no GPUs at all (CPU rehearsal) or enough GPUs: allowed."""
+    import bench
+    import torch
+
+    args = bench.parse(["--gpus", "8"])
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    with pytest.raises(SystemExit, match="refusing"):
+        bench.check_devices(args, 8)
+    assert bench.check_devices(bench.parse(["--gpus", "8", "--allow-shared-devices"]), 8) is True
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    assert bench.check_devices(args, 8) is False
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
+    assert bench.check_devices(args, 8) is False
+    # multi-node: 16 ranks, 8 on this node with 8 GPUs
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    assert bench.check_devices(args, 16) is False

@@ -642,3 +642,47 @@ def test_embedding_gather(gpu):
         got = ops.embedding(ids, table, lo, scale)
         want = ref.embedding(ids.cpu(), table.cpu(), lo, scale)
         assert torch.equal(got.cpu(), want)
+
+
+# ------------------------------------------------------------ decode-shape projection GEMM
+def _skinny_ref(x, w, epi):
+    y = x.float().cpu() @ w.float().cpu().t()
+    if epi == 2:
+        F = w.shape[0] // 2
+        y = torch.nn.functional.silu(y[:, :F]) * y[:, F:]
+    return y
+
+
+@pytest.mark.parametrize("M", [1, 17, 64, 200, 256, 512])
+def test_skinny_gemm_every_cfg(gpu, M):
+    """Every tile configuration x epilogue (bf16, fp32 K-split slabs, fused SwiGLU) against the
+    fp32 reference, including ragged token tiles (M = 1, 17, 200) and a ragged last weight
+    block (N = 1000 with BN 64-256); per-row relative error."""
+    C = ops.kernels()
+    torch.manual_seed(M)
+    K = 1024
+    x = _bf(M, K, dev=gpu)
+    w = _bf(1000, K, dev=gpu, scale=0.05)
+    wg = _bf(2 * 512, K, dev=gpu, scale=0.05)
+    ref0, ref2 = _skinny_ref(x, w, 0), _skinny_ref(x, wg, 2)
+    for cfg in range(C.skinny_cfg_count()):
+        BN, BM = C.skinny_cfg(cfg)[:2]
+        _close_rows(ops.skinny_gemm(x, w, cfg, 1, 0), ref0, rel=1e-2)
+        for s in (2, 5):
+            P = ops.skinny_gemm(x, w, cfg, s, 1)
+            _close_rows(P.sum(0), ref0, rel=1e-4)
+            _close_rows(ops.splitk_reduce(P), ref0, rel=1e-2)
+        if 512 % (BN // 2) == 0:
+            _close_rows(ops.skinny_gemm(x, wg, cfg, 1, 2), ref2, rel=2e-2)
+
+
+def test_splitk_add_rmsnorm(gpu):
+    torch.manual_seed(3)
+    S, M, H = 4, 77, 4096
+    P = torch.randn(S, M, H, device=gpu) * 0.3
+    resid, w = _bf(M, H, dev=gpu), _bf(H, dev=gpu)
+    r_ref = resid.cpu().float() + P.cpu().sum(0)
+    y_ref = ref.rmsnorm(r_ref.to(torch.bfloat16).float(), w.cpu().float(), 1e-5)
+    y = ops.splitk_add_rmsnorm(resid, P, w, 1e-5)
+    _close_rows(resid, r_ref, rel=5e-3)
+    _close_rows(y, y_ref, rel=1e-2)

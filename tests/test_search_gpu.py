@@ -90,6 +90,25 @@ def test_ivf_scan_matches_reference(gpu, nq, nprobe, k):
     assert bool((r[~fin] == -1).all())
 
 
+def test_ivf_scan_splits_past_item_limit(gpu):
+    """nlist 4,096 with 1,100 queries is 4,096 x 18 = 73,728 (list, query-chunk) items, past
+    the scan launch's 65,535: the queries run in two sub-batches and still match the reference."""
+    N, D, nlist, nq, nprobe, k = 40_000, 128, 4096, 1100, 4, 4
+    X, Q = _data(N, D, nq, 23, gpu)
+    sizes = torch.randint(0, 2 * N // nlist, (nlist,), generator=torch.Generator().manual_seed(2))
+    off = torch.cat([torch.zeros(1, dtype=torch.int64), sizes.cumsum(0)])
+    Xs = X[: int(off[-1])].contiguous()
+    beg, end = off[:-1].to(gpu), off[1:].to(gpu)
+    g = torch.Generator().manual_seed(5)
+    probes = torch.stack([torch.randperm(nlist, generator=g)[:nprobe] for _ in range(nq)]).to(gpu)
+    assert nlist * -(-nq // 64) > ops.IVF_MAX_ITEMS
+    v, r = ops.ivf_search_topk(Q, Xs, None, 1.0, probes, beg, end, int(sizes.max()), k)
+    rv, rr = ref.ivf_search_topk(Q, Xs, None, 1.0, probes, beg, end, k)
+    fin = torch.isfinite(rv)
+    assert v.shape == (nq, k) and torch.equal(torch.isfinite(v), fin)
+    assert torch.allclose(v[fin], rv[fin], atol=2e-3, rtol=1e-3)
+
+
 def test_ivf_index_recall_vs_flat_nlist64_nprobe16(gpu):
     """The reference's GPU_IVF_FLAT setting (nlist 64, nprobe 16) on clustered data: batched
     IVF search finds >= 95% of the flat index's top-10 (RetrievalAugmentedGeneration/common/
