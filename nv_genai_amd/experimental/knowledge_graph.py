@@ -10,10 +10,16 @@
 * retrieval: entities of the question are matched against graph nodes, their 1-2 hop
   neighbourhood is rendered as "subject relation object" facts (graphRAG), the text store is
   searched with hybrid dense+BM25 RRF (textRAG), or both (combinedRAG);
-* evaluation hook: answers of the three modes can be scored by any judge callable.
+* typed extraction (subject / subject type / relation / object / object type, the reference's
+  5-tuples, utils/preprocessor.py:26-80) and the entities / relations / triples CSV export
+  (utils/lc_graph.py:83-128);
+* evaluation: :mod:`nv_genai_amd.experimental.kg_eval` (QA generation, the three answer modes,
+  5-attribute reward scores, the reference's CSVs).
 """
 from __future__ import annotations
 
+import ast
+import csv
 import json
 import logging
 import os
@@ -42,6 +48,84 @@ def parse_triples(text: str) -> List[Tuple[str, str, str]]:
     for a, b, c in re.findall(r'\[\s*"([^"]+)"\s*,\s*"([^"]+)"\s*,\s*"([^"]+)"\s*\]', text):
         out.append((a, b, c))
     return out
+
+
+# typed extraction: entity categories and relation verbs of the reference's extraction prompt
+ENTITY_TYPES = ("ORG", "ORG/GOV", "ORG/REG", "PERSON", "GPE", "INSTITUTION", "PRODUCT", "EVENT", "FIELD",
+                "METRIC", "TOOL", "CONCEPT")
+RELATIONS = ("Has", "Announce", "Operate_In", "Introduce", "Produce", "Control", "Participates_In", "Impact",
+             "Positive_Impact_On", "Negative_Impact_On", "Relate_To", "Is_Member_Of", "Invests_In", "Raise",
+             "Decrease")
+TYPED_EXTRACT_PROMPT = (
+    "Extract knowledge-graph triples from the text as a Python list of tuples "
+    "(head, head_type, relation, object, object_type). Entity types: " + ", ".join(ENTITY_TYPES) +
+    ". Relations must be one of: " + ", ".join(RELATIONS) + ". Entities are specific names of at most "
+    "three words (no dates, numbers or percentages); merge aliases of the same entity. Output only the list."
+    "\n\nText:\n{text}")
+TRIPLE_KEYS = ("subject", "subject_type", "relation", "object", "object_type")
+
+
+def parse_typed_triples(text: str) -> List[Dict[str, str]]:
+    """The LLM's list of 5-tuples (Python or JSON literal, possibly fenced) as dicts with the
+    reference's keys; malformed tuples are skipped (process_response, preprocessor.py:26-43)."""
+    m = re.search(r"\[.*\]", text, re.S)
+    if not m:
+        return []
+    try:
+        items = ast.literal_eval(m.group(0))
+    except (ValueError, SyntaxError):
+        try:
+            items = json.loads(m.group(0))
+        except json.JSONDecodeError:
+            return []
+    out = []
+    for t in items if isinstance(items, (list, tuple)) else []:
+        if isinstance(t, (list, tuple)) and len(t) == 5 and all(isinstance(x, str) and x.strip() for x in t):
+            out.append(dict(zip(TRIPLE_KEYS, (x.strip() for x in t))))
+    return out
+
+
+def extract_typed_triples(text: str, llm) -> List[Dict[str, str]]:
+    return parse_typed_triples(llm.invoke([("user", TYPED_EXTRACT_PROMPT.format(text=text))]))
+
+
+def save_triples_to_csvs(triples: Sequence[Dict[str, str]], out_dir: str = ".") -> Dict[str, str]:
+    """entities.csv (entity_id, entity_name, entity_type), relations.csv (relation_id,
+    relation_name) and triples.csv (entity_id_1, relation_id, entity_id_2), ids in first-seen
+    order; an entity's type is its type where it first appears as a subject, else as an
+    object (lc_graph.py:83-128). Returns the three paths."""
+    rel_ids: Dict[str, int] = {}
+    for t in triples:
+        rel_ids.setdefault(t["relation"], len(rel_ids))
+    ent_ids: Dict[str, int] = {}
+    for t in triples:
+        ent_ids.setdefault(t["subject"], len(ent_ids))
+    for t in triples:
+        ent_ids.setdefault(t["object"], len(ent_ids))
+    ent_type: Dict[str, str] = {}
+    for t in triples:
+        ent_type.setdefault(t["subject"], t["subject_type"])
+    for t in triples:
+        if t["object"] not in ent_type and t.get("object_type"):
+            ent_type[t["object"]] = t["object_type"]
+    os.makedirs(out_dir, exist_ok=True)
+    paths = {k: os.path.join(out_dir, f"{k}.csv") for k in ("entities", "relations", "triples")}
+    with open(paths["entities"], "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["entity_id", "entity_name", "entity_type"])
+        for e, i in ent_ids.items():
+            w.writerow([i, e, ent_type.get(e, "Unknown")])
+    with open(paths["relations"], "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["relation_id", "relation_name"])
+        for r, i in rel_ids.items():
+            w.writerow([i, r])
+    with open(paths["triples"], "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["entity_id_1", "relation_id", "entity_id_2"])
+        for t in triples:
+            w.writerow([ent_ids[t["subject"]], rel_ids[t["relation"]], ent_ids[t["object"]]])
+    return paths
 
 
 def save_checkpoint(triples: List[Sequence[str]], processed: List[str], path: str) -> None:
@@ -75,6 +159,23 @@ class KnowledgeGraph:
     def add_triples(self, triples: Iterable[Sequence[str]]):
         for s, r, o in triples:
             self.g.add_edge(s.lower(), o.lower(), relation=r)
+
+    def add_typed(self, triples: Iterable[Dict[str, str]]):
+        for t in triples:
+            s, o = t["subject"].lower(), t["object"].lower()
+            self.g.add_edge(s, o, relation=t["relation"])
+            self.g.nodes[s].setdefault("type", t.get("subject_type"))
+            self.g.nodes[o].setdefault("type", t.get("object_type"))
+
+    def entity_knowledge(self, entity: str, depth: int = 2) -> List[str]:
+        """"subject relation object" along a depth-limited DFS from ``entity`` (LangChain's
+        NetworkxEntityGraph.get_entity_knowledge, used by evaluation.py:98-135)."""
+        import networkx as nx
+
+        e = entity.lower()
+        if not self.g.has_node(e):
+            return []
+        return [f"{a} {self.g[a][b]['relation']} {b}" for a, b in nx.dfs_edges(self.g, e, depth_limit=depth)]
 
     def entities_in(self, text: str) -> List[str]:
         t = text.lower()

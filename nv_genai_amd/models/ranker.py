@@ -93,26 +93,34 @@ class DecoderRanker:
     def forward(self, ids: torch.Tensor, pos: torch.Tensor, cu: torch.Tensor, max_len: int,
                 type_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Packed pairs -> [B, 1] fp32 relevance logits."""
-        m = self.lm
-        hq, hkv, D = m.hq, m.hkv, m.D
-        qd, kd = hq * D, hkv * D
-        resid = m.embed_tokens(ids)
-        L0 = m.layers[0]
-        x = m._norm(resid, L0["attn_norm"], L0.get("attn_norm_b"))
-        n = len(m.layers)
-        d = None
-        for li in range(n):
-            L = m.layers[li]
-            qkv = m._qkv(x, L)
-            ops.rope_cache_(qkv, pos, m.cos_sin, None, None, None, hq, hkv, D)
-            a = ops.varlen_attention(qkv[:, :qd], qkv[:, qd:qd + kd], qkv[:, qd + kd:], cu, hq, hkv, D,
-                                     max_len, m.scale, causal=False)
-            o = m._bias_rank0(m._lin(a, L, "wo"), L.get("bo"))
-            x = m._add_norm(resid, o, L["mlp_norm"], L.get("mlp_norm_b"))
-            d = m._mlp(x, L)
-            if li + 1 < n:
-                Ln = m.layers[li + 1]
-                x = m._add_norm(resid, d, Ln["attn_norm"], Ln.get("attn_norm_b"))
-        h = m._add_norm(resid, d, m.final_norm, m.final_norm_b)
+        h = packed_hidden(self.lm, ids, pos, cu, max_len, causal=False)
         pooled = ops.pool_l2norm(h, cu, 1, False)                     # masked mean, fp32
         return pooled @ self.head_w.float().t() + self.head_b
+
+
+def packed_hidden(m: LlamaModel, ids: torch.Tensor, pos: torch.Tensor, cu: torch.Tensor, max_len: int,
+                  causal: bool) -> torch.Tensor:
+    """Final-normed hidden rows of packed sequences through a decoder's weights and kernels,
+    with no KV cache: RMSNorm (fused residual add), the fused QKV GEMM, RoPE without a cache
+    write, packed GQA MFMA attention (bidirectional for the ranker, causal for the reward
+    model), the MLP."""
+    hq, hkv, D = m.hq, m.hkv, m.D
+    qd, kd = hq * D, hkv * D
+    resid = m.embed_tokens(ids)
+    L0 = m.layers[0]
+    x = m._norm(resid, L0["attn_norm"], L0.get("attn_norm_b"))
+    n = len(m.layers)
+    d = None
+    for li in range(n):
+        L = m.layers[li]
+        qkv = m._qkv(x, L)
+        ops.rope_cache_(qkv, pos, m.cos_sin, None, None, None, hq, hkv, D)
+        a = ops.varlen_attention(qkv[:, :qd], qkv[:, qd:qd + kd], qkv[:, qd + kd:], cu, hq, hkv, D,
+                                 max_len, m.scale, causal=causal)
+        o = m._bias_rank0(m._lin(a, L, "wo"), L.get("bo"))
+        x = m._add_norm(resid, o, L["mlp_norm"], L.get("mlp_norm_b"))
+        d = m._mlp(x, L)
+        if li + 1 < n:
+            Ln = m.layers[li + 1]
+            x = m._add_norm(resid, d, Ln["attn_norm"], Ln.get("attn_norm_b"))
+    return m._add_norm(resid, d, m.final_norm, m.final_norm_b)

@@ -27,6 +27,8 @@ import time
 import uuid
 from typing import Any, Dict, List, Optional, Union
 
+import torch
+
 from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
 from pydantic import BaseModel, Field
@@ -127,14 +129,18 @@ def _has_images(messages) -> bool:
 def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name: str = "meta/llama3-8b-instruct",
                embed_name: str = "snowflake/arctic-embed-l", rerank_name: str = "nv-rerank-qa-mistral-4b:1",
                batch_delay_s: float = 0.002, vlm=None, vlm_service=None, vlm_name: str = "ai-neva-22b",
-               deplot=None, deplot_names=("google/deplot", "ai-google-deplot")) -> FastAPI:
+               deplot=None, deplot_names=("google/deplot", "ai-google-deplot"), reward=None,
+               reward_name: str = "nvidia/nemotron-4-340b-reward") -> FastAPI:
     """``vlm`` / ``vlm_service``: a :class:`~nv_genai_amd.models.vision.VisionLanguageModel`
     and the :class:`EngineService` over its engine; chat requests with ``image_url`` parts
     (or ``model == vlm_name``) go there — the NeVA / DePlot endpoint contract of the
     reference's multimodal example (examples/multimodal_rag/llm/llm_client.py:37-42).
     ``deplot``: a :class:`~nv_genai_amd.models.pix2struct.DePlot` chart-to-table model; chat
     requests naming one of ``deplot_names`` are answered by it (the images of the request, its
-    text as the rendered header prompt; custom_pdf_parser.py:55-71)."""
+    text as the rendered header prompt; custom_pdf_parser.py:55-71). ``reward``: a
+    :class:`~nv_genai_amd.models.reward.RewardModel`; chat requests naming ``reward_name``
+    score their last user / assistant turns and answer "helpfulness:x,correctness:y,..." (the
+    reward endpoint the KG-RAG evaluation calls, evaluation.py:38-56)."""
     app = FastAPI(title="nv_genai_amd model server")
     metrics = Registry()
 
@@ -154,6 +160,7 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
     app.state.llm, app.state.embed, app.state.rerank, app.state.batcher = llm_service, embed_engine, rerank_engine, batcher
     app.state.vlm, app.state.vlm_service = vlm, vlm_service
     app.state.deplot = deplot
+    app.state.reward = reward
     deplot_batcher = None
     if deplot is not None:
         from ..models.pix2struct import DePlotBatcher
@@ -247,6 +254,19 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
         metrics.inc("chat_requests_total")
         if req.stream and req.n > 1:
             return JSONResponse({"error": "stream supports n = 1"}, status_code=400)
+        if app.state.reward is not None and req.model == reward_name:
+            from ..models.reward import format_scores
+
+            q = next((_content_text(m.content) for m in reversed(req.messages) if m.role == "user"), "")
+            a = next((_content_text(m.content) for m in reversed(req.messages) if m.role == "assistant"), "")
+            with tracer.span("chat.completions.reward", {"model": req.model}, request.headers.get("traceparent")):
+                sc = await asyncio.get_running_loop().run_in_executor(None, app.state.reward.score, q, a)
+            metrics.observe("request_seconds", time.perf_counter() - t0)
+            return {"id": f"chatcmpl-{uuid.uuid4().hex}", "object": "chat.completion", "created": int(time.time()),
+                    "model": req.model, "choices": [{"index": 0, "message": {"role": "assistant",
+                                                                             "content": format_scores(sc)},
+                                                     "finish_reason": "stop"}],
+                    "usage": {"prompt_tokens": 0, "completion_tokens": 0, "total_tokens": 0}}
         if app.state.deplot is not None and req.model in deplot_names:
             with tracer.span("chat.completions.deplot", {"model": req.model}, request.headers.get("traceparent")):
                 try:
@@ -418,6 +438,8 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
             out.append({"id": embed_name, "object": "model", "owned_by": "nv_genai_amd"})
         if app.state.rerank is not None:
             out.append({"id": rerank_name, "object": "model", "owned_by": "nv_genai_amd"})
+        if app.state.reward is not None:
+            out.append({"id": reward_name, "object": "model", "owned_by": "nv_genai_amd"})
         return {"object": "list", "data": out}
 
     @app.get("/v1/health/live")
@@ -453,6 +475,8 @@ def main(argv=None):
     ap.add_argument("--rerank", default="", help="reranker preset ('' to disable)")
     ap.add_argument("--vlm", default="", help="vision-language preset, e.g. neva-22b ('' to disable)")
     ap.add_argument("--deplot", default="", help="Pix2Struct chart-to-table preset, e.g. deplot ('' to disable)")
+    ap.add_argument("--reward", default="", help="reward model served as nvidia/nemotron-4-340b-reward, e.g. "
+                    "nvidia/nemotron-4-340b-reward or reward-small ('' to disable)")
     ap.add_argument("--weights", default="", help="safetensors dir for the LLM")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=8000)
@@ -500,8 +524,13 @@ def main(argv=None):
         from ..models.pix2struct import DePlot
 
         dp = DePlot(args.deplot, device=args.device)
+    rw = None
+    if args.reward:
+        from ..models.reward import RewardModel
+
+        rw = RewardModel(args.reward, device=args.device or ("cuda" if torch.cuda.is_available() else "cpu"))
     app = create_app(svc, emb, rr, vlm=vlm, vlm_service=vsvc, vlm_name=f"ai-{args.vlm}" if args.vlm else "ai-neva-22b",
-                     deplot=dp)
+                     deplot=dp, reward=rw)
     uvicorn.run(app, host=args.host, port=args.port, log_level=os.environ.get("LOGLEVEL", "info").lower())
 
 

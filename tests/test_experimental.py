@@ -197,3 +197,117 @@ def test_advanced_chat_turn_memory_factcheck_feedback(tmp_path):
     fb = FeedbackLog(str(tmp_path / "fb.jsonl"))
     row = fb.submit({"score": "🙂", "text": "ok"}, "q", "r")
     assert row["score"] == 4 and json.loads((tmp_path / "fb.jsonl").read_text())["comment"] == "Score: 4/5. Feedback: ok"
+
+
+# ---------------------------------------------------------------- KG-RAG evaluation (E4)
+class EvalLLM:
+    """QA generation, entity lists and answers for the evaluation pipeline."""
+
+    def __init__(self):
+        self.prompts = []
+
+    def invoke(self, messages, **kw):
+        text = messages[-1][1]
+        self.prompts.append((messages[0][1][:40], text))
+        if "synthetic evaluation data" in messages[0][1]:
+            if "weather" in text:
+                return "no json here"                    # dropped, like the reference
+            return '```json\n{"question": "What memory does the MI355X have?", "answer": "288 GB of HBM3E."}\n```'
+        if text.startswith("Return a JSON with a single key 'entities'"):
+            return '{"entities": ["MI355X"]}' if "MI355X" in text else "not json"
+        return "ANSWER(" + text.replace("\n", " ") + ")"
+
+
+def test_typed_triples_csv_export(tmp_path):
+    """entities / relations / triples CSVs of lc_graph.save_triples_to_csvs: ids in first-seen
+    order, entity types from the first subject (else object) occurrence."""
+    import csv
+
+    from nv_genai_amd.experimental.knowledge_graph import KnowledgeGraph, parse_typed_triples, save_triples_to_csvs
+
+    tr = parse_typed_triples("```[('AMD', 'ORG', 'Produce', 'MI355X', 'PRODUCT'), "
+                             "('MI355X', 'PRODUCT', 'Has', 'HBM3E', 'PRODUCT'), ('bad', 'tuple'), "
+                             "('AMD', 'ORG', 'Invests_In', 'ROCm', 'TOOL')]```")
+    assert len(tr) == 3 and tr[0]["subject_type"] == "ORG"
+    paths = save_triples_to_csvs(tr, str(tmp_path))
+    ents = list(csv.DictReader(open(paths["entities"])))
+    assert [(e["entity_id"], e["entity_name"], e["entity_type"]) for e in ents] == [
+        ("0", "AMD", "ORG"), ("1", "MI355X", "PRODUCT"), ("2", "HBM3E", "PRODUCT"), ("3", "ROCm", "TOOL")]
+    rels = list(csv.DictReader(open(paths["relations"])))
+    assert [r["relation_name"] for r in rels] == ["Produce", "Has", "Invests_In"]
+    trip = list(csv.DictReader(open(paths["triples"])))
+    assert [(t["entity_id_1"], t["relation_id"], t["entity_id_2"]) for t in trip] == [("0", "0", "1"), ("1", "1", "2"),
+                                                                                    ("0", "2", "3")]
+    kg = KnowledgeGraph()
+    kg.add_typed(tr)
+    assert kg.entity_knowledge("amd") == ["amd Produce mi355x", "mi355x Has hbm3e", "amd Invests_In rocm"]
+    assert kg.entity_knowledge("AMD", depth=1) == ["amd Produce mi355x", "amd Invests_In rocm"]
+    assert kg.g.nodes["rocm"]["type"] == "TOOL"
+
+
+def test_kg_evaluation_pipeline_writes_reference_csvs(tmp_path):
+    """QA pairs -> text / graph / combined answers -> 5-attribute reward scores from the
+    framework's reward model -> combined_results_with_scores.csv with the reference's columns
+    (pages/evaluation.py:156-258)."""
+    import csv
+
+    from nv_genai_amd.experimental.kg_eval import KGEvaluator, create_qa_pairs, mean_scores, read_csv
+    from nv_genai_amd.experimental.knowledge_graph import KnowledgeGraph
+    from nv_genai_amd.models.reward import ATTRIBUTES, RewardModel
+    from nv_genai_amd.rag.hybrid import HybridRetriever
+
+    llm = EvalLLM()
+    chunks = ["the mi355x gpu has 288 gb of hbm3e memory", "the weather today is sunny"]
+    qa = create_qa_pairs(chunks, llm, num=2, out_csv=str(tmp_path / "qa_data.csv"))
+    assert len(qa) == 1 and read_csv(str(tmp_path / "qa_data.csv")) == qa
+    kg = KnowledgeGraph()
+    kg.add_triples([("MI355X", "has", "HBM3E"), ("HBM3E", "capacity", "288 GB")])
+    hr = HybridRetriever(_store())
+    ev = KGEvaluator(kg, llm, search=lambda q, k: [d.page_content for d, _ in hr.search(q, k, pipeline="hybrid")])
+    rows = ev.run(qa + [{"question": "How is the weather?", "answer": "sunny"}],
+                  out_csv=str(tmp_path / "combined_results.csv"))
+    with open(tmp_path / "combined_results.csv") as f:
+        assert next(csv.reader(f)) == ["question", "gt_answer", "textRAG_answer", "graphRAG_answer", "combined_answer"]
+    r0 = rows[0]
+    assert "Here are the relevant passages from the knowledge base" in r0["textRAG_answer"]
+    assert "relationships from the knowledge graph" in r0["graphRAG_answer"]
+    ctx = [t for _, t in llm.prompts if t.startswith("Context: Here are the relevant") and "relationships" in t]
+    assert ctx and "mi355x has hbm3e" in ctx[0] and "hbm3e capacity 288 gb" in ctx[0]     # depth-2 DFS
+    assert "No graph triples were available" in rows[1]["graphRAG_answer"]            # entity JSON failed
+    rm = RewardModel("reward-tiny", device="cpu", dtype=__import__("torch").float32)
+    scored = ev.score(rows, rm, out_csv=str(tmp_path / "combined_results_with_scores.csv"))
+    with open(tmp_path / "combined_results_with_scores.csv") as f:
+        header = next(csv.reader(f))
+    assert header[:5] == ["question", "gt_answer", "textRAG_answer", "graphRAG_answer", "combined_answer"]
+    assert header[5:] == [f"{s}_{m}" for s in ("gt", "textRAG", "graphRAG", "combinedRAG") for m in ATTRIBUTES]
+    vals = [float(scored[0][c]) for c in header[5:]]
+    assert all(0.0 <= v <= 4.0 for v in vals) and len(set(vals)) > 1
+    # one packed forward per row equals scoring each pair alone
+    single = rm.score(rows[0]["question"], rows[0]["textRAG_answer"])
+    assert all(abs(single[m] - scored[0][f"textRAG_{m}"]) < 1e-3 for m in ATTRIBUTES)
+    ms = mean_scores(scored)
+    assert set(ms) == {"gt", "textRAG", "graphRAG", "combinedRAG"} and set(ms["gt"]) == set(ATTRIBUTES)
+
+
+def test_reward_endpoint_contract():
+    """The model server answers the reward model's name with "helpfulness:x,..." content;
+    RewardClient / parse_scores read it back (the reference's get_reward_scores format)."""
+    import torch
+    from fastapi.testclient import TestClient
+
+    from nv_genai_amd.experimental.kg_eval import RewardClient
+    from nv_genai_amd.models.reward import ATTRIBUTES, RewardModel, parse_scores
+    from nv_genai_amd.serving.model_server import create_app
+
+    rm = RewardModel("reward-tiny", device="cpu", dtype=torch.float32)
+    app = create_app(None, None, None, reward=rm)
+    with TestClient(app) as c:
+        assert "nvidia/nemotron-4-340b-reward" in [m["id"] for m in c.get("/v1/models").json()["data"]]
+        r = c.post("/v1/chat/completions", json={"model": "nvidia/nemotron-4-340b-reward", "messages": [
+            {"role": "user", "content": "q?"}, {"role": "assistant", "content": "a."}]})
+        assert r.status_code == 200
+        sc = parse_scores(r.json()["choices"][0]["message"]["content"])
+        want = rm.score("q?", "a.")
+        assert sc is not None and all(abs(sc[m] - want[m]) < 1e-3 for m in ATTRIBUTES)
+    assert parse_scores("garbage") is None
+    assert RewardClient("http://127.0.0.1:9").base.startswith("http://127.0.0.1:9")
