@@ -48,8 +48,8 @@ def test_bench_refuses_more_ranks_than_gpus():
     """Without --allow-shared-devices a 2-rank job on a 1-GPU box must not produce a record."""
     import torch
 
-    if torch.cuda.device_count() >= 2:
-        pytest.skip("box has enough GPUs")
+    if torch.cuda.device_count() != 1:
+        pytest.skip("needs a box with exactly one GPU")
     r = _run([], shared=False, expect_ok=False)
     assert r.returncode != 0 and "refusing" in (r.stderr + r.stdout)
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
