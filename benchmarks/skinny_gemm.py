@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--ms", default="64,128,256,512")
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--krot", type=int, default=0)
+    ap.add_argument("--wpack", action="store_true", help="tile-packed weights (ops.pack_weight)")
+    ap.add_argument("--xpack", action="store_true", help="tile-packed activations (ops.pack_rows)")
     ap.add_argument("--cfgs", default=None, help="comma list (default: all)")
     ap.add_argument("--check", action="store_true", help="numerics of the best config vs fp32")
     ap.add_argument("--all", action="store_true", help="print every (cfg, split) result")
@@ -67,8 +70,9 @@ def main():
             else:
                 lib_us = timeit(lambda i: x @ Ws[i].t(), n_rot, a.iters)
             res = []
+            packed = {}
             for c in cfgs:
-                BN, BM, WN, NS = info[c]
+                BN, BM, WN, WM, NS = info[c]
                 nn = (Nout // (BN // 2)) if epi_full == 2 else -(-N // BN)
                 if epi_full == 2 and Nout % (BN // 2):
                     continue
@@ -84,13 +88,24 @@ def main():
                     out = (torch.empty(s, M, N, dtype=torch.float32, device=dev) if epi == 1
                            else torch.empty(M, Nout, dtype=torch.bfloat16, device=dev))
                     red = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-                    t_g = timeit(lambda i: C.skinny_gemm(out, x, Ws[i], epi, s, c), n_rot, a.iters)
+                    if a.wpack:
+                        key = (BN, epi_full)
+                        if key not in packed:
+                            packed[key] = [ops.pack_weight(w, BN, epi_full) for w in Ws]
+                        Wu, pk, nout = packed[key], 1, Nout
+                    else:
+                        Wu, pk, nout = Ws, 0, 0
+                    if a.xpack:
+                        xu, xm = ops.pack_rows(x, BM), M
+                    else:
+                        xu, xm = x, 0
+                    t_g = timeit(lambda i: C.skinny_gemm(out, xu, Wu[i], epi, s, c, a.krot, pk, nout, xm, K), n_rot, a.iters)
                     if epi == 1:
-                        t_t = timeit(lambda i: (C.skinny_gemm(out, x, Ws[i], epi, s, c), C.splitk_reduce(red, out, s)),
-                                     n_rot, a.iters)
+                        t_t = timeit(lambda i: (C.skinny_gemm(out, xu, Wu[i], epi, s, c, a.krot, pk, nout, xm, K),
+                                                C.splitk_reduce(red, out, s)), n_rot, a.iters)
                     else:
                         t_t = t_g
-                    r = {"cfg": c, "tile": [BN, BM, WN, NS], "split": s, "blocks": blocks,
+                    r = {"cfg": c, "tile": [BN, BM, WN, WM, NS], "split": s, "blocks": blocks,
                          "gemm_us": round(t_g, 2), "total_us": round(t_t, 2)}
                     res.append(r)
                     if a.all:
@@ -107,7 +122,9 @@ def main():
                 c, s = best["cfg"], best["split"]
                 w = Ws[0]
                 epi = epi_full if s == 1 else 1
-                y = ops.skinny_gemm(x, w, c, s, epi)
+                BN = info[c][0]
+                y = (ops.skinny_gemm(x, ops.pack_weight(w, BN, epi_full), c, s, epi, krot=a.krot, n_out=Nout)
+                     if a.wpack else ops.skinny_gemm(x, w, c, s, epi, krot=a.krot))
                 if epi == 1:
                     y = y.sum(0)
                 refm = x.float() @ w.float().t()
@@ -116,6 +133,7 @@ def main():
                 err = ((y.float() - refm).norm(dim=1) / refm.norm(dim=1).clamp_min(1e-6)).max().item()
                 row["max_row_rel_err"] = float(f"{err:.3e}")
             print(json.dumps(row), flush=True)
+            del packed
         del Ws
         torch.cuda.empty_cache()
 

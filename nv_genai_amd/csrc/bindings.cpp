@@ -237,24 +237,29 @@ void moe_combine(Tensor y, Tensor inv, int64_t T, int64_t k, Tensor out) {
 
 // ------------------------------------------------------------------ decode-shape GEMM
 std::vector<int64_t> skinny_cfg(int64_t cfg) {
-  int info[4];
+  int info[5];
   nga::skinny_gemm_cfg_info((int)cfg, info);
-  return {info[0], info[1], info[2], info[3]};
+  return {info[0], info[1], info[2], info[3], info[4]};
 }
 
 // epi 0: out [M, N] bf16 = x @ w^T; 1: out fp32 [split, M, N] partial slabs; 2: out [M, F] bf16 =
 // silu(x @ w[:F]^T) * (x @ w[F:]^T)
-void skinny_gemm(Tensor out, Tensor x, Tensor w, int64_t epi, int64_t split, int64_t cfg) {
+// wpack: w is the pack_weight() image for this cfg ([nN * K/64 * BN, 64] rows); n_out: the
+// output features then (the packed tensor no longer carries them)
+// xpack > 0: x is the pack_rows() image for this cfg and xpack the real token rows M
+void skinny_gemm(Tensor out, Tensor x, Tensor w, int64_t epi, int64_t split, int64_t cfg, int64_t krot,
+                 int64_t wpack, int64_t n_out, int64_t xpack, int64_t k_in) {
   CHECK_BF16(x); CHECK_BF16(w); CHECK_DEV(out);
   CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() >= 2, "skinny_gemm: 2-D x / w");
   TORCH_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0, "skinny_gemm: x rows must be contiguous and 16-B aligned");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
               "skinny_gemm: x / w must be 16-B aligned");
-  const int64_t M = x.size(0), K = x.size(1);
-  TORCH_CHECK(w.size(1) == K && K % 64 == 0 && K >= 64, "skinny_gemm: K must match and be a multiple of 64");
+  const int64_t M = xpack ? xpack : x.size(0), K = xpack ? k_in : x.size(1);
+  TORCH_CHECK(K % 64 == 0 && K >= 64, "skinny_gemm: K must be a multiple of 64");
+  TORCH_CHECK(wpack || w.size(1) == K, "skinny_gemm: K must match");
   TORCH_CHECK(M >= 1 && M <= 65536, "skinny_gemm: 1 <= M <= 65536");
-  int info[4];
+  int info[5];
   nga::skinny_gemm_cfg_info((int)cfg, info);
   TORCH_CHECK(info[0] > 0, "skinny_gemm: unknown tile configuration ", cfg);
   const int BN = info[0], BM = info[1];
@@ -267,15 +272,27 @@ void skinny_gemm(Tensor out, Tensor x, Tensor w, int64_t epi, int64_t split, int
   p.M = (int)M;
   p.K = (int)K;
   p.split = (int)split;
+  p.krot = krot ? 1 : 0;
+  p.wpack = wpack ? 1 : 0;
+  p.xpack = xpack ? 1 : 0;
+  if (xpack) {
+    const int64_t nm = (M + info[1] - 1) / info[1];
+    TORCH_CHECK(x.size(1) == 64 && x.size(0) == nm * (K / 64) * info[1],
+                "skinny_gemm: packed x must be [nM * K/64 * BM, 64] for this cfg");
+  }
+  const int64_t wrows = wpack ? (epi == 2 ? 2 * n_out : n_out) : w.size(0);
   if (epi == 2) {
-    TORCH_CHECK(w.size(0) % 2 == 0, "skinny_gemm: SwiGLU weights are [gate | up] rows");
-    p.N = (int)(w.size(0) / 2);
+    TORCH_CHECK(wrows % 2 == 0, "skinny_gemm: SwiGLU weights are [gate | up] rows");
+    p.N = (int)(wrows / 2);
     TORCH_CHECK(p.N % (BN / 2) == 0, "skinny_gemm: F must be a multiple of BN / 2 = ", BN / 2);
     p.nN = p.N / (BN / 2);
   } else {
-    p.N = (int)w.size(0);
+    p.N = (int)wrows;
     p.nN = (p.N + BN - 1) / BN;
   }
+  if (wpack)   // the packed image holds nN whole tiles of every K step
+    TORCH_CHECK(w.dim() == 2 && w.size(1) == 64 && w.size(0) == (int64_t)p.nN * (K / 64) * BN,
+                "skinny_gemm: packed weights must be [nN * K/64 * BN, 64] for this cfg");
   TORCH_CHECK(p.N % 8 == 0, "skinny_gemm: N must be a multiple of 8");
   p.nM = (int)((M + BM - 1) / BM);
   TORCH_CHECK((int64_t)p.nN * p.nM * split < (1ll << 31));

@@ -10,7 +10,7 @@
 // by an in-kernel K split (fp32 partial slabs, reduced by the consumer kernel), never by
 // shrinking the tile below the MFMA-bound ratio.
 //
-// Block tile: BN weight rows x BM token rows x K slice, 4 waves as WN (weight) x WM (token);
+// Block tile: BN weight rows x BM token rows x K slice, 4 or 8 waves as WN (weight) x WM (token);
 // each wave owns (BN/WN) x (BM/WM) outputs as 16 x 16 MFMA tiles (mfma_f32_16x16x32_bf16).
 // Weight rows are the MFMA A operand and token rows the B operand, so a lane ends with 4
 // consecutive output features of one token (8-B bf16 / 16-B fp32 stores) and, for the fused
@@ -23,6 +23,10 @@
 // ds_read_b128 fragment reads conflict-free goes on each lane's global SOURCE chunk (the DMA
 // writes lane-linearly). One raw s_barrier per 64-deep K step after a counted vmcnt that
 // retires only this step's DMA (a __syncthreads would drain every DMA in flight).
+//
+// Weights: the nn.Linear layout, or (wpack) pre-packed per block tile as [nN][K/64][BN][64], so
+// each 64-deep K step of a block's weights is one contiguous BN x 128-B tile (the EPI 2 gate /
+// up row interleave baked in): whole DRAM pages instead of 128-B pieces at K x 2-B strides.
 //
 // Grid: nN x nM x split blocks, remapped so each XCD gets a contiguous range with the token
 // tile fastest: the blocks that read the same weight tile share an L2.
@@ -55,16 +59,17 @@ __device__ __forceinline__ void sk_wait_vm() {
 __device__ __forceinline__ float sk_silu(float x) { return x / (1.f + __expf(-x)); }
 }  // namespace
 
-template <int BN, int BM, int WN, int NSTAGE, int EPI>
-__global__ void __launch_bounds__(256) skinny_gemm_kernel(SkinnyGemmParams P) {
-  constexpr int WM = 4 / WN;
+template <int BN, int BM, int WN, int WM, int NSTAGE, int EPI>
+__global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmParams P) {
+  constexpr int NW = WN * WM;   // waves per workgroup (4 or 8)
   constexpr int RW = BN / WN;   // weight rows per wave
   constexpr int CW = BM / WM;   // token rows per wave
   constexpr int NTW = RW / 16, MTW = CW / 16;
-  static_assert(WN * WM == 4 && NTW >= 1 && MTW >= 1 && BN % 32 == 0 && BM % 32 == 0, "tile");
+  static_assert((NW == 4 || NW == 8) && NTW >= 1 && MTW >= 1, "tile");
+  static_assert(BN % (8 * NW) == 0 && BM % (8 * NW) == 0, "every wave stages whole 8-row DMA pieces");
   static_assert(EPI != 2 || NTW % 2 == 0, "SwiGLU pairs gate / up tiles inside a wave");
   static_assert(NSTAGE >= 2 && NSTAGE <= 4, "stage count");
-  constexpr int W_GL = BN / 32, X_GL = BM / 32;   // DMA instructions per wave per stage
+  constexpr int W_GL = BN / (8 * NW), X_GL = BM / (8 * NW);   // DMA instructions per wave per stage
   constexpr int NPS = W_GL + X_GL;
   constexpr int STAGE = (BN + BM) * SBK;          // uint16 elements per stage
   __shared__ __attribute__((aligned(16))) uint16_t smem[NSTAGE * STAGE];
@@ -101,7 +106,10 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(SkinnyGemmParams P) {
       wrow = nb * BN + r;
       if (wrow >= P.N) wrow = P.N - 1;   // ragged last block: any valid row (not stored)
     }
-    wsrc[i] = P.w + (int64_t)wrow * P.K + (int64_t)kb * SBK + ch * 8;
+    if (P.wpack)   // tile-packed weights [nN][K/64][BN][64]: a K step of a block is one contiguous tile
+      wsrc[i] = P.w + ((int64_t)nb * nk_all + kb) * (BN * SBK) + r * SBK + ch * 8;
+    else
+      wsrc[i] = P.w + (int64_t)wrow * P.K + (int64_t)kb * SBK + ch * 8;
   }
   const uint16_t* xsrc[X_GL];
 #pragma unroll
@@ -110,15 +118,26 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(SkinnyGemmParams P) {
     const int ch = (lane & 7) ^ ((r >> 1) & 7);
     int t = mi * BM + r;
     if (t >= P.M) t = P.M - 1;           // padding token rows: any valid row (not stored)
-    xsrc[i] = P.x + (int64_t)t * P.ldx + (int64_t)kb * SBK + ch * 8;
+    if (P.xpack)   // tile-packed activations [nM][K/64][BM][64] (rows past M are zero padding)
+      xsrc[i] = P.x + ((int64_t)mi * nk_all + kb) * (BM * SBK) + r * SBK + ch * 8;
+    else
+      xsrc[i] = P.x + (int64_t)t * P.ldx + (int64_t)kb * SBK + ch * 8;
   }
+  // krot: blocks walk their K range from different starting steps, so the blocks that share an
+  // operand slice (x for every weight block, W for every token tile) do not all address the
+  // same 128-B column of it at the same moment
+  const int rot = P.krot ? (int)((unsigned)(nb * 7 + mi * 3) % (unsigned)nk) : 0;
   auto issue = [&](int kt, int buf) {
     uint16_t* base = smem + buf * STAGE;
-    const int k0 = kt * SBK;
+    int ke = kt + rot;
+    if (ke >= nk) ke -= nk;
+    const int k0 = ke * SBK;
+    const int64_t wk0 = P.wpack ? (int64_t)ke * (BN * SBK) : (int64_t)k0;
 #pragma unroll
-    for (int i = 0; i < W_GL; ++i) glds16(wsrc[i] + k0, base + (wv * W_GL + i) * 8 * SBK);
+    for (int i = 0; i < W_GL; ++i) glds16(wsrc[i] + wk0, base + (wv * W_GL + i) * 8 * SBK);
+    const int64_t xk0 = P.xpack ? (int64_t)ke * (BM * SBK) : (int64_t)k0;
 #pragma unroll
-    for (int i = 0; i < X_GL; ++i) glds16(xsrc[i] + k0, base + BN * SBK + (wv * X_GL + i) * 8 * SBK);
+    for (int i = 0; i < X_GL; ++i) glds16(xsrc[i] + xk0, base + BN * SBK + (wv * X_GL + i) * 8 * SBK);
   };
 
   f32x4 acc[NTW][MTW];
@@ -285,36 +304,44 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(const float* _
 }
 
 // ------------------------------------------------------------------ launchers
-// tile configurations: {BN, BM, WN, NSTAGE}
-#define NGA_SKINNY_CFGS(X) \
-  X(0, 256, 128, 2, 3)     \
-  X(1, 128, 128, 2, 3)     \
-  X(2, 128, 64, 2, 3)      \
-  X(3, 64, 64, 2, 4)       \
-  X(4, 128, 256, 2, 2)     \
-  X(5, 64, 256, 1, 3)      \
-  X(6, 256, 64, 4, 3)      \
-  X(7, 128, 32, 4, 4)      \
-  X(8, 256, 32, 4, 3)      \
-  X(9, 64, 128, 1, 3)
+// tile configurations: {BN, BM, WN, WM, NSTAGE} (WN x WM waves)
+#define NGA_SKINNY_CFGS(X)  \
+  X(0, 256, 128, 2, 2, 3)   \
+  X(1, 128, 128, 2, 2, 3)   \
+  X(2, 128, 64, 2, 2, 3)    \
+  X(3, 64, 64, 2, 2, 4)     \
+  X(4, 128, 256, 2, 2, 2)   \
+  X(5, 64, 256, 1, 4, 3)    \
+  X(6, 256, 64, 4, 1, 3)    \
+  X(7, 128, 32, 4, 1, 4)    \
+  X(8, 256, 32, 4, 1, 3)    \
+  X(9, 64, 128, 1, 4, 3)    \
+  X(10, 128, 128, 2, 2, 4)  \
+  X(11, 128, 128, 2, 2, 2)  \
+  X(12, 256, 256, 4, 2, 2)  \
+  X(13, 256, 128, 4, 2, 3)  \
+  X(14, 128, 256, 2, 4, 2)  \
+  X(15, 64, 64, 2, 2, 2)    \
+  X(16, 256, 128, 2, 4, 3)
 
 int skinny_gemm_cfg_count() {
   int n = 0;
-#define NGA_COUNT(ID, BN, BM, WN, NS) ++n;
+#define NGA_COUNT(ID, BN, BM, WN, WM, NS) ++n;
   NGA_SKINNY_CFGS(NGA_COUNT)
 #undef NGA_COUNT
   return n;
 }
 
-// {BN, BM, WN, NSTAGE} of a configuration, or {0, 0, 0, 0}
+// {BN, BM, WN, WM, NSTAGE} of a configuration, or zeros
 void skinny_gemm_cfg_info(int cfg, int* info) {
-  info[0] = info[1] = info[2] = info[3] = 0;
-#define NGA_INFO(ID, BN, BM, WN, NS) \
-  if (cfg == ID) {                   \
-    info[0] = BN;                    \
-    info[1] = BM;                    \
-    info[2] = WN;                    \
-    info[3] = NS;                    \
+  info[0] = info[1] = info[2] = info[3] = info[4] = 0;
+#define NGA_INFO(ID, BN, BM, WN, WM, NS) \
+  if (cfg == ID) {                       \
+    info[0] = BN;                        \
+    info[1] = BM;                        \
+    info[2] = WN;                        \
+    info[3] = WM;                        \
+    info[4] = NS;                        \
   }
   NGA_SKINNY_CFGS(NGA_INFO)
 #undef NGA_INFO
@@ -323,13 +350,14 @@ void skinny_gemm_cfg_info(int cfg, int* info) {
 void launch_skinny_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t stream) {
   const int nblk = p.nN * p.nM * p.split;
   if (nblk == 0) return;
-  dim3 grid(nblk), block(256);
-#define NGA_LAUNCH(ID, BN, BM, WN, NS)                                                    \
-  if (cfg == ID) {                                                                        \
-    if (epi == 0) skinny_gemm_kernel<BN, BM, WN, NS, 0><<<grid, block, 0, stream>>>(p);   \
-    else if (epi == 1) skinny_gemm_kernel<BN, BM, WN, NS, 1><<<grid, block, 0, stream>>>(p); \
-    else skinny_gemm_kernel<BN, BM, WN, NS, 2><<<grid, block, 0, stream>>>(p);            \
-    return;                                                                               \
+  dim3 grid(nblk);
+#define NGA_LAUNCH(ID, BN, BM, WN, WM, NS)                                                            \
+  if (cfg == ID) {                                                                                    \
+    const dim3 block(64 * WN * WM);                                                                   \
+    if (epi == 0) skinny_gemm_kernel<BN, BM, WN, WM, NS, 0><<<grid, block, 0, stream>>>(p);           \
+    else if (epi == 1) skinny_gemm_kernel<BN, BM, WN, WM, NS, 1><<<grid, block, 0, stream>>>(p);      \
+    else skinny_gemm_kernel<BN, BM, WN, WM, NS, 2><<<grid, block, 0, stream>>>(p);                    \
+    return;                                                                                           \
   }
   NGA_SKINNY_CFGS(NGA_LAUNCH)
 #undef NGA_LAUNCH

@@ -166,9 +166,12 @@ struct SkinnyGemmParams {
   void* out;           // epi 0 / 2: bf16 [M, ldo]; epi 1: fp32 [split, M, N]
   int64_t ldo;
   int nN, nM;          // weight-row blocks, token-row tiles (set by the caller from the cfg)
+  int krot;            // 1: each block starts its K walk at a block-dependent step
+  int wpack;           // 1: w is tile-packed [nN][K/64][BN][64] for this cfg's BN (pack_weight)
+  int xpack;           // 1: x is tile-packed [nM][K/64][BM][64] for this cfg's BM (pack_rows)
 };
 int skinny_gemm_cfg_count();
-void skinny_gemm_cfg_info(int cfg, int* info);   // {BN, BM, WN, NSTAGE}
+void skinny_gemm_cfg_info(int cfg, int* info);   // {BN, BM, WN, WM, NSTAGE}
 void launch_skinny_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t stream);
 void launch_splitk_reduce(const float* P, int S, int M, int N, uint16_t* out, int64_t ldo,
                           hipStream_t stream);

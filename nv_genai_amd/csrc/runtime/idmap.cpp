@@ -46,13 +46,14 @@ class IdMap {
     return to_array(displaced);
   }
 
+  // all or nothing: a collision anywhere in the range leaves the map untouched
   void add_range(int64_t start, int64_t stride, int64_t n, int64_t first_row) {
     if (n < 0) throw std::invalid_argument("add_range: negative count");
-    reserve(n_ + n);
     for (int64_t j = 0; j < n; ++j) {
-      if (put(start + stride * j, first_row + j) >= 0)
-        throw std::invalid_argument("add_range: id already present");
+      if (find(start + stride * j) >= 0) throw std::invalid_argument("add_range: id already present");
     }
+    reserve(n_ + n);
+    for (int64_t j = 0; j < n; ++j) put(start + stride * j, first_row + j);
   }
 
   py::array_t<int64_t> remove(py::array_t<int64_t, py::array::c_style | py::array::forcecast> ids) {

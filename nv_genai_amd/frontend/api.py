@@ -161,9 +161,11 @@ def create_frontend(client: ChatClient, asr=None, tts=None) -> FastAPI:
         if asr is None:
             return JSONResponse({"message": "speech requires a speech endpoint (SPEECH_API_URI)"},
                                 status_code=501)
+        import wave
+
         try:
             pcm, sr = _pcm_of(await request.body(), rate)
-        except (ValueError, EOFError) as e:
+        except (ValueError, EOFError, wave.Error) as e:   # malformed RIFF / PCM: the client's fault
             return JSONResponse({"message": str(e)}, status_code=400)
         if getattr(asr, "rate", sr) != sr:
             return JSONResponse({"message": f"the recogniser takes {asr.rate} Hz audio, got {sr} Hz"},
@@ -189,24 +191,31 @@ def create_frontend(client: ChatClient, asr=None, tts=None) -> FastAPI:
         text = str(body.get("text", "")).strip()
         if not text:
             return JSONResponse({"message": "no text to synthesise"}, status_code=400)
+        from starlette.concurrency import run_in_threadpool
+
+        # the speech client does blocking HTTP: its calls run in the threadpool, never on the
+        # event loop (a long answer would otherwise stall every other route)
         gen = tts.synthesize(text, body.get("voice"))
-        first = next(gen, None)
+        first = await run_in_threadpool(next, gen, None)
         if first is None:
             return JSONResponse({"message": "the speech server returned no audio"}, status_code=502)
         rate = int(first[0])
         if format == "wav":
-            import io
-            import wave
+            def render() -> bytes:
+                import io
+                import wave
 
-            buf = io.BytesIO()
-            with wave.open(buf, "wb") as w:
-                w.setnchannels(1)
-                w.setsampwidth(2)
-                w.setframerate(rate)
-                w.writeframes(first[1].astype("<i2").tobytes())
-                for _, pcm in gen:
-                    w.writeframes(pcm.astype("<i2").tobytes())
-            return StreamingResponse(iter([buf.getvalue()]), media_type="audio/wav")
+                buf = io.BytesIO()
+                with wave.open(buf, "wb") as w:
+                    w.setnchannels(1)
+                    w.setsampwidth(2)
+                    w.setframerate(rate)
+                    w.writeframes(first[1].astype("<i2").tobytes())
+                    for _, pcm in gen:
+                        w.writeframes(pcm.astype("<i2").tobytes())
+                return buf.getvalue()
+
+            return StreamingResponse(iter([await run_in_threadpool(render)]), media_type="audio/wav")
 
         def chunks():
             yield first[1].astype("<i2").tobytes()

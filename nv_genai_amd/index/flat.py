@@ -100,6 +100,9 @@ class FlatIndex:
         start = self._map.max_id() + 1 if first_id is None else first_id
         if self.n + n > self.capacity:
             self._alloc(self.n + n)
+        # ids first: add_range is all-or-nothing, so a colliding range raises before any row of
+        # the slab (or self.n) changes
+        self._map.add_range(start, id_stride, n, self.n)
         for c in range(0, n, chunk):
             m = min(chunk, n - c)
             v = torch.randn(m, self.dim, device=self.device, generator=g)
@@ -109,8 +112,6 @@ class FlatIndex:
             self.bias[r0:r0 + m] = (-ops.row_sqnorm(self.X[r0:r0 + m])) if self.metric == "l2" else 0.0
             self.ids[r0:r0 + m] = start + id_stride * torch.arange(c, c + m, device=self.device)
             self.n += m
-        base = self.n - n
-        self._map.add_range(start, id_stride, n, base)
 
     def _tombstone(self, rows) -> None:
         """-inf bias on live rows (the map only ever returns rows it held live)."""

@@ -177,6 +177,11 @@ LLAMA_PRESETS = {
     "llama70b-tiny": LlamaConfig(name="llama70b-tiny", vocab_size=32768, hidden=256, layers=2, heads=64,
                                  kv_heads=8, head_dim=16, ffn=512, max_position=2048,
                                  bos_id=1, eos_ids=(2,)),
+    # Llama-3-8B's attention layout (32 q : 8 kv heads of 128) at a small width: the headline's
+    # GQA group and work-item counts in step-graph GPU tests
+    "llama3-gqa-small": LlamaConfig(name="llama3-gqa-small", vocab_size=32768, hidden=1024, layers=2, heads=32,
+                                    kv_heads=8, head_dim=128, ffn=2816, max_position=8192, bos_id=1,
+                                    eos_ids=(2,)),
     "llama-small": LlamaConfig(name="llama-small", vocab_size=32768, hidden=1024, layers=4,
                                heads=8, kv_heads=2, head_dim=128, ffn=2816,
                                max_position=8192, bos_id=1, eos_ids=(2,)),

@@ -117,12 +117,52 @@ def linear_rows_split(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tens
     return out
 
 
+def pack_weight(w: torch.Tensor, BN: int, epi: int = 0) -> torch.Tensor:
+    """Tile-packed image of an nn.Linear weight [N, K] for the skinny GEMM with a BN-row block:
+    [nN * K/64 * BN, 64] where tile (block nb, K step kt) holds the block's BN weight rows of
+    columns [64 kt, 64 kt + 64) contiguously — the order the kernel streams them. SwiGLU
+    (``epi`` 2, w = [gate | up]): each block's rows are [gate f..f+15 | up f..f+15] per 32-row
+    group of each wave's range, as the kernel reads them. A ragged last block repeats row N-1."""
+    N, K = w.shape
+    if epi == 2:
+        F = N // 2
+        nN = F // (BN // 2)
+        r = torch.arange(BN)
+        # the kernel's 2x2 / 4-wave layouts split BN over WN waves; the gate/up interleave is per
+        # 32-row group within a wave's RW rows, which for every WN equals per 32-row group of BN
+        f = (r >> 5) * 16 + (r & 15)
+        up = (r >> 4) & 1
+        rows = torch.stack([nb * (BN // 2) + f + up * F for nb in range(nN)])
+    else:
+        nN = -(-N // BN)
+        rows = (torch.arange(nN * BN).clamp_max(N - 1)).view(nN, BN)
+    nk = K // 64
+    g = w.index_select(0, rows.reshape(-1).to(w.device)).view(nN, BN, nk, 64)
+    return g.permute(0, 2, 1, 3).contiguous().view(nN * nk * BN, 64)
+
+
+def pack_rows(x: torch.Tensor, BM: int) -> torch.Tensor:
+    """Tile-packed image of activation rows x [M, K] for a BM-row token tile: [nM * K/64 * BM, 64]
+    (rows past M zero)."""
+    M, K = x.shape
+    nM = -(-M // BM)
+    xp = torch.zeros(nM * BM, K, dtype=x.dtype, device=x.device)
+    xp[:M] = x
+    return xp.view(nM, BM, K // 64, 64).permute(0, 2, 1, 3).contiguous().view(-1, 64)
+
+
 def skinny_gemm(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, epi: int = 0,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, krot: int = 0, n_out: int = 0,
+                x_rows: int = 0, k_in: int = 0) -> torch.Tensor:
     """Decode-shape projection GEMM (gemm_skinny.hip) with an explicit tile configuration:
     ``epi`` 0 -> bf16 ``x @ w^T``; 1 -> fp32 partial slabs [split, M, N] (K split ``split`` ways);
-    2 -> SwiGLU ``silu(x @ w[:F]^T) * (x @ w[F:]^T)`` [M, F]. CPU tensors: the fp32 reference."""
-    M = x.shape[0]
+    2 -> SwiGLU ``silu(x @ w[:F]^T) * (x @ w[F:]^T)`` [M, F]. CPU tensors: the fp32 reference.
+    ``n_out`` > 0: ``w`` is the :func:`pack_weight` image for this cfg and ``n_out`` the output
+    features (N, or F for SwiGLU). ``x_rows`` > 0: ``x`` is the :func:`pack_rows` image for
+    this cfg, ``x_rows`` its token rows and ``k_in`` its K."""
+    M = x_rows or x.shape[0]
+    if n_out and not _gpu(x):
+        raise ValueError("packed skinny weights are a GPU layout")
     if not _gpu(x):
         y = x.float() @ w.float().t()
         if epi == 2:
@@ -133,11 +173,12 @@ def skinny_gemm(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, epi:
             p[0] = y
             return p
         return y.to(x.dtype)
-    N = w.shape[0] // 2 if epi == 2 else w.shape[0]
+    N = n_out if n_out else (w.shape[0] // 2 if epi == 2 else w.shape[0])
     if out is None:
         out = (torch.empty(split, M, N, dtype=torch.float32, device=x.device) if epi == 1
                else torch.empty(M, N, dtype=x.dtype, device=x.device))
-    kernels().skinny_gemm(out, x, w, int(epi), int(split), int(cfg))
+    kernels().skinny_gemm(out, x, w, int(epi), int(split), int(cfg), int(krot), 1 if n_out else 0, int(n_out),
+                          int(x_rows), int(k_in))
     return out
 
 

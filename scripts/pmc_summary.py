@@ -43,10 +43,34 @@ def main():
             if pairs:   # KB per dispatch
                 tb = sum(c * 1024 / x / 1e6 for x, c in pairs) / len(pairs)
                 print(f"    {k} bandwidth (bytes / own duration) {tb:.2f} TB/s")
-        cyc = [c for _, c in rows if "SQ_BUSY_CU_CYCLES" in c and "SQ_VALU_MFMA_BUSY_CYCLES" in c]
+        # SQ_VALU_MFMA_BUSY_CYCLES sums the issuing SIMD's cycles of every MFMA (16 per
+        # 16x16x32 bf16, 32 per 32x32x16: 1,024 FLOP per counted cycle for both shapes), over
+        # all SIMDs; SQ_BUSY_CU_CYCLES sums busy cycles over CUs (~256 x the dispatch's cycles).
+        # A CU has 4 SIMDs, so utilisation = MFMA_BUSY / (4 x BUSY_CU), in [0, 1].
+        cyc = [(x, c) for x, c in rows if "SQ_BUSY_CU_CYCLES" in c and "SQ_VALU_MFMA_BUSY_CYCLES" in c]
         if cyc:
-            u = sum(c["SQ_VALU_MFMA_BUSY_CYCLES"] / max(1.0, c["SQ_BUSY_CU_CYCLES"]) for c in cyc) / len(cyc)
-            print(f"    MFMA busy / CU busy cycles  {u:.3f}")
+            u = sum(c["SQ_VALU_MFMA_BUSY_CYCLES"] / max(1.0, 4.0 * c["SQ_BUSY_CU_CYCLES"]) for _, c in cyc) / len(cyc)
+            print(f"    MFMA utilisation (MFMA busy / 4 SIMDs x CU busy)  {u:.3f}")
+            fl = [1024.0 * c["SQ_VALU_MFMA_BUSY_CYCLES"] / (x * 1e-6) for x, c in cyc if x]
+            if fl:
+                print(f"    MFMA FLOP/s implied by the counter (1,024 FLOP per busy cycle)  "
+                      f"{sum(fl) / len(fl) / 1e12:.1f} TFLOP/s")
+        # HBM read bytes from the raw TCC->EA request counters by size (the FETCH_SIZE derived
+        # formula of ROCm 7.2 is the gfx94x one, which prices gfx950's 128-B requests at 64 B)
+        req = [(x, c) for x, c in rows if "TCC_EA0_RDREQ_sum" in c]
+        if req:
+            def rd_bytes(c):
+                n = c["TCC_EA0_RDREQ_sum"]
+                n32 = c.get("TCC_EA0_RDREQ_32B_sum", 0.0)
+                n128 = c.get("TCC_EA0_RDREQ_128B_sum", None)
+                if n128 is None:   # 32 B and 64 B requests only
+                    return 32 * n32 + 64 * (n - n32)
+                return 32 * n32 + 128 * n128 + 64 * max(0.0, n - n32 - n128)
+            by = [rd_bytes(c) for _, c in req]
+            print(f"    HBM read bytes (TCC_EA0_RDREQ by size)  {sum(by) / len(by) / 1e6:.1f} MB")
+            bw = [rd_bytes(c) / (x * 1e-6) for x, c in req if x]
+            if bw:
+                print(f"    HBM read bandwidth (bytes / own duration)  {sum(bw) / len(bw) / 1e12:.2f} TB/s")
 
 
 if __name__ == "__main__":

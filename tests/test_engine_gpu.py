@@ -291,3 +291,67 @@ def test_step_graphs_equal_eager_steps(gpu, weights):
     for (a, la), (b, lb) in zip(outs[True], outs[False]):
         assert a == b
         assert max(abs(x - y) for x, y in zip(la, lb)) < 0.3
+
+
+@pytest.fixture(scope="module")
+def gqa_weights():
+    from nv_genai_amd.models.config import llama_config
+    from nv_genai_amd.models.llama import LlamaModel
+    from nv_genai_amd.parallel.dist import ParallelContext
+
+    m = LlamaModel(llama_config("llama3-gqa-small"), "cpu", dtype=torch.bfloat16, pctx=ParallelContext(), seed=5)
+    m.lm_head.mul_(40.0)
+    return m.state_dict()
+
+
+@pytest.mark.parametrize("pf_seq_min", ["384", "0"])
+def test_step_graphs_headline_gqa_4096_bucket(gpu, gqa_weights, pf_seq_min, monkeypatch):
+    """The headline's head ratio (32 q / 8 kv heads of 128) at the 4,096-token bucket with
+    decode rows: 8 decoding requests, then 5 x 1,000-token prompts arrive and 4,088 of their
+    tokens ride along as one mixed step of 4,096 rows (1,016 work items of the 32x32 prefill
+    kernel). NGA_PF_SEQ_MIN=384 runs that
+    work list after the decode attention (the shipped default), 0 the 16x16 kernel beside it;
+    both graphed runs must generate the eager steps' tokens with matching log-probs."""
+    from nv_genai_amd.engine.llm_engine import EngineConfig, LLMEngine, SamplingParams
+    from nv_genai_amd.parallel.dist import ParallelContext
+
+    monkeypatch.setenv("NGA_PF_SEQ_MIN", pf_seq_min)
+    p = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True, logprobs=True)
+    short = [[(11 * i + j) % 30000 + 10 for i in range(100 + 7 * j)] for j in range(8)]
+    long = [[(13 * i + 5 * j) % 30000 + 10 for i in range(1000)] for j in range(5)]
+    outs = {}
+    for graphs in (True, False):
+        e = LLMEngine(EngineConfig(model="llama3-gqa-small", max_num_seqs=16, max_batched_tokens=8192,
+                                   max_model_len=2048, kv_cache_blocks=256, graph_batch_sizes=(1, 2, 4, 8, 16),
+                                   use_graphs=True, mixed_graphs=graphs, mixed_prefill_tokens=4096),
+                      device="cuda", pctx=ParallelContext(), weights=gqa_weights)
+        reqs = [e.add_request(pr, p) for pr in short]
+        for _ in range(3):
+            e.step()
+        reqs += [e.add_request(pr, p) for pr in long]
+        e.run_until_done(reqs)
+        outs[graphs] = [(r.output_ids, r.logprobs) for r in reqs]
+        if graphs:
+            big = [k for k in e.mgraphs if k[0] == 4096 and k[1] > 0]
+            assert big, sorted(e.mgraphs)                          # the 4,096 bucket with decode rows ran
+            assert e._graph_pf_seq(big[0]) == (pf_seq_min == "384")
+    _same_greedy_run(outs[True], outs[False])
+
+
+def _same_greedy_run(ga, eg, lp_tol=0.3):
+    """Graphed vs eager greedy generations: the first token of every request (its prefill /
+    mixed-step output) equal; then equal tokens with log-probs within ``lp_tol`` up to a
+    request's first divergence, which is accepted only at a near-tie (neither run confident in
+    its choice: log-probs in [-1.5, -0.4], two candidates sharing the mass) — with 150+ greedy
+    decisions on random weights, bucket-padded GEMMs (other library kernels, another fp32
+    summation order) can flip an exact tie; a wrong kernel changes first tokens and log-probs."""
+    diverged = []
+    for i, ((a, la), (b, lb)) in enumerate(zip(ga, eg)):
+        assert a[0] == b[0], (i, a[:3], b[:3], la[:3], lb[:3])
+        d = next((j for j, (x, y) in enumerate(zip(a, b)) if x != y), None)
+        upto = len(a) if d is None else d
+        assert max(abs(x - y) for x, y in zip(la[:upto], lb[:upto])) < lp_tol, (i, la[:upto], lb[:upto])
+        if d is not None:
+            assert all(-1.5 <= v <= -0.4 for v in (la[d], lb[d])), ("divergence without a near-tie", i, d, la[d], lb[d])
+            diverged.append(i)
+    assert len(diverged) <= max(1, len(ga) // 4), diverged

@@ -118,3 +118,23 @@ def test_load_rejects_corrupt_graph(tmp_path):
             HNSWIndex.load(path)
     s, i = HNSWIndex.load(str(good)).search(X[:4], 3)
     assert i.numpy()[:, 0].tolist() == [0, 1, 2, 3]
+
+
+def test_flat_add_random_collision_leaves_index_unchanged():
+    """add_random with ids that collide with existing ones raises before touching the slab or
+    the id map (the map and the rows used to diverge)."""
+    import pytest
+    import torch
+
+    from nv_genai_amd.index.flat import FlatIndex
+
+    idx = FlatIndex(32, "cosine", "cpu", capacity=64)
+    idx.add_random(10, seed=1)
+    n0, X0 = idx.n, idx.X[:10].clone()
+    with pytest.raises(ValueError):
+        idx.add_random(5, seed=2, first_id=7)          # ids 7..11 overlap 0..9
+    assert idx.n == n0 and torch.equal(idx.X[:10], X0)
+    idx.add_random(5, seed=2)                           # the next free ids still work
+    assert idx.n == 15
+    v, r = idx.search(idx.X[12:13].float(), 1)
+    assert int(r[0, 0]) == 12

@@ -673,7 +673,17 @@ def test_skinny_gemm_every_cfg(gpu, M):
             _close_rows(P.sum(0), ref0, rel=1e-4)
             _close_rows(ops.splitk_reduce(P), ref0, rel=1e-2)
         if 512 % (BN // 2) == 0:
-            _close_rows(ops.skinny_gemm(x, wg, cfg, 1, 2), ref2, rel=2e-2)
+            y2 = ops.skinny_gemm(x, wg, cfg, 1, 2)
+            _close_rows(y2, ref2, rel=2e-2)
+            # tile-packed weights and the rotated K walk: the same products (fp32 sums in
+            # another order for krot)
+            assert torch.equal(ops.skinny_gemm(x, ops.pack_weight(wg, BN, 2), cfg, 1, 2, n_out=512), y2)
+        y0 = ops.skinny_gemm(x, w, cfg, 1, 0)
+        assert torch.equal(ops.skinny_gemm(x, ops.pack_weight(w, BN), cfg, 1, 0, n_out=1000), y0)
+        assert torch.equal(ops.skinny_gemm(ops.pack_rows(x, BM), ops.pack_weight(w, BN), cfg, 1, 0, n_out=1000,
+                                           x_rows=M, k_in=K), y0)
+        _close_rows(ops.skinny_gemm(x, ops.pack_weight(w, BN), cfg, 3, 1, n_out=1000, krot=1).sum(0), ref0,
+                    rel=1e-4)
 
 
 def test_splitk_add_rmsnorm(gpu):

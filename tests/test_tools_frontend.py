@@ -172,6 +172,9 @@ def test_frontend_speech_against_a_fake_speech_server(monkeypatch):
         with wave.open(io.BytesIO(w.content)) as wf:
             assert wf.getframerate() == 22050 and wf.getnframes() == 100 * len(seen["tts"][-1])
         assert c.post("/api/tts", json={"text": "  "}).status_code == 400
+        # a RIFF header with a broken body is the client's error, not a server fault
+        bad = b"RIFF" + (36).to_bytes(4, "little") + b"WAVEfmt " + b"\x10\x00\x00\x00" + b"\x07" * 16
+        assert c.post("/api/asr", content=bad).status_code == 400
     finally:
         srv.should_exit = True
         t.join(timeout=5)
