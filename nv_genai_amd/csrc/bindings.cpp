@@ -117,7 +117,7 @@ void bias_gelu(Tensor x, c10::optional<Tensor> bias, int64_t mode) {
 // ------------------------------------------------------------------ rope + kv cache
 void rope_cache(Tensor qkv, Tensor pos, Tensor cos_sin, c10::optional<Tensor> slots,
                 c10::optional<Tensor> kc, c10::optional<Tensor> vc, int64_t Hq, int64_t Hkv,
-                int64_t D, double k_scale, double v_scale) {
+                int64_t D, double k_scale, double v_scale, c10::optional<Tensor> part) {
   CHECK_BF16(qkv); CHECK_CONTIG(qkv);
   CHECK_DEV(pos); CHECK_DT(pos, at::kInt);
   CHECK_DEV(cos_sin); CHECK_DT(cos_sin, at::kFloat); CHECK_CONTIG(cos_sin);
@@ -144,9 +144,18 @@ void rope_cache(Tensor qkv, Tensor pos, Tensor cos_sin, c10::optional<Tensor> sl
     kp = kc->data_ptr();
     vp = vc->data_ptr();
   }
+  const float* pp = nullptr;
+  int S = 0;
+  if (part.has_value()) {
+    CHECK_DEV(*part); CHECK_DT(*part, at::kFloat); CHECK_CONTIG(*part);
+    TORCH_CHECK(part->dim() == 3 && part->size(1) == qkv.size(0) && part->size(2) == qkv.size(1),
+                "rope_cache: partial slabs must be [S, T, (Hq+2Hkv)*D]");
+    pp = part->data_ptr<float>();
+    S = (int)part->size(0);
+  }
   nga::launch_rope_cache(bfp(qkv), pos.data_ptr<int32_t>(), cos_sin.data_ptr<float>(), sp, kp, vp,
                          qkv.size(0), (int)Hq, (int)Hkv, (int)D, BS, fp8, (float)(1.0 / k_scale),
-                         (float)(1.0 / v_scale), cur_stream(qkv));
+                         (float)(1.0 / v_scale), cur_stream(qkv), pp, S);
 }
 
 // ------------------------------------------------------------------ MoE

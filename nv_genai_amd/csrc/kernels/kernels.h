@@ -24,11 +24,13 @@ void launch_bias_gelu(uint16_t* x, const uint16_t* bias, int64_t T, int F, int m
                       hipStream_t stream);
 
 // rope.hip
-// kc / vc: bf16 caches, or fp8 e4m3fn ones (kv_fp8) storing k * inv_ks and v * inv_vs
+// kc / vc: bf16 caches, or fp8 e4m3fn ones (kv_fp8) storing k * inv_ks and v * inv_vs.
+// part: optional fp32 K-split partial slabs [S, T, row] of the qkv projection; their bf16 sum is
+// rotated / copied into qkv (which is then output only)
 void launch_rope_cache(uint16_t* qkv, const int32_t* pos, const float* cos_sin,
                        const int32_t* slots, void* kc, void* vc, int64_t T, int Hq,
                        int Hkv, int D, int BS, bool kv_fp8, float inv_ks, float inv_vs,
-                       hipStream_t stream);
+                       hipStream_t stream, const float* part = nullptr, int S = 0);
 
 // attention_decode.hip
 int decode_attn_pages_per_part(int num_seqs, int Hkv, int max_ctx);

@@ -46,12 +46,58 @@ __device__ __forceinline__ void put1(CT* dst, uint16_t v, float inv_s) {
   else *dst = f32_to_fp8(bf2f(v) * inv_s);
 }
 
+// Source of the qkv values: the bf16 projection output, or (part != nullptr) the S fp32 K-split
+// partial slabs of the skinny GEMM [S, T, row], summed here and rounded to bf16 exactly as the
+// materialised projection would be — the rotated / copied result is written to qkv either way,
+// so the projection output never makes a separate bf16 round trip.
+struct QkvSrc {
+  const float* part;
+  int S;
+  int64_t slab;   // T * row
+};
+
+__device__ __forceinline__ u16x8 ld8(const uint16_t* qkv, const QkvSrc& src, int64_t i) {
+  if (src.part == nullptr) return load8(qkv + i);
+  const float* p = src.part + i;
+  f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+  for (int s = 1; s < src.S; ++s) {
+    a += *reinterpret_cast<const f32x4*>(p + s * src.slab);
+    b += *reinterpret_cast<const f32x4*>(p + s * src.slab + 4);
+  }
+  u16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = f2bf(a[j]);
+    r[4 + j] = f2bf(b[j]);
+  }
+  return r;
+}
+
+__device__ __forceinline__ u16x4 ld4(const uint16_t* qkv, const QkvSrc& src, int64_t i) {
+  if (src.part == nullptr) return *reinterpret_cast<const u16x4*>(qkv + i);
+  const float* p = src.part + i;
+  f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  for (int s = 1; s < src.S; ++s) a += *reinterpret_cast<const f32x4*>(p + s * src.slab);
+  u16x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = f2bf(a[j]);
+  return r;
+}
+
+__device__ __forceinline__ uint32_t ld2(const uint16_t* qkv, const QkvSrc& src, int64_t i) {
+  if (src.part == nullptr) return *reinterpret_cast<const uint32_t*>(qkv + i);
+  const float* p = src.part + i;
+  f32x2 a = *reinterpret_cast<const f32x2*>(p);
+  for (int s = 1; s < src.S; ++s) a += *reinterpret_cast<const f32x2*>(p + s * src.slab);
+  return (uint32_t)f2bf(a[0]) | ((uint32_t)f2bf(a[1]) << 16);
+}
+
 template <int D, typename CT>
 __global__ void rope_cache_kernel(uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos,
                                   const float* __restrict__ cos_sin,
                                   const int32_t* __restrict__ slots, CT* __restrict__ kc,
                                   CT* __restrict__ vc, int Hq, int Hkv, int BS, float inv_ks,
-                                  float inv_vs) {
+                                  float inv_vs, QkvSrc src) {
   constexpr int HALF = D / 2;
   constexpr int G4 = HALF / 4;  // 4-element groups per half
   const int64_t t = blockIdx.x;
@@ -70,8 +116,9 @@ __global__ void rope_cache_kernel(uint16_t* __restrict__ qkv, const int32_t* __r
       const int h = w / G4;  // 0..Hq+Hkv-1 (q heads then k heads, contiguous in qkv)
       const int i0 = (w % G4) * 4;
       uint16_t* x = base + (int64_t)h * D;
-      u16x4 a = *reinterpret_cast<const u16x4*>(x + i0);
-      u16x4 b = *reinterpret_cast<const u16x4*>(x + HALF + i0);
+      const int64_t xi = t * row + (int64_t)h * D;
+      u16x4 a = ld4(qkv, src, xi + i0);
+      u16x4 b = ld4(qkv, src, xi + HALF + i0);
       u16x4 oa, ob;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -88,14 +135,18 @@ __global__ void rope_cache_kernel(uint16_t* __restrict__ qkv, const int32_t* __r
         put4(dst + i0, oa, inv_ks);
         put4(dst + HALF + i0, ob, inv_ks);
       }
-    } else if (slot >= 0) {
+    } else if (slot >= 0 || src.part != nullptr) {
       const int r = w - n_rot;
       const int vh = r / (D / 8);
       const int d0 = (r % (D / 8)) * 8;
-      u16x8 v = load8(base + (int64_t)(Hq + Hkv + vh) * D + d0);
-      CT* dst = vc + ((blk * Hkv + vh) * D + d0) * BS + off;
+      const int64_t vi = (int64_t)(Hq + Hkv + vh) * D + d0;
+      u16x8 v = ld8(qkv, src, t * row + vi);
+      if (src.part != nullptr) store8(base + vi, v);
+      if (slot >= 0) {
+        CT* dst = vc + ((blk * Hkv + vh) * D + d0) * BS + off;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) put1(dst + (int64_t)j * BS, v[j], inv_vs);
+        for (int j = 0; j < 8; ++j) put1(dst + (int64_t)j * BS, v[j], inv_vs);
+      }
     }
   }
 }
@@ -113,7 +164,7 @@ template <int D, typename CT>
 __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos, const float* __restrict__ cos_sin,
     const int32_t* __restrict__ slots, CT* __restrict__ kc, CT* __restrict__ vc,
-    int64_t T, int Hq, int Hkv, int BS, int hg, float inv_ks, float inv_vs) {
+    int64_t T, int Hq, int Hkv, int BS, int hg, float inv_ks, float inv_vs, QkvSrc src) {
   constexpr int HALF = D / 2;
   constexpr int CH = HALF / 8;       // 8-element chunks per half
   constexpr int RT = 256 / CH;       // tokens per tile (one thread per token and chunk)
@@ -135,12 +186,13 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     const float4 s0 = *reinterpret_cast<const float4*>(cs + HALF + i0);
     const float4 s1 = *reinterpret_cast<const float4*>(cs + HALF + i0 + 4);
     uint16_t* xr = qkv + t * row + i0;
+    const int64_t xi = t * row + i0;
     u16x8 a[HGMAX], b[HGMAX];
 #pragma unroll
     for (int j = 0; j < HGMAX; ++j)
       if (h0 + j < h1) {
-        a[j] = load8(xr + (int64_t)(h0 + j) * D);
-        b[j] = load8(xr + (int64_t)(h0 + j) * D + HALF);
+        a[j] = ld8(qkv, src, xi + (int64_t)(h0 + j) * D);
+        b[j] = ld8(qkv, src, xi + (int64_t)(h0 + j) * D + HALF);
       }
     const float c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
     const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
@@ -166,16 +218,22 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     }
     return;
   }
-  if (slots == nullptr) return;
+  if (slots == nullptr && src.part == nullptr) return;
   const int vh = blockIdx.y - ngroups;
-  // stage V[t0:t0+RT, vh, :] (4-byte pairs; padded rows keep 4-B alignment)
+  // stage V[t0:t0+RT, vh, :] (4-byte pairs; padded rows keep 4-B alignment); from partial
+  // slabs the summed bf16 V is also written back to qkv
   for (int i = threadIdx.x; i < RT * (D / 2); i += blockDim.x) {
     const int r = i / (D / 2), c2 = i % (D / 2);
     const int64_t t = t0 + r;
     uint32_t v = 0;
-    if (t < T) v = *reinterpret_cast<const uint32_t*>(qkv + t * row + (int64_t)(Hq + Hkv + vh) * D + 2 * c2);
+    if (t < T) {
+      const int64_t vi = t * row + (int64_t)(Hq + Hkv + vh) * D + 2 * c2;
+      v = ld2(qkv, src, vi);
+      if (src.part != nullptr) *reinterpret_cast<uint32_t*>(qkv + vi) = v;
+    }
     *reinterpret_cast<uint32_t*>(tile + r * LDP + 2 * c2) = v;
   }
+  if (slots == nullptr) return;
   __syncthreads();
   // lane -> (token = lane % RT, d-phase = lane / RT): RT lanes store one d row's tokens
   constexpr int PH = 64 / RT;
@@ -191,7 +249,7 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
 template <typename CT>
 static void rope_dispatch(uint16_t* qkv, const int32_t* pos, const float* cos_sin,
                           const int32_t* slots, CT* kc, CT* vc, int64_t T, int Hq, int Hkv, int D,
-                          int BS, float inv_ks, float inv_vs, hipStream_t stream) {
+                          int BS, float inv_ks, float inv_vs, QkvSrc src, hipStream_t stream) {
   const int rt = 4096 / D;   // tokens per tile of the tiled kernel
   if (T >= rt) {
     // rotary heads per workgroup: enough workgroups to fill the chip, up to 8 heads sharing
@@ -201,13 +259,13 @@ static void rope_dispatch(uint16_t* qkv, const int32_t* pos, const float* cos_si
     int hg = 8;
     while (hg > 1 && tiles * ((nrot + hg - 1) / hg) < 512) hg /= 2;
     dim3 grid((unsigned)tiles, (unsigned)((nrot + hg - 1) / hg + Hkv)), block(256);
-#define NGA_RT(DD) rope_cache_tiled_kernel<DD, CT><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS, hg, inv_ks, inv_vs)
+#define NGA_RT(DD) rope_cache_tiled_kernel<DD, CT><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS, hg, inv_ks, inv_vs, src)
     if (D == 128) NGA_RT(128); else if (D == 256) NGA_RT(256); else if (D == 64) NGA_RT(64);
 #undef NGA_RT
     return;
   }
   dim3 grid((unsigned)T), block(256);
-#define NGA_R1(DD) rope_cache_kernel<DD, CT><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, BS, inv_ks, inv_vs)
+#define NGA_R1(DD) rope_cache_kernel<DD, CT><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, BS, inv_ks, inv_vs, src)
   if (D == 128) NGA_R1(128); else if (D == 256) NGA_R1(256); else if (D == 64) NGA_R1(64);
 #undef NGA_R1
 }
@@ -215,14 +273,15 @@ static void rope_dispatch(uint16_t* qkv, const int32_t* pos, const float* cos_si
 void launch_rope_cache(uint16_t* qkv, const int32_t* pos, const float* cos_sin,
                        const int32_t* slots, void* kc, void* vc, int64_t T, int Hq,
                        int Hkv, int D, int BS, bool kv_fp8, float inv_ks, float inv_vs,
-                       hipStream_t stream) {
+                       hipStream_t stream, const float* part, int S) {
   if (T == 0) return;
+  const QkvSrc src{part, S, T * (int64_t)(Hq + 2 * Hkv) * D};
   if (kv_fp8)
     rope_dispatch(qkv, pos, cos_sin, slots, static_cast<uint8_t*>(kc), static_cast<uint8_t*>(vc), T,
-                  Hq, Hkv, D, BS, inv_ks, inv_vs, stream);
+                  Hq, Hkv, D, BS, inv_ks, inv_vs, src, stream);
   else
     rope_dispatch(qkv, pos, cos_sin, slots, static_cast<uint16_t*>(kc), static_cast<uint16_t*>(vc),
-                  T, Hq, Hkv, D, BS, 1.f, 1.f, stream);
+                  T, Hq, Hkv, D, BS, 1.f, 1.f, src, stream);
 }
 
 }  // namespace nga

@@ -139,6 +139,12 @@ class LlamaModel:
         # 428 -> 373 us, gate/up 694 -> 686 us per layer (profiles/r3_rowsplit). q/k/v loses
         # (167 -> 184 us) and stays whole. NGA_ROW_SPLIT=0 turns it off
         self.row_split = os.environ.get("NGA_ROW_SPLIT", "1") != "0"
+        # decode-shape projections (M <= 512 rows) on the skinny MFMA GEMM where the measured
+        # table (ops.skinny) says it beats the library GEMM: K-split o / down partials summed by
+        # the residual add + RMSNorm kernel, SwiGLU fused into gate / up, fp32 logits straight
+        # from the LM head. One TP rank, one stage (the partial sums never cross a collective)
+        self.skinny = (self.device.type == "cuda" and dtype == torch.bfloat16 and self.p.tp_size == 1
+                       and self.p.pp_size == 1 and ops.skinny.enabled())
         self.fp8 = False
         if fp8:
             self.quantize_fp8()
@@ -164,13 +170,28 @@ class LlamaModel:
         if self.device.type == "cuda":
             torch.cuda.empty_cache()
 
-    def _lin(self, x: torch.Tensor, L: dict, name: str, swiglu: bool = False) -> torch.Tensor:
+    def _pick(self, w: torch.Tensor, M: int):
+        """(cfg, split) of the skinny GEMM for x[M, K] @ w^T, or None (library GEMM)."""
+        if not self.skinny or self.fp8:
+            return None
+        return ops.skinny.table().pick(w.shape[0], w.shape[1], M)
+
+    def _lin(self, x: torch.Tensor, L: dict, name: str, swiglu: bool = False, partial_ok: bool = False):
         """x @ W^T for projection ``name`` (bf16, or FP8 W8A8 when quantised); ``swiglu``:
-        x is the [M, 2F] gate|up output and the projection consumes silu(gate) * up."""
+        x is the [M, 2F] gate|up output and the projection consumes silu(gate) * up.
+        ``partial_ok``: the caller sums K-split partials itself (``_reduce_add_norm``), so a
+        skinny K-split result may come back as an ``ops.PartialSum``."""
         if not self.fp8:
             a = ops.silu_mul(x) if swiglu else x
             w = L[name]
             M = a.shape[0]
+            pk = self._pick(w, M)
+            if pk is not None:
+                cfg, split = pk
+                if split == 1:
+                    return ops.skinny_gemm(a, w, cfg, 1, 0)
+                part = ops.PartialSum(ops.skinny_gemm(a, w, cfg, split, 1))
+                return part if partial_ok else part.materialize()
             if self.row_split and name in ("wo", "wd", "wgu") and self.cfg.hidden == 4096 and M > 4096 and M % 4096:
                 return ops.linear_rows_split(a, w, split=M // 4096 * 4096)
             return a @ w.t()
@@ -463,22 +484,28 @@ class LlamaModel:
             y.add_(b)
         return y
 
-    def _qkv(self, x, L):
+    def _qkv(self, x, L, partial_ok: bool = False):
         if "bqkv" in L:
             return torch.addmm(L["bqkv"], x, L["wqkv"].t())
-        return self._lin(x, L, "wqkv")
+        return self._lin(x, L, "wqkv", partial_ok=partial_ok)
 
-    def _mlp(self, x, L):
-        """MLP of one layer on normed rows; returns the (TP partial) output."""
+    def _mlp(self, x, L, partial_ok: bool = False):
+        """MLP of one layer on normed rows; returns the (TP partial) output (an
+        ``ops.PartialSum`` of K-split slabs when ``partial_ok`` and the down GEMM split K)."""
         cfg = self.cfg
         if cfg.is_moe:
             return ops.moe_ffn(x, L["router"], L["w13"], L["w2"], cfg.experts_per_tok,
                                expert0=self.expert0, act=cfg.act, ws=self.moe_ws)
         if cfg.gated_mlp:
+            if cfg.act == "silu":
+                pk = self._pick(L["wgu"], x.shape[0]) if "wgu" in L else None
+                if pk is not None:   # SwiGLU in the gate|up GEMM's epilogue: [M, F] straight out
+                    h = ops.skinny_gemm(x, L["wgu"], pk[0], 1, 2)
+                    return self._lin(h, L, "wd", partial_ok=partial_ok)
             gu = self._lin(x, L, "wgu")
             if cfg.act == "silu":
-                return self._lin(gu, L, "wd", swiglu=True)
-            return self._lin(ops.gelu_tanh_mul(gu), L, "wd")
+                return self._lin(gu, L, "wd", swiglu=True, partial_ok=partial_ok)
+            return self._lin(ops.gelu_tanh_mul(gu), L, "wd", partial_ok=partial_ok)
         h = x @ L["wgu"].t()
         ops.bias_gelu_(h, L.get("bgu"), approximate=cfg.act == "gelu_tanh")
         return self._bias_rank0(h @ L["wd"].t(), L.get("bd"))
@@ -571,7 +598,12 @@ class LlamaModel:
     def _reduce_add_norm(self, partial, resid, w, b=None):
         """resid += all_reduce_TP(partial); returns norm(resid). A small TP message goes
         through the custom all-reduce's fused add+RMSNorm epilogue kernel (one launch, the
-        sum never round-trips through HBM); otherwise all-reduce, then the add+norm kernel."""
+        sum never round-trips through HBM); otherwise all-reduce, then the add+norm kernel.
+        K-split skinny partials (one rank) are summed inside the add+RMSNorm kernel."""
+        if isinstance(partial, ops.PartialSum):
+            if b is None and self.p.tp_size == 1:
+                return ops.splitk_add_rmsnorm(resid, partial.slabs, w, self.cfg.eps)
+            partial = partial.materialize()
         if self.p.tp_size > 1:
             car = custom_all_reduce_for(self.p.tp_group)
             if b is None and car is not None and car.fused_norm_eligible(partial):
@@ -579,23 +611,30 @@ class LlamaModel:
             tp_all_reduce(partial, self.p)
         return self._add_norm(resid, partial, w, b)
 
-    def _attn_block(self, li: int, x, pos, meta: AttnMeta, T: int):
-        """qkv projection + RoPE/KV write + attention + o projection (TP partial)."""
+    def _attn_block(self, li: int, x, pos, meta: AttnMeta, T: int, partial_ok: bool = False):
+        """qkv projection + RoPE/KV write + attention + o projection (TP partial; an
+        ``ops.PartialSum`` when ``partial_ok`` and the o GEMM split K)."""
         L = self.layers[li]
-        qkv = self._qkv(x, L)
+        qkv = self._qkv(x, L, partial_ok=True)
+        part = None
+        if isinstance(qkv, ops.PartialSum):   # K-split projection: the RoPE kernel sums the slabs
+            part = qkv
+            qkv = torch.empty(part.shape, dtype=x.dtype, device=x.device)
         ops.rope_cache_(qkv, pos, self.cos_sin, meta.slots, self.k_cache[li],
-                        self.v_cache[li], self.hq, self.hkv, self.D, kv_scales=self.kv_scales)
+                        self.v_cache[li], self.hq, self.hkv, self.D, kv_scales=self.kv_scales, partial=part)
         attn = self._attention(qkv[:, :self.hq * self.D], qkv, li, meta, T)
-        return self._bias_rank0(self._lin(attn, L, "wo"), L.get("bo"))
+        if "bo" in L:
+            return self._bias_rank0(self._lin(attn, L, "wo"), L.get("bo"))
+        return self._lin(attn, L, "wo", partial_ok=partial_ok)
 
     def _layer(self, li: int, x, resid, pos, meta: AttnMeta):
         """One decoder layer on rows (x = norm(resid)); returns the MLP output d — still
         a TP partial sum — which the caller reduces into resid with the next layer's (or
         the final) norm."""
         L = self.layers[li]
-        o = self._attn_block(li, x, pos, meta, x.shape[0])
+        o = self._attn_block(li, x, pos, meta, x.shape[0], partial_ok=True)
         x = self._reduce_add_norm(o, resid, L["mlp_norm"], L.get("mlp_norm_b"))
-        return self._mlp(x, L)
+        return self._mlp(x, L, partial_ok="bd" not in L)
 
     def _final(self, resid, d, sample_idx):
         """Final norm of resid + d (all rows, or only the sampling rows)."""
@@ -614,6 +653,8 @@ class LlamaModel:
                 Ln = self.layers[li + 1]
                 x = self._reduce_add_norm(d, resid, Ln["attn_norm"], Ln.get("attn_norm_b"))
                 continue
+            if isinstance(d, ops.PartialSum):
+                d = d.materialize()
             tp_all_reduce(d, self.p)
             return self._final(resid, d, sample_idx)
         raise RuntimeError("model has no layers")
@@ -709,6 +750,8 @@ class LlamaModel:
             if li + 1 < n:
                 Ln = self.layers[li + 1]
                 x = self._reduce_add_norm(d, resid, Ln["attn_norm"], Ln.get("attn_norm_b"))
+        if isinstance(d, ops.PartialSum):
+            d = d.materialize()
         tp_all_reduce(d, self.p)
         rows = T if sample_idx is None else int(sample_idx.shape[0])
         if not self.last_stage:
@@ -762,8 +805,15 @@ class LlamaModel:
         return torch.cat([hd, hp])
 
     def logits(self, h: torch.Tensor) -> torch.Tensor:
-        """fp32 logits over the full vocabulary (vocab-parallel head + all-gather)."""
-        lg = (h @ self.lm_head.t()).float()
+        """fp32 logits over the full vocabulary (vocab-parallel head + all-gather). Where the
+        skinny table picks it, the LM head GEMM writes fp32 straight from its accumulators
+        (no bf16 logits tensor and no conversion pass)."""
+        pk = self._pick(self.lm_head, h.shape[0]) if (self.skinny and h.is_cuda and h.dtype == torch.bfloat16
+                                                       and self.lm_head.dtype == torch.bfloat16) else None
+        if pk is not None and pk[1] == 1 and h.stride(1) == 1 and h.stride(0) % 8 == 0:
+            lg = ops.skinny_gemm(h, self.lm_head, pk[0], 1, 1)[0]
+        else:
+            lg = (h @ self.lm_head.t()).float()
         return tp_all_gather(lg, dim=-1, ctx=self.p)
 
 

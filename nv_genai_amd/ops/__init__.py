@@ -12,6 +12,8 @@ from typing import Optional, Tuple
 import torch
 
 from . import reference as ref
+from . import skinny
+from .skinny import PartialSum
 
 _C = None
 _C_ERR: Optional[BaseException] = None
@@ -234,13 +236,18 @@ def bias_gelu_(x: torch.Tensor, bias: Optional[torch.Tensor], approximate=False)
 
 # ------------------------------------------------------------------------- rope / kv
 def rope_cache_(qkv, pos, cos_sin, slots, kc, vc, Hq: int, Hkv: int, D: int,
-                kv_scales=(1.0, 1.0)):
+                kv_scales=(1.0, 1.0), partial: Optional[PartialSum] = None):
     """RoPE on q / k in place + paged KV write. The caches are bf16, or fp8 e4m3fn holding
-    k / kv_scales[0] and v / kv_scales[1]."""
+    k / kv_scales[0] and v / kv_scales[1]. ``partial``: the projection came as K-split fp32
+    slabs; the kernel sums them and fills ``qkv`` (then output only) with the rotated q / k and
+    the v columns."""
+    if partial is not None and not _gpu(qkv):
+        qkv.copy_(partial.slabs.sum(0).to(qkv.dtype))
+        partial = None
     if not _gpu(qkv):
         return ref.rope_cache_(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, D, kv_scales)
     kernels().rope_cache(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, D, float(kv_scales[0]),
-                         float(kv_scales[1]))
+                         float(kv_scales[1]), None if partial is None else partial.slabs)
     return qkv
 
 

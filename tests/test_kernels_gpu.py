@@ -99,6 +99,28 @@ def test_rope_cache(gpu, Hq, Hkv, D, T):
     _close(vc, vc_r, 1e-6)
 
 
+@pytest.mark.parametrize("T", [7, 256, 300])
+def test_rope_cache_from_splitk_partials(gpu, T):
+    """The RoPE / KV-write kernel fed the qkv projection as K-split fp32 slabs (the skinny
+    GEMM's output) writes exactly what the bf16-materialised projection + RoPE writes: q / k
+    rotated, v columns, and both caches (per-token and tiled forms)."""
+    torch.manual_seed(4)
+    Hq, Hkv, D, S = 32, 8, 128, 3
+    P = torch.randn(S, T, (Hq + 2 * Hkv) * D, device=gpu)
+    pos = torch.randint(0, 4000, (T,), dtype=torch.int32, device=gpu)
+    cs = ops.rope_cos_sin(4096, D).to(gpu)
+    nb = (T + 63) // 64 + 4
+    kc, vc = _make_cache(nb, Hkv, D, gpu)
+    slots = torch.randperm(nb * 64, device=gpu)[:T].to(torch.int32)
+    slots[3] = -1
+    kc2, vc2 = kc.clone(), vc.clone()
+    want = ops.splitk_reduce(P)
+    ops.rope_cache_(want, pos, cs, slots, kc, vc, Hq, Hkv, D)
+    got = torch.full_like(want, float("nan"))
+    ops.rope_cache_(got, pos, cs, slots, kc2, vc2, Hq, Hkv, D, partial=ops.PartialSum(P))
+    assert torch.equal(got, want) and torch.equal(kc2, kc) and torch.equal(vc2, vc)
+
+
 def _paged_setup(ctxs, Hkv, D, dev, seed=0):
     torch.manual_seed(seed)
     pages = [(c + 63) // 64 for c in ctxs]
