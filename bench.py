@@ -78,8 +78,10 @@ def parse(argv=None):
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
-    ap.add_argument("--step-timing", action="store_true",
-                    help="GPU events around every engine step: in-step time vs idle between steps")
+    ap.add_argument("--no-step-timing", dest="step_timing", action="store_false",
+                    help="skip the GPU events around every engine step (in-step time vs idle between "
+                         "steps, reported as gpu_step_timing; on by default, two event records per step)")
+    ap.add_argument("--step-timing", dest="step_timing", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--mode", choices=("closed", "wave"), default="closed")
     ap.add_argument("--fp8", action="store_true",
                     help="W8A8 FP8 projections (not the headline: that is measured in bf16)")

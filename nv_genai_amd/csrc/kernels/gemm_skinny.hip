@@ -35,7 +35,6 @@
 // splitk_add_rmsnorm / the consumer), 2 = SwiGLU bf16 out [M, F] (N = F, gate rows [0, F),
 // up rows [F, 2F)).
 #include <cstdlib>
-#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
@@ -60,7 +59,7 @@ __device__ __forceinline__ void sk_wait_vm() {
 __device__ __forceinline__ float sk_silu(float x) { return x / (1.f + __expf(-x)); }
 }  // namespace
 
-template <int BN, int BM, int WN, int WM, int NSTAGE, int EPI, bool IL>
+template <int BN, int BM, int WN, int WM, int NSTAGE, int EPI>
 __global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmParams P) {
   constexpr int NW = WN * WM;   // waves per workgroup (4 or 8)
   constexpr int RW = BN / WN;   // weight rows per wave
@@ -179,43 +178,19 @@ __global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmPar
     else sk_wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     const uint16_t* ws = smem + (kt % NSTAGE) * STAGE;
-    if constexpr (IL) {
-      // interleaved form: this step's fragment reads first, then the next stage's DMA pieces
-      // spread one by one between the MFMAs (the TA takes a 1-KiB piece while the SIMD
-      // multiplies, instead of the wave stalling on a burst of NPS pieces at the barrier)
-      auto body = [&](auto has_next) {
-        read_frags(ws, 0);
-        read_frags(ws, 1);
-        if constexpr (decltype(has_next)::value) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
-        mfmas(0);
-        mfmas(1);
-        constexpr int MPG = (2 * NM) / NPS > 0 ? (2 * NM) / NPS : 1;
-        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);        // k-step 0 reads
+    if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
+    // k-step 0's fragments first; then its MFMAs with k-step 1's reads interleaved
+    read_frags(ws, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_frags(ws, 1);
+    mfmas(0);
 #pragma unroll
-        for (int g = 0; g < NPS; ++g) {
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);       // one DMA piece
-          if (g < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // a k-step 1 read
-          __builtin_amdgcn_sched_group_barrier(0x008, MPG, 0);     // MFMAs
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      if (kt + NSTAGE - 1 < nk) body(std::true_type{});
-      else body(std::false_type{});
-    } else {
-      if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
-      // k-step 0's fragments first; then its MFMAs with k-step 1's reads interleaved
-      read_frags(ws, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      read_frags(ws, 1);
-      mfmas(0);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, GM, 0);   // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, GR, 0);   // DS read
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      mfmas(1);
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, GM, 0);   // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, GR, 0);   // DS read
     }
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(1);
   }
   sk_wait_vm<0>();   // no DMA may still target this CU's LDS when the workgroup ends
 
@@ -329,37 +304,31 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(const float* _
 }
 
 // ------------------------------------------------------------------ launchers
-// tile configurations: {BN, BM, WN, WM, NSTAGE, IL} (WN x WM waves; IL: DMA pieces interleaved
-// with the MFMAs)
+// tile configurations: {BN, BM, WN, WM, NSTAGE} (WN x WM waves). Measured and dropped: the
+// next stage's DMA pieces spread one by one between the MFMAs instead of issued together at the
+// barrier (5-30 % slower at every tile; 256 x 256 collapsed; profiles/r4_headline_ab/sweep_il.jsonl)
 #define NGA_SKINNY_CFGS(X)     \
-  X(0, 256, 128, 2, 2, 3, 0)   \
-  X(1, 128, 128, 2, 2, 3, 0)   \
-  X(2, 128, 64, 2, 2, 3, 0)    \
-  X(3, 64, 64, 2, 2, 4, 0)     \
-  X(4, 128, 256, 2, 2, 2, 0)   \
-  X(5, 64, 256, 1, 4, 3, 0)    \
-  X(6, 256, 64, 4, 1, 3, 0)    \
-  X(7, 128, 32, 4, 1, 4, 0)    \
-  X(8, 256, 32, 4, 1, 3, 0)    \
-  X(9, 64, 128, 1, 4, 3, 0)    \
-  X(10, 128, 128, 2, 2, 4, 0)  \
-  X(11, 128, 128, 2, 2, 2, 0)  \
-  X(12, 256, 256, 4, 2, 2, 0)  \
-  X(13, 256, 128, 4, 2, 3, 0)  \
-  X(14, 128, 256, 2, 4, 2, 0)  \
-  X(15, 64, 64, 2, 2, 2, 0)    \
-  X(16, 256, 128, 2, 4, 3, 0)  \
-  X(17, 128, 128, 2, 2, 3, 1)  \
-  X(18, 256, 128, 4, 2, 3, 1)  \
-  X(19, 256, 128, 2, 4, 3, 1)  \
-  X(20, 128, 64, 2, 2, 3, 1)   \
-  X(21, 64, 64, 2, 2, 4, 1)    \
-  X(22, 256, 256, 4, 2, 2, 1)  \
-  X(23, 128, 128, 2, 2, 4, 1)
+  X(0, 256, 128, 2, 2, 3)   \
+  X(1, 128, 128, 2, 2, 3)   \
+  X(2, 128, 64, 2, 2, 3)    \
+  X(3, 64, 64, 2, 2, 4)     \
+  X(4, 128, 256, 2, 2, 2)   \
+  X(5, 64, 256, 1, 4, 3)    \
+  X(6, 256, 64, 4, 1, 3)    \
+  X(7, 128, 32, 4, 1, 4)    \
+  X(8, 256, 32, 4, 1, 3)    \
+  X(9, 64, 128, 1, 4, 3)    \
+  X(10, 128, 128, 2, 2, 4)  \
+  X(11, 128, 128, 2, 2, 2)  \
+  X(12, 256, 256, 4, 2, 2)  \
+  X(13, 256, 128, 4, 2, 3)  \
+  X(14, 128, 256, 2, 4, 2)  \
+  X(15, 64, 64, 2, 2, 2)    \
+  X(16, 256, 128, 2, 4, 3)
 
 int skinny_gemm_cfg_count() {
   int n = 0;
-#define NGA_COUNT(ID, BN, BM, WN, WM, NS, IL) ++n;
+#define NGA_COUNT(ID, BN, BM, WN, WM, NS) ++n;
   NGA_SKINNY_CFGS(NGA_COUNT)
 #undef NGA_COUNT
   return n;
@@ -368,7 +337,7 @@ int skinny_gemm_cfg_count() {
 // {BN, BM, WN, WM, NSTAGE} of a configuration, or zeros
 void skinny_gemm_cfg_info(int cfg, int* info) {
   info[0] = info[1] = info[2] = info[3] = info[4] = 0;
-#define NGA_INFO(ID, BN, BM, WN, WM, NS, IL) \
+#define NGA_INFO(ID, BN, BM, WN, WM, NS) \
   if (cfg == ID) {                       \
     info[0] = BN;                        \
     info[1] = BM;                        \
@@ -384,12 +353,12 @@ void launch_skinny_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t
   const int nblk = p.nN * p.nM * p.split;
   if (nblk == 0) return;
   dim3 grid(nblk);
-#define NGA_LAUNCH(ID, BN, BM, WN, WM, NS, IL)                                                        \
+#define NGA_LAUNCH(ID, BN, BM, WN, WM, NS)                                                        \
   if (cfg == ID) {                                                                                    \
     const dim3 block(64 * WN * WM);                                                                   \
-    if (epi == 0) skinny_gemm_kernel<BN, BM, WN, WM, NS, 0, IL><<<grid, block, 0, stream>>>(p);       \
-    else if (epi == 1) skinny_gemm_kernel<BN, BM, WN, WM, NS, 1, IL><<<grid, block, 0, stream>>>(p);  \
-    else skinny_gemm_kernel<BN, BM, WN, WM, NS, 2, IL><<<grid, block, 0, stream>>>(p);                \
+    if (epi == 0) skinny_gemm_kernel<BN, BM, WN, WM, NS, 0><<<grid, block, 0, stream>>>(p);       \
+    else if (epi == 1) skinny_gemm_kernel<BN, BM, WN, WM, NS, 1><<<grid, block, 0, stream>>>(p);  \
+    else skinny_gemm_kernel<BN, BM, WN, WM, NS, 2><<<grid, block, 0, stream>>>(p);                \
     return;                                                                                           \
   }
   NGA_SKINNY_CFGS(NGA_LAUNCH)

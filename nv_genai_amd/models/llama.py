@@ -194,7 +194,7 @@ class LlamaModel:
                 return part if partial_ok else part.materialize()
             if self.row_split and name in ("wo", "wd", "wgu") and self.cfg.hidden == 4096 and M > 4096 and M % 4096:
                 return ops.linear_rows_split(a, w, split=M // 4096 * 4096)
-            return a @ w.t()
+            return ops.linear(a, w)
         x8, sx = ops.quant_fp8_rows(x, mode=1 if swiglu else 0)
         return ops.fp8_linear(x8, sx, L[name + "8"], L[name + "_s"], x.shape[0])
 

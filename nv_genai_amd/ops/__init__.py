@@ -102,6 +102,27 @@ def gelu_tanh_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None):
     return out
 
 
+def check_gemm_weight(w: torch.Tensor, what: str = "weight") -> torch.Tensor:
+    """Library-GEMM operand guard: a weight must be a plain row-major matrix (2-D, unit column
+    stride, row stride >= its width, 16-B aligned). The round-3 small-M probe faulted the GPU
+    (hipErrorIllegalAddress) inside the library's batched split-K GEMM when it was handed a
+    permuted [s, K/s, N] view of a weight (the batch dimension carved out of K, so each batch's
+    rows are strided views into the transposed matrix); such views are rejected here instead of
+    reaching the library. Returns ``w``."""
+    if w.dim() != 2 or w.stride(1) != 1 or w.stride(0) < w.shape[1] or w.data_ptr() % 16:
+        raise ValueError(f"{what}: the GEMM takes a contiguous row-major [N, K] matrix, got shape "
+                         f"{tuple(w.shape)} strides {tuple(w.stride())}; make it .contiguous() once at load")
+    return w
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``x @ w^T`` on the library GEMM with the operand guard (:func:`check_gemm_weight`)."""
+    check_gemm_weight(w)
+    if x.dim() != 2 or x.stride(1) != 1:
+        x = x.contiguous()
+    return torch.matmul(x, w.t(), out=out) if out is not None else x @ w.t()
+
+
 def linear_rows_split(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
                       split: int = 0) -> torch.Tensor:
     """``x @ w^T`` (library GEMM) with the rows cut at ``split`` when ``x`` has more: the first
@@ -110,6 +131,7 @@ def linear_rows_split(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tens
     second wave — while 4,096 rows are exactly one wave and the 256-row remainder runs right
     after on MALL-warm weights (benchmarks/row_split_gemm.py)."""
     M = x.shape[0]
+    check_gemm_weight(w)
     if out is None:
         out = torch.empty(M, w.shape[0], dtype=x.dtype, device=x.device)
     if split <= 0 or M <= split:

@@ -63,9 +63,12 @@ def main():
                 n = c["TCC_EA0_RDREQ_sum"]
                 n32 = c.get("TCC_EA0_RDREQ_32B_sum", 0.0)
                 n128 = c.get("TCC_EA0_RDREQ_128B_sum", None)
-                if n128 is None:   # 32 B and 64 B requests only
+                n64 = c.get("TCC_EA0_RDREQ_64B_sum", None)
+                if n128 is None:   # size split not collected: 32 B and 64 B requests assumed
                     return 32 * n32 + 64 * (n - n32)
-                return 32 * n32 + 128 * n128 + 64 * max(0.0, n - n32 - n128)
+                if n64 is None:
+                    n64 = max(0.0, n - n32 - n128)
+                return 32 * n32 + 64 * n64 + 128 * n128
             by = [rd_bytes(c) for _, c in req]
             print(f"    HBM read bytes (TCC_EA0_RDREQ by size)  {sum(by) / len(by) / 1e6:.1f} MB")
             bw = [rd_bytes(c) / (x * 1e-6) for x, c in req if x]

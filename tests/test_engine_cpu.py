@@ -323,3 +323,24 @@ def test_linear_rows_split_matches_matmul():
     buf = torch.empty(300, 48)
     x = torch.randn(300, 96, generator=g)
     assert ops.linear_rows_split(x, w, buf, 256).data_ptr() == buf.data_ptr()
+
+
+def test_gemm_operand_guard_rejects_strided_weight_views():
+    """ops.linear / linear_rows_split refuse the permuted split-K weight view that faulted the
+    library GEMM in the round-3 probe; plain weights pass and match x @ w^T."""
+    import pytest
+    import torch
+
+    from nv_genai_amd import ops
+
+    x = torch.randn(8, 64)
+    w = torch.randn(32, 64)
+    assert torch.allclose(ops.linear(x, w), x @ w.t())
+    assert torch.allclose(ops.linear_rows_split(x, w, split=4), x @ w.t())
+    batched = w.t().reshape(4, 16, 32).permute(0, 2, 1)            # the probe's [s, N, K/s] split-K view
+    with pytest.raises(ValueError, match="contiguous row-major"):
+        ops.linear(x[:, :16], batched)
+    with pytest.raises(ValueError):
+        ops.linear(x, w.t().contiguous().t())                      # column-major storage
+    with pytest.raises(ValueError):
+        ops.linear_rows_split(x, w[:, ::2], split=4)
