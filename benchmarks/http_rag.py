@@ -9,7 +9,9 @@ query batcher on its own HIP stream. Generation goes through the continuous-batc
 
 The load generator is a separate CPU-only asyncio process. It runs a closed loop: each of
 ``--concurrency`` clients posts a generated question, reads the SSE stream to ``[DONE]`` and posts
-the next. Once ``--warmup`` requests have completed, the next ``--requests`` completions are
+the next. Clients start staggered over ``--ramp-s`` (bench.py ramps its clients in the same
+way), so arrivals are spread in time rather than synchronized into waves that all prefill at
+once. Once ``--warmup`` requests have completed, the next ``--requests`` completions are
 timed, with every client still busy (no drain inside the window, as in bench.py). The script
 prints one JSON line with QPS and the p50/p95 latency and TTFT of the timed requests.
 
@@ -41,6 +43,51 @@ def _free_port() -> int:
     return p
 
 
+def _server_quantiles(text: str) -> dict:
+    """p50 (ms) of the chain server's own request-phase summaries (whole run, warmup included):
+    chain_wait = request arrival -> retrieval + prompt queued on the engine (worker-thread
+    queueing included), chain = that work alone, ttft = arrival -> first token."""
+    out = {}
+    for line in text.splitlines():
+        if line.startswith("chain_server_") and 'quantile="0.5"' in line:
+            name = line.split("{")[0][len("chain_server_"):]
+            if name == "retrieval_batch_size":
+                out[name] = float(line.rsplit(" ", 1)[1])
+            elif name.endswith("_seconds"):
+                try:
+                    out[name[:-len("_seconds")]] = round(1e3 * float(line.rsplit(" ", 1)[1]), 2)
+                except ValueError:
+                    pass
+    return out
+
+
+def _gauges(text: str) -> dict:
+    out = {}
+    for line in text.splitlines():
+        if line.startswith("chain_server_") and "{" not in line:
+            k, _, v = line.partition(" ")
+            try:
+                out[k[len("chain_server_"):]] = float(v)
+            except ValueError:
+                pass
+    return out
+
+
+def _engine_window(m0, m1) -> dict:
+    """Engine counters over the timed window (same fields as bench.py's ``host_s``): steps by
+    kind and host seconds per phase; ``wait`` is the engine thread blocked on the GPU."""
+    if not m0 or not m1:
+        return {}
+    d = {k: m1[k] - m0.get(k, 0.0) for k in m1 if k in m0}
+    steps = d.get("steps", 0.0)
+    out = {"steps": int(steps), "decode_steps": int(d.get("decode_steps", 0)), "mixed_steps": int(d.get("mixed_steps", 0)),
+           "host_s": {k[5:-2]: round(d.get(k, 0.0), 3) for k in ("host_sched_s", "host_launch_s", "host_between_s",
+                                                                 "host_wait_s", "host_finalize_s")}}
+    if steps:
+        out["host_ms_per_step"] = {k: round(1e3 * v / steps, 3) for k, v in out["host_s"].items()}
+    return out
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--llm", default="llama3-8b")
@@ -50,6 +97,8 @@ def parse(argv=None):
     ap.add_argument("--requests", type=int, default=512)
     ap.add_argument("--warmup", type=int, default=256)
     ap.add_argument("--max-tokens", type=int, default=256)
+    ap.add_argument("--ramp-s", type=float, default=6.0,
+                    help="client k starts k/concurrency * ramp_s after the first (0: all at once)")
     ap.add_argument("--example", default="developer_rag")
     ap.add_argument("--device", default="", help="engine device for the server ('' = cuda if available)")
     ap.add_argument("--startup-timeout", type=float, default=600.0)
@@ -86,11 +135,16 @@ async def _load(url, args, questions):
     completed until ``--requests`` more have, while every client is still busy."""
     import httpx
 
+    metrics_url = url.rsplit("/", 1)[0] + "/metrics"
     limits = httpx.Limits(max_connections=args.concurrency + 8, max_keepalive_connections=args.concurrency + 8)
     results = []
     state = {"done": 0, "t_start": None, "stop": False, "issued": 0}
 
-    async def client_loop(client):
+    async def client_loop(client, k):
+        # staggered start (bench.py's ramp): client k joins k/concurrency of the way through
+        # one request's lifetime, so completions and re-arrivals spread evenly over time
+        # instead of all clients prefilling together in synchronized waves
+        await asyncio.sleep(k * args.ramp_s / max(1, args.concurrency))
         while not state["stop"]:
             i = state["issued"]
             state["issued"] += 1
@@ -99,14 +153,16 @@ async def _load(url, args, questions):
             state["done"] += 1
             if state["done"] == args.warmup:
                 state["t_start"] = now
+                state["m0"] = _gauges((await client.get(metrics_url)).text)
             elif state["t_start"] is not None and not state["stop"]:
                 results.append((lat, ttft, chars, now))
                 if len(results) >= args.requests:
                     state["stop"] = True
+                    state["m1"] = _gauges((await client.get(metrics_url)).text)
 
     async with httpx.AsyncClient(timeout=httpx.Timeout(600.0), limits=limits) as client:
-        await asyncio.gather(*(client_loop(client) for _ in range(args.concurrency)))
-    return results, state["t_start"]
+        await asyncio.gather(*(client_loop(client, k) for k in range(args.concurrency)))
+    return results, state["t_start"], _engine_window(state.get("m0"), state.get("m1"))
 
 
 def main(argv=None):
@@ -145,7 +201,8 @@ def main(argv=None):
         setup_s = time.time() - t0
         gen = TextGen(seed=100)
         questions = [gen.question() for _ in range(4096)]
-        results, t_start = asyncio.run(_load(base + "/generate", args, questions))
+        results, t_start, engine_window = asyncio.run(_load(base + "/generate", args, questions))
+        server_side = _server_quantiles(httpx.get(base + "/metrics", timeout=30).text)
         t_end = max(r[3] for r in results)
         elapsed = t_end - t_start
         lat = sorted(r[0] for r in results)
@@ -153,6 +210,7 @@ def main(argv=None):
         res = {"metric": "end-to-end RAG QPS + p50 latency through the chain-server REST API (POST /generate, SSE)",
                "value": round(len(results) / elapsed, 4), "unit": "requests/s", "n_gpus": 1,
                "requests": len(results), "concurrency": args.concurrency, "elapsed_s": round(elapsed, 3),
+               "ramp_s": args.ramp_s,
                "p50_latency_ms": round(1e3 * statistics.median(lat), 1),
                "p95_latency_ms": round(1e3 * lat[min(len(lat) - 1, int(0.95 * len(lat)))], 1),
                "p50_ttft_ms": round(1e3 * statistics.median(ttft), 1) if ttft else None,
@@ -160,7 +218,8 @@ def main(argv=None):
                "config": {"model": f"{args.llm} + {args.embed}", "index_size": args.index_size,
                           "example": args.example, "max_tokens": args.max_tokens},
                "dtype": "bf16", "data": "synthetic: random-init weights, 1M random unit-vector index, generated questions",
-               "setup_s": round(setup_s, 1)}
+               "setup_s": round(setup_s, 1), "server_p50_ms": server_side,
+               "engine_window": engine_window}
         line = json.dumps(res)
         print(line, flush=True)
         if args.out:

@@ -34,6 +34,7 @@ from fastapi.exceptions import RequestValidationError
 from fastapi.middleware.cors import CORSMiddleware
 from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
 from pydantic import BaseModel, Field, constr, field_validator
+from starlette.concurrency import run_in_threadpool
 from starlette.status import HTTP_422_UNPROCESSABLE_ENTITY
 
 from ..observability.metrics import METRICS
@@ -164,6 +165,12 @@ def import_example() -> None:
     import anyio.to_thread
 
     anyio.to_thread.current_default_thread_limiter().total_tokens = int(os.environ.get("APP_THREADPOOL", "2048"))
+    # GIL hand-off interval (tuning knob; measured: 0.2 / 0.5 ms did not beat CPython's 5 ms
+    # default on the REST RAG benchmark, profiles/r4_http/)
+    if os.environ.get("APP_GIL_SWITCH_US"):
+        import sys
+
+        sys.setswitchinterval(float(os.environ["APP_GIL_SWITCH_US"]) * 1e-6)
     if getattr(app, "example", None) is None:
         app.example = load_example()
     # in-process engines are built (weights, KV cache, decode hipGraphs) before traffic arrives
@@ -277,8 +284,22 @@ async def generate_answer(request: Request, prompt: Prompt) -> StreamingResponse
         # on the event loop it would serialise every request's retrieval and stall all streams,
         # and concurrent requests' searches could never share a batch (VectorStore batcher)
         chain = example.rag_chain if prompt.use_knowledge_base else example.llm_chain
-        generator = await asyncio.to_thread(chain, query=last_user_message, chat_history=chat_history,
-                                            **llm_settings)
+
+        def run_chain():
+            t0 = time.perf_counter()
+            g = chain(query=last_user_message, chat_history=chat_history, **llm_settings)
+            if hasattr(g, "prepare"):
+                t1 = time.perf_counter()
+                g.prepare()      # prompt tokenised + queued on the engine from this thread
+                METRICS.observe("prepare_seconds", time.perf_counter() - t1)
+            METRICS.observe("chain_seconds", time.perf_counter() - t0)
+            return g
+
+        # anyio's pool (limiter raised to APP_THREADPOOL at startup), not asyncio's default
+        # executor of min(32, cpus + 4) threads: every concurrent request's retrieval must be
+        # in flight at once for the vector store's batcher to coalesce them
+        generator = await run_in_threadpool(run_chain)
+        METRICS.observe("chain_wait_seconds", time.perf_counter() - t_start)
     except Exception as e:  # noqa: BLE001
         logger.error("Error from /generate endpoint. Error details: %s", e)
         METRICS.inc("generate_errors_total")

@@ -247,13 +247,21 @@ class LimitRetrievedNodesLength:
 
     def __init__(self, limit: int = DEFAULT_MAX_CONTEXT, count=None):
         self.limit = limit
-        self.count = count or llm_tokenizer_len
+        self.count = count
 
     def postprocess(self, docs):
+        texts = [d.page_content if hasattr(d, "page_content") else d[0].page_content for d in docs]
+        if self.count is None:
+            # one batched encode (the Rust tokenizer runs it without the GIL) instead of a
+            # GIL-holding encode per document on every request's worker thread
+            from ..utils.tokenizer import llm_tokenizer
+
+            counts = [len(ids) for ids in llm_tokenizer().encode_batch(texts)] if texts else []
+        else:
+            counts = [self.count(t) for t in texts]
         out, total = [], 0
-        for d in docs:
-            text = d.page_content if hasattr(d, "page_content") else d[0].page_content
-            total += self.count(text)
+        for d, n in zip(docs, counts):
+            total += n
             if total > self.limit:
                 break
             out.append(d)

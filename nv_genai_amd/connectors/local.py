@@ -71,10 +71,16 @@ class LocalChatModel:
             if not h.done.is_set():
                 h.cancel()
 
-    async def astream(self, messages: Messages, coalesce: bool = False, **kw):
+    def submit(self, messages: Messages, **kw) -> StreamHandle:
+        """Queue the request now; stream it later with ``astream(..., handle=h)``."""
+        return self._submit(messages, **kw)
+
+    async def astream(self, messages: Messages, coalesce: bool = False, handle: Optional[StreamHandle] = None,
+                      **kw):
         """Async token stream straight from the engine's asyncio queue (no worker thread);
-        ``coalesce`` joins the deltas that are already queued into one chunk."""
-        h = self._submit(messages, **kw)
+        ``coalesce`` joins the deltas that are already queued into one chunk; ``handle``: a
+        request already queued by :meth:`submit`."""
+        h = handle if handle is not None else self._submit(messages, **kw)
         try:
             async for d in h.aiter(coalesce=coalesce):
                 yield d

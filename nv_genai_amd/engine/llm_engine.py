@@ -234,6 +234,7 @@ class LLMEngine:
                       "host_wait_s": 0.0, "host_finalize_s": 0.0, "graph_steps": 0, "graph_captures": 0,
                       "graph_capture_s": 0.0}
         self.lock = threading.RLock()
+        self._inbox: "collections.deque" = collections.deque()   # requests queued while a step held the lock
         self._pending: Optional[dict] = None
         self._tok_flip = 0
         self._up_ev = None  # marks the last host->device upload of the pinned step buffers
@@ -338,18 +339,40 @@ class LLMEngine:
             req.json_state = rt.JsonState(True)
         elif params.response_format not in (None, "text"):
             raise ValueError(f"unsupported response_format {params.response_format!r}")
-        with self.lock:
-            self.sched.add(rid, req.prompt_ids, max_new)
-            if params.beam_width > 1:
-                g = BeamGroup(req, int(params.beam_width), float(params.length_penalty))
-                g.beams[rid] = 0.0
-                self._beam_of[rid] = g
-            else:
-                self.requests[rid] = req
+        # A step holds the engine lock for its whole duration (GPU wait included). A producer
+        # thread must not queue behind it: when the lock is busy the request goes to the
+        # inbox, which the next step admits first (same order, no lost wake-ups).
+        if self.lock.acquire(blocking=False):
+            try:
+                self._admit(req, max_new)
+            finally:
+                self.lock.release()
+        else:
+            self._inbox.append((req, max_new))
         return req
+
+    def _admit(self, req: Request, max_new: int):
+        while self._inbox:      # earlier arrivals first
+            self._admit_one(*self._inbox.popleft())
+        self._admit_one(req, max_new)
+
+    def _admit_one(self, req: Request, max_new: int):
+        rid, params = req.id, req.params
+        self.sched.add(rid, req.prompt_ids, max_new)
+        if params.beam_width > 1:
+            g = BeamGroup(req, int(params.beam_width), float(params.length_penalty))
+            g.beams[rid] = 0.0
+            self._beam_of[rid] = g
+        else:
+            self.requests[rid] = req
+
+    def _admit_inbox(self):
+        while self._inbox:
+            self._admit_one(*self._inbox.popleft())
 
     def abort(self, rid: int):
         with self.lock:
+            self._admit_inbox()
             req = self.requests.pop(rid, None)
             self.sched.finish(rid)
             g = next((g for g in set(self._beam_of.values()) if g.req.id == rid), None)
@@ -364,7 +387,7 @@ class LLMEngine:
                 req.finish_time = time.perf_counter()
 
     def has_work(self) -> bool:
-        return self.sched.has_work()
+        return bool(self._inbox) or self.sched.has_work()
 
     # ------------------------------------------------------------------ step
     def _fill_params(self, reqs, pending_ids=()):
@@ -397,6 +420,7 @@ class LLMEngine:
         (``mixed_prefill_tokens``) a step carries the decode rows of every running sequence
         plus a prefill chunk, so decode rows ride on the prefill GEMMs."""
         with self.lock:
+            self._admit_inbox()
             self._nstep += 1
             if self._faults:
                 self._faults.check(self._nstep, "driver")

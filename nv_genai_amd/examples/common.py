@@ -25,6 +25,15 @@ class LLMStream:
     def __init__(self, cb, llm, messages, kwargs):
         self.cb, self.llm, self.messages, self.kwargs = cb, llm, messages, kwargs
         self.rid = uuid.uuid4().hex
+        self._handle = None
+
+    def prepare(self) -> "LLMStream":
+        """Tokenise the prompt and queue it on the engine now (the chain server calls this on
+        the request's worker thread, so chat-template encoding stays off the event loop and
+        the request enters the scheduler as soon as its context is ready)."""
+        if self._handle is None and self.supports_async and hasattr(self.llm, "submit"):
+            self._handle = self.llm.submit(self.messages)
+        return self
 
     def _start(self):
         self.cb.on_llm_start(self.rid, self.messages, **{k: v for k, v in self.kwargs.items() if v is not None})
@@ -50,7 +59,7 @@ class LLMStream:
         self._start()
         out: List[str] = []
         try:
-            async for chunk in self.llm.astream(self.messages, coalesce=True):
+            async for chunk in self.llm.astream(self.messages, coalesce=True, handle=self._handle):
                 self.cb.on_llm_new_token(self.rid, chunk)
                 out.append(chunk)
                 yield chunk

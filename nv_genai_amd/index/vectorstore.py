@@ -9,12 +9,14 @@ from __future__ import annotations
 import json
 import os
 import threading
+import time
 from dataclasses import dataclass, field
 from pathlib import Path
 from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple
 
 import torch
 
+from ..observability.metrics import METRICS
 from .docstore import DocStore
 from .flat import FlatIndex
 from .ivf import IVFFlatIndex
@@ -65,23 +67,25 @@ class _QueryBatcher:
         import concurrent.futures as cf
 
         fut = cf.Future()
-        self.q.put((query, k, fut))
+        self.q.put((query, k, fut, time.perf_counter()))
         return fut
 
     def _loop(self):
-        import time as _time
-
         while True:
             batch = [self.q.get()]
-            deadline = _time.monotonic() + self.wait_s
+            deadline = time.monotonic() + self.wait_s
             while len(batch) < self.max_batch:
-                left = deadline - _time.monotonic()
+                left = deadline - time.monotonic()
                 if left <= 0:
                     break
                 try:
                     batch.append(self.q.get(timeout=left))
                 except self._empty:
                     break
+            t0 = time.perf_counter()
+            for b in batch:
+                METRICS.observe("retrieval_queue_seconds", t0 - b[3])
+            METRICS.observe("retrieval_batch_size", len(batch))
             try:
                 if self.stream is not None:
                     ev = self.store._write_ev
@@ -93,12 +97,13 @@ class _QueryBatcher:
                 else:
                     res = self.store.similarity_search_with_score_batch([b[0] for b in batch],
                                                                         max(b[1] for b in batch))
-                for (_, k, fut), r in zip(batch, res):
+                METRICS.observe("retrieval_exec_seconds", time.perf_counter() - t0)
+                for (_, k, fut, _), r in zip(batch, res):
                     fut.set_result(r[:k])
                 self.batches += 1
                 self.queries += len(batch)
             except BaseException as e:  # noqa: BLE001 - delivered to every waiting request
-                for _, _, fut in batch:
+                for _, _, fut, _ in batch:
                     if not fut.done():
                         fut.set_exception(e)
 
@@ -133,7 +138,8 @@ class VectorStore:
             dev.type == "cuda" and self.index_device().type == "cuda"
             and os.environ.get("NGA_BATCH_QUERIES", "1") != "0")
         if use:
-            self._batcher = _QueryBatcher(self, dev)
+            # NGA_QUERY_BATCH_WAIT_MS: how long the first query of a batch waits for company
+            self._batcher = _QueryBatcher(self, dev, wait_s=float(os.environ.get("NGA_QUERY_BATCH_WAIT_MS", "2")) / 1e3)
         self.persist_dir = persist_dir
         if persist_dir and (Path(persist_dir) / "index.json").exists():
             self.load(persist_dir)

@@ -26,6 +26,11 @@ class EngineError(RuntimeError):
     pass
 
 
+def _deliver(items):
+    for aq, item in items:
+        aq.put_nowait(item)
+
+
 class StreamHandle:
     """Token-delta stream of one request (sync and async iteration).
 
@@ -42,11 +47,32 @@ class StreamHandle:
         self._lock = threading.Lock()
         self._loop: Optional[asyncio.AbstractEventLoop] = None
         self._aq: Optional[asyncio.Queue] = None
+        self._buf: List[str] = []       # deltas held back by the stream interval
+        self._sent_step = -1            # service step of the last delivery (-1: none yet)
 
     def _put(self, item):
         with self._lock:
             if self._aq is not None:
-                self._loop.call_soon_threadsafe(self._aq.put_nowait, item)
+                svc = self.service
+                if threading.current_thread() is svc.thread:
+                    # engine thread: deliveries of one step go to each event loop in ONE
+                    # call_soon_threadsafe (one self-pipe write + one loop wake-up per step,
+                    # not one per open stream per token). Text deltas are held for up to
+                    # ``stream_interval`` steps (the first one and the end go out at once), so
+                    # an open stream costs the event loop one wake-up + one SSE frame per
+                    # interval instead of per token.
+                    if item is not _END:
+                        self._buf.append(item)
+                        if self._sent_step >= 0 and svc.steps - self._sent_step < svc.stream_interval:
+                            return
+                    if self._buf:
+                        svc._pending.setdefault(self._loop, []).append((self._aq, "".join(self._buf)))
+                        self._buf = []
+                        self._sent_step = svc.steps
+                    if item is _END:
+                        svc._pending.setdefault(self._loop, []).append((self._aq, _END))
+                else:
+                    self._loop.call_soon_threadsafe(self._aq.put_nowait, item)
             else:
                 self.q.put(item)
 
@@ -128,13 +154,16 @@ class StreamHandle:
 
 class EngineService:
     def __init__(self, engine: LLMEngine, watchdog_s: float = 300.0, name: str = "llm",
-                 quiet_gc: bool = True, fail_fast: bool = False):
+                 quiet_gc: bool = True, fail_fast: bool = False, stream_interval: Optional[int] = None):
         if quiet_gc:   # no multi-ms GC pauses on the thread that launches GPU steps
             from ..utils.runtime import quiet_gc as _quiet
 
             _quiet()
         self.engine = engine
         self.watchdog_s = watchdog_s
+        # async streams: deliver text at most every N engine steps (NGA_STREAM_INTERVAL)
+        self.stream_interval = max(1, int(stream_interval if stream_interval is not None
+                                          else os.environ.get("NGA_STREAM_INTERVAL", "8")))
         self.name = name
         self.cv = threading.Condition()
         self.handles = {}
@@ -143,6 +172,7 @@ class EngineService:
         self.last_error: Optional[str] = None
         self.steps = 0
         self.tasks: "queue.Queue" = queue.Queue()   # callables run on the engine thread
+        self._pending: dict = {}                     # event loop -> [(asyncio queue, item)] of this step
         self.fail_fast = fail_fast
         self.thread = threading.Thread(target=self._loop, name=f"{name}-engine", daemon=True)
         self.thread.start()
@@ -212,6 +242,7 @@ class EngineService:
                 break
             if not self.tasks.empty():
                 self.engine.drain_and_run(self._run_tasks)
+                self._flush()
                 if not self.engine.has_work():
                     continue
             try:
@@ -238,6 +269,18 @@ class EngineService:
                     os._exit(70)
             finally:
                 self.step_started = None
+                self._flush()
+
+    def _flush(self):
+        """Hand the step's stream deliveries to their event loops, one callback per loop."""
+        if not self._pending:
+            return
+        pending, self._pending = self._pending, {}
+        for loop, items in pending.items():
+            try:
+                loop.call_soon_threadsafe(_deliver, items)
+            except RuntimeError:   # loop closed (server shutting down): nobody is listening
+                pass
 
     def healthy(self) -> bool:
         st = self.step_started

@@ -87,3 +87,57 @@ def test_cancel_aborts_request_and_frees_blocks(service):
     assert h.request.finish_reason == "abort"
     assert not eng.has_work() and eng.sched.used_blocks() == used0
     assert len(h.request.output_ids) < 400
+
+
+def test_async_streams_batch_deliveries_per_interval():
+    """Async consumers get the same text as a sync stream, with text deltas held for up to
+    ``stream_interval`` engine steps (first delta and end immediately) and every step's
+    deliveries handed to the event loop in one callback."""
+    import asyncio
+
+    eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=8, max_batched_tokens=256, max_model_len=512,
+                                 kv_cache_blocks=64), device="cpu")
+    svc = EngineService(eng, quiet_gc=False, stream_interval=4)
+    try:
+        want = svc.submit([5, 6, 7, 8] * 4, _params(24)).text()
+
+        async def run():
+            return await asyncio.gather(*[_collect(h) for h in
+                                          [svc.submit([5, 6, 7, 8] * 4, _params(24)) for _ in range(3)]])
+
+        async def _collect(h):
+            return [c async for c in h.aiter(coalesce=True)]
+
+        outs = asyncio.run(run())
+        for chunks in outs:
+            assert "".join(chunks) == want
+            assert len(chunks) <= 24 // 4 + 2, chunks
+        assert svc._pending == {}
+    finally:
+        svc.shutdown()
+
+
+def test_add_request_does_not_wait_for_a_running_step():
+    """A step holds the engine lock for its whole duration; add_request from another thread
+    queues in the inbox instead of blocking, and the next step admits it in arrival order."""
+    eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=8, max_batched_tokens=256, max_model_len=512,
+                                 kv_cache_blocks=64), device="cpu")
+    held, release = threading.Event(), threading.Event()
+
+    def hold():
+        with eng.lock:
+            held.set()
+            release.wait(10)
+
+    t = threading.Thread(target=hold)
+    t.start()
+    held.wait(5)
+    t0 = time.perf_counter()
+    a = eng.add_request([5, 6, 7], _params(3))
+    b = eng.add_request([8, 9, 10], _params(3))
+    assert time.perf_counter() - t0 < 0.5
+    assert eng.has_work() and a.id not in eng.requests and len(eng._inbox) == 2
+    release.set()
+    t.join()
+    eng.run_until_done([a, b])
+    assert len(a.output_ids) == 3 and len(b.output_ids) == 3 and not eng._inbox
