@@ -196,7 +196,8 @@ def main():
         # causal FLOPs: query i of a ql-row chunk ending at ctx sees ctx - ql + i + 1 keys
         flops = sum(2 * 2 * (ql * (c - ql) + ql * (ql + 1) / 2) * D * Hq for c, ql in zip(lens, qls))
         out[name] = {}
-        for impl, tag in ((0, "auto"), (4, "auto_alone"), (1, "mfma16"), (2, "mfma32"), (3, "mfma32_ks2")):
+        for impl, tag in ((0, "auto"), (4, "auto_alone"), (1, "mfma16"), (2, "mfma32"), (3, "mfma32_ks2"),
+                          (5, "mfma32_w8"), (6, "mfma32_stg")):
             us = timeit(lambda: ops.prefill_attention_paged(q, kc, vc, bt, cu, ctx, Hq, Hkv, D, max(qls),
                                                             D ** -0.5, impl=impl))
             out[name][tag] = {"us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1)}

@@ -99,12 +99,19 @@ def main():
                     continue
                 nn = (N // 2) // (BN // 2) if name == "gate_up" else -(-N // BN)
                 nm = -(-M // BM)
-                splits = [1] if name in ("gate_up", "lm_head") else [s for s in (1, 2, 3, 4, 6, 8, 12, 16) if s <= K // 64]
+                splits = [1] if name == "lm_head" else [s for s in (1, 2, 3, 4, 6, 8, 12, 16) if s <= K // 64]
+                if name == "gate_up":
+                    splits = [s for s in splits if s <= 4]
                 for s in splits:
                     blocks = nn * nm * s
                     if blocks < 16 or blocks > 4096 or (s > 1 and nn * nm >= 512):
                         continue
-                    if name == "gate_up":
+                    if name == "gate_up" and s > 1:   # K-split slabs summed by the SwiGLU kernel
+                        out = torch.empty(s, M, N, device=dev)
+                        h = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
+                        fn = (lambda i, out=out, c=c, s=s, h=h: (C.skinny_gemm(out, x, Ws[i], 1, s, c, 0, 0, 0, 0, 0),
+                                                                 C.splitk_swiglu(h, out, s)))
+                    elif name == "gate_up":
                         out = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
                         fn = (lambda i, out=out, c=c: C.skinny_gemm(out, x, Ws[i], 2, 1, c, 0, 0, 0, 0, 0))
                     elif name == "lm_head":

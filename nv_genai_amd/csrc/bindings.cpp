@@ -320,6 +320,16 @@ void skinny_gemm(Tensor out, Tensor x, Tensor w, int64_t epi, int64_t split, int
   nga::launch_skinny_gemm(p, (int)cfg, (int)epi, cur_stream(x));
 }
 
+void splitk_swiglu(Tensor out, Tensor P, int64_t S) {
+  CHECK_DEV(P); CHECK_BF16(out);
+  TORCH_CHECK(out.device() == P.device(), "splitk_swiglu: out and P on one device");
+  const int64_t M = out.size(0), F = out.size(1);
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.stride(0) % 8 == 0, "splitk_swiglu: out [M, F] rows 16-B aligned");
+  TORCH_CHECK(P.is_contiguous() && P.scalar_type() == at::kFloat, "splitk_swiglu: P fp32 contiguous");
+  TORCH_CHECK(S >= 1 && F % 8 == 0 && P.numel() >= S * M * 2 * F, "splitk_swiglu: P must hold S x M x 2F floats");
+  nga::launch_splitk_swiglu(P.data_ptr<float>(), (int)S, (int)M, (int)F, bfp(out), out.stride(0), cur_stream(P));
+}
+
 void splitk_reduce(Tensor out, Tensor P, int64_t S) {
   CHECK_DEV(P); CHECK_DT(P, at::kFloat); CHECK_CONTIG(P); CHECK_BF16(out);
   TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.stride(0) % 8 == 0, "splitk_reduce: out [M, N] rows 16-B aligned");
@@ -453,7 +463,9 @@ void prefill_attention(Tensor out, Tensor q, c10::optional<Tensor> k, c10::optio
                        int64_t max_q_len, double scale, bool causal, int64_t window,
                        int64_t impl, double k_scale, double v_scale) {
   CHECK_BF16(out); CHECK_BF16(q);
-  TORCH_CHECK(impl >= 0 && impl <= 4, "prefill_attention: impl is 0 (auto), 1, 2, 3 or 4 (auto, alone)");
+  TORCH_CHECK(impl >= 0 && impl <= 6,
+              "prefill_attention: impl is 0 (auto), 1, 2, 3, 4 (auto, alone), 5 (32x32, 8 waves per tile) "
+              "or 6 (32x32, register-staged tiles)");
   CHECK_DEV(cu_q); CHECK_DT(cu_q, at::kInt); CHECK_CONTIG(cu_q);
   TORCH_CHECK(D == 64 || D == 128 || (D == 32 && !kc.has_value()) || (D == 256 && kc.has_value()),
               "prefill_attention: head_dim must be 64 or 128 (32: packed only, 256: paged only)");
@@ -830,6 +842,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("skinny_cfg_count", [] { return (int64_t)nga::skinny_gemm_cfg_count(); });
   m.def("skinny_gemm", checked("skinny_gemm", &skinny_gemm));
   m.def("splitk_reduce", checked("splitk_reduce", &splitk_reduce));
+  m.def("splitk_swiglu", checked("splitk_swiglu", &splitk_swiglu));
   m.def("splitk_add_rmsnorm", checked("splitk_add_rmsnorm", &splitk_add_rmsnorm));
   m.def("sample", checked("sample", &sample));
   m.def("embedding", checked("embedding", &embedding));

@@ -260,6 +260,37 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ P, int S, int M, 
   }
 }
 
+// out[m, f] = bf16(silu(sum_s P[s, m, f]) * sum_s P[s, m, F + f]): the K-split gate / up
+// projection (slabs in the standard [gate | up] column order) summed by its SwiGLU consumer
+__global__ void splitk_swiglu_kernel(const float* __restrict__ P, int S, int M, int F,
+                                     uint16_t* __restrict__ out, int64_t ldo) {
+  const int nv = F / 8;
+  const int64_t total = (int64_t)M * nv;
+  const int64_t slab = (int64_t)M * 2 * F;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / nv;
+    const int c = (int)(i - m * nv) * 8;
+    const float* p = P + m * 2 * F + c;
+    f32x4 g0 = *reinterpret_cast<const f32x4*>(p), g1 = *reinterpret_cast<const f32x4*>(p + 4);
+    f32x4 u0 = *reinterpret_cast<const f32x4*>(p + F), u1 = *reinterpret_cast<const f32x4*>(p + F + 4);
+    for (int s = 1; s < S; ++s) {
+      const float* q = p + s * slab;
+      g0 += *reinterpret_cast<const f32x4*>(q);
+      g1 += *reinterpret_cast<const f32x4*>(q + 4);
+      u0 += *reinterpret_cast<const f32x4*>(q + F);
+      u1 += *reinterpret_cast<const f32x4*>(q + F + 4);
+    }
+    u16x8 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      o[r] = f2bf(sk_silu(g0[r]) * u0[r]);
+      o[4 + r] = f2bf(sk_silu(g1[r]) * u1[r]);
+    }
+    store8(out + m * ldo + c, o);
+  }
+}
+
 // resid += sum_s P[s] (one rounding to the bf16 residual); out = rmsnorm(resid) * w.
 // One workgroup per row, 8 features per lane (the add_rmsnorm kernel with the split-K sum of
 // the producing GEMM folded into its load).
@@ -371,6 +402,14 @@ void launch_splitk_reduce(const float* P, int S, int M, int N, uint16_t* out, in
   int64_t g = ((int64_t)M * (N / 8) + 255) / 256;
   if (g > 2048) g = 2048;
   splitk_reduce_kernel<<<(unsigned)g, 256, 0, stream>>>(P, S, M, N, out, ldo);
+}
+
+void launch_splitk_swiglu(const float* P, int S, int M, int F, uint16_t* out, int64_t ldo,
+                          hipStream_t stream) {
+  if (M == 0) return;
+  int64_t g = ((int64_t)M * (F / 8) + 255) / 256;
+  if (g > 2048) g = 2048;
+  splitk_swiglu_kernel<<<(unsigned)g, 256, 0, stream>>>(P, S, M, F, out, ldo);
 }
 
 void launch_splitk_add_rmsnorm(const float* P, int S, int M, uint16_t* resid, const uint16_t* w,

@@ -175,6 +175,8 @@ struct SkinnyGemmParams {
 int skinny_gemm_cfg_count();
 void skinny_gemm_cfg_info(int cfg, int* info);   // {BN, BM, WN, WM, NSTAGE}
 void launch_skinny_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t stream);
+void launch_splitk_swiglu(const float* P, int S, int M, int F, uint16_t* out, int64_t ldo,
+                          hipStream_t stream);
 void launch_splitk_reduce(const float* P, int S, int M, int N, uint16_t* out, int64_t ldo,
                           hipStream_t stream);
 void launch_splitk_add_rmsnorm(const float* P, int S, int M, uint16_t* resid, const uint16_t* w,

@@ -500,7 +500,10 @@ class LlamaModel:
             if cfg.act == "silu":
                 pk = self._pick(L["wgu"], x.shape[0]) if "wgu" in L else None
                 if pk is not None:   # SwiGLU in the gate|up GEMM's epilogue: [M, F] straight out
-                    h = ops.skinny_gemm(x, L["wgu"], pk[0], 1, 2)
+                    if pk[1] == 1:
+                        h = ops.skinny_gemm(x, L["wgu"], pk[0], 1, 2)
+                    else:            # K split: the SwiGLU kernel sums the fp32 slabs
+                        h = ops.splitk_swiglu(ops.skinny_gemm(x, L["wgu"], pk[0], pk[1], 1))
                     return self._lin(h, L, "wd", partial_ok=partial_ok)
             gu = self._lin(x, L, "wgu")
             if cfg.act == "silu":

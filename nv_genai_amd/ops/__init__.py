@@ -217,6 +217,20 @@ def splitk_reduce(P: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.
     return out
 
 
+def splitk_swiglu(P: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(gate) * up of a K-split gate / up projection: P [S, M, 2F] fp32 partial slabs in the
+    standard [gate | up] column order -> bf16 [M, F]."""
+    S, M, N2 = P.shape
+    F = N2 // 2
+    if not _gpu(P):
+        s = P.float().sum(0)
+        return (torch.nn.functional.silu(s[:, :F]) * s[:, F:]).to(torch.bfloat16)
+    if out is None:
+        out = torch.empty(M, F, dtype=torch.bfloat16, device=P.device)
+    kernels().splitk_swiglu(out, P, int(S))
+    return out
+
+
 def splitk_add_rmsnorm(resid: torch.Tensor, P: torch.Tensor, w: torch.Tensor, eps: float,
                        out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """resid += sum of the partial slabs P [S, M, H] (in place, one bf16 rounding); returns
@@ -359,8 +373,10 @@ def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
     split-key form (few prompts: two wave groups walk alternate key tiles of the same row
     block and merge in LDS) — for tests and A/B runs; 4 picks by size for a prefill that
     runs alone (no decode attention beside it: the 32x32 kernel from one prompt up, the
-    split-key form for ~one row block per CU). fp8 e4m3fn caches (``kv_scales``) run the
-    16x16 kernel."""
+    split-key form for ~one row block per CU); 5 the 32x32 kernel's 8-wave shared-tile form
+    (2 x 32 rows of each head of a GQA group of 4 per K / V^T tile; other head ratios run
+    impl 2); 6 the 32x32 kernel with register-staged K / V^T tiles instead of LDS-DMA (GQA
+    groups of 4; A/B). fp8 e4m3fn caches (``kv_scales``) run the 16x16 kernel."""
     if not _gpu(q):
         r = ref.prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
                                         scale, causal, window, kv_scales)

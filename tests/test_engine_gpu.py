@@ -360,7 +360,8 @@ def _same_greedy_run(ga, eg, lp_tol=0.3):
 def test_skinny_gemm_path_matches_library_path(gpu, weights, tmp_path, monkeypatch):
     """The decode-shape GEMM path end to end on llama-small's shapes (a test table that sends
     every projection to the skinny kernel: K-split qkv summed by the RoPE kernel, K-split o /
-    down summed by the add + RMSNorm kernel, fused SwiGLU gate/up, fp32 LM head) against the
+    down summed by the add + RMSNorm kernel, fused SwiGLU gate/up or K-split gate/up summed by
+    the SwiGLU kernel, fp32 LM head) against the
     library path: prefill logits agree to bf16 rounding, greedy generations (graphed decode and
     mixed steps) agree up to near-ties."""
     import json
@@ -371,7 +372,7 @@ def test_skinny_gemm_path_matches_library_path(gpu, weights, tmp_path, monkeypat
     tab = {"arch": "gfx950", "table": {
         "1536x1024": {"shape": "qkv", "by_m": {"16": [3, 2], "512": [1, 4]}},
         "1024x1024": {"shape": "o", "by_m": {"16": [3, 4], "512": [1, 4]}},
-        "5632x1024": {"shape": "gate_up", "by_m": {"16": [2, 1], "512": [13, 1]}},
+        "5632x1024": {"shape": "gate_up", "by_m": {"16": [2, 1], "64": [1, 2], "512": [13, 1]}},
         "1024x2816": {"shape": "down", "by_m": {"16": [3, 4], "512": [13, 4]}},
         "32768x1024": {"shape": "lm_head", "by_m": {"16": [2, 1], "512": [12, 1]}}}}
     path = tmp_path / "skinny.json"

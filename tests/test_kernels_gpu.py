@@ -219,13 +219,13 @@ def test_prefill_attention_v2_layouts(gpu, Hkv, G, window, causal):
     ctx_t = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
     scale = 1 / math.sqrt(D)
     o_ref = ref.prefill_attention_paged(q.float(), kc, vc, bt, cu_t, ctx_t, Hq, Hkv, D, scale, causal, window)
-    for impl in (2, 3):      # 4-wave, and 8-wave split-key
+    for impl in (2, 3, 5, 6):   # 4-wave, 8-wave split-key, 8-wave shared tiles, register-staged
         out = ops.prefill_attention_paged(q, kc, vc, bt, cu_t, ctx_t, Hq, Hkv, D, max(qls), scale,
                                           causal=causal, window=window, impl=impl)
         _close_rows(out, o_ref, width=D)
 
 
-@pytest.mark.parametrize("impl", [0, 1, 2, 3])
+@pytest.mark.parametrize("impl", [0, 1, 2, 3, 5, 6])
 @pytest.mark.parametrize("ctxs,qls,window", [
     ([1200], [940], 0),            # one prompt after a 260-token prefix hit
     ([1200] * 6, [1200] * 6, 0),   # six prompts (the size rule picks the 32x32 kernel)
@@ -706,6 +706,17 @@ def test_skinny_gemm_every_cfg(gpu, M):
                                            x_rows=M, k_in=K), y0)
         _close_rows(ops.skinny_gemm(x, ops.pack_weight(w, BN), cfg, 3, 1, n_out=1000, krot=1).sum(0), ref0,
                     rel=1e-4)
+
+
+def test_splitk_swiglu(gpu):
+    """silu(sum of gate slabs) * sum of up slabs, against fp32."""
+    torch.manual_seed(4)
+    S, M, F = 3, 45, 1024
+    P = torch.randn(S, M, 2 * F, device=gpu)
+    s_ = P.cpu().sum(0)
+    y_ref = torch.nn.functional.silu(s_[:, :F]) * s_[:, F:]
+    y = ops.splitk_swiglu(P)
+    _close_rows(y, y_ref, rel=1e-2)
 
 
 def test_splitk_add_rmsnorm(gpu):
