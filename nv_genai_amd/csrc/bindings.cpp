@@ -284,6 +284,11 @@ void skinny_gemm(Tensor out, Tensor x, Tensor w, int64_t epi, int64_t split, int
   p.krot = krot ? 1 : 0;
   p.wpack = wpack ? 1 : 0;
   p.xpack = xpack ? 1 : 0;
+  static const int wnt_env = [] {   // NGA_SKINNY_WNT=1: non-temporal weight DMA (A/B)
+    const char* e = getenv("NGA_SKINNY_WNT");
+    return e ? atoi(e) : 0;
+  }();
+  p.wnt = wnt_env;
   if (xpack) {
     const int64_t nm = (M + info[1] - 1) / info[1];
     TORCH_CHECK(x.size(1) == 64 && x.size(0) == nm * (K / 64) * info[1],

@@ -133,8 +133,14 @@ __global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmPar
     if (ke >= nk) ke -= nk;
     const int k0 = ke * SBK;
     const int64_t wk0 = P.wpack ? (int64_t)ke * (BN * SBK) : (int64_t)k0;
+    if (P.wnt) {
 #pragma unroll
-    for (int i = 0; i < W_GL; ++i) glds16(wsrc[i] + wk0, base + (wv * W_GL + i) * 8 * SBK);
+      for (int i = 0; i < W_GL; ++i)
+        __builtin_amdgcn_global_load_lds((gptr_t)(wsrc[i] + wk0), (lptr_t)(base + (wv * W_GL + i) * 8 * SBK), 16, 0, 2);
+    } else {
+#pragma unroll
+      for (int i = 0; i < W_GL; ++i) glds16(wsrc[i] + wk0, base + (wv * W_GL + i) * 8 * SBK);
+    }
     const int64_t xk0 = P.xpack ? (int64_t)ke * (BM * SBK) : (int64_t)k0;
 #pragma unroll
     for (int i = 0; i < X_GL; ++i) glds16(xsrc[i] + xk0, base + BN * SBK + (wv * X_GL + i) * 8 * SBK);

@@ -171,6 +171,7 @@ struct SkinnyGemmParams {
   int krot;            // 1: each block starts its K walk at a block-dependent step
   int wpack;           // 1: w is tile-packed [nN][K/64][BN][64] for this cfg's BN (pack_weight)
   int xpack;           // 1: x is tile-packed [nM][K/64][BM][64] for this cfg's BM (pack_rows)
+  int wnt;             // 1: weight DMA with the non-temporal cache policy (streamed once)
 };
 int skinny_gemm_cfg_count();
 void skinny_gemm_cfg_info(int cfg, int* info);   // {BN, BM, WN, WM, NSTAGE}
