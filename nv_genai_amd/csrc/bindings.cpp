@@ -325,6 +325,33 @@ void skinny_gemm(Tensor out, Tensor x, Tensor w, int64_t epi, int64_t split, int
   nga::launch_skinny_gemm(p, (int)cfg, (int)epi, cur_stream(x));
 }
 
+void gemv(Tensor out, Tensor x, Tensor w, int64_t epi) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "gemv: 2-D x / w / out");
+  TORCH_CHECK(x.device() == w.device() && x.device() == out.device(), "gemv: one device");
+  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && w.is_contiguous(), "gemv: x rows / w contiguous, 16-B aligned");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) | reinterpret_cast<uintptr_t>(w.data_ptr())) % 16 == 0,
+              "gemv: x / w must be 16-B aligned");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(M >= 1 && M <= 4 && K % 8 == 0 && w.size(1) == K && M * K * 2 <= 160 * 1024,
+              "gemv: 1 <= M <= 4, K % 8 == 0, M x K bf16 within 160 KiB");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "gemv: epi 0 (bf16), 1 (fp32), 2 (SwiGLU)");
+  const int64_t N = epi == 2 ? w.size(0) / 2 : w.size(0);
+  TORCH_CHECK(epi != 2 || w.size(0) % 2 == 0, "gemv: SwiGLU weight has 2F rows");
+  TORCH_CHECK(out.size(0) == M && out.size(1) >= N && out.stride(1) == 1, "gemv: out [M, >= N]");
+  TORCH_CHECK(epi == 1 ? out.scalar_type() == at::kFloat : out.scalar_type() == at::kBFloat16, "gemv: out dtype");
+  nga::GemvParams p{};
+  p.x = bfp(x);
+  p.ldx = x.stride(0);
+  p.w = bfp(w);
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.out = out.data_ptr();
+  p.ldo = out.stride(0);
+  TORCH_CHECK(nga::launch_gemv(p, (int)epi, cur_stream(x)), "gemv: shape out of range");
+}
+
 void splitk_swiglu(Tensor out, Tensor P, int64_t S) {
   CHECK_DEV(P); CHECK_BF16(out);
   TORCH_CHECK(out.device() == P.device(), "splitk_swiglu: out and P on one device");
@@ -848,6 +875,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("skinny_gemm", checked("skinny_gemm", &skinny_gemm));
   m.def("splitk_reduce", checked("splitk_reduce", &splitk_reduce));
   m.def("splitk_swiglu", checked("splitk_swiglu", &splitk_swiglu));
+  m.def("gemv", checked("gemv", &gemv));
   m.def("splitk_add_rmsnorm", checked("splitk_add_rmsnorm", &splitk_add_rmsnorm));
   m.def("sample", checked("sample", &sample));
   m.def("embedding", checked("embedding", &embedding));

@@ -159,6 +159,17 @@ void launch_moe_combine(const uint16_t* y, const int32_t* inv, int T, int k, int
                         hipStream_t stream);
 
 // gemm_skinny.hip (decode-shape projection GEMM, out = x . W^T)
+struct GemvParams {
+  const uint16_t* x;   // [M, K] rows, stride ldx (16-B aligned)
+  int64_t ldx;
+  const uint16_t* w;   // [N, K] (epi 2: [2N, K] = [gate | up])
+  int M, N, K;         // M <= 4; K % 8 == 0, M * K * 2 <= 160 KiB
+  void* out;           // epi 0 / 2: bf16 [M, ldo]; epi 1: fp32 [M, ldo]
+  int64_t ldo;
+};
+// out = x . W^T for M <= 4 rows (gemv.hip); false if the shape is out of range
+bool launch_gemv(const GemvParams& p, int epi, hipStream_t stream);
+
 struct SkinnyGemmParams {
   const uint16_t* x;   // [M, K] rows, stride ldx (16-B aligned)
   int64_t ldx;

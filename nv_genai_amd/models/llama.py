@@ -489,6 +489,12 @@ class LlamaModel:
             return torch.addmm(L["bqkv"], x, L["wqkv"].t())
         return self._lin(x, L, "wqkv", partial_ok=partial_ok)
 
+    @staticmethod
+    def _gemv_ok(x, w) -> bool:
+        return (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.is_contiguous()
+                and x.stride(1) == 1 and x.stride(0) % 8 == 0 and x.shape[1] % 8 == 0
+                and x.shape[0] * x.shape[1] * 2 <= 160 * 1024)
+
     def _mlp(self, x, L, partial_ok: bool = False):
         """MLP of one layer on normed rows; returns the (TP partial) output (an
         ``ops.PartialSum`` of K-split slabs when ``partial_ok`` and the down GEMM split K)."""
@@ -498,6 +504,9 @@ class LlamaModel:
                                expert0=self.expert0, act=cfg.act, ws=self.moe_ws)
         if cfg.gated_mlp:
             if cfg.act == "silu":
+                if self.skinny and "wgu" in L and x.shape[0] <= ops.GEMV_MAX_M and self._gemv_ok(x, L["wgu"]):
+                    # 1-4 rows: weight-streaming GEMV with the SwiGLU epilogue (5.0-5.8 TB/s)
+                    return self._lin(ops.gemv(x, L["wgu"], 2), L, "wd", partial_ok=partial_ok)
                 pk = self._pick(L["wgu"], x.shape[0]) if "wgu" in L else None
                 if pk is not None:   # SwiGLU in the gate|up GEMM's epilogue: [M, F] straight out
                     if pk[1] == 1:
@@ -811,9 +820,13 @@ class LlamaModel:
         """fp32 logits over the full vocabulary (vocab-parallel head + all-gather). Where the
         skinny table picks it, the LM head GEMM writes fp32 straight from its accumulators
         (no bf16 logits tensor and no conversion pass)."""
-        pk = self._pick(self.lm_head, h.shape[0]) if (self.skinny and h.is_cuda and h.dtype == torch.bfloat16
-                                                       and self.lm_head.dtype == torch.bfloat16) else None
-        if pk is not None and pk[1] == 1 and h.stride(1) == 1 and h.stride(0) % 8 == 0:
+        ok = (self.skinny and h.is_cuda and h.dtype == torch.bfloat16 and self.lm_head.dtype == torch.bfloat16
+              and h.stride(1) == 1 and h.stride(0) % 8 == 0)
+        pk = self._pick(self.lm_head, h.shape[0]) if ok else None
+        if ok and h.shape[0] <= ops.GEMV_MAX_M and self.lm_head.is_contiguous():
+            # 1-4 rows (batch-1..4 decode): the weight-streaming GEMV (6.4 TB/s vs 5.9 library)
+            lg = ops.gemv(h, self.lm_head, 1)
+        elif pk is not None and pk[1] == 1:
             lg = ops.skinny_gemm(h, self.lm_head, pk[0], 1, 1)[0]
         else:
             lg = (h @ self.lm_head.t()).float()

@@ -206,6 +206,27 @@ def skinny_gemm(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, epi:
     return out
 
 
+GEMV_MAX_M = 4
+
+
+def gemv(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Weight-streaming GEMV for M <= 4 token rows (gemv.hip): ``epi`` 0 -> bf16 ``x @ w^T``,
+    1 -> fp32 ``x @ w^T`` (LM-head logits), 2 -> SwiGLU ``silu(x @ w[:F]^T) * (x @ w[F:]^T)``.
+    CPU tensors: the fp32 reference."""
+    if not _gpu(x):
+        y = x.float() @ w.float().t()
+        if epi == 2:
+            F = w.shape[0] // 2
+            return (torch.nn.functional.silu(y[:, :F]) * y[:, F:]).to(x.dtype)
+        return y if epi == 1 else y.to(x.dtype)
+    M = x.shape[0]
+    N = w.shape[0] // 2 if epi == 2 else w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32 if epi == 1 else x.dtype, device=x.device)
+    kernels().gemv(out, x, w, int(epi))
+    return out
+
+
 def splitk_reduce(P: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """bf16 sum of the K-split partial slabs P [S, M, N]."""
     S, M, N = P.shape

@@ -708,6 +708,23 @@ def test_skinny_gemm_every_cfg(gpu, M):
                     rel=1e-4)
 
 
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,K", [(37, 1000), (4096, 4096), (300, 14336)])
+def test_gemv(gpu, M, N, K):
+    """Weight-streaming GEMV (M <= 4) in its three epilogues against fp32: a ragged last wave
+    (N % 4), a K that is not a multiple of the 512-element step, and the down projection's K."""
+    torch.manual_seed(M + N)
+    x = _bf(M, K, dev=gpu)
+    w = _bf(2 * N, K, dev=gpu) * 0.05
+    y_ref = x.cpu().float() @ w.cpu().float().t()
+    _close_rows(ops.gemv(x, w[:N].contiguous(), 0), y_ref[:, :N], rel=1e-2)
+    y1 = ops.gemv(x, w[:N].contiguous(), 1)
+    assert y1.dtype == torch.float32
+    _close_rows(y1, y_ref[:, :N], rel=1e-4)
+    sw = torch.nn.functional.silu(y_ref[:, :N]) * y_ref[:, N:]
+    _close_rows(ops.gemv(x, w, 2), sw, rel=1e-2)
+
+
 def test_splitk_swiglu(gpu):
     """silu(sum of gate slabs) * sum of up slabs, against fp32."""
     torch.manual_seed(4)
