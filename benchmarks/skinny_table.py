@@ -52,12 +52,14 @@ def main():
     ap.add_argument("--iters", type=int, default=25)
     ap.add_argument("--out", default=None, help="table file (default: the shipped asset)")
     ap.add_argument("--merge", default=None, help="update this table file with the measured shapes only")
+    ap.add_argument("--tp", type=int, default=1, help="per-rank shapes of a TP group of this size "
+                    "(column-parallel q/k/v, gate/up, LM head; row-parallel o, down)")
     a = ap.parse_args()
     use_tuned_gemms()
     cfg = llama_config(a.model)
-    H, F, D = cfg.hidden, cfg.ffn, cfg.head_dim
-    shapes = {"qkv": ((cfg.heads + 2 * cfg.kv_heads) * D, H), "o": (H, cfg.heads * D), "gate_up": (2 * F, H),
-              "down": (H, F), "lm_head": (cfg.vocab_size, H)}
+    H, F, D, tp = cfg.hidden, cfg.ffn // a.tp, cfg.head_dim, a.tp
+    shapes = {"qkv": ((cfg.heads + 2 * cfg.kv_heads) // tp * D, H), "o": (H, cfg.heads // tp * D),
+              "gate_up": (2 * F, H), "down": (H, F), "lm_head": (-(-cfg.vocab_size // tp), H)}
     C = ops.kernels()
     cfgs = list(range(C.skinny_cfg_count()))
     info = {c: C.skinny_cfg(c) for c in cfgs}
@@ -71,7 +73,7 @@ def main():
         Ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16, generator=g) * 0.02 for _ in range(n_rot)]
         nw = torch.ones(N if name in ("o", "down") else 1, device=dev, dtype=torch.bfloat16)
         # qkv feeds the RoPE kernel, which sums K-split slabs itself (no cache write here)
-        Hq, Hkv = cfg.heads, cfg.kv_heads
+        Hq, Hkv = cfg.heads // tp, max(1, cfg.kv_heads // tp)
         cos_sin = ops.rope_cos_sin(64, D, cfg.rope_theta).to(dev)
 
         def rope(q, part=None):
@@ -155,7 +157,7 @@ def main():
         old.update(table)
         table = old
     with open(out, "w") as f:
-        json.dump({"arch": "gfx950", "model": a.model, "note": "decode-shape GEMM choice per (N x K, M): "
+        json.dump({"arch": "gfx950", "model": a.model if not a.merge else "llama3-8b; llama3-70b TP=8 ranks", "note": "decode-shape GEMM choice per (N x K, M): "
                    "[cfg, split] of csrc/kernels/gemm_skinny.hip or 'lib'; benchmarks/skinny_table.py",
                    "table": table}, f, indent=1)
     print("table written:", os.path.abspath(out), flush=True)

@@ -142,8 +142,10 @@ class LlamaModel:
         # decode-shape projections (M <= 512 rows) on the skinny MFMA GEMM where the measured
         # table (ops.skinny) says it beats the library GEMM: K-split o / down partials summed by
         # the residual add + RMSNorm kernel, SwiGLU fused into gate / up, fp32 logits straight
-        # from the LM head. One TP rank, one stage (the partial sums never cross a collective)
-        self.skinny = (self.device.type == "cuda" and dtype == torch.bfloat16 and self.p.tp_size == 1
+        # from the LM head. One pipeline stage; under TP the table holds each rank's shard shapes
+        # (llama3-70b TP=8) and row-parallel K-split partials are summed before the all-reduce
+        # (``_reduce_add_norm``), so partial sums never cross a collective
+        self.skinny = (self.device.type == "cuda" and dtype == torch.bfloat16
                        and self.p.pp_size == 1 and ops.skinny.enabled())
         self.fp8 = False
         if fp8:

@@ -21,9 +21,22 @@ def _free_port():
     return p
 
 
-def _worker(rank, port, q):
+# llama-small's TP=2 rank shapes, every projection on the decode-shape kernel: K-split q/k/v
+# (RoPE sums the slabs), K-split o / down (summed before the all-reduce), SwiGLU gate/up, fp32
+# vocab-shard LM head
+SKINNY_TP2_TABLE = {"arch": "gfx950", "table": {
+    "768x1024": {"shape": "qkv", "by_m": {"16": [3, 2], "512": [1, 2]}},
+    "1024x512": {"shape": "o", "by_m": {"16": [3, 2], "512": [1, 2]}},
+    "2816x1024": {"shape": "gate_up", "by_m": {"16": [2, 1], "512": [13, 1]}},
+    "1024x1408": {"shape": "down", "by_m": {"16": [3, 2], "512": [1, 2]}},
+    "16384x1024": {"shape": "lm_head", "by_m": {"16": [2, 1], "512": [12, 1]}}}}
+
+
+def _worker(rank, port, q, table=None):
     os.environ.update(RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
+    if table:
+        os.environ["NGA_SKINNY_TABLE"] = table
     res = {"rank": rank}
     try:
         from nv_genai_amd.engine.llm_engine import EngineConfig, LLMEngine, SamplingParams
@@ -52,6 +65,8 @@ def _worker(rank, port, q):
                         ctx_lens=torch.tensor([T], dtype=torch.int32, device=dev), block_tables=bt,
                         max_q_len=T, max_ctx=T)
         lg = eng.model.logits(eng.model.forward(ids, pos, meta)).float()
+        res["skinny_picks"] = sum(eng.model._pick(eng.model.layers[0][n], T) is not None
+                                  for n in ("wqkv", "wo", "wgu", "wd"))
         if rank == 0:
             single = LlamaModel(cfg, dev, pctx=pd.ParallelContext(), weights=full)
             single.allocate_kv_cache(8)
@@ -78,13 +93,23 @@ def _worker(rank, port, q):
     q.put(res)
 
 
-def test_tp2_on_one_gpu_with_custom_all_reduce():
+@pytest.mark.parametrize("skinny", [False, True])
+def test_tp2_on_one_gpu_with_custom_all_reduce(skinny, tmp_path):
+    """``skinny``: the rank-shard projections run the decode-shape kernel (test table), K-split
+    row-parallel partials summed before the custom all-reduce."""
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
+    import json
+
+    table = None
+    if skinny:
+        table = str(tmp_path / "skinny_tp2.json")
+        with open(table, "w") as f:
+            json.dump(SKINNY_TP2_TABLE, f)
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, port, q, table)) for r in range(2)]
     for p in procs:
         p.start()
     results = sorted([q.get(timeout=200) for _ in range(2)], key=lambda r: r["rank"])
@@ -96,6 +121,7 @@ def test_tp2_on_one_gpu_with_custom_all_reduce():
         assert r["custom_ar"], r
         assert r["ar_error"] == 0, r
     r0 = results[0]
+    assert r0["skinny_picks"] == (4 if skinny else 0), r0
     assert r0["gen_lens"] == [8, 8]
     assert r0["max_abs_diff"] <= 0.05 * r0["ref_abs_max"] + 0.05, r0
     assert r0["argmax_agree"] >= 0.9, r0
