@@ -344,3 +344,28 @@ def test_gemm_operand_guard_rejects_strided_weight_views():
         ops.linear(x, w.t().contiguous().t())                      # column-major storage
     with pytest.raises(ValueError):
         ops.linear_rows_split(x, w[:, ::2], split=4)
+
+
+def test_decode_shape_ops_cpu_fallbacks_match_fp32():
+    """The CPU paths of the decode-shape ops (what the engine runs without a GPU) agree with a
+    plain fp32 formulation: GEMV epilogues, split-K SwiGLU, split-K add + RMSNorm."""
+    from nv_genai_amd import ops
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(3, 64, generator=g).to(torch.bfloat16)
+    w = (torch.randn(20, 64, generator=g) * 0.1).to(torch.bfloat16)
+    y = x.float() @ w.float().t()
+    assert torch.allclose(ops.gemv(x, w, 1), y, atol=1e-5)
+    assert torch.allclose(ops.gemv(x, w, 0).float(), y, atol=2e-2, rtol=1e-2)
+    sw = torch.nn.functional.silu(y[:, :10]) * y[:, 10:]
+    assert torch.allclose(ops.gemv(x, w, 2).float(), sw, atol=2e-2, rtol=1e-2)
+    P = torch.randn(3, 5, 16, generator=g)
+    s = P.sum(0)
+    assert torch.allclose(ops.splitk_swiglu(P).float(), torch.nn.functional.silu(s[:, :8]) * s[:, 8:],
+                          atol=3e-2, rtol=1e-2)
+    resid = torch.randn(5, 16, generator=g).to(torch.bfloat16)
+    nw = torch.ones(16, dtype=torch.bfloat16)
+    r0 = resid.float() + s
+    out = ops.splitk_add_rmsnorm(resid, P, nw, 1e-5)
+    assert torch.allclose(resid.float(), r0, atol=3e-2, rtol=1e-2)
+    assert torch.allclose(out.float(), ref.rmsnorm(resid.float(), nw.float(), 1e-5), atol=3e-2, rtol=1e-2)
