@@ -286,11 +286,10 @@ def test_step_graphs_equal_eager_steps(gpu, weights):
         else:
             assert not e.mgraphs
     # same tokens; log-probs agree to bf16 GEMM rounding (the graphs run bucket-padded M, so
-    # hipBLASLt may pick other kernels; the test head is scaled x40 for peaky logits, which
-    # amplifies hidden-state rounding 40x in the logits)
-    for (a, la), (b, lb) in zip(outs[True], outs[False]):
-        assert a == b
-        assert max(abs(x - y) for x, y in zip(la, lb)) < 0.3
+    # other kernels run: hipBLASLt solutions, the decode-shape table's rows, the 1-4-row GEMV in
+    # eager steps; the test head is scaled x40 for peaky logits, which amplifies hidden-state
+    # rounding 40x in the logits) — a divergence is accepted only at a near-tie
+    _same_greedy_run(outs[True], outs[False])
 
 
 @pytest.fixture(scope="module")
