@@ -288,7 +288,7 @@ class EngineService:
 
     def metrics(self) -> dict:
         e = self.engine
-        return {"running": e.sched.num_running(), "waiting": e.sched.num_waiting(),
+        return {"running": e.sched.num_running(), "waiting": e.sched.num_waiting() + len(e._inbox),
                 "kv_usage": e.kv_usage(), "steps": self.steps, **e.stats,
                 "prefix_hit_blocks": e.sched.prefix_hits(), "preemptions": e.sched.preemptions()}
 
