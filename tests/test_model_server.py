@@ -126,6 +126,8 @@ def test_http_connectors_roundtrip(http_url):
 
 
 def test_metrics_exposed(client):
+    client.post("/v1/chat/completions", json={"model": "tiny-llm", "max_tokens": 2,
+                                              "messages": [{"role": "user", "content": "hi"}]})
     t = client.get("/metrics").text
     assert "model_server_chat_requests_total" in t and "model_server_kv_usage" in t
 
