@@ -17,6 +17,7 @@ from typing import List, Optional, Sequence
 
 import torch
 
+from ..utils.runtime import capture_guard
 from ..observability.markers import gpu_range
 
 from ..models.config import EncoderConfig, encoder_config
@@ -98,7 +99,8 @@ class EmbeddingEngine:
         if n == 0:
             return out
         order = sorted(range(n), key=lambda i: len(seqs[i]))
-        with self.lock:
+        # capture_guard: no library GEMM of ours starts while another thread captures a graph
+        with self.lock, capture_guard():
             i = 0
             while i < n:
                 batch, tok = [], 0

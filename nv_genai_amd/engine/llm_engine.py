@@ -30,6 +30,7 @@ from typing import Callable, Deque, Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
+from ..utils.runtime import capture_guard
 from .. import ops
 from ..observability.markers import gpu_range
 from .._native import rt
@@ -1186,7 +1187,8 @@ class LLMEngine:
         with torch.cuda.stream(stream):
             self._graph_body(key)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self._graph_pool, stream=stream, capture_error_mode="thread_local"):
+            with capture_guard(), torch.cuda.graph(g, pool=self._graph_pool, stream=stream,
+                                                   capture_error_mode="thread_local"):
                 self._graph_body(key)
         torch.cuda.current_stream(dev).wait_stream(stream)
         torch.cuda.synchronize(dev)
@@ -1267,7 +1269,8 @@ class LLMEngine:
                 g = torch.cuda.CUDAGraph()
                 # thread_local: other threads of a serving process (retrieval, embeddings, other
                 # engines) keep launching on their own streams while this one captures
-                with torch.cuda.graph(g, pool=pool, stream=stream, capture_error_mode="thread_local"):
+                with capture_guard(), torch.cuda.graph(g, pool=pool, stream=stream,
+                                                       capture_error_mode="thread_local"):
                     self._decode_body(bs)
                 pool = g.pool()
                 self.graphs[bs] = g

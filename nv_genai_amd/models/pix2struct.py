@@ -43,6 +43,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
+from ..utils.runtime import capture_guard
 from .. import ops
 
 
@@ -481,7 +482,7 @@ class Pix2StructModel:
                 self._step(st)
             torch.cuda.current_stream(dev).wait_stream(s)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=s, capture_error_mode="thread_local"):
+            with capture_guard(), torch.cuda.graph(graph, stream=s, capture_error_mode="thread_local"):
                 self._step(st)
             st["t"].zero_()
             st["done"].zero_()

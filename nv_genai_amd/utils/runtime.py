@@ -14,7 +14,23 @@ passes. Reference counting still frees acyclic garbage immediately.
 """
 from __future__ import annotations
 
+import contextlib
 import gc
+import threading
+
+# Held while a thread captures a hipGraph, and by the other components of a serving process
+# that issue library GEMMs from their own threads (the embedding / reranking encoder). The first
+# use of a hipBLASLt solution in a thread runs set-up operations that are not permitted while
+# another thread's stream is capturing (hipErrorStreamCaptureImplicit / ...Unsupported from
+# hipblaslt.cpp, which invalidates the capture: scripts/dev/capture_race.py). Captures are rare
+# (one per new graph bucket), so the lock is almost always free.
+GPU_CAPTURE_LOCK = threading.RLock()
+
+
+@contextlib.contextmanager
+def capture_guard():
+    with GPU_CAPTURE_LOCK:
+        yield
 
 
 def quiet_gc(gen0_threshold: int = 50_000) -> None:

@@ -395,3 +395,45 @@ def test_skinny_gemm_path_matches_library_path(gpu, weights, tmp_path, monkeypat
         res[on + "lg"] = e.model.logits(hs).float()
     assert torch.allclose(res["1lg"], res["0lg"], rtol=0.02, atol=0.05 * float(res["0lg"].abs().max()))
     _same_greedy_run(res["1"], res["0"])
+
+
+def test_step_graph_capture_beside_encoder_thread(gpu, weights):
+    """A serving process encodes queries on other threads while the engine captures step
+    graphs lazily. The first use of a library GEMM solution in such a thread is not permitted
+    during another thread's capture (it invalidated the capture in the 8B agent benchmark);
+    the encoder and the captures share ``utils.runtime.capture_guard``, so both proceed."""
+    import threading
+
+    from nv_genai_amd.engine.embed_engine import EmbeddingEngine
+    from nv_genai_amd.engine.llm_engine import SamplingParams
+
+    emb = EmbeddingEngine("encoder-tiny", device="cuda")
+    stop, errs, done = threading.Event(), [], [0]
+
+    def encode_loop():
+        i = 0
+        while not stop.is_set():
+            try:
+                emb.embed(["word " * (1 + i % 97)] * (1 + i % 5), "query")   # a new M every call
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+                return
+            i += 1
+            done[0] = i
+
+    t = threading.Thread(target=encode_loop)
+    t.start()
+    try:
+        e = _engine(weights, "cuda", use_graphs=True, mixed_graphs=True, mixed_prefill_tokens=512)
+        p = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
+        reqs = [e.add_request(pr, p) for pr in PROMPTS[:2]]
+        for _ in range(3):
+            e.step()
+        reqs += [e.add_request(pr, p) for pr in PROMPTS[2:]]
+        e.run_until_done(reqs)
+        assert e.mgraphs and all(len(r.output_ids) == 12 for r in reqs)
+    finally:
+        stop.set()
+        t.join()
+    assert not errs, errs
+    assert done[0] > 0
