@@ -459,7 +459,13 @@ class Pix2StructModel:
                  use_graph: Optional[bool] = None, ignore_eos: bool = False) -> List[List[int]]:
         """Greedy generation for a batch of images (their real patches). Returns each image's
         token ids up to (excluding) EOS. On a GPU the decode step replays as a hipGraph.
-        ``ignore_eos``: every row runs all ``max_new_tokens`` steps (fixed-work benchmarks)."""
+        ``ignore_eos``: every row runs all ``max_new_tokens`` steps (fixed-work benchmarks).
+        Runs on request threads under ``capture_guard`` (its library GEMMs never launch beside
+        another thread's graph capture)."""
+        with capture_guard():
+            return self._generate(patches, max_new_tokens, use_graph, ignore_eos)
+
+    def _generate(self, patches, max_new_tokens, use_graph, ignore_eos):
         c, dev = self.cfg, self.device
         enc, cu = self.encode(patches)
         B, S = len(patches), int(max_new_tokens)

@@ -338,10 +338,15 @@ class VisionLanguageModel:
     # ---------------------------------------------------------------- images
     @torch.no_grad()
     def encode_images(self, pixels: torch.Tensor) -> torch.Tensor:
-        """[B, 3, S, S] -> projected features [B, P, H_llm] (bf16, on the engine device)."""
-        f = self.tower.forward(pixels)
-        B, P, Hv = f.shape
-        return self.projector(f.reshape(B * P, Hv).contiguous()).view(B, P, -1)
+        """[B, 3, S, S] -> projected features [B, P, H_llm] (bf16, on the engine device).
+        Runs on request threads: its library GEMMs hold ``capture_guard`` (no graph capture of
+        another thread is in progress while they launch)."""
+        from ..utils.runtime import capture_guard
+
+        with capture_guard():
+            f = self.tower.forward(pixels)
+            B, P, Hv = f.shape
+            return self.projector(f.reshape(B * P, Hv).contiguous()).view(B, P, -1)
 
     def _images_of(self, content) -> Tuple[List[object], List[bytes]]:
         return split_image_parts(content)
