@@ -2,12 +2,10 @@
 from __future__ import annotations
 
 import logging
-import os
 import uuid
 from typing import Iterator, List, Optional, Sequence
 
 from ..chain_server import utils
-from ..index.vectorstore import Document
 from ..observability.tracing import TracingCallback, get_tracer
 from ..rag.loaders import load_file
 

@@ -6,7 +6,6 @@ GPU call raises (so a GPU test can never pass on an eager-PyTorch substitute).
 """
 from __future__ import annotations
 
-import math
 from typing import Optional, Tuple
 
 import torch
