@@ -545,6 +545,8 @@ def main(argv=None):
                         "launches_by_token_bucket": dict(sorted(llm.bucket_hist.items())),
                         "launches_by_tokens_128": dict(sorted(llm.ntok_hist.items()))},
         "prefix_cache_hit_blocks": int(llm.sched.prefix_hits()),
+        **({"kv_page_refs_per_unique": round(llm.stats["kv_page_refs"] / max(1, llm.stats["kv_pages_unique"]), 4)}
+           if llm.stats.get("kv_pages_unique") else {}),
         "distinct_docs_retrieved": len({d for r in results for d in r.doc_ids}),
     }
     if rank == 0:

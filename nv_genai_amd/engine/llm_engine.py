@@ -42,6 +42,7 @@ from ..utils.tokenizer import IncrementalDetokenizer, LLMTokenizer, llm_tokenize
 from .beam import BeamGroup, advance
 
 log = logging.getLogger(__name__)
+_KV_SHARE_STATS = os.environ.get("NGA_KV_SHARE_STATS", "0") == "1"
 
 
 @dataclass
@@ -444,6 +445,11 @@ class LLMEngine:
         t_sched = time.perf_counter()
         kind, n, ntok = self.sched.schedule(ids, pos, sl, cu, ctx, bt, sid, smp)
         nd = n if kind == 2 else (self.sched.last_num_decode() if kind == 3 else 0)
+        if _KV_SHARE_STATS and nd:   # diagnostics: KV pages the decode rows share (prefix cache)
+            nb = (ctx[:nd] + 63) // 64
+            refs = np.concatenate([bt[i, :nb[i]] for i in range(nd)])
+            self.stats["kv_page_refs"] = self.stats.get("kv_page_refs", 0) + int(refs.size)
+            self.stats["kv_pages_unique"] = self.stats.get("kv_pages_unique", 0) + int(np.unique(refs).size)
         src = None
         sids = sid[:n].tolist()
         # rows that need the host between steps (penalty history, beam candidates) run the
