@@ -341,7 +341,9 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(const float* _
 }
 
 // ------------------------------------------------------------------ launchers
-// tile configurations: {BN, BM, WN, WM, NSTAGE} (WN x WM waves). Measured and dropped: the
+// tile configurations: {BN, BM, WN, WM, NSTAGE} (WN x WM waves). Measured and dropped: two-stage
+// tiles small enough for 2-3 workgroups (16-24 waves) per CU — {128,128,2,4,2}, {256,64,4,2,2},
+// {128,64,2,4,2} — 10-70 % slower than the table's picks (profiles/r4_skinny/sweep_more_waves.jsonl); the
 // next stage's DMA pieces spread one by one between the MFMAs instead of issued together at the
 // barrier (5-30 % slower at every tile; 256 x 256 collapsed; profiles/r4_headline_ab/sweep_il.jsonl)
 #define NGA_SKINNY_CFGS(X)     \
