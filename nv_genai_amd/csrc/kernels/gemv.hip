@@ -33,6 +33,22 @@ __global__ void __launch_bounds__(64 * GV_WAVES) gemv_kernel(GemvParams P) {
   const int K = P.K;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int f0 = (blockIdx.x * GV_WAVES + wv) * R;   // first output feature of this wave
+  constexpr int NR = EPI == 2 ? 2 * R : R;   // weight rows streamed per wave
+  const uint16_t* wr[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    int f = min(f0 + (r % R), P.N - 1);           // ragged last wave: any valid row, not stored
+    const int row = (EPI == 2 && r >= R) ? P.N + f : f;
+    wr[r] = P.w + (int64_t)row * K + lane * 8;
+  }
+  // the first K step's weights are requested before x is staged: the stage's L2 round trip
+  // and the weights' HBM round trip overlap instead of running back to back
+  u16x8 wcur[NR];
+  if (f0 < P.N && lane * 8 < K) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r) wcur[r] = load8_nt(wr[r]);
+  }
   {
     const int per_row = K / 8;
     for (int i = tid; i < M * per_row; i += 64 * GV_WAVES) {
@@ -41,29 +57,22 @@ __global__ void __launch_bounds__(64 * GV_WAVES) gemv_kernel(GemvParams P) {
     }
   }
   __syncthreads();
-  const int f0 = (blockIdx.x * GV_WAVES + wv) * R;   // first output feature of this wave
   if (f0 >= P.N) return;
-  constexpr int NR = EPI == 2 ? 2 * R : R;   // weight rows streamed per wave
-  const uint16_t* wr[NR];
-#pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    int f = f0 + (r % R);
-    if (f >= P.N) f = P.N - 1;                    // ragged last wave: any valid row, not stored
-    const int row = (EPI == 2 && r >= R) ? P.N + f : f;
-    wr[r] = P.w + (int64_t)row * K + lane * 8;
-  }
   float acc[NR][M];
 #pragma unroll
   for (int r = 0; r < NR; ++r)
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
 
-#pragma unroll 4
+#pragma unroll 2
   for (int k = 0; k < K; k += 512) {
     if (k + lane * 8 >= K) break;                 // K % 512 != 0: the tail step's idle lanes
-    u16x8 wv8[NR];
+    const bool more = k + 512 + lane * 8 < K;
+    u16x8 wnext[NR];
+    if (more) {                                   // one K step of weights in flight ahead
 #pragma unroll
-    for (int r = 0; r < NR; ++r) wv8[r] = load8_nt(wr[r] + k);
+      for (int r = 0; r < NR; ++r) wnext[r] = load8_nt(wr[r] + k + 512);
+    }
     float xf[M][8];
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -75,10 +84,14 @@ __global__ void __launch_bounds__(64 * GV_WAVES) gemv_kernel(GemvParams P) {
     for (int r = 0; r < NR; ++r)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float wf = bf2f(wv8[r][j]);
+        const float wf = bf2f(wcur[r][j]);
 #pragma unroll
         for (int m = 0; m < M; ++m) acc[r][m] = __builtin_fmaf(wf, xf[m][j], acc[r][m]);
       }
+    if (more) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) wcur[r] = wnext[r];
+    }
   }
 #pragma unroll
   for (int r = 0; r < NR; ++r)
@@ -109,12 +122,14 @@ __global__ void __launch_bounds__(64 * GV_WAVES) gemv_kernel(GemvParams P) {
 template <int M, int R, int EPI>
 static void gemv_launch(const GemvParams& p, hipStream_t stream) {
   const size_t lds = (size_t)M * p.K * 2;
-  static bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)gemv_kernel<M, R, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    return true;
-  }();
-  (void)attr;
+  if (lds > 64 * 1024) {   // only x images past the default limit need the attribute (it loads the kernel)
+    static bool attr = [] {
+      (void)hipFuncSetAttribute((const void*)gemv_kernel<M, R, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      return true;
+    }();
+    (void)attr;
+  }
   const int waves = (p.N + R - 1) / R;
   dim3 grid((waves + GV_WAVES - 1) / GV_WAVES);
   gemv_kernel<M, R, EPI><<<grid, 64 * GV_WAVES, lds, stream>>>(p);

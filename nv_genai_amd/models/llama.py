@@ -187,6 +187,9 @@ class LlamaModel:
             a = ops.silu_mul(x) if swiglu else x
             w = L[name]
             M = a.shape[0]
+            if M == 1 and self.skinny and self._gemv_ok(a, w):
+                # one row (batch-1 decode): the weight-streaming GEMV (profiles/r4_gemv/)
+                return ops.gemv(a, w, 0)
             pk = self._pick(w, M)
             if pk is not None:
                 cfg, split = pk
