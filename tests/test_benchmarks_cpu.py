@@ -35,6 +35,9 @@ def test_http_rag_benchmark_cpu(tmp_path):
     assert r.returncode == 0, (r.stderr[-3000:], (tmp_path / "server.log").read_text()[-3000:])
     res = json.loads(out.read_text())
     assert res["requests"] == 8 and res["value"] > 0 and res["p50_ttft_ms"] is not None
+    # the server's own phase summaries and the engine counters over the timed window
+    assert {"chain", "chain_wait", "prepare", "ttft"} <= set(res["server_p50_ms"]), res["server_p50_ms"]
+    assert res["engine_window"]["steps"] > 0 and "wait" in res["engine_window"]["host_s"], res["engine_window"]
 
 
 def test_headline_bench_two_ranks_gloo():
