@@ -24,7 +24,12 @@ def main():
     ap.add_argument("--lib", action="store_true", help="the library GEMM instead")
     ap.add_argument("--krot", type=int, default=0)
     ap.add_argument("--wpack", action="store_true")
+    ap.add_argument("--tuned", action="store_true", help="library GEMM with the shipped TunableOp table")
     a = ap.parse_args()
+    if a.tuned:
+        from nv_genai_amd.ops.gemm_tuning import use_tuned_gemms
+
+        use_tuned_gemms()
     N, K, epi = SHAPES[a.shape]
     n_rot = max(2, math.ceil(640e6 / (N * K * 2)))
     dev = torch.device("cuda")
