@@ -151,7 +151,7 @@ def build_runtime(force: bool = False, jobs: int = 8, out_dir: Path | None = Non
         list(ex.map(_run, jobs_list))
     if force or jobs_list or not out.exists():
         tmp = out.with_suffix(".tmp.so")
-        _run([cxx, "-shared", *map(str, objs), *extra, "-o", str(tmp)])
+        _run([cxx, "-shared", *map(str, objs), *extra, "-o", str(tmp), "-lrt"])
         os.replace(tmp, out)
     return out
 

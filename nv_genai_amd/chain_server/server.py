@@ -34,6 +34,7 @@ from fastapi.exceptions import RequestValidationError
 from fastapi.middleware.cors import CORSMiddleware
 from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
 from pydantic import BaseModel, Field, constr, field_validator
+from starlette.background import BackgroundTask
 from starlette.concurrency import run_in_threadpool
 from starlette.status import HTTP_422_UNPROCESSABLE_ENTITY
 
@@ -362,7 +363,11 @@ async def generate_answer(request: Request, prompt: Prompt) -> StreamingResponse
             tracer.end(span)
 
     if generator is not None and getattr(generator, "supports_async", False):
-        return StreamingResponse(response_agen(), media_type="text/event-stream")
+        # the request is already queued on the engine (prepare): if the body is never iterated
+        # (client gone before the first chunk) the background task still cancels it
+        cancel = getattr(generator, "cancel", None)
+        return StreamingResponse(response_agen(), media_type="text/event-stream",
+                                 background=BackgroundTask(cancel) if cancel else None)
     return StreamingResponse(response_generator(), media_type="text/event-stream")
 
 

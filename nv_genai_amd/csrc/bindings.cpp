@@ -246,9 +246,9 @@ void moe_combine(Tensor y, Tensor inv, int64_t T, int64_t k, Tensor out) {
 
 // ------------------------------------------------------------------ decode-shape GEMM
 std::vector<int64_t> skinny_cfg(int64_t cfg) {
-  int info[5];
+  int info[6];
   nga::skinny_gemm_cfg_info((int)cfg, info);
-  return {info[0], info[1], info[2], info[3], info[4]};
+  return {info[0], info[1], info[2], info[3], info[4], info[5]};
 }
 
 // epi 0: out [M, N] bf16 = x @ w^T; 1: out fp32 [split, M, N] partial slabs; 2: out [M, F] bf16 =
@@ -268,9 +268,10 @@ void skinny_gemm(Tensor out, Tensor x, Tensor w, int64_t epi, int64_t split, int
   TORCH_CHECK(K % 64 == 0 && K >= 64, "skinny_gemm: K must be a multiple of 64");
   TORCH_CHECK(wpack || w.size(1) == K, "skinny_gemm: K must match");
   TORCH_CHECK(M >= 1 && M <= 65536, "skinny_gemm: 1 <= M <= 65536");
-  int info[5];
+  int info[6];
   nga::skinny_gemm_cfg_info((int)cfg, info);
   TORCH_CHECK(info[0] > 0, "skinny_gemm: unknown tile configuration ", cfg);
+  TORCH_CHECK(info[5] == 0 || (!wpack && !xpack), "skinny_gemm: the weight-in-registers tiles take plain x / w");
   const int BN = info[0], BM = info[1];
   TORCH_CHECK(epi >= 0 && epi <= 2, "skinny_gemm: epi 0, 1 or 2");
   TORCH_CHECK(split >= 1 && split <= K / 64 && (epi == 1 || split == 1), "skinny_gemm: 1 <= split <= K / 64 (> 1 only for epi 1)");
@@ -811,6 +812,16 @@ struct CustomAR {
     impl->run_add_rmsnorm(inp.data_ptr(), bfp(resid), bfp(w), bfp(out), (int)inp.size(0), (int)inp.size(1),
                           (float)eps, cur_stream(inp));
   }
+  // out [rows, world * cols] = every rank's inp [rows, cols] side by side (rank order)
+  void all_gather(Tensor inp, Tensor out) {
+    CHECK_DEV(inp); CHECK_DEV(out); CHECK_CONTIG(inp); CHECK_CONTIG(out);
+    TORCH_CHECK(inp.scalar_type() == out.scalar_type() && inp.dim() == 2 && out.dim() == 2 &&
+                out.size(0) == inp.size(0) && out.size(1) == inp.size(1) * impl->world(),
+                "custom all-gather: out must be [rows, world * cols] of inp's dtype");
+    const int64_t row_bytes = inp.size(1) * inp.element_size();
+    TORCH_CHECK(row_bytes % 16 == 0, "custom all-gather: row bytes must be a multiple of 16");
+    impl->run_gather(inp.data_ptr(), out.data_ptr(), inp.size(0), row_bytes, cur_stream(inp));
+  }
   int64_t error() const { return impl->error(); }
   int64_t capacity() const { return impl->capacity(); }
   void set_two_shot_threshold(int64_t b) { impl->set_two_shot_threshold(b); }
@@ -898,6 +909,7 @@ PYBIND11_MODULE(_C, m) {
       .def("open", &CustomAR::open)
       .def("all_reduce", &CustomAR::all_reduce, py::arg("inp"), py::arg("out"), py::arg("algo") = 0)
       .def("all_reduce_add_rmsnorm", &CustomAR::all_reduce_add_rmsnorm)
+      .def("all_gather", &CustomAR::all_gather)
       .def("error", &CustomAR::error)
       .def("capacity", &CustomAR::capacity)
       .def("set_two_shot_threshold", &CustomAR::set_two_shot_threshold);

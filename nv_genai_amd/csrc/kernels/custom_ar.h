@@ -30,6 +30,9 @@ class CustomAllReduce {
   // resid += sum over ranks of in; out = rmsnorm(resid) * w (bf16 [rows, H], one-shot).
   void run_add_rmsnorm(const void* in, uint16_t* resid, const uint16_t* w, uint16_t* out, int rows, int H,
                        float eps, hipStream_t stream);
+  // out[row][r * row_bytes ...] = rank r's in[row] (all-gather along the last dim; `in` is
+  // [rows, row_bytes] bytes, `out` [rows, world * row_bytes]; row_bytes % 16 == 0).
+  void run_gather(const void* in, void* out, int64_t rows, int64_t row_bytes, hipStream_t stream);
   // Sticky barrier-timeout flag (synchronous read; call outside graph capture).
   int error() const;
 

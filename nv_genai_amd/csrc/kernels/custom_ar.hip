@@ -283,6 +283,34 @@ __global__ __launch_bounds__(kThreads) void ar_add_rmsnorm(ArArgs a, uint16_t* _
   end_call(a, flag, ok);
 }
 
+// All-gather along the last dim: out[row][r * cols + c] = in_r[row][c] for every rank r (the
+// vocab-parallel LM head's logits, CC4). Every rank copies its shard into its own staging
+// buffer; after the per-block barrier each block copies the same input packets it staged
+// from every rank's staging buffer into the right column block of `out` (block b touches the
+// same packet set on every rank, so the per-block barrier suffices, as in the one-shot).
+__global__ __launch_bounds__(kThreads) void ag_last_dim(ArArgs a, int64_t rows, int64_t cpk) {
+  uint32_t flag;
+  if (!begin_call(a, flag)) return;
+  const uint32_t par = flag & 1u;
+  const uint4* in = reinterpret_cast<const uint4*>(a.in);
+  uint4* mine = stage_of(a, a.rank, par);
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  const int64_t i0 = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  for (int64_t i = i0; i < a.nvec; i += stride) mine[i] = in[i];
+  bool ok = block_barrier(a, offsetof(Signal, start), flag);
+  if (ok) {
+    uint4* out = reinterpret_cast<uint4*>(a.out);
+    for (int r = 0; r < a.world; ++r) {
+      const uint4* src = stage_of(a, r, par);
+      for (int64_t i = i0; i < a.nvec; i += stride) {
+        const int64_t row = i / cpk, c = i - row * cpk;
+        out[(row * a.world + r) * cpk + c] = src[i];
+      }
+    }
+  }
+  end_call(a, flag, ok);
+}
+
 void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -388,6 +416,27 @@ void CustomAllReduce::run_add_rmsnorm(const void* in, uint16_t* resid, const uin
   a.is_bf16 = 1;
   const int g = rows < kArMaxBlocks ? rows : kArMaxBlocks;
   hipLaunchKernelGGL(ar_add_rmsnorm, dim3(g), dim3(kThreads), 0, stream, a, resid, w, out, rows, H, eps);
+}
+
+void CustomAllReduce::run_gather(const void* in, void* out, int64_t rows, int64_t row_bytes, hipStream_t stream) {
+  if (!opened_) throw std::runtime_error("custom all-reduce: open() the peer handles first");
+  const int64_t bytes = rows * row_bytes;
+  if (rows <= 0 || row_bytes <= 0 || row_bytes % 16 != 0 || bytes > cap_)
+    throw std::runtime_error("custom all-gather: rows > 0, row bytes a multiple of 16, shard within capacity");
+  if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15)
+    throw std::runtime_error("custom all-gather: buffers must be 16-B aligned");
+  ArArgs a;
+  for (int r = 0; r < kArMaxRanks; ++r) a.base[r] = static_cast<const uint8_t*>(r < world_ ? peers_[r] : nullptr);
+  a.in = in;
+  a.out = out;
+  a.nvec = bytes / 16;
+  a.cap = cap_;
+  a.timeout = timeout_ticks_;
+  a.rank = rank_;
+  a.world = world_;
+  a.is_bf16 = 0;
+  const int g = grid_for(a.nvec, false);
+  hipLaunchKernelGGL(ag_last_dim, dim3(g), dim3(kThreads), 0, stream, a, rows, row_bytes / 16);
 }
 
 int CustomAllReduce::error() const {

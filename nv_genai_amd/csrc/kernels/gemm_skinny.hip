@@ -370,12 +370,13 @@ int skinny_gemm_cfg_count() {
 #define NGA_COUNT(ID, BN, BM, WN, WM, NS) ++n;
   NGA_SKINNY_CFGS(NGA_COUNT)
 #undef NGA_COUNT
-  return n;
+  return n + wreg_gemm_cfg_count();   // gemm_wreg.hip's configurations continue the IDs
 }
 
-// {BN, BM, WN, WM, NSTAGE} of a configuration, or zeros
+// {BN, BM, WN, WM, NSTAGE, kind} of a configuration (kind 0: both operands via LDS, this file;
+// 1: weights in registers, gemm_wreg.hip), or zeros
 void skinny_gemm_cfg_info(int cfg, int* info) {
-  info[0] = info[1] = info[2] = info[3] = info[4] = 0;
+  info[0] = info[1] = info[2] = info[3] = info[4] = info[5] = 0;
 #define NGA_INFO(ID, BN, BM, WN, WM, NS) \
   if (cfg == ID) {                       \
     info[0] = BN;                        \
@@ -383,17 +384,19 @@ void skinny_gemm_cfg_info(int cfg, int* info) {
     info[2] = WN;                        \
     info[3] = WM;                        \
     info[4] = NS;                        \
+    return;                              \
   }
   NGA_SKINNY_CFGS(NGA_INFO)
 #undef NGA_INFO
+  wreg_gemm_cfg_info(cfg, info);
 }
 
 void launch_skinny_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t stream) {
   const int nblk = p.nN * p.nM * p.split;
-  if (nblk == 0) return;
   dim3 grid(nblk);
 #define NGA_LAUNCH(ID, BN, BM, WN, WM, NS)                                                        \
   if (cfg == ID) {                                                                                    \
+    if (nblk == 0) return;                                                                            \
     const dim3 block(64 * WN * WM);                                                                   \
     if (epi == 0) skinny_gemm_kernel<BN, BM, WN, WM, NS, 0><<<grid, block, 0, stream>>>(p);       \
     else if (epi == 1) skinny_gemm_kernel<BN, BM, WN, WM, NS, 1><<<grid, block, 0, stream>>>(p);  \
@@ -402,6 +405,7 @@ void launch_skinny_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t
   }
   NGA_SKINNY_CFGS(NGA_LAUNCH)
 #undef NGA_LAUNCH
+  launch_wreg_gemm(p, cfg, epi, stream);
 }
 
 void launch_splitk_reduce(const float* P, int S, int M, int N, uint16_t* out, int64_t ldo,

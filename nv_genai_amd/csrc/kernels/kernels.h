@@ -185,8 +185,12 @@ struct SkinnyGemmParams {
   int wnt;             // 1: weight DMA with the non-temporal cache policy (streamed once)
 };
 int skinny_gemm_cfg_count();
-void skinny_gemm_cfg_info(int cfg, int* info);   // {BN, BM, WN, WM, NSTAGE}
+void skinny_gemm_cfg_info(int cfg, int* info);   // {BN, BM, WN, WM, NSTAGE, kind}: 6 ints
 void launch_skinny_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t stream);
+// gemm_wreg.hip: the weight-in-registers tile family (IDs after gemm_skinny.hip's)
+int wreg_gemm_cfg_count();
+bool wreg_gemm_cfg_info(int cfg, int* info);
+bool launch_wreg_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t stream);
 void launch_splitk_swiglu(const float* P, int S, int M, int F, uint16_t* out, int64_t ldo,
                           hipStream_t stream);
 void launch_splitk_reduce(const float* P, int S, int M, int N, uint16_t* out, int64_t ldo,

@@ -611,6 +611,7 @@ void register_text(py::module_& m);
 void register_json(py::module_& m);
 void register_hnsw(py::module_& m);
 void register_idmap(py::module_& m);
+void register_shm(py::module_& m);
 
 PYBIND11_MODULE(_rt, m) {
   m.doc() = "nv_genai_amd native host runtime";
@@ -662,4 +663,5 @@ PYBIND11_MODULE(_rt, m) {
   register_json(m);
   register_hnsw(m);
   register_idmap(m);
+  register_shm(m);
 }

@@ -82,6 +82,7 @@ class Request:
     on_token: Optional[Callable[["Request", str], None]] = None
     detok: Optional[IncrementalDetokenizer] = None
     cached_prefix: int = 0
+    error: Optional[str] = None    # finish_reason "error": why the engine refused the request
     beams: List[tuple] = field(default_factory=list)   # beam search: (score, token ids, text)
     json_state: Optional[object] = None    # _rt.JsonState of a response_format=json_object request
     # multimodal prompt: (position, features [n, hidden]) — rows whose input embeddings are
@@ -237,6 +238,8 @@ class LLMEngine:
                       "graph_capture_s": 0.0}
         self.lock = threading.RLock()
         self._inbox: "collections.deque" = collections.deque()   # requests queued while a step held the lock
+        self._live_ids: set = set()       # ids queued or running (duplicates refused in add_request)
+        self._rejected: List[Request] = []   # refused at admission, reported by the next step()
         self._pending: Optional[dict] = None
         self._tok_flip = 0
         self._up_ev = None  # marks the last host->device upload of the pinned step buffers
@@ -262,16 +265,32 @@ class LLMEngine:
         self._beam_of: Dict[int, BeamGroup] = {}   # live beam seq id -> its group
         self._beam_rows: List[tuple] = []         # (row, seq id) of beam rows in this step
         self._beam_out = None
+        self._chan = None
+        self._msg = None
+        self._tp_gathers = 0    # follower steps that gathered ids from their own previous step
         if self.p.mp_size > 1:
-            # followers replay from broadcast host buffers; the device-side id gather of the
-            # pipelined path is not replicated, so TP/PP steps run synchronously; pipeline
-            # stages exchange activations with p2p sends, which stay out of hipGraphs
-            over = {"async_decode": False}
-            if self.p.pp_size > 1 or (self.gpu and self.p.backend == "gloo"):
-                # gloo collectives (ranks sharing one GPU) go through host copies, which a
-                # graph capture cannot contain; RCCL's can be captured
+            # the replica's step channel: followers rebuild every step from the driver's layout
+            # (shared memory on one node: publishing never waits for the driver's GPU, so
+            # steps pipeline exactly as on one rank — each follower gathers the ids the
+            # in-flight step is still producing from its OWN sampled tokens, which equal the
+            # driver's: same gathered logits, same per-row seeds)
+            from ..parallel import step_channel
+
+            nbytes = self._step_msg_bytes(T, S)
+            self._msg = np.zeros(nbytes, dtype=np.uint8)
+            self._chan = step_channel.create(self.p, nbytes)
+            over = {}
+            if not self._chan.pipelined or self.p.pp_size > 1:
+                # a collective channel stages the layout through the driver's stream, and pipeline
+                # stages exchange activations with p2p sends: such replicas step synchronously
+                over["async_decode"] = False
+            if self.p.pp_size > 1:
+                over["use_graphs"] = False   # stage-to-stage sends stay out of hipGraphs
+            elif self.gpu and self.p.backend == "gloo" and not self.model.ipc_collectives_cover(S, S):
+                # ranks sharing one GPU over gloo: a graph may hold only the IPC collectives
                 over["use_graphs"] = False
-            self.cfg = cfg = type(cfg)(**{**cfg.__dict__, **over})
+            if over:
+                self.cfg = cfg = type(cfg)(**{**cfg.__dict__, **over})
         # ---- prefill / mixed step graphs (step layout in device buffers)
         self.mgraphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         # step-graph launches by token bucket and by real token count (128-token bins):
@@ -281,10 +300,13 @@ class LLMEngine:
         self._graph_pool = None
         self._cap_stream = None
         self._mg_ok = self._mixed_graphs_eligible()
-        if self._mg_ok:
+        if self._mg_ok:   # (may turn False below: collectives the graphs could not hold)
             step = max(1, cfg.graph_token_step)
             mx = cfg.max_graph_tokens or (cfg.mixed_prefill_tokens + cfg.max_num_seqs)
             self._mg_max_tokens = min(-(-mx // step) * step, T // step * step)
+            if (self.p.mp_size > 1 and self.p.backend == "gloo"
+                    and not self.model.ipc_collectives_cover(S, self._mg_max_tokens)):
+                self._mg_ok = False
             self._nd_buckets = sorted({b for b in (8, 16, 32, 64, 128, 256, 512) if b < S} | {S})
             cap = self._mg_max_tokens // 32 + S + 16     # >= row blocks (32 or 64 rows) of any step
             self.h_ctxd, self.d_ctxd = hbuf(S), dbuf(S)
@@ -322,7 +344,13 @@ class LLMEngine:
             for off, f in mm:
                 if off < 0 or off + f.shape[0] > len(prompt_ids) or f.shape[1] != self.mcfg.hidden:
                     raise ValueError("multimodal features must cover prompt rows of the model's hidden size")
+        if not prompt_ids:
+            raise ValueError("empty prompt")
         rid = request_id if request_id is not None else next(self._ids)
+        # what the scheduler would refuse at admission is refused here, before the request
+        # can wait in the inbox (a step admits the inbox: a failure there is not the caller's)
+        if rid in self._live_ids:
+            raise ValueError(f"duplicate request id {rid}")
         max_new = max(1, min(params.max_tokens, self.cfg.max_model_len - len(prompt_ids)))
         if len(prompt_ids) >= self.cfg.max_model_len:
             raise ValueError(f"prompt of {len(prompt_ids)} tokens exceeds max_model_len "
@@ -344,19 +372,20 @@ class LLMEngine:
         # A step holds the engine lock for its whole duration (GPU wait included). A producer
         # thread must not queue behind it: when the lock is busy the request goes to the
         # inbox, which the next step admits first (same order, no lost wake-ups).
+        self._live_ids.add(rid)
         if self.lock.acquire(blocking=False):
             try:
-                self._admit(req, max_new)
+                self._rejected += self._admit_inbox()   # earlier arrivals first
+                try:
+                    self._admit_one(req, max_new)
+                except Exception:
+                    self._live_ids.discard(rid)
+                    raise
             finally:
                 self.lock.release()
         else:
             self._inbox.append((req, max_new))
         return req
-
-    def _admit(self, req: Request, max_new: int):
-        while self._inbox:      # earlier arrivals first
-            self._admit_one(*self._inbox.popleft())
-        self._admit_one(req, max_new)
 
     def _admit_one(self, req: Request, max_new: int):
         rid, params = req.id, req.params
@@ -368,15 +397,33 @@ class LLMEngine:
         else:
             self.requests[rid] = req
 
-    def _admit_inbox(self):
+    def _admit_inbox(self) -> List[Request]:
+        """Admit the queued requests in arrival order; one that the scheduler refuses finishes
+        alone with finish_reason "error" (its stream ends with the message), the others and the
+        step go on. Returns the refused ones."""
+        bad = []
         while self._inbox:
-            self._admit_one(*self._inbox.popleft())
+            req, max_new = self._inbox.popleft()
+            try:
+                self._admit_one(req, max_new)
+            except Exception as e:  # noqa: BLE001 - this request's failure, not the step's
+                self._live_ids.discard(req.id)
+                req.finished, req.finish_reason, req.error = True, "error", str(e)
+                req.finish_time = time.perf_counter()
+                if req.on_token is not None:
+                    try:
+                        req.on_token(req, "")
+                    except Exception:  # noqa: BLE001
+                        log.exception("on_token callback failed")
+                bad.append(req)
+        return bad
 
     def abort(self, rid: int):
         with self.lock:
-            self._admit_inbox()
+            self._rejected += self._admit_inbox()
             req = self.requests.pop(rid, None)
             self.sched.finish(rid)
+            self._live_ids.discard(rid)
             g = next((g for g in set(self._beam_of.values()) if g.req.id == rid), None)
             if g is not None:
                 req = g.req
@@ -422,11 +469,13 @@ class LLMEngine:
         (``mixed_prefill_tokens``) a step carries the decode rows of every running sequence
         plus a prefill chunk, so decode rows ride on the prefill GEMMs."""
         with self.lock:
-            self._admit_inbox()
+            done = self._admit_inbox()
+            if self._rejected:
+                done, self._rejected = self._rejected + done, []
             self._nstep += 1
             if self._faults:
                 self._faults.check(self._nstep, "driver")
-            done = self._step(between)
+            done += self._step(between)
         return done
 
     def _step(self, between) -> List[Request]:
@@ -588,7 +637,7 @@ class LLMEngine:
                 if key is not None:
                     self._graph_step(key, kind, n, ntok, max_q, max_ctx, nd, src)
                 else:
-                    self._sync_step(kind, n, ntok, max_q, max_ctx, 0, nd)
+                    self._sync_step(kind, n, ntok, max_q, max_ctx, 0, nd, src=src)
                     self._upload(n, ntok)
                     self._gather_ids(src)
                     logits = self._prefill_forward(n, ntok, max_q, max_ctx, nd)
@@ -634,13 +683,9 @@ class LLMEngine:
         bs = next((b for b in sorted(self.graphs) if b >= n), None)
         if bs is not None:
             self._pad_rows(n, bs)
-        self._sync_step(2, n, n, 1, self.cfg.max_model_len, bs or 0)
+        self._sync_step(2, n, n, 1, self.cfg.max_model_len, bs or 0, src=src)
         self._upload(bs or n, bs or n)
-        if src is not None and len(src[0]) == n:
-            _, prev = self._stage_gather(src)
-            self.d_ids[:n] = self.d_tok.index_select(0, prev)
-        else:
-            self._gather_ids(src)
+        self._apply_decode_src(n, src)
         if bs is not None:
             self.graphs[bs].replay()
         else:
@@ -714,58 +759,120 @@ class LLMEngine:
     def is_driver(self) -> bool:
         return self.p.mp_size == 1 or (self.p.tp_rank == 0 and self.p.pp_rank == 0)
 
-    def _tp_src(self) -> int:
-        return self.p.mp_src
+    _HDR = 12   # int64 header: kind, n, ntok, max_q, max_ctx, bs, nd, gb, nsrc, prow, npairs, 0
 
-    def _bcast(self, t: torch.Tensor) -> torch.Tensor:
-        import torch.distributed as dist
-
-        dev = self.device if self.p.backend == "nccl" else torch.device("cpu")
-        x = t.to(dev)
-        dist.broadcast(x, src=self._tp_src(), group=self.p.mp_group)
-        return x
+    def _step_msg_bytes(self, T: int, S: int) -> int:
+        """Largest step message: header, token rows (ids / positions / slots), sequence rows
+        (cu_seqlens, contexts, block tables), S rows of sampling parameters and a pipelined
+        id gather over every token row."""
+        return (8 * self._HDR + 4 * (3 * T + (S + 1) + S + S * self.max_blocks) + 8
+                + S * (4 + 4 + 4 + 8 + 8) + 16 * T + 64)
 
     def _sync_step(self, kind: int, n: int, ntok: int, max_q: int, max_ctx: int, bs: int, nd: int = 0,
-                   gb: int = 0) -> None:
-        """Driver: publish the step (header + packed int buffers) to the replica's ranks.
-        ``gb``: token bucket of a graph-captured prefill / mixed step (its padded token rows
-        travel too, so followers replay the same graph on the same inputs)."""
+                   gb: int = 0, src=None, pairs=None) -> None:
+        """Driver: publish a step (or a command, kind < 0) to the replica's ranks. ``gb``: token
+        bucket of a graph-captured prefill / mixed step (its padded token rows travel too, so
+        followers replay the same graph on the same inputs); ``src``: the pipelined id gather
+        (token rows, rows of the in-flight step) — every follower applies it to its own sampled
+        tokens; the sampling parameters travel so followers sample exactly what the driver
+        samples. ``pairs``: [2, k] copy-on-fork pages (kind -2)."""
         if self.p.mp_size == 1:
             return
-        hdr = torch.tensor([kind, n, ntok, max_q, max_ctx, bs, nd, gb], dtype=torch.int64)
-        self._bcast(hdr)
-        if kind < 0:
-            return
-        rows = max(n, bs)
-        toks = max(ntok, bs, gb)
-        payload = torch.cat([self.h_ids[:toks], self.h_pos[:toks], self.h_slots[:toks],
-                             self.h_cu[: rows + 1], self.h_ctx[:rows], self.h_bt[:rows].reshape(-1)])
-        self._bcast(payload)
+        rows, toks = max(n, bs), max(ntok, bs, gb)
+        prow = max(rows, self.cfg.max_num_seqs if gb else 0) if kind >= 0 else 0
+        nsrc = 0 if src is None else len(src[0])
+        npairs = 0 if pairs is None else int(pairs.shape[1])
+        m = self._msg
+        m[:8 * self._HDR].view(np.int64)[:] = (kind, n, ntok, max_q, max_ctx, bs, nd, gb, nsrc, prow, npairs, 0)
+        o = 8 * self._HDR
+
+        def put(a):
+            nonlocal o
+            b = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+            m[o:o + b.size] = b
+            o += b.size
+
+        if kind >= 0:
+            ids, pos, sl, cu, ctx, bt = self._np[:6]
+            for a in (ids[:toks], pos[:toks], sl[:toks], cu[:rows + 1], ctx[:rows], bt[:rows]):
+                put(a)
+            o = (o + 7) & ~7
+            for a in (self.n_temp, self.n_topk, self.n_topp, self.n_seed, self.n_step):
+                put(a[:prow])
+            if nsrc:
+                put(np.asarray(src[0], dtype=np.int64))
+                put(np.asarray(src[1], dtype=np.int64))
+        elif npairs:
+            put(np.asarray(pairs, dtype=np.int32))
+        self._chan.send(m[:o])
 
     def _recv_step(self):
-        hdr = self._bcast(torch.zeros(8, dtype=torch.int64)).cpu().tolist()
-        kind, n, ntok, max_q, max_ctx, bs, nd, gb = hdr
-        self._recv_gb = gb
+        """Follower: the next message into the host step buffers. Returns (kind, n, ntok, max_q,
+        max_ctx, bs, nd, gb, src, pairs)."""
+        msg = self._chan.recv()
+        hdr = msg[:8 * self._HDR].view(np.int64).tolist()
+        kind, n, ntok, max_q, max_ctx, bs, nd, gb, nsrc, prow, npairs, _ = hdr
+        o = 8 * self._HDR
+
+        def take(dtype, count):
+            nonlocal o
+            nb = np.dtype(dtype).itemsize * count
+            a = msg[o:o + nb].view(dtype)
+            o += nb
+            return a
+
         if kind < 0:
-            return kind, n, 0, 0, 0, 0, 0
+            pairs = take(np.int32, 2 * npairs).reshape(2, npairs).copy() if npairs else None
+            return kind, n, 0, 0, 0, 0, 0, 0, None, pairs
         rows, toks = max(n, bs), max(ntok, bs, gb)
-        size = 3 * toks + (rows + 1) + rows + rows * self.max_blocks
-        payload = self._bcast(torch.zeros(size, dtype=torch.int32)).cpu()
         if self._up_ev is not None:
+            # the previous step's upload may still be reading the pinned buffers
             self._up_ev.synchronize()
-        o = 0
-        for buf, m in ((self.h_ids, toks), (self.h_pos, toks), (self.h_slots, toks), (self.h_cu, rows + 1),
-                       (self.h_ctx, rows)):
-            buf[:m] = payload[o:o + m]
-            o += m
-        self.h_bt[:rows] = payload[o:o + rows * self.max_blocks].view(rows, self.max_blocks)
-        return kind, n, ntok, max_q, max_ctx, bs, nd
+        ids, pos, sl, cu, ctx, bt = self._np[:6]
+        ids[:toks] = take(np.int32, toks)
+        pos[:toks] = take(np.int32, toks)
+        sl[:toks] = take(np.int32, toks)
+        cu[:rows + 1] = take(np.int32, rows + 1)
+        ctx[:rows] = take(np.int32, rows)
+        bt[:rows] = take(np.int32, rows * self.max_blocks).reshape(rows, self.max_blocks)
+        o = (o + 7) & ~7
+        self.n_temp[:prow] = take(np.float32, prow)
+        self.n_topk[:prow] = take(np.int32, prow)
+        self.n_topp[:prow] = take(np.float32, prow)
+        self.n_seed[:prow] = take(np.int64, prow)
+        self.n_step[:prow] = take(np.int64, prow)
+        self.n_pen[:prow] = 1.0
+        src = None
+        if nsrc:
+            src = (take(np.int64, nsrc).copy(), take(np.int64, nsrc).copy())
+        return kind, n, ntok, max_q, max_ctx, bs, nd, gb, src, None
+
+    def _apply_decode_src(self, n: int, src) -> None:
+        """Pipelined decode: input ids of rows still being produced by the in-flight step."""
+        if src is not None and len(src[0]) == n:
+            _, prev = self._stage_gather(src)
+            self.d_ids[:n] = self.d_tok.index_select(0, prev)
+        else:
+            self._gather_ids(src)
+
+    def _follower_sample(self, logits, n: int) -> None:
+        """Sample the step's rows exactly as the driver does (same logits after the vocab
+        all-gather, same per-row temperature / top-k / top-p / seed / step), so the next
+        pipelined step's id gather reads the same tokens on every rank."""
+        if logits is None:   # a pipeline stage without the LM head
+            return
+        tok, lp = ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n],
+                             self.d_seed[:n], self.d_step[:n], None, None,
+                             out_tok=self.d_tok[:n], out_lp=self.d_lp[:n])
+        if tok.data_ptr() != self.d_tok.data_ptr():   # reference path returns fresh tensors
+            self.d_tok[:n].copy_(tok[:n])
+            self.d_lp[:n].copy_(lp[:n])
 
     def run_follower(self, hooks: Optional[Dict[int, Callable[[int], None]]] = None) -> None:
         """Non-driver TP ranks: execute every step the driver publishes, and the hook for
         each command kind (<= -3) it broadcasts (``broadcast_command``)."""
         while True:
-            kind, n, ntok, max_q, max_ctx, bs, nd = self._recv_step()
+            kind, n, ntok, max_q, max_ctx, bs, nd, gb, src, pairs = self._recv_step()
             self._nstep += 1
             if self._faults:
                 self._faults.check(self._nstep, "follower")
@@ -774,25 +881,33 @@ class LLMEngine:
                     raise RuntimeError(f"follower has no hook for command {kind}")
                 hooks[kind](n)
                 continue
-            if kind == -2:   # copy-on-fork pages (beam search), n pairs
-                pairs = self._bcast(torch.zeros(2 * n, dtype=torch.int32)).cpu().view(2, n)
-                self.model.copy_kv_blocks(pairs[0], pairs[1])
+            if kind == -2:   # copy-on-fork pages (beam search)
+                self.model.copy_kv_blocks(torch.from_numpy(pairs[0]), torch.from_numpy(pairs[1]))
                 continue
             if kind < 0:
                 return
-            if kind in (1, 3) and self._recv_gb:
+            if src is not None:
+                self._tp_gathers += 1
+            prow = max(n, bs, self.cfg.max_num_seqs if gb else 0)
+            if kind in (1, 3) and gb:
                 key = self._graph_key(n, ntok, nd)
-                if key is None or key[0] != self._recv_gb:
-                    raise RuntimeError(f"follower cannot replay the driver's step graph {self._recv_gb}")
-                self._graph_step(key, kind, n, ntok, max_q, max_ctx, nd, None, follower=True)
+                if key is None or key[0] != gb:
+                    raise RuntimeError(f"follower cannot replay the driver's step graph {gb}")
+                self._graph_step(key, kind, n, ntok, max_q, max_ctx, nd, src, follower=True)
             elif kind in (1, 3):
                 self._upload(n, ntok)
-                self._prefill_forward(n, ntok, max_q, max_ctx, nd)
+                self._gather_ids(src)
+                self._follower_sample(self._prefill_forward(n, ntok, max_q, max_ctx, nd), n)
             elif bs:
-                self._upload(bs, bs)
+                self._upload(bs, bs, nparam=prow)
+                self._apply_decode_src(n, src)
                 self.graphs[bs].replay()
             else:
-                self._decode_eager(n)
+                self._upload(n, n)
+                self._apply_decode_src(n, src)
+                meta = self._meta("decode", n, n, 1, self.cfg.max_model_len)
+                h = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta)
+                self._follower_sample(None if h is None else self.model.logits(h), n)
 
     def stop_followers(self) -> None:
         if self.p.mp_size > 1 and self.is_driver:
@@ -839,14 +954,13 @@ class LLMEngine:
             src = torch.tensor([c[0] for c in copies], dtype=torch.int32)
             dst = torch.tensor([c[1] for c in copies], dtype=torch.int32)
             if self.p.mp_size > 1:
-                hdr = torch.tensor([-2, len(copies), 0, 0, 0, 0, 0, 0], dtype=torch.int64)
-                self._bcast(hdr)
-                self._bcast(torch.cat([src, dst]))
+                self._sync_step(-2, len(copies), 0, 0, 0, 0, 0, pairs=torch.stack([src, dst]).numpy())
             self.model.copy_kv_blocks(src, dst)
         return done
 
     def _beam_finish(self, g: BeamGroup, now: float) -> None:
         r = g.req
+        self._live_ids.discard(r.id)
         for score, toks, eos in g.hyps:
             text = self.tok.decode([t for t in toks if t not in self.stop_ids]) if self.cfg.detokenize else ""
             for s in r.params.stop:
@@ -904,6 +1018,7 @@ class LLMEngine:
             r.finished, r.finish_reason, r.finish_time = True, reason, now
             self.sched.finish(r.id)
             self.requests.pop(r.id, None)
+            self._live_ids.discard(r.id)
             if r.on_token is not None:
                 try:
                     r.on_token(r, "")
@@ -1229,7 +1344,7 @@ class LLMEngine:
         sidx[n:S] = 0
         self._pad_params(n, S)
         if not follower:
-            self._sync_step(kind, n, ntok, max_q, max_ctx, 0, nd, gb=tb)
+            self._sync_step(kind, n, ntok, max_q, max_ctx, 0, nd, gb=tb, src=src)
         # lazy capture only after the step header and payload went out: under TP the warm-up
         # and captured forwards issue all-reduces, which the followers (blocked in _recv_step
         # until the broadcast) must meet in the same order. The capture leaves the host-side

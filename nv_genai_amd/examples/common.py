@@ -33,6 +33,14 @@ class LLMStream:
             self._handle = self.llm.submit(self.messages)
         return self
 
+    def cancel(self) -> None:
+        """Abort the request ``prepare`` queued if its stream never finished being consumed
+        (the chain server runs this after every response: a client that disconnects before
+        the body starts would otherwise leave the request decoding to max_tokens)."""
+        h = self._handle
+        if h is not None and not h.done.is_set():
+            h.cancel()
+
     def _start(self):
         self.cb.on_llm_start(self.rid, self.messages, **{k: v for k, v in self.kwargs.items() if v is not None})
 

@@ -821,6 +821,21 @@ class LlamaModel:
         resid.record_stream(aux)
         return torch.cat([hd, hp])
 
+    def ipc_collectives_cover(self, rows: int, tokens: int) -> bool:
+        """True when every collective of a forward over ``tokens`` token rows that samples
+        ``rows`` rows goes through the TP group's IPC custom kernels (all-reduces of [tokens,
+        hidden] bf16, the [rows, vocab / tp] fp32 logits all-gather), which a hipGraph can
+        hold whatever the process-group backend (gloo's host-copy collectives it cannot)."""
+        if self.p.tp_size == 1:
+            return True
+        car = custom_all_reduce_for(self.p.tp_group)
+        if car is None or not car.enabled or self.expert_parallel:
+            return False
+        ar = tokens * self.cfg.hidden * 2
+        ag = rows * self.vocab_local * 4
+        return (ar <= car.capacity and ag <= car.capacity and (self.cfg.hidden * 2) % 16 == 0
+                and (self.vocab_local * 4) % 16 == 0)
+
     def logits(self, h: torch.Tensor) -> torch.Tensor:
         """fp32 logits over the full vocabulary (vocab-parallel head + all-gather). Where the
         skinny table picks it, the LM head GEMM writes fp32 straight from its accumulators

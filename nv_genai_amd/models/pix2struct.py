@@ -460,12 +460,34 @@ class Pix2StructModel:
         """Greedy generation for a batch of images (their real patches). Returns each image's
         token ids up to (excluding) EOS. On a GPU the decode step replays as a hipGraph.
         ``ignore_eos``: every row runs all ``max_new_tokens`` steps (fixed-work benchmarks).
-        Runs on request threads under ``capture_guard`` (its library GEMMs never launch beside
-        another thread's graph capture)."""
-        with capture_guard():
-            return self._generate(patches, max_new_tokens, use_graph, ignore_eos)
+        Runs on request threads: the encoder, the warm-up step and the capture hold
+        ``capture_guard`` (their library GEMMs never launch beside another thread's graph
+        capture); graph replays do not, so a long generation never holds up an LLM engine
+        that needs to capture a step graph meanwhile."""
+        return self._generate(patches, max_new_tokens, use_graph, ignore_eos)
 
     def _generate(self, patches, max_new_tokens, use_graph, ignore_eos):
+        c, dev = self.cfg, self.device
+        if use_graph is None:
+            use_graph = dev.type == "cuda"
+        with capture_guard():
+            st, graph = self._prepare(patches, max_new_tokens, use_graph, ignore_eos)
+        S = int(max_new_tokens)
+        for i in range(S):
+            if graph is not None:
+                graph.replay()
+            else:
+                with capture_guard():   # eager steps issue library GEMMs
+                    self._step(st)
+            if (i + 1) % 32 == 0 and bool(st["done"].all()):
+                break
+        out = st["out"].tolist()
+        if ignore_eos:
+            return out
+        return [r[: r.index(c.eos_id)] if c.eos_id in r else r for r in out]
+
+    def _prepare(self, patches, max_new_tokens, use_graph, ignore_eos):
+        """Encoder pass, decode state and (use_graph) the captured decode step."""
         c, dev = self.cfg, self.device
         enc, cu = self.encode(patches)
         B, S = len(patches), int(max_new_tokens)
@@ -477,8 +499,6 @@ class Pix2StructModel:
               "done": torch.zeros(B, dtype=torch.bool, device=dev),
               "out": torch.full((B, S), c.pad_id, dtype=torch.long, device=dev), "ignore_eos": ignore_eos}
         graph = None
-        if use_graph is None:
-            use_graph = dev.type == "cuda"
         if use_graph:
             # warm up on a side stream (allocator pools, hipBLASLt handles), then capture one
             # step; the warm-up step is undone by resetting the state it advanced
@@ -494,17 +514,7 @@ class Pix2StructModel:
             st["done"].zero_()
             st["tok"].fill_(c.decoder_start_id)
             st["out"].fill_(c.pad_id)
-        for i in range(S):
-            if graph is not None:
-                graph.replay()
-            else:
-                self._step(st)
-            if (i + 1) % 32 == 0 and bool(st["done"].all()):
-                break
-        out = st["out"].tolist()
-        if ignore_eos:
-            return out
-        return [r[: r.index(c.eos_id)] if c.eos_id in r else r for r in out]
+        return st, graph
 
 
 class DePlot:

@@ -12,9 +12,12 @@ here), like the ranker's head.
 """
 from __future__ import annotations
 
+import threading
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
+
+from ..utils.runtime import capture_guard
 
 from .config import llama_config
 from .llama import LlamaModel
@@ -50,6 +53,10 @@ class RewardModel:
             self.head_w = torch.empty(len(ATTRIBUTES), cfg.hidden, device=dev).normal_(0, 0.02, generator=g)
             self.head_b = torch.zeros(len(ATTRIBUTES), device=dev)
         self._tok = None
+        # one forward at a time (executor threads of a server share the model), and none while
+        # another thread captures a hipGraph: a library GEMM's first use beside a capture
+        # invalidates it (utils.runtime.capture_guard)
+        self.lock = threading.Lock()
 
     @property
     def tok(self):
@@ -79,10 +86,12 @@ class RewardModel:
         ids = torch.tensor([t for s in seqs for t in s], dtype=torch.int32, device=dev)
         pos = torch.tensor([i for n in lens for i in range(n)], dtype=torch.int32, device=dev)
         cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0).tolist()), dtype=torch.int32, device=dev)
-        h = packed_hidden(self.lm, ids, pos, cu, max(lens), causal=True)
-        last = h.index_select(0, (cu[1:] - 1).long()).float()
-        s = 4.0 * torch.sigmoid(last @ self.head_w.t() + self.head_b)
-        return [{a: round(float(v), 4) for a, v in zip(ATTRIBUTES, row)} for row in s.cpu()]
+        with self.lock, capture_guard():
+            h = packed_hidden(self.lm, ids, pos, cu, max(lens), causal=True)
+            last = h.index_select(0, (cu[1:] - 1).long()).float()
+            s = 4.0 * torch.sigmoid(last @ self.head_w.t() + self.head_b)
+            s = s.cpu()
+        return [{a: round(float(v), 4) for a, v in zip(ATTRIBUTES, row)} for row in s]
 
     def score(self, question: str, answer: str) -> Dict[str, float]:
         return self.score_batch([(question, answer)])[0]

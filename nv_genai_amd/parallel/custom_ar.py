@@ -27,6 +27,10 @@ log = logging.getLogger(__name__)
 
 ALGO_AUTO, ALGO_ONE_SHOT, ALGO_TWO_SHOT = 0, 1, 2
 TWO_SHOT_THRESHOLD_BYTES = 512 * 1024   # the kernel's default (custom_ar.h)
+# per staging buffer (x2 for the call-parity double buffer, uncached HBM): the largest message
+# a step graph may hold — a 4,352-token mixed step of a hidden-8,192 model (71 MB bf16) and
+# 256 rows of an 8B model's half vocabulary at TP=2 (66 MB fp32 logits)
+DEFAULT_CAPACITY_MB = 80
 
 
 def choose_algo(nbytes: int, world: int, threshold: int = TWO_SHOT_THRESHOLD_BYTES) -> int:
@@ -51,6 +55,7 @@ class CustomAllReduce:
         self.two_shot_threshold = (int(two_shot_threshold_kb * 1024) if two_shot_threshold_kb is not None
                                    else TWO_SHOT_THRESHOLD_BYTES)
         self.algo_counts = {ALGO_ONE_SHOT: 0, ALGO_TWO_SHOT: 0}
+        self.gather_count = 0
         self.enabled = False
         self.impl = None
         # every stage ends with an agreement among the ranks, so a failure on one rank
@@ -112,6 +117,22 @@ class CustomAllReduce:
         self.impl.all_reduce_add_rmsnorm(x, resid, w, out, float(eps))
         return out
 
+    def gather_eligible(self, x: torch.Tensor) -> bool:
+        """The IPC all-gather along the last dim takes contiguous 2-D device tensors whose rows
+        are whole 16-B packets and whose shard fits the staging buffer."""
+        return (self.enabled and x.is_cuda and x.is_contiguous() and x.dim() == 2
+                and (x.shape[1] * x.element_size()) % 16 == 0 and x.data_ptr() % 16 == 0
+                and 0 < x.numel() * x.element_size() <= self.capacity)
+
+    def all_gather(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """[rows, cols] per rank -> [rows, world * cols], rank r's shard in columns
+        [r * cols, (r + 1) * cols) (the vocab-parallel LM head's logits). Capture-safe."""
+        if out is None:
+            out = torch.empty(x.shape[0], self.world * x.shape[1], dtype=x.dtype, device=x.device)
+        self.gather_count += 1
+        self.impl.all_gather(x, out)
+        return out
+
     def error(self) -> int:
         return int(self.impl.error())
 
@@ -129,6 +150,13 @@ class CustomAllReduce:
         dist.all_reduce(y, group=self.group)
         return y.to(x.device)
 
+    def _reference_gather(self, x: torch.Tensor) -> torch.Tensor:
+        backend = dist.get_backend(self.group)
+        y = x.contiguous() if backend == "nccl" else x.cpu()
+        parts = [torch.empty_like(y) for _ in range(self.world)]
+        dist.all_gather(parts, y, group=self.group)
+        return torch.cat(parts, dim=1).to(x.device)
+
     def _self_test(self) -> bool:
         ok = True
         dev = torch.device("cuda", torch.cuda.current_device())
@@ -142,6 +170,13 @@ class CustomAllReduce:
                 torch.cuda.synchronize(dev)
                 # no early exit: every rank must issue the same collectives
                 ok = ok and not self.error() and torch.allclose(got.float(), ref, atol=0.05, rtol=0.02)
+            # the all-gather: fp32 shards with a rank-dependent pattern, compared bit for bit
+            g = torch.Generator(device="cpu").manual_seed(2000 + self.rank)
+            shard = torch.randn(3, 68, generator=g).to(dev)
+            want = self._reference_gather(shard)
+            got = self.all_gather(shard)
+            torch.cuda.synchronize(dev)
+            ok = ok and not self.error() and torch.equal(got, want)
         except Exception as e:  # noqa: BLE001 - any failure means "use RCCL"
             log.warning("custom all-reduce self-test raised: %r", e)
             ok = False
@@ -177,7 +212,7 @@ def maybe_create(group, world: int) -> Optional[CustomAllReduce]:
     if os.environ.get("NGA_CUSTOM_AR", "1") == "0":
         return None
     try:
-        car = CustomAllReduce(group, capacity_mb=float(os.environ.get("NGA_CUSTOM_AR_MB", "64")))
+        car = CustomAllReduce(group, capacity_mb=float(os.environ.get("NGA_CUSTOM_AR_MB", str(DEFAULT_CAPACITY_MB))))
     except Exception as e:  # noqa: BLE001
         log.warning("custom all-reduce unavailable (%r); TP all-reduces use RCCL", e)
         _STATUS = {"state": "failed", "world": world, "error": repr(e)[:200]}

@@ -180,6 +180,13 @@ def tp_all_gather(x: torch.Tensor, dim: int = -1, ctx: Optional[ParallelContext]
     ctx = ctx or _CTX
     if ctx.tp_size == 1:
         return x
+    if x.is_cuda and x.dim() == 2 and dim in (-1, 1):
+        # the IPC all-gather (direct peer reads over xGMI; capture-safe with any backend)
+        from .comm import custom_all_reduce_for
+
+        car = custom_all_reduce_for(ctx.tp_group)
+        if car is not None and car.gather_eligible(x):
+            return car.all_gather(x)
     y = x.contiguous()
     if ctx.backend == "gloo" and y.is_cuda:   # gloo gathers host tensors
         y = y.cpu()

@@ -1,0 +1,149 @@
+"""Driver -> follower channel for the step layouts of a model-parallel replica (CC5).
+
+Every step of a TP / PP replica is scheduled once, on its driver (tp rank 0, stage 0), and
+each follower rank must run the same forward on the same layout. The layout is host data
+(token ids, positions, cache slots, block tables, sampling parameters, and the rows whose
+input ids the previous step is still producing on the device). Two transports:
+
+* :class:`ShmStepChannel` — all ranks of the replica on one node (the TP=8 agent, the TP=2
+  one-GPU rehearsal): a ring of shared-memory slots (``_rt.ShmChannel``, C++). Publishing is a
+  memcpy plus a release store, so the driver never waits on its GPU to publish and followers
+  start launching step k + 1 while step k still runs — the pipelined TP engine.
+* :class:`DistStepChannel` — anything else: a length-prefixed broadcast over the replica's
+  process group (RCCL or gloo). Correct everywhere, but over RCCL the host payload is staged
+  through the driver's current stream, so the engine keeps such replicas unpipelined.
+
+The reference's TP engine hides this inside TensorRT-LLM's in-flight batching with
+``tensor_para_size`` (experimental/fm-asr-streaming-rag/nim/configs/mistral-7b.yaml:26-39).
+"""
+from __future__ import annotations
+
+import os
+import socket
+import uuid
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .._native import rt
+from .dist import ParallelContext
+
+# one slot must hold the largest step message; the ring depth bounds how far the driver may
+# run ahead of the slowest follower (the engine itself keeps at most one step in flight)
+DEFAULT_SLOTS = 4
+
+
+class StepChannel:
+    pipelined = False   # True: publishing never waits for the driver's GPU
+
+    def send(self, msg: np.ndarray) -> None:
+        raise NotImplementedError
+
+    def recv(self) -> np.ndarray:
+        raise NotImplementedError
+
+    def close(self) -> None:
+        pass
+
+
+class ShmStepChannel(StepChannel):
+    pipelined = True
+
+    def __init__(self, pctx: ParallelContext, slot_bytes: int, nslots: int = DEFAULT_SLOTS,
+                 timeout_s: float = 600.0):
+        self.p = pctx
+        self.timeout = float(timeout_s)
+        self.slot_bytes = int(slot_bytes)
+        driver = pctx.tp_rank == 0 and pctx.pp_rank == 0
+        name = None
+        err = None
+        if driver:
+            name = f"/nga_step_{os.getpid()}_{uuid.uuid4().hex[:12]}"
+            try:
+                self.ch = rt.ShmChannel(name, True, nslots, self.slot_bytes, pctx.mp_size - 1, 0)
+            except Exception as e:  # noqa: BLE001
+                err, name = e, None
+        obj = [name]
+        dist.broadcast_object_list(obj, src=pctx.mp_src, group=pctx.mp_group)
+        name = obj[0]
+        if name is None:
+            raise RuntimeError(f"shm step channel: the driver could not create its segment ({err!r})")
+        if not driver:
+            # reader index: this rank's position among the replica's followers
+            local = pctx.rank - pctx.mp_src
+            self.ch = rt.ShmChannel(name, False, 0, 0, 0, local - 1)
+            self._buf = np.empty(self.ch.slot_bytes(), dtype=np.uint8)
+        # every follower attached: drop the name so nothing is left in /dev/shm on a crash
+        if pctx.backend == "nccl":
+            _nccl_barrier(pctx)
+        else:
+            dist.barrier(group=pctx.mp_group)
+        if driver:
+            self.ch.unlink()
+        self.driver = driver
+
+    def send(self, msg: np.ndarray) -> None:
+        if not self.ch.write(np.ascontiguousarray(msg), self.timeout):
+            raise RuntimeError("step channel: followers stopped consuming (timeout or closed)")
+
+    def recv(self) -> np.ndarray:
+        n = self.ch.read(self._buf, self.timeout)
+        if n == -2:
+            raise RuntimeError("step channel closed by the driver")
+        if n < 0:
+            raise TimeoutError("step channel: no step from the driver")
+        return self._buf[:n]
+
+    def close(self) -> None:
+        self.ch.close()
+
+
+def _nccl_barrier(pctx: ParallelContext) -> None:
+    t = torch.zeros(1, device=pctx.device)
+    dist.all_reduce(t, group=pctx.mp_group)
+    torch.cuda.synchronize(pctx.device)
+
+
+class DistStepChannel(StepChannel):
+    """Length-prefixed broadcast over the replica's process group (device tensors on RCCL)."""
+
+    def __init__(self, pctx: ParallelContext, slot_bytes: int):
+        self.p = pctx
+        self.slot_bytes = int(slot_bytes)
+        self.dev = pctx.device if pctx.backend == "nccl" else torch.device("cpu")
+
+    def _bcast(self, t: torch.Tensor) -> torch.Tensor:
+        x = t.to(self.dev)
+        dist.broadcast(x, src=self.p.mp_src, group=self.p.mp_group)
+        return x
+
+    def send(self, msg: np.ndarray) -> None:
+        b = torch.from_numpy(np.ascontiguousarray(msg).view(np.uint8))
+        self._bcast(torch.tensor([b.numel()], dtype=torch.int64))
+        self._bcast(b)
+
+    def recv(self) -> np.ndarray:
+        n = int(self._bcast(torch.zeros(1, dtype=torch.int64)).cpu()[0])
+        return self._bcast(torch.empty(n, dtype=torch.uint8)).cpu().numpy()
+
+
+def same_host(pctx: ParallelContext) -> bool:
+    """Every rank of this rank's replica runs on this node (collective over the replica)."""
+    names = [None] * pctx.mp_size
+    dist.all_gather_object(names, socket.gethostname(), group=pctx.mp_group)
+    return len(set(names)) == 1
+
+
+def create(pctx: ParallelContext, slot_bytes: int, transport: Optional[str] = None) -> StepChannel:
+    """The replica's step channel (collective over its ranks). ``transport``: "shm", "dist" or
+    None (shm when the replica is on one node; ``NGA_STEP_CHANNEL`` overrides)."""
+    transport = transport or os.environ.get("NGA_STEP_CHANNEL") or None
+    if transport is None:
+        transport = "shm" if same_host(pctx) else "dist"
+    if transport == "shm":
+        return ShmStepChannel(pctx, slot_bytes)
+    if transport == "dist":
+        return DistStepChannel(pctx, slot_bytes)
+    raise ValueError(f"step channel transport must be shm or dist, not {transport!r}")

@@ -49,6 +49,7 @@ class StreamHandle:
         self._aq: Optional[asyncio.Queue] = None
         self._buf: List[str] = []       # deltas held back by the stream interval
         self._sent_step = -1            # service step of the last delivery (-1: none yet)
+        self._sent_time = 0.0
 
     def _put(self, item):
         with self._lock:
@@ -64,11 +65,9 @@ class StreamHandle:
                     if item is not _END:
                         self._buf.append(item)
                         if self._sent_step >= 0 and svc.steps - self._sent_step < svc.stream_interval:
+                            svc._held.add(self)   # flushed by the interval or by time (_flush)
                             return
-                    if self._buf:
-                        svc._pending.setdefault(self._loop, []).append((self._aq, "".join(self._buf)))
-                        self._buf = []
-                        self._sent_step = svc.steps
+                    self._release()
                     if item is _END:
                         svc._pending.setdefault(self._loop, []).append((self._aq, _END))
                 else:
@@ -76,11 +75,23 @@ class StreamHandle:
             else:
                 self.q.put(item)
 
+    def _release(self):
+        """Queue the held deltas for delivery with this step (engine thread, under _lock)."""
+        svc = self.service
+        if self._buf:
+            svc._pending.setdefault(self._loop, []).append((self._aq, "".join(self._buf)))
+            self._buf = []
+        self._sent_step = svc.steps
+        self._sent_time = time.monotonic()
+        svc._held.discard(self)
+
     # engine-thread side
     def _on_token(self, req: Request, delta: str):
         if delta:
             self._put(delta)
         if req.finished and not self.done.is_set():
+            if req.finish_reason == "error":   # refused at admission: this stream fails alone
+                self.error = EngineError(req.error or "request refused by the engine")
             self.done.set()
             self._put(_END)
 
@@ -154,16 +165,23 @@ class StreamHandle:
 
 class EngineService:
     def __init__(self, engine: LLMEngine, watchdog_s: float = 300.0, name: str = "llm",
-                 quiet_gc: bool = True, fail_fast: bool = False, stream_interval: Optional[int] = None):
+                 quiet_gc: bool = True, fail_fast: bool = False, stream_interval: Optional[int] = None,
+                 stream_max_hold_ms: Optional[float] = None):
         if quiet_gc:   # no multi-ms GC pauses on the thread that launches GPU steps
             from ..utils.runtime import quiet_gc as _quiet
 
             _quiet()
         self.engine = engine
         self.watchdog_s = watchdog_s
-        # async streams: deliver text at most every N engine steps (NGA_STREAM_INTERVAL)
+        # async streams: every token's text goes out with the step that produced it, as the
+        # reference streams each chunk as produced (common/server.py:289-301). A throughput
+        # deployment may batch deltas over N steps (NGA_STREAM_INTERVAL, opt-in); held text
+        # is still flushed within stream_max_hold_s even if its request stalls (preemption)
         self.stream_interval = max(1, int(stream_interval if stream_interval is not None
-                                          else os.environ.get("NGA_STREAM_INTERVAL", "8")))
+                                          else os.environ.get("NGA_STREAM_INTERVAL", "1")))
+        self.stream_max_hold_s = float(stream_max_hold_ms if stream_max_hold_ms is not None
+                                       else os.environ.get("NGA_STREAM_MAX_HOLD_MS", "100")) / 1e3
+        self._held: set = set()                      # handles holding deltas back
         self.name = name
         self.cv = threading.Condition()
         self.handles = {}
@@ -272,7 +290,16 @@ class EngineService:
                 self._flush()
 
     def _flush(self):
-        """Hand the step's stream deliveries to their event loops, one callback per loop."""
+        """Hand the step's stream deliveries to their event loops, one callback per loop.
+        Deltas held by the stream interval go out once the interval or the hold time has
+        passed, whether or not their request produced another token."""
+        if self._held:
+            now = time.monotonic()
+            for h in list(self._held):
+                if (self.steps - h._sent_step >= self.stream_interval
+                        or now - h._sent_time >= self.stream_max_hold_s):
+                    with h._lock:
+                        h._release()
         if not self._pending:
             return
         pending, self._pending = self._pending, {}

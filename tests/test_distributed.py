@@ -53,6 +53,75 @@ def _tp_worker(rank, world, port, q, tp=2, pp=1, sp=False, model="llama-tiny", o
     pd.destroy()
 
 
+def _tp_pipeline_worker(rank, world, port, q):
+    """TP=2 engine with pipelined steps: the driver launches step k + 1 before it reads step
+    k's tokens, and every follower gathers those ids from its own sampled tokens."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    from nv_genai_amd.engine.llm_engine import EngineConfig, LLMEngine, SamplingParams
+    from nv_genai_amd.models.config import llama_config
+    from nv_genai_amd.models.llama import LlamaModel
+    from nv_genai_amd.parallel import dist as pd
+
+    single = pd.ParallelContext()
+    cfg = llama_config("llama-tiny")
+    full = LlamaModel(cfg, "cpu", pctx=single, seed=7).state_dict()
+    ecfg = EngineConfig(model="llama-tiny", max_num_seqs=4, max_batched_tokens=256, max_model_len=512,
+                        kv_cache_blocks=32)
+    prompts = [[5, 6, 7, 8] * 20, [9, 10, 11] * 11, [3, 4] * 9]
+    f32 = torch.float32
+    greedy = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True)
+    hot = SamplingParams(temperature=0.9, top_p=0.9, max_tokens=10, ignore_eos=True, seed=11)
+    ref = None
+    if rank == 0:
+        e1 = LLMEngine(ecfg, device="cpu", pctx=single, model_cfg=cfg,
+                       model=LlamaModel(cfg, "cpu", dtype=f32, pctx=single, weights=full))
+        ref = [r.output_ids for r in e1.generate(prompts, greedy)]
+    pctx = pd.init_distributed(tp_size=2, backend="gloo", device="cpu")
+    eng = LLMEngine(ecfg, device="cpu", pctx=pctx, model_cfg=cfg,
+                    model=LlamaModel(cfg, "cpu", dtype=f32, pctx=pctx, weights=full))
+    res = {"rank": rank, "async": eng.cfg.async_decode, "chan": type(eng._chan).__name__}
+    if eng.is_driver:
+        res["out"] = [r.output_ids for r in eng.generate(prompts, greedy)]
+        res["hot"] = [r.output_ids for r in eng.generate(prompts, hot)]
+        res["ref"] = ref
+        res["unpipelined"] = eng.stats["unpipelined_steps"]
+        res["pipelined"] = len(eng._host_steps)
+        eng.stop_followers()
+    else:
+        eng.run_follower()
+        res["gathers"] = eng._tp_gathers
+    res["last_tok"] = eng.d_tok[:3].tolist()
+    q.put(res)
+    pd.destroy()
+
+
+def test_tensor_parallel_steps_pipeline():
+    """TP=2 over the shared-memory step channel keeps ``async_decode`` on: greedy tokens equal
+    TP=1, most steps are launched before the previous step is read back, the follower applies
+    the pipelined id gather to its own samples, and with temperature sampling both ranks end
+    on the same sampled tokens (a follower that sampled differently would feed the all-reduces
+    different embeddings and the driver's output would drift)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_tp_pipeline_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda r: r["rank"])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    drv, fol = res
+    assert drv["chan"] == "ShmStepChannel" and drv["async"] and fol["async"]
+    assert drv["out"] == drv["ref"]
+    assert all(len(o) == 10 for o in drv["hot"])
+    assert drv["pipelined"] >= 10 and drv["unpipelined"] <= 4, drv
+    assert fol["gathers"] >= 10, fol
+    assert drv["last_tok"] == fol["last_tok"]
+
+
 def test_tensor_parallel_matches_single():
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")

@@ -397,6 +397,49 @@ def test_skinny_gemm_path_matches_library_path(gpu, weights, tmp_path, monkeypat
     _same_greedy_run(res["1"], res["0"])
 
 
+def test_step_graph_capture_beside_reward_thread(gpu, weights):
+    """As below with the model server's reward endpoint: RewardModel.score runs library GEMMs
+    on executor threads (several at once) while the engine captures step graphs lazily; the
+    reward forward holds capture_guard and its own model lock."""
+    import threading
+
+    from nv_genai_amd.engine.llm_engine import SamplingParams
+    from nv_genai_amd.models.reward import RewardModel
+
+    rm = RewardModel("reward-tiny", device="cuda")
+    stop, errs, done = threading.Event(), [], [0]
+
+    def score_loop(k):
+        i = 0
+        while not stop.is_set():
+            try:
+                rm.score("question " * (1 + (i + k) % 37), "answer " * (1 + i % 53))   # new shapes
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+                return
+            i += 1
+            done[0] += 1
+
+    ts = [threading.Thread(target=score_loop, args=(k,)) for k in range(2)]
+    for t in ts:
+        t.start()
+    try:
+        e = _engine(weights, "cuda", use_graphs=True, mixed_graphs=True, mixed_prefill_tokens=512)
+        p = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
+        reqs = [e.add_request(pr, p) for pr in PROMPTS[:2]]
+        for _ in range(3):
+            e.step()
+        reqs += [e.add_request(pr, p) for pr in PROMPTS[2:]]
+        e.run_until_done(reqs)
+        assert e.mgraphs and all(len(r.output_ids) == 12 for r in reqs)
+    finally:
+        stop.set()
+        for t in ts:
+            t.join()
+    assert not errs, errs
+    assert done[0] > 0
+
+
 def test_step_graph_capture_beside_encoder_thread(gpu, weights):
     """A serving process encodes queries on other threads while the engine captures step
     graphs lazily. The first use of a library GEMM solution in such a thread is not permitted

@@ -2,6 +2,7 @@
 a step that raises fails every in-flight stream with EngineError and the service keeps
 serving; a step that overruns the watchdog makes readiness report unhealthy; a cancelled stream
 aborts its request and frees its KV blocks."""
+import os
 import threading
 import time
 
@@ -97,7 +98,7 @@ def test_async_streams_batch_deliveries_per_interval():
 
     eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=8, max_batched_tokens=256, max_model_len=512,
                                  kv_cache_blocks=64), device="cpu")
-    svc = EngineService(eng, quiet_gc=False, stream_interval=4)
+    svc = EngineService(eng, quiet_gc=False, stream_interval=4, stream_max_hold_ms=60_000)
     try:
         want = svc.submit([5, 6, 7, 8] * 4, _params(24)).text()
 
@@ -113,6 +114,29 @@ def test_async_streams_batch_deliveries_per_interval():
             assert "".join(chunks) == want
             assert len(chunks) <= 24 // 4 + 2, chunks
         assert svc._pending == {}
+    finally:
+        svc.shutdown()
+
+
+def test_held_deltas_flush_by_time_and_default_is_per_token():
+    """The default stream interval is one step (a delta per token, as the reference streams);
+    with a long interval, held text still goes out once it has waited stream_max_hold_ms."""
+    import asyncio
+
+    eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=8, max_batched_tokens=256, max_model_len=512,
+                                 kv_cache_blocks=64), device="cpu")
+    if "NGA_STREAM_INTERVAL" not in os.environ:
+        d = EngineService(eng, quiet_gc=False)
+        d.shutdown()
+        assert d.stream_interval == 1
+    svc = EngineService(eng, quiet_gc=False, stream_interval=1000, stream_max_hold_ms=0)
+    try:
+        async def run():
+            h = svc.submit([5, 6, 7, 8] * 4, _params(12))
+            return [c async for c in h.aiter(coalesce=False)]
+
+        chunks = asyncio.run(run())
+        assert len(chunks) >= 6, chunks   # not one burst at the end: flushed step by step
     finally:
         svc.shutdown()
 
@@ -141,3 +165,81 @@ def test_add_request_does_not_wait_for_a_running_step():
     t.join()
     eng.run_until_done([a, b])
     assert len(a.output_ids) == 3 and len(b.output_ids) == 3 and not eng._inbox
+
+
+def test_inbox_admission_failure_fails_only_that_request(service):
+    """A queued request that the scheduler refuses at admission (here: a forced failure of
+    sched.add for one id) finishes alone with finish_reason "error" and its stream raises;
+    the step goes on and the other streams complete. Empty prompts and duplicate ids are
+    refused by add_request itself, before they can wait in the inbox."""
+    eng = service.engine
+    with pytest.raises(ValueError, match="empty prompt"):
+        eng.add_request([], _params(2))
+    first = eng.add_request([5, 6, 7], _params(2), request_id=777)
+    with pytest.raises(ValueError, match="duplicate"):
+        eng.add_request([5, 6, 7], _params(2), request_id=777)
+    eng.run_until_done([first])
+    real_add = eng.sched.add
+
+    class Sched:   # the native scheduler's add, failing for one id
+        def __getattr__(self, k):
+            return getattr(real_sched, k)
+
+        def add(self, rid, prompt, max_new):
+            if rid == 4242:
+                raise RuntimeError("injected admission failure")
+            return real_add(rid, prompt, max_new)
+
+    real_sched = eng.sched
+    eng.sched = Sched()
+    try:
+        held, release = threading.Event(), threading.Event()
+
+        def hold():
+            with eng.lock:
+                held.set()
+                release.wait(10)
+
+        t = threading.Thread(target=hold)
+        t.start()
+        held.wait(5)
+        from nv_genai_amd.serving.engine_service import StreamHandle
+
+        ok1 = service.submit([8, 9, 10, 11], _params(4))
+        bad = StreamHandle(service)   # a stream on the id the scheduler refuses
+        bad2 = eng.add_request([4, 5, 6], _params(4), request_id=4242, on_token=bad._on_token)
+        bad.request = bad2
+        ok2 = service.submit([12, 13, 14], _params(4))
+        release.set()
+        t.join()
+        assert len(ok1.text()) >= 0 and len(ok2.text()) >= 0
+        with pytest.raises(EngineError, match="injected admission failure"):
+            bad.text()
+        assert bad2.finished and bad2.finish_reason == "error"
+        assert ok1.request.finished and ok1.request.finish_reason == "length"
+        assert ok2.request.finished and ok2.request.finish_reason == "length"
+    finally:
+        eng.sched = real_sched
+
+
+def test_prepared_stream_never_consumed_is_cancelled(service):
+    """The chain server queues a request on the engine before its response body starts
+    (LLMStream.prepare); a client that disconnects before the first chunk never iterates the
+    body, so the response's background task cancels the prepared request instead of letting
+    it decode to max_tokens with nobody reading (chain_server/server.py generate_answer)."""
+    from nv_genai_amd.connectors.local import LocalChatModel
+    from nv_genai_amd.examples.common import LLMStream
+    from nv_genai_amd.observability.tracing import TracingCallback, get_tracer
+
+    llm = LocalChatModel(service, "local", max_tokens=400, temperature=0.1)
+    s = LLMStream(TracingCallback(get_tracer("test")), llm, [{"role": "user", "content": "hello there"}], {})
+    s.prepare()
+    h = s._handle
+    assert h is not None and not h.done.is_set()
+    s.cancel()
+    assert h.done.is_set() and h.request.finish_reason == "abort"
+    deadline = time.time() + 5
+    while service.engine.sched.num_running() + service.engine.sched.num_waiting() and time.time() < deadline:
+        time.sleep(0.02)
+    assert service.engine.sched.num_running() == 0 and service.engine.sched.num_waiting() == 0
+    s.cancel()   # idempotent once done
