@@ -109,6 +109,8 @@ def parse(argv=None):
                     help="prefill / mixed steps eagerly (A/B of the step hipGraphs)")
     ap.add_argument("--graph-token-step", type=int, default=None,
                     help="token-count bucket of the prefill / mixed step graphs (engine default)")
+    ap.add_argument("--no-prefix-cache", dest="prefix_cache", action="store_false",
+                    help="turn the engine's prefix cache off (the A/B of the hit share the JSON reports)")
     ap.add_argument("--allow-shared-devices", action="store_true",
                     help="let more ranks than GPUs share devices (a multi-rank rehearsal on a small box: "
                          "gloo host groups, not a scaling record)")
@@ -138,6 +140,8 @@ def rank_devices(pctx) -> dict:
     from nv_genai_amd.parallel import dist as pd
 
     me = {"rank": pctx.rank, "local_rank": pctx.local_rank, "device": str(pctx.device)}
+    if pd.PLACEMENT is not None:   # CPU / NUMA binding made before the GPU was touched
+        me.update(pd.PLACEMENT.record())
     if pctx.device.type == "cuda":
         pr = torch.cuda.get_device_properties(pctx.device)
         me.update(name=pr.name, pci_bus_id=getattr(pr, "pci_bus_id", None),
@@ -157,6 +161,12 @@ def rank_devices(pctx) -> dict:
         except Exception as e:  # noqa: BLE001
             rec["rccl_version"] = f"unavailable ({e!r})"[:80]
     return rec
+
+
+def progress(msg: str, on: bool = True) -> None:
+    """One progress line on stderr (the JSON result alone goes to stdout)."""
+    if on:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
 def _free_port() -> int:
@@ -279,6 +289,10 @@ def main(argv=None):
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env} ranks were launched")
+    if world_env > 1:
+        from nv_genai_amd.parallel.dist import bind_numa
+
+        bind_numa()   # each rank on its GPU's NUMA node's cores, before any HIP call
     shared = check_devices(args, world_env)
     if args.workload == "agent":
         run_agent(args, world_env, shared)
@@ -325,9 +339,10 @@ def main(argv=None):
                         mixed_prefill_tokens=args.mixed_prefill_tokens,
                         mixed_min_tokens=args.mixed_min_tokens, mixed_max_wait=args.mixed_max_wait,
                         fp8=args.fp8, kv_cache_dtype="fp8" if args.kv_fp8 else "auto",
-                        mixed_graphs=not args.no_step_graphs,
+                        mixed_graphs=not args.no_step_graphs, enable_prefix_caching=args.prefix_cache,
                         **({"graph_token_step": args.graph_token_step} if args.graph_token_step else {}))
     llm = LLMEngine(ecfg, device=dev, pctx=pctx)
+    progress(f"engine up ({time.time() - t_setup:.0f} s)", llm.is_driver)
     from nv_genai_amd.models.config import encoder_config
 
     dim = encoder_config(args.embed_model).hidden
@@ -356,6 +371,7 @@ def main(argv=None):
     else:
         index = FlatIndex(emb.dim, "cosine", dev, capacity=args.index_size)
         index.add_random(args.index_size, seed=1234)
+    progress(f"index up ({time.time() - t_setup:.0f} s)")
     docs = SyntheticDocStore(args.index_size)
     rag = RAGPipeline(llm, emb, index, docs, top_k=args.top_k)
     gen = TextGen(seed=100 + pctx.dp_rank)
@@ -388,7 +404,7 @@ def main(argv=None):
     queued = []                     # (question, arrival time) waiting for a retrieval batch
     clients = [0]                   # clients with a question in the system (retrieving or generating)
 
-    def closed_loop(n_done: int, ramping: bool):
+    def closed_loop(n_done: int, ramping: bool, st_name: str = "step"):
         """Serve until ``n_done`` requests complete; a completed client re-submits at once.
         The client/retrieval host work (prompts for finished retrievals, the next retrieval
         batch on the retrieval stream) runs inside ``llm.step`` between launching the next
@@ -426,6 +442,8 @@ def main(argv=None):
                 if res is not None:
                     out.append(res)
                     clients[0] -= 1
+                    if len(out) % R == 0:
+                        progress(f"{st_name} {len(out) // R}/{n_done // R} ({time.time() - t_setup:.0f} s)")
             if not llm.has_work():
                 host_work(block=True)
         return out
@@ -434,7 +452,7 @@ def main(argv=None):
         for _ in range(args.warmup):
             one_step()
     else:
-        closed_loop(max(1, args.warmup) * R, ramping=True)
+        closed_loop(max(1, args.warmup) * R, ramping=True, st_name="warmup")
     if not args.no_quiet_gc:
         from nv_genai_amd.utils.runtime import quiet_gc
 
@@ -462,7 +480,7 @@ def main(argv=None):
         for _ in range(args.steps):
             results += one_step()
     else:
-        results = closed_loop(args.steps * R, ramping=False)
+        results = closed_loop(args.steps * R, ramping=False, st_name="timed")
     world_barrier()
     elapsed = time.perf_counter() - t0
     llm.stop_followers()
@@ -479,6 +497,7 @@ def main(argv=None):
     lat = sorted(r.latency for r in results)
     ttft = sorted(r.ttft for r in results)
     ptoks = [r.prompt_tokens for r in results]
+    hit_tok = int(sum(r.request.cached_prefix for r in results))
     out_tok = sum(len(r.request.output_ids) for r in results) * replicas
     p50 = statistics.median(lat)
     p95 = lat[min(len(lat) - 1, int(0.95 * len(lat)))]
@@ -545,6 +564,11 @@ def main(argv=None):
                         "launches_by_token_bucket": dict(sorted(llm.bucket_hist.items())),
                         "launches_by_tokens_128": dict(sorted(llm.ntok_hist.items()))},
         "prefix_cache_hit_blocks": int(llm.sched.prefix_hits()),
+        # the timed requests' prompt tokens served from cached KV pages (skipped in prefill):
+        # the share of prefill work the synthetic corpus's shared passages save
+        "prefix_cache": {"enabled": bool(args.prefix_cache),
+                         "hit_tokens": hit_tok, "prompt_tokens_total": sum(ptoks),
+                         "hit_share": round(hit_tok / max(1, sum(ptoks)), 4)},
         **({"kv_page_refs_per_unique": round(llm.stats["kv_page_refs"] / max(1, llm.stats["kv_pages_unique"]), 4)}
            if llm.stats.get("kv_pages_unique") else {}),
         "distinct_docs_retrieved": len({d for r in results for d in r.doc_ids}),

@@ -15,6 +15,15 @@ once. Once ``--warmup`` requests have completed, the next ``--requests`` complet
 timed, with every client still busy (no drain inside the window, as in bench.py). The script
 prints one JSON line with QPS and the p50/p95 latency and TTFT of the timed requests.
 
+``--topology split`` runs the reference's deployed shape instead
+(``deploy/compose/docker-compose-nim-ms.yaml:1-84``, ``common/utils.py:265-316``): the LLM and
+the embedding encoder are served by ``serving/model_server.py`` (OpenAI / NIM API) in a second
+process on the same GPU, and the chain server reaches them over HTTP
+(``APP_LLM_MODELENGINE=nim``, ``APP_EMBEDDINGS_MODELENGINE=nim``); the index stays in the chain
+server. ``--stream-interval`` sets ``NGA_STREAM_INTERVAL`` in the serving processes (1, the
+default: one SSE frame per generated token, as the reference streams). The JSON reports the
+gaps between a stream's SSE frames (p50 / p99 over the timed requests).
+
 Each request follows the reference's path, not bench.py's. The chain server forwards only
 temperature, top_p and max_tokens (utils.py:271-286 quirk), so generation may stop early at an
 EOS token. Output tokens are therefore counted from the streamed text and reported.
@@ -61,13 +70,13 @@ def _server_quantiles(text: str) -> dict:
     return out
 
 
-def _gauges(text: str) -> dict:
+def _gauges(text: str, prefix: str = "chain_server_") -> dict:
     out = {}
     for line in text.splitlines():
-        if line.startswith("chain_server_") and "{" not in line:
+        if line.startswith(prefix) and "{" not in line:
             k, _, v = line.partition(" ")
             try:
-                out[k[len("chain_server_"):]] = float(v)
+                out[k[len(prefix):]] = float(v)
             except ValueError:
                 pass
     return out
@@ -94,7 +103,7 @@ def parse(argv=None):
     ap.add_argument("--embed", default="arctic-embed-l")
     ap.add_argument("--index-size", type=int, default=1_000_000)
     ap.add_argument("--concurrency", type=int, default=256)
-    ap.add_argument("--requests", type=int, default=512)
+    ap.add_argument("--requests", type=int, default=2048)
     ap.add_argument("--warmup", type=int, default=256)
     ap.add_argument("--max-tokens", type=int, default=256)
     ap.add_argument("--ramp-s", type=float, default=6.0,
@@ -103,13 +112,18 @@ def parse(argv=None):
     ap.add_argument("--device", default="", help="engine device for the server ('' = cuda if available)")
     ap.add_argument("--startup-timeout", type=float, default=600.0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--topology", choices=("inprocess", "split"), default="inprocess",
+                    help="split: LLM + encoder in a model-server process, reached over HTTP")
+    ap.add_argument("--stream-interval", type=int, default=1,
+                    help="NGA_STREAM_INTERVAL of the serving processes (1: a frame per token)")
     return ap.parse_args(argv)
 
 
-async def _one(client, url, question, max_tokens):
+async def _one(client, url, question, max_tokens, gaps=None):
     t0 = time.perf_counter()
     ttft = None
     chars = 0
+    last = None
     body = {"messages": [{"role": "user", "content": question}], "use_knowledge_base": True,
             "temperature": 0.2, "top_p": 0.7, "max_tokens": max_tokens}
     async with client.stream("POST", url, json=body) as r:
@@ -121,8 +135,13 @@ async def _one(client, url, question, max_tokens):
             frame = json.loads(line[6:])
             ch = frame["choices"][0]
             text = ch["message"]["content"]
+            now = time.perf_counter()
             if text and ttft is None:
-                ttft = time.perf_counter() - t0
+                ttft = now - t0
+            if text:
+                if last is not None and gaps is not None:
+                    gaps.append(now - last)
+                last = now
             chars += len(text)
             if ch.get("finish_reason") == "[DONE]":
                 break
@@ -135,7 +154,8 @@ async def _load(url, args, questions):
     completed until ``--requests`` more have, while every client is still busy."""
     import httpx
 
-    metrics_url = url.rsplit("/", 1)[0] + "/metrics"
+    metrics_url = args.engine_metrics_url or url.rsplit("/", 1)[0] + "/metrics"
+    prefix = args.engine_metrics_prefix
     limits = httpx.Limits(max_connections=args.concurrency + 8, max_keepalive_connections=args.concurrency + 8)
     results = []
     state = {"done": 0, "t_start": None, "stop": False, "issued": 0}
@@ -148,21 +168,53 @@ async def _load(url, args, questions):
         while not state["stop"]:
             i = state["issued"]
             state["issued"] += 1
-            lat, ttft, chars = await _one(client, url, questions[i % len(questions)], args.max_tokens)
+            g = []
+            lat, ttft, chars = await _one(client, url, questions[i % len(questions)], args.max_tokens, g)
             now = time.perf_counter()
             state["done"] += 1
             if state["done"] == args.warmup:
                 state["t_start"] = now
-                state["m0"] = _gauges((await client.get(metrics_url)).text)
+                state["m0"] = _gauges((await client.get(metrics_url)).text, prefix)
             elif state["t_start"] is not None and not state["stop"]:
                 results.append((lat, ttft, chars, now))
+                state.setdefault("gaps", []).extend(g)
                 if len(results) >= args.requests:
                     state["stop"] = True
-                    state["m1"] = _gauges((await client.get(metrics_url)).text)
+                    state["m1"] = _gauges((await client.get(metrics_url)).text, prefix)
 
     async with httpx.AsyncClient(timeout=httpx.Timeout(600.0), limits=limits) as client:
         await asyncio.gather(*(client_loop(client, k) for k in range(args.concurrency)))
-    return results, state["t_start"], _engine_window(state.get("m0"), state.get("m1"))
+    return results, state["t_start"], _engine_window(state.get("m0"), state.get("m1")), state.get("gaps", [])
+
+
+def _wait_up(proc, url, log_path, timeout):
+    import httpx
+
+    t0 = time.time()
+    while True:
+        if proc.poll() is not None:
+            raise RuntimeError(f"server exited ({proc.returncode}); see {log_path}")
+        try:
+            if httpx.get(url, timeout=5).status_code == 200:
+                return
+        except Exception:  # noqa: BLE001 - not up yet
+            pass
+        if time.time() - t0 > timeout:
+            raise RuntimeError(f"server at {url} did not come up; see {log_path}")
+        time.sleep(1.0)
+
+
+def _embed_dim(preset: str) -> int:
+    from nv_genai_amd.models.config import encoder_config
+
+    return encoder_config(preset).hidden
+
+
+def _pct(xs, q):
+    if not xs:
+        return None
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(q * len(xs)))]
 
 
 def main(argv=None):
@@ -170,38 +222,52 @@ def main(argv=None):
     from nv_genai_amd.utils.synthetic import TextGen
 
     port = _free_port()
-    env = dict(os.environ, EXAMPLE_NAME=args.example, APP_LLM_MODELENGINE="local",
-               APP_EMBEDDINGS_MODELENGINE="local", APP_ENGINE_LLMPRESET=args.llm, APP_ENGINE_EMBEDPRESET=args.embed,
-               APP_INDEX_SYNTHETICDOCS=str(args.index_size), APP_ENGINE_MAXNUMSEQS=str(max(args.concurrency, 1)),
-               APP_ENGINE_DEVICE=args.device, PYTHONPATH=ROOT, LOGLEVEL=os.environ.get("LOGLEVEL", "WARNING"))
-    log_path = os.environ.get("NGA_HTTP_BENCH_LOG", os.path.join(ROOT, "gpurun_out", "http_rag_server.log"))
-    os.makedirs(os.path.dirname(log_path), exist_ok=True)
+    log_dir = os.path.dirname(os.environ.get("NGA_HTTP_BENCH_LOG", os.path.join(ROOT, "gpurun_out", "x")))
+    os.makedirs(log_dir, exist_ok=True)
+    common = dict(os.environ, PYTHONPATH=ROOT, LOGLEVEL=os.environ.get("LOGLEVEL", "WARNING"),
+                  NGA_STREAM_INTERVAL=str(args.stream_interval))
+    env = dict(common, EXAMPLE_NAME=args.example, APP_INDEX_SYNTHETICDOCS=str(args.index_size),
+               APP_ENGINE_MAXNUMSEQS=str(max(args.concurrency, 1)), APP_ENGINE_DEVICE=args.device)
+    procs = []
+    args.engine_metrics_url, args.engine_metrics_prefix = None, "chain_server_"
+    if args.topology == "split":
+        mport = _free_port()
+        mlog_path = os.path.join(log_dir, "http_rag_model_server.log")
+        cmd = [sys.executable, "-m", "nv_genai_amd.serving.model_server", "--llm", args.llm, "--embed", args.embed,
+               "--host", "127.0.0.1", "--port", str(mport), "--max-num-seqs", str(max(args.concurrency, 1))]
+        if args.device:
+            cmd += ["--device", args.device]
+        procs.append(subprocess.Popen(cmd, env=dict(common, LOGLEVEL="warning"), stdout=open(mlog_path, "w"),
+                                      stderr=subprocess.STDOUT))
+        _wait_up(procs[-1], f"http://127.0.0.1:{mport}/v1/health/ready", mlog_path, args.startup_timeout)
+        murl = f"http://127.0.0.1:{mport}/v1"
+        env.update(APP_LLM_MODELENGINE="nim", APP_LLM_SERVERURL=murl, APP_LLM_MODELNAME=args.llm,
+                   APP_EMBEDDINGS_MODELENGINE="nim", APP_EMBEDDINGS_SERVERURL=murl,
+                   APP_EMBEDDINGS_MODELNAME=args.embed, APP_EMBEDDINGS_DIMENSIONS=str(_embed_dim(args.embed)))
+        args.engine_metrics_url = f"http://127.0.0.1:{mport}/metrics"
+        args.engine_metrics_prefix = "model_server_"
+    else:
+        env.update(APP_LLM_MODELENGINE="local", APP_EMBEDDINGS_MODELENGINE="local",
+                   APP_ENGINE_LLMPRESET=args.llm, APP_ENGINE_EMBEDPRESET=args.embed)
+    log_path = os.environ.get("NGA_HTTP_BENCH_LOG", os.path.join(log_dir, "http_rag_server.log"))
     log = open(log_path, "w")
-    server = subprocess.Popen([sys.executable, "-m", "uvicorn", "nv_genai_amd.chain_server.server:app",
-                               "--host", "127.0.0.1", "--port", str(port), "--log-level", "warning"],
-                              env=env, stdout=log, stderr=subprocess.STDOUT)
+    procs.append(subprocess.Popen([sys.executable, "-m", "uvicorn", "nv_genai_amd.chain_server.server:app",
+                                   "--host", "127.0.0.1", "--port", str(port), "--log-level", "warning"],
+                                  env=env, stdout=log, stderr=subprocess.STDOUT))
+    server = procs[-1]
     try:
         import httpx
 
         base = f"http://127.0.0.1:{port}"
         t0 = time.time()
-        while True:
-            if server.poll() is not None:
-                raise RuntimeError(f"chain server exited ({server.returncode}); see {log_path}")
-            try:
-                if httpx.get(base + "/health", timeout=5).status_code == 200:
-                    break
-            except Exception:  # noqa: BLE001 - not up yet
-                pass
-            if time.time() - t0 > args.startup_timeout:
-                raise RuntimeError("chain server did not come up")
-            time.sleep(1.0)
+        _wait_up(server, base + "/health", log_path, args.startup_timeout)
         # first search builds the engines and fills the synthetic collection
         httpx.post(base + "/search", json={"query": "warm up", "top_k": 4}, timeout=args.startup_timeout)
         setup_s = time.time() - t0
+        print(f"[http_rag] servers up ({setup_s:.0f} s), topology {args.topology}", file=sys.stderr, flush=True)
         gen = TextGen(seed=100)
         questions = [gen.question() for _ in range(4096)]
-        results, t_start, engine_window = asyncio.run(_load(base + "/generate", args, questions))
+        results, t_start, engine_window, gaps = asyncio.run(_load(base + "/generate", args, questions))
         server_side = _server_quantiles(httpx.get(base + "/metrics", timeout=30).text)
         t_end = max(r[3] for r in results)
         elapsed = t_end - t_start
@@ -210,10 +276,15 @@ def main(argv=None):
         res = {"metric": "end-to-end RAG QPS + p50 latency through the chain-server REST API (POST /generate, SSE)",
                "value": round(len(results) / elapsed, 4), "unit": "requests/s", "n_gpus": 1,
                "requests": len(results), "concurrency": args.concurrency, "elapsed_s": round(elapsed, 3),
-               "ramp_s": args.ramp_s,
+               "ramp_s": args.ramp_s, "topology": args.topology, "stream_interval": args.stream_interval,
                "p50_latency_ms": round(1e3 * statistics.median(lat), 1),
                "p95_latency_ms": round(1e3 * lat[min(len(lat) - 1, int(0.95 * len(lat)))], 1),
                "p50_ttft_ms": round(1e3 * statistics.median(ttft), 1) if ttft else None,
+               # time between consecutive text frames of one stream (per-token streaming: ~one
+               # engine step; an interval of N steps: ~N steps)
+               "sse_gap_ms": {"p50": round(1e3 * _pct(gaps, 0.5), 2) if gaps else None,
+                              "p99": round(1e3 * _pct(gaps, 0.99), 2) if gaps else None,
+                              "frames": len(gaps) + len(results)},
                "mean_output_chars": round(sum(r[2] for r in results) / len(results), 1),
                "config": {"model": f"{args.llm} + {args.embed}", "index_size": args.index_size,
                           "example": args.example, "max_tokens": args.max_tokens},
@@ -226,12 +297,13 @@ def main(argv=None):
             with open(args.out, "w") as f:
                 f.write(line + "\n")
     finally:
-        server.terminate()
-        try:
-            server.wait(timeout=30)
-        except subprocess.TimeoutExpired:
-            server.kill()
-            server.wait()
+        for p in reversed(procs):
+            p.terminate()
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
 
 
 if __name__ == "__main__":

@@ -76,6 +76,37 @@ class ChatClient:
                     if delta:
                         yield delta
 
+    async def astream(self, messages: Messages, coalesce: bool = False, handle=None, **kw):
+        """The same SSE stream on the caller's event loop (httpx, one pooled client per loop):
+        an async server forwards an upstream model server's tokens without parking a thread
+        per open stream. ``coalesce`` joins the deltas of frames that arrived together."""
+        client = _async_client(self.timeout)
+        body = self._body(messages, True, **kw)
+        async with client.stream("POST", f"{self.base}/chat/completions", json=body,
+                                 headers={**_headers(self.api_key), **self.extra_headers}) as r:
+            if r.status_code != 200:
+                await r.aread()
+                raise RuntimeError(f"chat/completions returned {r.status_code}: {r.text[:200]}")
+            carry = [""]
+            async for chunk in r.aiter_text():
+                parts = []
+                for line in _sse_lines(carry, chunk):
+                    if line == "[DONE]":
+                        if parts:
+                            yield "".join(parts)
+                        return
+                    for ch in json.loads(line).get("choices", []):
+                        delta = ch.get("delta", {}).get("content")
+                        if delta:
+                            parts.append(delta)
+                if not parts:
+                    continue
+                if coalesce:
+                    yield "".join(parts)
+                else:
+                    for p in parts:
+                        yield p
+
     def invoke(self, messages: Messages, **kw) -> str:
         r = requests.post(f"{self.base}/chat/completions", json=self._body(messages, False, **kw),
                           headers={**_headers(self.api_key), **self.extra_headers}, timeout=self.timeout)
@@ -83,6 +114,33 @@ class ChatClient:
         return r.json()["choices"][0]["message"]["content"]
 
     __call__ = invoke
+
+
+def _sse_lines(carry: list, text: str):
+    """Complete ``data:`` payloads in a text chunk of an SSE stream; a partial last line is
+    kept in ``carry[0]`` (one per stream) until the next chunk completes it."""
+    *lines, carry[0] = (carry[0] + text).split("\n")
+    for line in lines:
+        if line.startswith("data:"):
+            yield line[5:].strip()
+
+
+_ASYNC_CLIENTS = {}
+
+
+def _async_client(timeout: float):
+    """One pooled httpx.AsyncClient per event loop (connections are reused across streams)."""
+    import asyncio
+
+    import httpx
+
+    loop = asyncio.get_running_loop()
+    c = _ASYNC_CLIENTS.get(id(loop))
+    if c is None or c[0] is not loop:
+        c = (loop, httpx.AsyncClient(timeout=httpx.Timeout(timeout),
+                                     limits=httpx.Limits(max_connections=4096, max_keepalive_connections=1024)))
+        _ASYNC_CLIENTS[id(loop)] = c
+    return c[1]
 
 
 class EmbeddingsClient:
@@ -110,6 +168,27 @@ class EmbeddingsClient:
 
     def embed_query(self, text: str) -> List[float]:
         return self._embed([text], "query")[0]
+
+    def embed_query_tensor(self, texts: Sequence[str]):
+        """[n, dim] fp32 tensor of a batch of queries in ONE request (the vector store's query
+        batcher coalesces concurrent searches), base64 little-endian fp32 on the wire."""
+        import base64
+
+        import numpy as np
+        import torch
+
+        out = []
+        for i in range(0, len(texts), self.batch_size):
+            body = {"input": list(texts[i:i + self.batch_size]), "model": self.model, "input_type": "query",
+                    "truncate": self.truncate, "encoding_format": "base64"}
+            r = requests.post(f"{self.base}/embeddings", json=body, headers=_headers(self.api_key),
+                              timeout=self.timeout)
+            r.raise_for_status()
+            for d in sorted(r.json()["data"], key=lambda d: d["index"]):
+                e = d["embedding"]
+                out.append(np.frombuffer(base64.b64decode(e), dtype="<f4") if isinstance(e, str)
+                           else np.asarray(e, dtype=np.float32))
+        return torch.from_numpy(np.stack(out).astype(np.float32)) if out else torch.zeros(0, 0)
 
     def embed_documents(self, texts: Sequence[str]) -> List[List[float]]:
         return self._embed(texts, "passage")

@@ -132,6 +132,9 @@ class EngineConfig:
     graph_eager: bool = False
     graph_token_step: int = 256
     max_graph_tokens: int = 0     # 0: mixed_prefill_tokens + max_num_seqs, rounded up
+    # numerics checks: every step's fp32 logits of its sampling rows are copied (before
+    # sampling, inside captured graphs too) to ``LLMEngine.d_tap`` for ``step_hook``
+    logits_tap: bool = False
 
 
 _INERT = Request(id=-1, prompt_ids=[0], params=SamplingParams(temperature=0.0))
@@ -218,6 +221,11 @@ class LLMEngine:
         self.d_pen = dbuf(S, dtype=torch.float32)
         self.d_tok = dbuf(S)
         self.d_lp = dbuf(S, dtype=torch.float32)
+        self.d_tap = dbuf(S, self.mcfg.vocab_size, dtype=torch.float32) if cfg.logits_tap else None
+        # synchronous steps: step_hook(engine, n, tokens) runs after each step with the
+        # sampled tokens of its n rows (d_tap holds their logits when logits_tap); a returned
+        # list replaces the tokens (teacher forcing: later steps consume the forced ids)
+        self.step_hook: Optional[Callable[["LLMEngine", int, List[int]], Optional[List[int]]]] = None
         self.decode_ws = ops.DecodeWorkspace(S, self.model.hq, self.model.hkv, cfg.max_model_len,
                                              dev, cfg.decode_pages_per_part, D=self.model.D,
                                              kv_fp8=cfg.kv_cache_dtype == "fp8") if self.gpu else None
@@ -563,6 +571,8 @@ class LLMEngine:
             toks, lps = self._prefill(n, ntok, nd)
         toks = toks.tolist()
         lps = lps.tolist()
+        if self.step_hook is not None:
+            toks = self.step_hook(self, n, toks) or toks
         self.stats[key] += time.perf_counter() - t0
         now = time.perf_counter()
         for i, (r, s) in enumerate(zip(reqs, smp[:n].tolist())):
@@ -1058,7 +1068,12 @@ class LLMEngine:
             self._up_ev = torch.cuda.Event()
             self._up_ev.record()
 
+    def _tap(self, logits, rows: int) -> None:
+        if self.d_tap is not None and logits is not None:
+            self.d_tap[:rows].copy_(logits[:rows])
+
     def _sample(self, logits, n):
+        self._tap(logits, n)
         if self._beam_rows and logits is not None:
             rows = torch.tensor([i for i, _ in self._beam_rows], device=logits.device)
             k = max(2 * self._beam_of[s].width for _, s in self._beam_rows)
@@ -1196,6 +1211,7 @@ class LLMEngine:
         meta = self._meta("decode", bs, bs, 1, self.cfg.max_model_len)
         h = self.model.forward(self.d_ids[:bs], self.d_pos[:bs], meta)
         logits = self.model.logits(h)
+        self._tap(logits, bs)
         ops.sample(logits, self.d_temp[:bs], self.d_topk[:bs], self.d_topp[:bs],
                    self.d_seed[:bs], self.d_step[:bs], None, None,
                    out_tok=self.d_tok[:bs], out_lp=self.d_lp[:bs])
@@ -1280,6 +1296,7 @@ class LLMEngine:
         S = self.cfg.max_num_seqs
         h = self.model.forward(self.d_ids[:tb], self.d_pos[:tb], self._graph_meta(key), self.d_sidx[:S])
         logits = self.model.logits(h)
+        self._tap(logits, S)
         tok, lp = ops.sample(logits, self.d_temp[:S], self.d_topk[:S], self.d_topp[:S], self.d_seed[:S],
                              self.d_step[:S], None, None, out_tok=self.d_tok[:S], out_lp=self.d_lp[:S])
         if tok.data_ptr() != self.d_tok.data_ptr():   # reference path returns fresh tensors

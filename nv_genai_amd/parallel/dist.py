@@ -67,6 +67,22 @@ class ParallelContext:
 
 
 _CTX = ParallelContext()
+PLACEMENT = None   # utils.affinity.Placement of this rank (multi-rank GPU jobs)
+
+
+def bind_numa(world: Optional[int] = None) -> None:
+    """Bind this rank's threads to its GPU's NUMA node (utils/affinity.py). Must run before the
+    first HIP call of the process — it only counts devices through sysfs — so threads the HIP
+    runtime starts inherit the mask. Once per process; single-rank jobs are left alone."""
+    global PLACEMENT
+    if PLACEMENT is not None:
+        return
+    w, _, local = env_world() if world is None else (world, 0, int(os.environ.get("LOCAL_RANK", "0")))
+    if w <= 1:
+        return
+    from ..utils.affinity import bind_local_rank
+
+    PLACEMENT = bind_local_rank(local, int(os.environ.get("LOCAL_WORLD_SIZE", w)))
 
 
 def get_context() -> ParallelContext:
@@ -90,6 +106,8 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
     """
     global _CTX
     world, rank, local = env_world()
+    if world > 1 and (device is None or device.startswith("cuda")):
+        bind_numa()   # before torch.cuda.is_available() starts the HIP runtime's threads
     use_gpu = torch.cuda.is_available() if device is None else device.startswith("cuda")
     ngpu = torch.cuda.device_count() if use_gpu else 0
     # ranks on THIS node against its GPUs (a multi-node job has world > device_count on

@@ -22,7 +22,6 @@ import base64
 import json
 import logging
 import os
-import struct
 import time
 import uuid
 from typing import Any, Dict, List, Optional, Union
@@ -189,17 +188,20 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
 
     async def _run_stream(handle, rid: str, model: str, obj: str, chat: bool, t0: float):
         first = True
+        created = int(time.time())
+        # every token frame is the same JSON around its text: built once per stream, the delta
+        # spliced in (byte-identical to json.dumps of the chunk, without a dict + encode per token)
+        mark = "\x00"
+        ch = ({"index": 0, "delta": {"role": "assistant", "content": mark}, "finish_reason": None} if chat
+              else {"index": 0, "text": mark, "finish_reason": None})
+        head, tail = ("data: " + json.dumps({"id": rid, "object": obj, "created": created, "model": model,
+                                             "choices": [ch]}) + "\n\n").split(json.dumps(mark))
         try:
             async for delta in handle.aiter():
                 if first:
                     metrics.observe("ttft_seconds", time.perf_counter() - t0)
                     first = False
-                if chat:
-                    ch = {"index": 0, "delta": {"role": "assistant", "content": delta}, "finish_reason": None}
-                else:
-                    ch = {"index": 0, "text": delta, "finish_reason": None}
-                yield "data: " + json.dumps({"id": rid, "object": obj, "created": int(time.time()),
-                                             "model": model, "choices": [ch]}) + "\n\n"
+                yield head + json.dumps(delta) + tail
             fin = {"index": 0, "finish_reason": handle.finish_reason or "stop"}
             fin.update({"delta": {}} if chat else {"text": ""})
             yield "data: " + json.dumps({"id": rid, "object": obj, "created": int(time.time()), "model": model,
@@ -363,8 +365,8 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
         metrics.inc("embed_texts_total", len(texts))
         data = []
         for i, v in enumerate(vecs):
-            if req.encoding_format == "base64":
-                emb: Any = base64.b64encode(struct.pack(f"<{v.numel()}f", *v.tolist())).decode()
+            if req.encoding_format == "base64":   # little-endian fp32, as the OpenAI API encodes it
+                emb: Any = base64.b64encode(v.float().numpy().astype("<f4").tobytes()).decode()
             else:
                 emb = v.tolist()
             data.append({"object": "embedding", "index": i, "embedding": emb})

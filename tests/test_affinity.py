@@ -1,0 +1,81 @@
+"""NUMA placement of one-process-per-GPU ranks (utils/affinity.py) from a fake sysfs tree:
+an 8-GPU, two-socket node (GPUs 0-3 on node 0, 4-7 on node 1), visibility masks, ranks that
+share a node split its cores, and a process whose CPU set excludes the node."""
+import os
+
+from nv_genai_amd.utils import affinity
+
+
+def _node(root, n, props):
+    d = root / "sys/class/kfd/kfd/topology/nodes" / str(n)
+    d.mkdir(parents=True)
+    (d / "properties").write_text("".join(f"{k} {v}\n" for k, v in props.items()))
+
+
+def _tree(tmp_path):
+    root = tmp_path
+    # KFD: two CPU nodes first, then eight GPUs (bus 0x05, 0x15, ... ; HIP's order)
+    _node(root, 0, {"cpu_cores_count": 48, "simd_count": 0})
+    _node(root, 1, {"cpu_cores_count": 48, "simd_count": 0})
+    for g in range(8):
+        bus = 0x05 + 0x10 * g
+        _node(root, 2 + g, {"cpu_cores_count": 0, "simd_count": 1024, "location_id": bus << 8, "domain": 0,
+                            "gpu_id": 1000 + g})
+        pci = root / "sys/bus/pci/devices" / f"0000:{bus:02x}:00.0"
+        pci.mkdir(parents=True)
+        (pci / "numa_node").write_text(f"{0 if g < 4 else 1}\n")
+    for n, cpus in ((0, "0-47,96-143"), (1, "48-95,144-191")):
+        d = root / f"sys/devices/system/node/node{n}"
+        d.mkdir(parents=True)
+        (d / "cpulist").write_text(cpus + "\n")
+    return str(root)
+
+
+def test_cpulist_roundtrip():
+    assert affinity.parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+    assert affinity._ranges([0, 1, 2, 3, 8, 10, 11]) == "0-3,8,10-11"
+
+
+def test_eight_ranks_split_their_sockets(tmp_path):
+    root = _tree(tmp_path)
+    allowed = list(range(192))
+    gpus = affinity.visible_gpus(root, env={})
+    assert [g.pci for g in gpus][:2] == ["0000:05:00.0", "0000:15:00.0"] and len(gpus) == 8
+    seen = set()
+    for r in range(8):
+        pl = affinity.plan(r, 8, root, env={}, allowed=allowed)
+        node = 0 if r < 4 else 1
+        assert pl.numa_node == node and pl.gpu.index == r
+        assert len(pl.cpus) == 24                       # 96 node CPUs over 4 ranks
+        node_cpus = set(affinity.parse_cpulist("0-47,96-143" if node == 0 else "48-95,144-191"))
+        assert set(pl.cpus) <= node_cpus
+        assert not (set(pl.cpus) & seen)                # disjoint between ranks
+        seen |= set(pl.cpus)
+        rec = pl.record()
+        assert rec["numa_node"] == node and rec["cpu_affinity"]
+
+
+def test_visibility_mask_and_foreign_cpuset(tmp_path):
+    root = _tree(tmp_path)
+    # the job sees GPUs 6 and 1 (in that order): local rank 0 is GPU 6 on node 1
+    pl = affinity.plan(0, 2, root, env={"HIP_VISIBLE_DEVICES": "6,1"}, allowed=list(range(192)))
+    assert pl.gpu.pci == "0000:65:00.0" and pl.numa_node == 1 and len(pl.cpus) == 96
+    pl1 = affinity.plan(1, 2, root, env={"HIP_VISIBLE_DEVICES": "6,1"}, allowed=list(range(192)))
+    assert pl1.numa_node == 0
+    # a container limited to node 0's first cores: rank on node 1 is left unbound
+    pl = affinity.plan(5, 8, root, env={}, allowed=list(range(8)))
+    assert pl.cpus == [] and "outside" in pl.reason
+    # no KFD: nothing to do
+    assert affinity.plan(0, 2, str(tmp_path / "nothing"), env={}).reason == "no KFD topology"
+
+
+def test_bind_applies_and_sizes_pools(tmp_path, monkeypatch):
+    root = _tree(tmp_path)
+    calls = []
+    monkeypatch.setattr(os, "sched_setaffinity", lambda pid, cpus: calls.append(sorted(cpus)))
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(192)))
+    env = {}
+    pl = affinity.bind_local_rank(3, 8, root, env=env)
+    assert pl.applied and calls == [pl.cpus] and env["RAYON_NUM_THREADS"] == "24"
+    off = affinity.bind_local_rank(3, 8, root, env={"NGA_NUMA_BIND": "0"})
+    assert not off.applied and len(calls) == 1

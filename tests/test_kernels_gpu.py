@@ -751,3 +751,85 @@ def test_splitk_add_rmsnorm(gpu):
     y = ops.splitk_add_rmsnorm(resid, P, w, 1e-5)
     _close_rows(resid, r_ref, rel=5e-3)
     _close_rows(y, y_ref, rel=1e-2)
+
+
+def _table_cases():
+    """(N, K, shape, M, cfg, split) of every kernel entry of the shipped decode-shape table."""
+    import json
+
+    from nv_genai_amd.ops.skinny import ASSET
+
+    with open(ASSET) as f:
+        doc = json.load(f)
+    out = []
+    for key, ent in doc["table"].items():
+        n, k = (int(v) for v in key.split("x"))
+        for m, c in sorted(ent["by_m"].items(), key=lambda kv: int(kv[0])):
+            if c != "lib":
+                out.append((n, k, ent["shape"], int(m), int(c[0]), int(c[1])))
+    return out
+
+
+def test_skinny_table_production_shapes(gpu):
+    """Every (cfg, split) the shipped table (assets/skinny_gemm_gfx950.json) picks — llama3-8b,
+    llama3-70b at TP=8 (rank shards) and TP=1 — at its own M and real shape, run the way the
+    model runs it WITH its consumer, against fp32: q/k/v K-split slabs summed by the RoPE /
+    KV-write kernel (q, k, v and both caches), o / down slabs summed by the residual add +
+    RMSNorm kernel, gate / up through the SwiGLU epilogue (split 1) or the split-K SwiGLU
+    kernel, the LM head's fp32 logits. Per-row relative error."""
+    cases = _table_cases()
+    assert len(cases) > 100
+    by_shape = {}
+    for c in cases:
+        by_shape.setdefault((c[0], c[1], c[2]), []).append(c[3:])
+    eps, D = 1e-5, 128
+    for (N, K, shape), rows in by_shape.items():
+        torch.manual_seed(N + K)
+        w = _bf(N, K, dev=gpu, scale=0.02)
+        for M, cfg, split in rows:
+            x = _bf(M, K, dev=gpu)
+            ref = x.float() @ w.float().t()
+            tag = f"{shape} {N}x{K} M={M} cfg={cfg} split={split}"
+            if shape == "qkv":
+                Hkv = N // D // 10 if N // D % 10 == 0 else N // D // 6    # 8B: 32+8+8, 70B: 64+8+8 / 8+1+1
+                Hq = N // D - 2 * Hkv
+                P = ops.skinny_gemm(x, w, cfg, split, 1 if split > 1 else 0)
+                pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=gpu)
+                cs = ops.rope_cos_sin(4096, D).to(gpu)
+                nb = (M + 63) // 64 + 2
+                kc, vc = _make_cache(nb, Hkv, D, gpu)
+                slots = torch.randperm(nb * 64, device=gpu)[:M].to(torch.int32)
+                kc2, vc2 = kc.clone(), vc.clone()
+                want = ref.to(torch.bfloat16)
+                ops.rope_cache_(want, pos, cs, slots, kc, vc, Hq, Hkv, D)
+                if split > 1:
+                    got = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+                    ops.rope_cache_(got, pos, cs, slots, kc2, vc2, Hq, Hkv, D, partial=ops.PartialSum(P))
+                else:
+                    got = P
+                    ops.rope_cache_(got, pos, cs, slots, kc2, vc2, Hq, Hkv, D)
+                _close_rows(got, want, width=D, rel=2e-2)
+                _close_rows(kc2.float(), kc.float(), width=D, rel=2e-2)
+                _close_rows(vc2.float().transpose(-1, -2), vc.float().transpose(-1, -2), width=D, rel=2e-2)
+            elif shape in ("o", "down"):
+                resid = _bf(M, N, dev=gpu)
+                nw = (1.0 + 0.1 * torch.randn(N, device=gpu)).to(torch.bfloat16)
+                r32 = resid.float() + ref
+                want = r32 * torch.rsqrt(r32.pow(2).mean(1, keepdim=True) + eps) * nw.float()
+                P = ops.skinny_gemm(x, w, cfg, split, 1)
+                out = ops.splitk_add_rmsnorm(resid, P, nw, eps)
+                _close_rows(resid, r32, rel=1e-2)
+                _close_rows(out, want, rel=2e-2)
+                _close_rows(P.sum(0), ref, rel=1e-4)
+            elif shape == "gate_up":
+                F = N // 2
+                want = torch.nn.functional.silu(ref[:, :F]) * ref[:, F:]
+                got = (ops.skinny_gemm(x, w, cfg, 1, 2) if split == 1
+                       else ops.splitk_swiglu(ops.skinny_gemm(x, w, cfg, split, 1)))
+                _close_rows(got, want, rel=2e-2)
+            else:   # lm_head: fp32 logits straight from the accumulators
+                got = ops.skinny_gemm(x, w, cfg, split, 1)
+                _close_rows(got.sum(0), ref, rel=1e-4)
+            del ref
+        del w
+        torch.cuda.empty_cache()

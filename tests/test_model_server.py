@@ -81,6 +81,10 @@ def test_chat_stream_frames(client):
     assert frames[-1] == "[DONE]"
     objs = [json.loads(f) for f in frames[:-1]]
     assert all(o["object"] == "chat.completion.chunk" for o in objs)
+    # token frames carry one delta each, in the OpenAI chunk form, one id / created per stream
+    assert len({(o["id"], o["created"]) for o in objs}) == 1
+    assert all(o["choices"][0]["delta"]["role"] == "assistant" and o["choices"][0]["finish_reason"] is None
+               for o in objs[:-1])
     assert objs[-1]["choices"][0]["finish_reason"] == "length"
     assert objs[-1]["usage"]["completion_tokens"] == 5
 
@@ -118,9 +122,24 @@ def test_http_connectors_roundtrip(http_url):
     streamed = "".join(chat.stream([("user", "hi")], ignore_eos=True))
     whole = chat.invoke([("user", "hi")], ignore_eos=True)
     assert streamed == whole
+    # the async stream (what an async chain server forwards in the split topology) carries the
+    # same text, per token or coalesced
+    import asyncio
+
+    async def agather(coalesce):
+        return [d async for d in chat.astream([("user", "hi")], coalesce=coalesce, ignore_eos=True)]
+
+    per_tok = asyncio.run(agather(False))
+    assert "".join(per_tok) == whole and len(per_tok) >= 2
+    assert "".join(asyncio.run(agather(True))) == whole
     emb = EmbeddingsClient(http_url, "tiny-embed")
     assert len(emb.embed_query("hello")) == 128
     assert len(emb.embed_documents(["a", "b", "c"])) == 3
+    # batched query embeddings over base64: one request, the per-query vectors
+    import torch
+
+    qt = emb.embed_query_tensor(["hello", "world", "x"])
+    assert qt.shape == (3, 128) and torch.allclose(qt[0], torch.tensor(emb.embed_query("hello")), atol=1e-6)
     rk = RerankClient(http_url, "tiny-rerank").rank("q", ["x", "y"])
     assert len(rk) == 2
 
