@@ -17,6 +17,7 @@ like the reference's ``RetrievalAugmentedGeneration/example``).
 from __future__ import annotations
 
 import asyncio
+import contextlib
 import importlib
 import json
 import importlib.util
@@ -46,7 +47,13 @@ from .sanitize import clean
 logging.basicConfig(level=os.environ.get("LOGLEVEL", "INFO").upper())
 logger = logging.getLogger(__name__)
 
-app = FastAPI(title="nv_genai_amd chain server")
+@contextlib.asynccontextmanager
+async def _lifespan(_app):
+    import_example()
+    yield
+
+
+app = FastAPI(title="nv_genai_amd chain server", lifespan=_lifespan)
 app.add_middleware(CORSMiddleware, allow_origins=["*"], allow_credentials=False,
                    allow_methods=["*"], allow_headers=["*"])
 tracer = get_tracer("chain-server")
@@ -159,8 +166,8 @@ def load_example():
     return cls
 
 
-@app.on_event("startup")
 def import_example() -> None:
+    """Start-up (the app's lifespan): thread pool sizing, example discovery, engines."""
     # every open /generate stream parks a worker thread on its token queue between chunks
     # (sync example generators): size the pool for the serving concurrency, not anyio's 40
     import anyio.to_thread

@@ -493,7 +493,7 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
   // workgroups of 128 (row, head) pairs — one wave per SIMD, measured no faster than the
   // 16x16 kernel's ~500 half-size workgroups standalone and 1.6% slower end to end when it
   // shares the chip with the decode attention of a mixed step (benchmarks/kernel_bench.py
-  // and scripts/gpu_r2_attn_ab.sh). From ~6 such prompts (or long ones) up it is 15-25% faster.
+  // and scripts/archive/gpu_r2_attn_ab.sh). From ~6 such prompts (or long ones) up it is 15-25% faster.
   // Few row blocks (~one per CU, e.g. one ~1.2K-token prompt): the 8-wave split-key form.
   // impl 4 ("alone": a prefill with no decode attention beside it, e.g. a prefill-only step)
   // drops the sharing concern: standalone this kernel wins from one prompt up — 2 x 1,200
