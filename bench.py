@@ -286,6 +286,11 @@ def run_agent(args, world: int, shared: bool = False) -> None:
 def main(argv=None):
     args = parse(argv)
     self_launch(args)
+    if os.environ.get("NGA_STACK_DUMP_S"):
+        # hang diagnosis: every rank dumps all its threads' Python stacks to stderr periodically
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["NGA_STACK_DUMP_S"]), repeat=True)
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env} ranks were launched")
@@ -317,7 +322,7 @@ def main(argv=None):
     world, rank = pctx.world_size, pctx.rank
     assert world == args.gpus, (world, args.gpus)
     replicas = world // tp
-    devices = rank_devices(pctx) if world > 1 else None
+    devices = None   # per-rank run record, collected after the timed region (rank_devices)
     dev = str(pctx.device)
     gpu = pctx.device.type == "cuda"
     if world > 1:
@@ -363,6 +368,7 @@ def main(argv=None):
         llm.run_follower(hooks=hooks)
         pd.all_reduce_max(0.0)
         pd.all_gather_objects(None)
+        rank_devices(pctx)
         pd.destroy()
         return
     emb = EmbeddingEngine(args.embed_model, device=dev, seed=pctx.dp_rank)
@@ -492,6 +498,8 @@ def main(argv=None):
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40))
     t_max = pd.all_reduce_max(elapsed)
     per_replica = pd.all_gather_objects(round(R * args.steps / elapsed, 3))
+    # after the run: the custom collectives' call counts and sticky timeout flag cover it
+    devices = rank_devices(pctx) if world > 1 else None
     n_req = R * args.steps * replicas
     qps = n_req / t_max
     lat = sorted(r.latency for r in results)

@@ -74,7 +74,7 @@ __device__ __forceinline__ uint4 wr_load16(const uint16_t* p) {
 }
 }  // namespace
 
-template <int RT, int NW, int MT, int NS, int EPI>
+template <int RT, int NW, int MT, int NS, int BPF, int EPI>
 __global__ void __launch_bounds__(64 * NW) wreg_gemm_kernel(SkinnyGemmParams P) {
   constexpr int BN = 32 * RT * NW;          // weight rows per block
   constexpr int BM = 32 * MT;               // token rows per block
@@ -159,17 +159,41 @@ __global__ void __launch_bounds__(64 * NW) wreg_gemm_kernel(SkinnyGemmParams P) 
 
   auto compute = [&](int u) {
     const uint16_t* xs = smem + u * STAGE;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      bf16x8 b[MT];
+    if constexpr (BPF) {
+      // token fragments of k-step j + 1 requested before k-step j's MFMAs (one wave per SIMD has
+      // no partner wave to cover the LDS latency)
+      bf16x8 b[2][MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-        b[mt] = as_bf16x8(*reinterpret_cast<const u16x8*>(&xs[wr_swz(mt * 32 + l32, 4 * h + j)]));
+        b[0][mt] = as_bf16x8(*reinterpret_cast<const u16x8*>(&xs[wr_swz(mt * 32 + l32, 4 * h)]));
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        const bf16x8 a = u4_bf(wreg[u][rt * 4 + j]);
+      for (int j = 0; j < 4; ++j) {
+        if (j < 3) {
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = mfma32x16(a, b[mt], acc[rt][mt]);
+          for (int mt = 0; mt < MT; ++mt)
+            b[(j + 1) & 1][mt] =
+                as_bf16x8(*reinterpret_cast<const u16x8*>(&xs[wr_swz(mt * 32 + l32, 4 * h + j + 1)]));
+        }
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const bf16x8 a = u4_bf(wreg[u][rt * 4 + j]);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = mfma32x16(a, b[j & 1][mt], acc[rt][mt]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bf16x8 b[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          b[mt] = as_bf16x8(*reinterpret_cast<const u16x8*>(&xs[wr_swz(mt * 32 + l32, 4 * h + j)]));
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const bf16x8 a = u4_bf(wreg[u][rt * 4 + j]);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = mfma32x16(a, b[mt], acc[rt][mt]);
+        }
       }
     }
   };
@@ -255,35 +279,39 @@ __global__ void __launch_bounds__(64 * NW) wreg_gemm_kernel(SkinnyGemmParams P) 
 // configurations {RT, NW, MT, NS}: RT 32-row weight tiles per wave, NW waves, MT 32-token
 // tiles (BM = 32 MT), NS pipeline steps in flight. IDs continue gemm_skinny.hip's list.
 #define NGA_WREG_CFGS(X) \
-  X(17, 1, 8, 8, 3)      \
-  X(18, 2, 4, 8, 3)      \
-  X(19, 1, 4, 8, 3)      \
-  X(20, 1, 8, 8, 2)      \
-  X(21, 1, 4, 8, 4)      \
-  X(22, 1, 8, 4, 3)      \
-  X(23, 2, 4, 4, 3)      \
-  X(24, 1, 4, 4, 4)      \
-  X(25, 1, 8, 4, 4)      \
-  X(26, 1, 8, 2, 4)      \
-  X(27, 2, 4, 2, 4)      \
-  X(28, 1, 4, 2, 4)      \
-  X(29, 1, 4, 1, 4)      \
-  X(30, 2, 4, 1, 4)      \
-  X(31, 1, 8, 6, 3)      \
-  X(32, 2, 4, 6, 3)      \
-  X(33, 1, 8, 8, 4)      \
-  X(34, 2, 4, 8, 4)
+  X(17, 1, 8, 8, 3, 0)      \
+  X(18, 2, 4, 8, 3, 0)      \
+  X(19, 1, 4, 8, 3, 0)      \
+  X(20, 1, 8, 8, 2, 0)      \
+  X(21, 1, 4, 8, 4, 0)      \
+  X(22, 1, 8, 4, 3, 0)      \
+  X(23, 2, 4, 4, 3, 0)      \
+  X(24, 1, 4, 4, 4, 0)      \
+  X(25, 1, 8, 4, 4, 0)      \
+  X(26, 1, 8, 2, 4, 0)      \
+  X(27, 2, 4, 2, 4, 0)      \
+  X(28, 1, 4, 2, 4, 0)      \
+  X(29, 1, 4, 1, 4, 0)      \
+  X(30, 2, 4, 1, 4, 0)      \
+  X(31, 1, 8, 6, 3, 0)      \
+  X(32, 2, 4, 6, 3, 0)      \
+  X(33, 1, 8, 8, 4, 0)      \
+  X(34, 2, 4, 8, 4, 0)      \
+  X(35, 1, 4, 8, 3, 1)      \
+  X(36, 2, 4, 8, 3, 1)      \
+  X(37, 1, 4, 8, 4, 1)      \
+  X(38, 2, 4, 8, 4, 1)
 
 int wreg_gemm_cfg_count() {
   int n = 0;
-#define NGA_COUNT(ID, RT, NW, MT, NS) ++n;
+#define NGA_COUNT(ID, RT, NW, MT, NS, BPF) ++n;
   NGA_WREG_CFGS(NGA_COUNT)
 #undef NGA_COUNT
   return n;
 }
 
 bool wreg_gemm_cfg_info(int cfg, int* info) {
-#define NGA_INFO(ID, RT, NW, MT, NS) \
+#define NGA_INFO(ID, RT, NW, MT, NS, BPF) \
   if (cfg == ID) {                   \
     info[0] = 32 * RT * NW;          \
     info[1] = 32 * MT;               \
@@ -300,13 +328,13 @@ bool wreg_gemm_cfg_info(int cfg, int* info) {
 
 bool launch_wreg_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t stream) {
   const int nblk = p.nN * p.nM * p.split;
-#define NGA_LAUNCH(ID, RT, NW, MT, NS)                                                          \
+#define NGA_LAUNCH(ID, RT, NW, MT, NS, BPF)                                                        \
   if (cfg == ID) {                                                                              \
     if (nblk == 0) return true;                                                                 \
     const dim3 grid(nblk), block(64 * NW);                                                      \
-    if (epi == 0) wreg_gemm_kernel<RT, NW, MT, NS, 0><<<grid, block, 0, stream>>>(p);           \
-    else if (epi == 1) wreg_gemm_kernel<RT, NW, MT, NS, 1><<<grid, block, 0, stream>>>(p);      \
-    else wreg_gemm_kernel<RT, NW, MT, NS, 2><<<grid, block, 0, stream>>>(p);                    \
+    if (epi == 0) wreg_gemm_kernel<RT, NW, MT, NS, BPF, 0><<<grid, block, 0, stream>>>(p);           \
+    else if (epi == 1) wreg_gemm_kernel<RT, NW, MT, NS, BPF, 1><<<grid, block, 0, stream>>>(p);      \
+    else wreg_gemm_kernel<RT, NW, MT, NS, BPF, 2><<<grid, block, 0, stream>>>(p);                    \
     return true;                                                                                \
   }
   NGA_WREG_CFGS(NGA_LAUNCH)

@@ -22,6 +22,7 @@ import itertools
 import logging
 import os
 import random
+import sys
 import threading
 import time
 from dataclasses import dataclass, field
@@ -43,6 +44,7 @@ from .beam import BeamGroup, advance
 
 log = logging.getLogger(__name__)
 _KV_SHARE_STATS = os.environ.get("NGA_KV_SHARE_STATS", "0") == "1"
+_TRACE_CAPTURE = os.environ.get("NGA_TRACE_CAPTURE", "0") == "1"   # per-rank timings of lazy captures
 
 
 @dataclass
@@ -1310,7 +1312,11 @@ class LLMEngine:
         tb, ndb = key
         dev = self.device
         t0 = time.perf_counter()
+        trace = _TRACE_CAPTURE and (lambda m: print(f"[capture rank{self.p.rank} {key}] {m} "
+                                                    f"+{time.perf_counter() - t0:.3f}s", file=sys.stderr, flush=True))
         torch.cuda.synchronize(dev)
+        if trace:
+            trace("drained")
         keep = (self.d_tok.clone(), self.d_lp.clone())
         self.d_ids[:tb].zero_()
         self.d_pos[:tb].zero_()
@@ -1324,12 +1330,17 @@ class LLMEngine:
         stream.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(stream):
             self._graph_body(key)
+            if trace:
+                stream.synchronize()
+                trace("warm-up done")
             g = torch.cuda.CUDAGraph()
             with capture_guard(), torch.cuda.graph(g, pool=self._graph_pool, stream=stream,
                                                    capture_error_mode="thread_local"):
                 self._graph_body(key)
         torch.cuda.current_stream(dev).wait_stream(stream)
         torch.cuda.synchronize(dev)
+        if trace:
+            trace("captured")
         self._graph_pool = g.pool()
         self.d_tok.copy_(keep[0])
         self.d_lp.copy_(keep[1])

@@ -197,6 +197,10 @@ def status() -> dict:
     counts of the Python entry point (calls recorded into a hipGraph count once, at capture)."""
     s = dict(_STATUS)
     if _LAST is not None:
+        try:   # the kernels' sticky barrier-timeout flag (0: every call met its peers in time)
+            s["timeout_flag"] = _LAST.error()
+        except Exception as e:  # noqa: BLE001
+            s["timeout_flag"] = repr(e)[:80]
         s["algo_counts"] = {"one_shot": _LAST.algo_counts.get(ALGO_ONE_SHOT, 0),
                             "two_shot": _LAST.algo_counts.get(ALGO_TWO_SHOT, 0)}
     return s
