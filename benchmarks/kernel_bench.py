@@ -105,10 +105,10 @@ def main():
             o = torch.empty_like(r)
             res = {}
             for tag, env in (("wave", "1"), ("row_block", "0")):
-                os.environ["NGA_RMSNORM_WAVE"] = env
+                ops.kernels().set_kernel_form("rmsnorm_wave", int(env))
                 us = timeit(lambda: ops.add_rmsnorm(r, dlt, w, 1e-5, out=o))
                 res[tag] = {"us": round(us, 1), "TBps": round(4 * T * 4096 * 2 / us / 1e6, 2)}
-            os.environ.pop("NGA_RMSNORM_WAVE")   # back to the default (row-per-block)
+            ops.kernels().set_kernel_form("rmsnorm_wave", 0)   # back to the default (row-per-block)
             out[f"add_rmsnorm_{T}x4096"] = res
         if args.only == "norm":
             print(json.dumps(out))
@@ -135,12 +135,12 @@ def main():
             us = timeit(lambda: ops.score(Q, X, None, 1.0))
             us_all = timeit(lambda: ops.topk(ops.score(Q, X, None, 1.0), 4))
             us_f = timeit(lambda: ops.search_topk(Q, X, bias, 1.0, 4))
-            os.environ["NGA_SEARCH_DMA"] = "0"    # the register-load form
+            ops.kernels().set_kernel_form("search_dma", 0)    # the register-load form
             us_reg = timeit(lambda: ops.search_topk(Q, X, bias, 1.0, 4))
-            os.environ["NGA_SEARCH_NT"] = "1"
+            ops.kernels().set_kernel_form("search_nt", 1)
             us_nt = timeit(lambda: ops.search_topk(Q, X, bias, 1.0, 4))
-            os.environ.pop("NGA_SEARCH_NT")
-            os.environ.pop("NGA_SEARCH_DMA")
+            ops.kernels().set_kernel_form("search_nt", 0)
+            ops.kernels().set_kernel_form("search_dma", 1)
             out[f"search_1Mx1024_q{nq}"] = {"reg_us": round(us_reg, 1),
                                              "reg_TBps": round(N * Dx * 2 / us_reg / 1e6, 2),
                                              "fused_nt_us": round(us_nt, 1),
@@ -156,9 +156,9 @@ def main():
         for nq in (8, 64):
             Q = torch.nn.functional.normalize(torch.randn(nq, Dx, device=dev), dim=1).to(torch.bfloat16)
             us_f = timeit(lambda: ops.search_topk(Q, Xs, bs, 1.0, 4))
-            os.environ["NGA_SEARCH_DMA"] = "0"
+            ops.kernels().set_kernel_form("search_dma", 0)
             us_reg = timeit(lambda: ops.search_topk(Q, Xs, bs, 1.0, 4))
-            os.environ.pop("NGA_SEARCH_DMA")
+            ops.kernels().set_kernel_form("search_dma", 1)
             out[f"search_shard1.25Mx1024_q{nq}"] = {"reg_us": round(us_reg, 1), "fused_us": round(us_f, 1),
                                                     "fused_TBps": round(Xs.numel() * 2 / us_f / 1e6, 2)}
         del Xs, bs
@@ -171,9 +171,9 @@ def main():
         for nq in (1, 8, 64):
             Q = torch.nn.functional.normalize(torch.randn(nq, Dx, device=dev), dim=1)
             us_i = timeit(lambda: ivf.search(Q, 4))
-            os.environ["NGA_SEARCH_DMA"] = "0"
+            ops.kernels().set_kernel_form("search_dma", 0)
             us_ir = timeit(lambda: ivf.search(Q, 4))
-            os.environ.pop("NGA_SEARCH_DMA")
+            ops.kernels().set_kernel_form("search_dma", 1)
             out[f"ivf_1Mx1024_nlist64_nprobe16_q{nq}"] = {"us": round(us_i, 1), "reg_us": round(us_ir, 1)}
         del ivf
         del X
@@ -223,10 +223,10 @@ def main():
             res = {"1": [], "2": []}
             for _ in range(3):
                 for form in ("1", "2"):
-                    os.environ["NGA_DECODE_DMA"] = form
+                    ops.kernels().set_kernel_form("decode_dma", int(form))
                     res[form].append(round(timeit_graph(lambda: ops.decode_attention(
                         qx, kcx, vcx, btx, ctxx, Hq, Hkv, 8192, D ** -0.5, ws=wsx)), 1))
-            os.environ.pop("NGA_DECODE_DMA")
+            ops.kernels().set_kernel_form("decode_dma", 1)
             out[f"decode_{Bs}x1400_dma_forms"] = {
                 "whole_page_us": res["1"], "ring_us": res["2"],
                 "TBps_whole_ring": [round(Bs * L * Hkv * D * 4 / min(res[f]) / 1e6, 2) for f in ("1", "2")]}
@@ -300,9 +300,9 @@ def main():
                 ws = ops.DecodeWorkspace(Bs, Hq_, Hkv_, 8192, torch.device(dev), ppp)
                 fn = lambda: ops.decode_attention(q3, kc3, vc3, bt3, ctx3, Hq_, Hkv_, 8192, D ** -0.5, ws=ws)  # noqa: E731
                 for kern in ("0", "1"):
-                    os.environ["NGA_DECODE_DMA"] = kern
+                    ops.kernels().set_kernel_form("decode_dma", int(kern))
                     res[f"{'dma' if kern == '1' else 'reg'}_ppp{ppp}"] = round(timeit_graph(fn), 1)
-                os.environ.pop("NGA_DECODE_DMA")
+                ops.kernels().set_kernel_form("decode_dma", 1)
             best = min(res, key=res.get)
             out[f"decode_small_{name}"] = {"graph_us": res, "best": best,
                                            "best_TBps": round(Bs * L * Hkv_ * D * 4 / res[best] / 1e6, 2)}

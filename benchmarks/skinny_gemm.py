@@ -72,7 +72,7 @@ def main():
             res = []
             packed = {}
             for c in cfgs:
-                BN, BM, WN, WM, NS = info[c][:5]
+                BN, BM, WN, WM, NS = info[c]
                 nn = (Nout // (BN // 2)) if epi_full == 2 else -(-N // BN)
                 if epi_full == 2 and Nout % (BN // 2):
                     continue

@@ -2,6 +2,7 @@
 // Every entry point validates dtype / device / shape / contiguity against what its kernel
 // and launch grid assume before launching (a malformed launch on the GPU box can fault the
 // device), and launches on PyTorch's current HIP stream so calls are hipGraph-capturable.
+#include <atomic>
 #include <torch/extension.h>
 
 #include <cstdlib>
@@ -246,9 +247,9 @@ void moe_combine(Tensor y, Tensor inv, int64_t T, int64_t k, Tensor out) {
 
 // ------------------------------------------------------------------ decode-shape GEMM
 std::vector<int64_t> skinny_cfg(int64_t cfg) {
-  int info[6];
+  int info[5];
   nga::skinny_gemm_cfg_info((int)cfg, info);
-  return {info[0], info[1], info[2], info[3], info[4], info[5]};
+  return {info[0], info[1], info[2], info[3], info[4]};
 }
 
 // epi 0: out [M, N] bf16 = x @ w^T; 1: out fp32 [split, M, N] partial slabs; 2: out [M, F] bf16 =
@@ -268,10 +269,9 @@ void skinny_gemm(Tensor out, Tensor x, Tensor w, int64_t epi, int64_t split, int
   TORCH_CHECK(K % 64 == 0 && K >= 64, "skinny_gemm: K must be a multiple of 64");
   TORCH_CHECK(wpack || w.size(1) == K, "skinny_gemm: K must match");
   TORCH_CHECK(M >= 1 && M <= 65536, "skinny_gemm: 1 <= M <= 65536");
-  int info[6];
+  int info[5];
   nga::skinny_gemm_cfg_info((int)cfg, info);
   TORCH_CHECK(info[0] > 0, "skinny_gemm: unknown tile configuration ", cfg);
-  TORCH_CHECK(info[5] == 0 || (!wpack && !xpack), "skinny_gemm: the weight-in-registers tiles take plain x / w");
   const int BN = info[0], BM = info[1];
   TORCH_CHECK(epi >= 0 && epi <= 2, "skinny_gemm: epi 0, 1 or 2");
   TORCH_CHECK(split >= 1 && split <= K / 64 && (epi == 1 || split == 1), "skinny_gemm: 1 <= split <= K / 64 (> 1 only for epi 1)");
@@ -285,11 +285,7 @@ void skinny_gemm(Tensor out, Tensor x, Tensor w, int64_t epi, int64_t split, int
   p.krot = krot ? 1 : 0;
   p.wpack = wpack ? 1 : 0;
   p.xpack = xpack ? 1 : 0;
-  static const int wnt_env = [] {   // NGA_SKINNY_WNT=1: non-temporal weight DMA (A/B)
-    const char* e = getenv("NGA_SKINNY_WNT");
-    return e ? atoi(e) : 0;
-  }();
-  p.wnt = wnt_env;
+  p.wnt = 0;   // non-temporal weight DMA: measured within noise (NGA_SKINNY_WNT, removed)
   if (xpack) {
     const int64_t nm = (M + info[1] - 1) / info[1];
     TORCH_CHECK(x.size(1) == 64 && x.size(0) == nm * (K / 64) * info[1],
@@ -862,9 +858,52 @@ std::function<void(A...)> checked(const char* name, void (*f)(A...)) {
 
 }  // namespace
 
+
+// ---- kernel-form registry (kernels.h): environment read once, then set explicitly
+namespace nga {
+namespace {
+struct FormSpec {
+  const char* name;
+  const char* env;
+  int dflt;
+};
+const FormSpec kForms[KF_COUNT] = {
+    {"decode_dma", "NGA_DECODE_DMA", 1}, {"decode_nt", "NGA_DECODE_NT", 0},
+    {"rmsnorm_wave", "NGA_RMSNORM_WAVE", 0}, {"search_dma", "NGA_SEARCH_DMA", 1},
+    {"search_nt", "NGA_SEARCH_NT", 0}, {"prefill_v1", "NGA_PREFILL_V1", 0},
+    {"prefill_ks", "NGA_PREFILL_KS", 0}};
+std::atomic<int>* forms() {
+  static std::atomic<int> v[KF_COUNT];
+  static const bool init = [] {
+    for (int i = 0; i < KF_COUNT; ++i) {
+      const char* e = std::getenv(kForms[i].env);
+      v[i].store(e && e[0] ? std::atoi(e) : kForms[i].dflt);
+    }
+    return true;
+  }();
+  (void)init;
+  return v;
+}
+}  // namespace
+int kernel_form(KernelForm f) { return forms()[f].load(std::memory_order_relaxed); }
+void set_kernel_form(KernelForm f, int value) { forms()[f].store(value); }
+const char* kernel_form_name(KernelForm f) { return kForms[f].name; }
+}  // namespace nga
+
+namespace {
+int form_id(const std::string& name) {
+  for (int i = 0; i < nga::KF_COUNT; ++i)
+    if (name == nga::kernel_form_name((nga::KernelForm)i)) return i;
+  TORCH_CHECK(false, "unknown kernel form ", name);
+  return -1;
+}
+}  // namespace
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "nv_genai_amd gfx950 HIP kernels";
   m.def("debug_sync", &debug_sync);
+  m.def("kernel_form", [](const std::string& n) { return (int64_t)nga::kernel_form((nga::KernelForm)form_id(n)); });
+  m.def("set_kernel_form", [](const std::string& n, int64_t v) { nga::set_kernel_form((nga::KernelForm)form_id(n), (int)v); });
   m.def("rmsnorm", checked("rmsnorm", &rmsnorm));
   m.def("add_rmsnorm", checked("add_rmsnorm", &add_rmsnorm));
   m.def("layernorm", checked("layernorm", &layernorm));

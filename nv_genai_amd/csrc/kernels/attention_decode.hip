@@ -704,11 +704,8 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
   dim3 grid(num_seqs, Hkv, nparts);
   dim3 g2(num_seqs, Hq);
   if (!kv_fp8) k_scale = v_scale = 1.f;
-  // A/B knob: non-temporal KV loads (each page is streamed once per step)
-  static const int nt = [] {
-    const char* e = getenv("NGA_DECODE_NT");
-    return e && atoi(e) ? 1 : 0;
-  }();
+  // A/B form: non-temporal KV loads (each page is streamed once per step)
+  const int nt = kernel_form(KF_DECODE_NT) ? 1 : 0;
   const float sc = scale * k_scale;
 #define NGA_DEC(DD, CT)                                                                        \
   decode_attn_kernel<DD, CT><<<grid, 256, 0, stream>>>(                                        \
@@ -726,11 +723,9 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
     // register kernel's ~2,048 (graph replay, profiles/r3_search_dma/kb_decode_small_sweep.json):
     // 16 x 1,400 22.1 -> 18.6 us (2 partitions), 64 x 1,400 81.5 -> 59.6 us (1 partition),
     // 4 x 1,400 9.6 -> 8.1 us, the 70B TP=8 rank's 32 x 1,400 9.9 -> 8.8 us; 256 x 1,400
-    // 257 -> 224 us (profiles/r3_dma). A/B knob: NGA_DECODE_DMA=0 / 1 forces the register /
-    // DMA kernel.
-    // NGA_DECODE_DMA=2: the half-page ring form of the DMA kernel.
-    const char* dma_e = getenv("NGA_DECODE_DMA");   // read per call (kernel_bench sweeps it)
-    const int dma = dma_e == nullptr ? 1 : atoi(dma_e);
+    // 257 -> 224 us (profiles/r3_dma). Form KF_DECODE_DMA (NGA_DECODE_DMA): 0 / 1 forces the
+    // register / DMA kernel, 2 the half-page ring form of the DMA kernel.
+    const int dma = kernel_form(KF_DECODE_DMA);
     if (kv_fp8) NGA_DEC(128, uint8_t);
     else if (dma && (pages + nparts - 1) / nparts <= DMA_MAX_PAGES) {
       if (dma == 2)

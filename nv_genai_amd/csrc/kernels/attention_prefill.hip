@@ -341,14 +341,10 @@ void launch_prefill_attention(const PrefillParams& p, int num_seqs, int max_q_le
   if (num_seqs == 0 || max_q_len == 0) return;
   // large paged head_dim-128 prefills run the 32x32-MFMA kernel (attention_prefill_v2.hip)
   if (launch_prefill_attention_v2(p, num_seqs, max_q_len, D, paged, causal, stream)) return;
-  // 64-row query tiles. The 128-row variant (two column groups per wave) halves the LDS
-  // fragment traffic per MFMA but needs ~300 VGPR+AGPR, i.e. one wave per SIMD, and measured
-  // 1.4-1.5x slower on MI355X (benchmarks/kernel_bench.py); NGA_PREFILL_NCG=2 selects it.
-  static const int forced = [] {
-    const char* e = getenv("NGA_PREFILL_NCG");
-    return e ? atoi(e) : 0;
-  }();
-  const int ncg = forced == 2 ? 2 : 1;
+  // 64-row query tiles (a 128-row variant with two column groups per wave halved the LDS
+  // fragment traffic per MFMA but needed ~300 VGPR+AGPR — one wave per SIMD — and measured
+  // 1.4-1.5x slower on MI355X; removed)
+  const int ncg = 1;
   PrefillParams pp = p;
   pp.ntiles = (max_q_len + 64 * ncg - 1) / (64 * ncg);
   const int64_t total = (int64_t)pp.ntiles * p.Hq * num_seqs;

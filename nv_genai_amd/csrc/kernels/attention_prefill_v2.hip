@@ -71,25 +71,16 @@ constexpr int V2_TILE = 64 * 128;       // elements of one K (or V^T) tile: 16 K
 
 // One row block: query rows [RW qb, RW qb + RW) of sequence b, head group hg (its HPW heads
 // share each K / V^T tile), over the row block's whole causal key range.
-// Measured (profiles/r4_prefill/): neither form below beats the shipped 4-wave DMA form — at
-// 4 x 4,096 602.7 us (STG = 1) and 603-625 us (NWV = 8) vs 602-608 us; the diagnostic
-// ablations show the DMA's landing time is not exposed (V issued a whole iteration early:
-// 596 us; no vmcnt wait at all: 594 us). Both stay selectable (impl 5 / 6) for A/B runs.
-//
-// NWV = 8 (one group of 8 waves, KS = 1): twice the query rows share every K / V^T tile —
-// 2 x 32 rows of each of the 4 heads of a GQA group — halving the L2 -> CU tile traffic per
-// FLOP (at 4 x 4,096 the 4-wave form streams ~7 TB/s of tile re-reads from L2); one workgroup
-// per CU, still two waves per SIMD, the same 64 KiB of LDS.
-// STG = 1 (register staging, KS = 1): each wave loads its pieces of K(i+1) and V^T(i+1) into
-// VGPRs at the top of iteration i (same per-lane source addresses as the DMA) and writes them
-// to LDS with ds_write_b128 — K before the mid-iteration barrier, V^T right after it — so both
-// tiles have half an iteration or more in flight and no LDS-DMA runs beside the fragment reads.
-template <bool CAUSAL, int HPW, int ABL, int KS, int RA = 8, int NWV = 4, int STG = 0>
+// Measured and removed (profiles/r4_prefill/): an 8-wave group sharing every tile (2 x 32 rows
+// of each of 4 GQA heads: half the L2 -> CU tile re-reads) 603-625 us and register-staged
+// tiles (ds_write_b128 of K / V^T around the mid-iteration barrier) 602.7 us, against 602-608 us
+// for this 4-wave DMA form at 4 x 4,096; the diagnostic ablations show the DMA's landing time
+// is not exposed (V issued a whole iteration early: 596 us; no vmcnt wait at all: 594 us).
+template <bool CAUSAL, int HPW, int ABL, int KS, int RA = 8>
 __device__ __forceinline__ void v2_row_block(const PrefillParams& P, uint16_t* smem, int b, int hg, int qb) {
   constexpr int D = 128, KT = 64;
   constexpr int TILE = V2_TILE;
-  static_assert(NWV == 4 || (NWV == 8 && KS == 1), "8-wave groups only without the key split");
-  static_assert(STG == 0 || KS == 1, "register staging only without the key split");
+  constexpr int NWV = 4;                // waves per wave group
   constexpr int RB = NWV / HPW;         // 32-row query blocks per workgroup
   constexpr int RW = 32 * RB;           // query rows per workgroup
   constexpr int NI = 16 / NWV;          // DMA instructions per wave per 16-KiB tile
@@ -170,21 +161,6 @@ __device__ __forceinline__ void v2_row_block(const PrefillParams& P, uint16_t* s
 #pragma unroll
     for (int i = 0; i < NI; ++i)
       glds16(reinterpret_cast<const uint16_t*>(src + voff[i]), dst + (NI * w + i) * 512);
-  };
-  [[maybe_unused]] u16x8 kst[NI], vst[NI];
-  auto load_k = [&](int t) {
-    const char* src = reinterpret_cast<const char*>(P.kc + page(t));
-#pragma unroll
-    for (int i = 0; i < NI; ++i) kst[i] = *reinterpret_cast<const u16x8*>(src + koff[i]);
-  };
-  auto load_v = [&](int t) {
-    const char* src = reinterpret_cast<const char*>(P.vc + page(t));
-#pragma unroll
-    for (int i = 0; i < NI; ++i) vst[i] = *reinterpret_cast<const u16x8*>(src + voff[i]);
-  };
-  auto write_st = [&](const u16x8 (&st)[NI], uint16_t* dst) {
-#pragma unroll
-    for (int i = 0; i < NI; ++i) *reinterpret_cast<u16x8*>(dst + (NI * w + i) * 512 + lane * 8) = st[i];
   };
   auto sync_tiles = [&]() {
     // this wave's DMA has landed; the barrier makes every wave's visible and guarantees every
@@ -321,16 +297,8 @@ __device__ __forceinline__ void v2_row_block(const PrefillParams& P, uint16_t* s
   auto iter = [&](int i, int par, bool first) {
     const int t = tile_of(i);
     const uint16_t* kc_ = kbuf + par * TILE;
-    if constexpr (STG) {
-      __syncthreads();   // K(i), V(i) written by every wave; iteration i-1's reads are done
-      if (i + 1 < nt) {
-        load_k(t + 1);
-        load_v(t + 1);
-      }
-    } else {
-      sync_tiles();   // K(i), V(i) landed; every wave is done with iteration i-1
-    }
-    if constexpr (ABL != 1 && ABL != 4 && !STG)
+    sync_tiles();   // K(i), V(i) landed; every wave is done with iteration i-1
+    if constexpr (ABL != 1 && ABL != 4)
       if (i + 1 < nt) issue_k(t + KS, kbuf + (par ^ 1) * TILE);
     if constexpr (ABL == 8)
       if (i + 1 < nt) issue_v(t + KS, vbuf + (par ^ 1) * TILE);
@@ -342,27 +310,14 @@ __device__ __forceinline__ void v2_row_block(const PrefillParams& P, uint16_t* s
         stage(Sb, vbuf + (par ^ 1) * TILE, 1, Sa, kc_, 0, t, false);
       }
     }
-    if constexpr (STG) {
-      if (i + 1 < nt) write_st(kst, kbuf + (par ^ 1) * TILE);   // K(i-1)'s buffer: free since the top
-      __syncthreads();                                             // V(i-1) is free
-      if (i + 1 < nt) write_st(vst, vbuf + (par ^ 1) * TILE);
-    } else {
-      if constexpr (ABL != 4) __builtin_amdgcn_s_barrier();   // V(i-1) is free
-    }
-    if constexpr (ABL != 1 && ABL != 4 && ABL != 8 && !STG)
+    if constexpr (ABL != 4) __builtin_amdgcn_s_barrier();   // V(i-1) is free
+    if constexpr (ABL != 1 && ABL != 4 && ABL != 8)
       if (i + 1 < nt) issue_v(t + KS, vbuf + (par ^ 1) * TILE);
     if constexpr (ABL != 2) stage(Sa, vbuf + par * TILE, 0, Sb, kc_, 1, t, KS > 1 && t >= n_tiles);
   };
 
-  if constexpr (STG) {
-    load_k(tile_of(0));
-    load_v(tile_of(0));
-    write_st(kst, kbuf);
-    write_st(vst, vbuf);
-  } else {
-    issue_k(tile_of(0), kbuf);
-    issue_v(tile_of(0), vbuf);
-  }
+  issue_k(tile_of(0), kbuf);
+  issue_v(tile_of(0), vbuf);
   iter(0, 0, true);
   for (int i = 1; i < nt; i += 2) {
     iter(i, 1, false);
@@ -431,8 +386,8 @@ __device__ __forceinline__ void v2_row_block(const PrefillParams& P, uint16_t* s
 //   P.n_items on the device): a fixed grid walks items it = blockIdx.x + k gridDim.x with
 //   head group it % NG. The grid does not depend on the step, so a hipGraph captures it once
 //   and each replay reads that step's list (engine mixed-step graphs).
-template <bool CAUSAL, int HPW, int ABL = 0, int KS = 1, int RA = 8, int NWV = 4, int STG = 0>
-__global__ void __launch_bounds__(64 * NWV * KS, (KS == 1 && NWV == 4) ? 2 : 1) prefill_attn_v2_kernel(PrefillParams P) {
+template <bool CAUSAL, int HPW, int ABL = 0, int KS = 1, int RA = 8>
+__global__ void __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) prefill_attn_v2_kernel(PrefillParams P) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[KS * 4 * V2_TILE + 2 * V2_MAX_TILES];
   const int G = P.Hq / P.Hkv;
   const int ngrp = G / HPW;
@@ -442,7 +397,7 @@ __global__ void __launch_bounds__(64 * NWV * KS, (KS == 1 && NWV == 4) ? 2 : 1) 
     for (int it = blockIdx.x; it < total; it += gridDim.x) {
       __syncthreads();   // the previous item's waves are done with the block-id table
       const int k = it / NG;
-      v2_row_block<CAUSAL, HPW, ABL, KS, RA, NWV, STG>(P, smem, P.items[2 * k], it % NG, P.items[2 * k + 1]);
+      v2_row_block<CAUSAL, HPW, ABL, KS, RA>(P, smem, P.items[2 * k], it % NG, P.items[2 * k + 1]);
     }
     return;
   }
@@ -454,29 +409,16 @@ __global__ void __launch_bounds__(64 * NWV * KS, (KS == 1 && NWV == 4) ? 2 : 1) 
   const int qb = P.ntiles - 1 - L % P.ntiles;
   const int hg = (L / P.ntiles) % NG;
   const int b = L / (P.ntiles * NG);
-  v2_row_block<CAUSAL, HPW, ABL, KS, RA, NWV, STG>(P, smem, b, hg, qb);
+  v2_row_block<CAUSAL, HPW, ABL, KS, RA>(P, smem, b, hg, qb);
 }
-
-// the 8-wave form by default from this many 64-row workgroups (one per CU, ~4 waves of them)
-static bool v2_nwv8_default(int64_t total8) { return false && total8 >= 1024; }
 
 bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q_len, int D,
                                  bool paged, bool causal, hipStream_t stream) {
-  static const bool disabled = [] {
-    const char* e = getenv("NGA_PREFILL_V1");
-    return e && atoi(e) != 0;
-  }();
+  const bool disabled = kernel_form(KF_PREFILL_V1) != 0;
   if (p.impl == 1 || ((p.impl == 0 || p.impl == 4) && disabled) || D != 128 || !paged || p.kv_fp8 ||
       p.max_blocks > V2_MAX_TILES)
     return false;
-  static const int ks_env = [] {   // NGA_PREFILL_KS=1|2 forces the wave-group count (A/B)
-    const char* e = getenv("NGA_PREFILL_KS");
-    return e ? atoi(e) : 0;
-  }();
-  static const int nwv_env = [] {  // NGA_PREFILL_NWV=4|8: waves sharing each tile (A/B)
-    const char* e = getenv("NGA_PREFILL_NWV");
-    return e ? atoi(e) : 0;
-  }();
+  const int ks_env = kernel_form(KF_PREFILL_KS);   // 1 | 2 forces the wave-group count (A/B)
   if (num_seqs == 0 || max_q_len == 0) return true;
   const int G = p.Hq / p.Hkv;
   const int hpw = G % 4 == 0 ? 4 : G % 2 == 0 ? 2 : 1;
@@ -484,10 +426,6 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
   PrefillParams pp = p;
   pp.ntiles = (max_q_len + rw - 1) / rw;
   const int64_t total = (int64_t)pp.ntiles * (p.Hq / hpw) * num_seqs;
-  // 8-wave shared-tile form: GQA groups of 4 and enough 64-row blocks to fill the chip
-  const int64_t total8 = (int64_t)((max_q_len + 63) / 64) * (p.Hq / hpw) * num_seqs;
-  const bool nwv8 = hpw == 4 && (p.impl == 5 || ((p.impl == 0 || p.impl == 4) &&
-                                                  (nwv_env == 8 || (nwv_env == 0 && v2_nwv8_default(total8)))));
   // Size rule: this kernel needs about two of its workgroups per CU (two waves per SIMD) to
   // overlap one wave's softmax with the other's MFMAs. A single ~1K-token prompt is ~300
   // workgroups of 128 (row, head) pairs — one wave per SIMD, measured no faster than the
@@ -498,27 +436,12 @@ bool launch_prefill_attention_v2(const PrefillParams& p, int num_seqs, int max_q
   // impl 4 ("alone": a prefill with no decode attention beside it, e.g. a prefill-only step)
   // drops the sharing concern: standalone this kernel wins from one prompt up — 2 x 1,200
   // tokens 47.6 vs 75.9 us, 3 x 1,200 59.6 vs 97.6 us (profiles/r3_kernels/kb_prefill.json).
-  int ks = p.impl == 3 ? 2 : (p.impl == 2 || p.impl == 5 || p.impl == 6) ? 1 : (total <= 320 ? 2 : 1);
+  int ks = p.impl == 3 ? 2 : p.impl == 2 ? 1 : (total <= 320 ? 2 : 1);
   if (ks_env == 1 || ks_env == 2) ks = ks_env;
-  if (p.impl == 0 && ks == 1 && total < 2 * 256 * 2 && !nwv8) return false;
-  if (nwv8 && (ks == 1 || p.impl == 5)) {
-    rw = 64;
-    pp.ntiles = (max_q_len + rw - 1) / rw;
-    pp.total = (int)total8;
-    pp.per_xcd = (int)((total8 + 7) / 8);
-    dim3 grid8(8 * pp.per_xcd);
-    if (causal) prefill_attn_v2_kernel<true, 4, 0, 1, 8, 8><<<grid8, 512, 0, stream>>>(pp);
-    else prefill_attn_v2_kernel<false, 4, 0, 1, 8, 8><<<grid8, 512, 0, stream>>>(pp);
-    return true;
-  }
+  if (p.impl == 0 && ks == 1 && total < 2 * 256 * 2) return false;
   pp.total = (int)total;
   pp.per_xcd = (int)((total + 7) / 8);
   dim3 grid(8 * pp.per_xcd);
-  if (p.impl == 6 && hpw == 4) {   // register-staged tiles (A/B)
-    if (causal) prefill_attn_v2_kernel<true, 4, 0, 1, 8, 4, 1><<<grid, 256, 0, stream>>>(pp);
-    else prefill_attn_v2_kernel<false, 4, 0, 1, 8, 4, 1><<<grid, 256, 0, stream>>>(pp);
-    return true;
-  }
 #define NGA_PF2(CS, HP)                                                                   \
   do {                                                                                      \
     if (ks == 2) prefill_attn_v2_kernel<CS, HP, 0, 2><<<grid, 512, 0, stream>>>(pp);        \

@@ -370,13 +370,12 @@ int skinny_gemm_cfg_count() {
 #define NGA_COUNT(ID, BN, BM, WN, WM, NS) ++n;
   NGA_SKINNY_CFGS(NGA_COUNT)
 #undef NGA_COUNT
-  return n + wreg_gemm_cfg_count();   // gemm_wreg.hip's configurations continue the IDs
+  return n;
 }
 
-// {BN, BM, WN, WM, NSTAGE, kind} of a configuration (kind 0: both operands via LDS, this file;
-// 1: weights in registers, gemm_wreg.hip), or zeros
+// {BN, BM, WN, WM, NSTAGE} of a configuration, or zeros
 void skinny_gemm_cfg_info(int cfg, int* info) {
-  info[0] = info[1] = info[2] = info[3] = info[4] = info[5] = 0;
+  info[0] = info[1] = info[2] = info[3] = info[4] = 0;
 #define NGA_INFO(ID, BN, BM, WN, WM, NS) \
   if (cfg == ID) {                       \
     info[0] = BN;                        \
@@ -388,7 +387,6 @@ void skinny_gemm_cfg_info(int cfg, int* info) {
   }
   NGA_SKINNY_CFGS(NGA_INFO)
 #undef NGA_INFO
-  wreg_gemm_cfg_info(cfg, info);
 }
 
 void launch_skinny_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t stream) {
@@ -405,7 +403,6 @@ void launch_skinny_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t
   }
   NGA_SKINNY_CFGS(NGA_LAUNCH)
 #undef NGA_LAUNCH
-  launch_wreg_gemm(p, cfg, epi, stream);
 }
 
 void launch_splitk_reduce(const float* P, int S, int M, int N, uint16_t* out, int64_t ldo,

@@ -6,6 +6,24 @@
 
 namespace nga {
 
+// Kernel-form selection for A/B runs and tests. Each form starts from its NGA_* environment
+// variable, read ONCE (first use); launchers read the table, never the environment, and
+// tests / benchmarks switch forms explicitly through ops.kernel_forms (no per-launch getenv).
+enum KernelForm {
+  KF_DECODE_DMA = 0,   // NGA_DECODE_DMA: 1 whole-page LDS-DMA decode kernel (default), 2 its ring form, 0 register kernel
+  KF_DECODE_NT,        // NGA_DECODE_NT: 1 non-temporal KV loads in the register decode kernel
+  KF_RMSNORM_WAVE,     // NGA_RMSNORM_WAVE: 1 wave-per-row RMSNorm
+  KF_SEARCH_DMA,       // NGA_SEARCH_DMA: 0 forces the register form of the fused search kernel
+  KF_SEARCH_NT,        // NGA_SEARCH_NT: 1 non-temporal index-row loads (register search form)
+  KF_PREFILL_V1,       // NGA_PREFILL_V1: 1 disables the 32x32 prefill kernel
+  KF_PREFILL_KS,       // NGA_PREFILL_KS: 1 / 2 forces the 32x32 prefill kernel's wave-group count
+  KF_COUNT
+};
+int kernel_form(KernelForm f);
+void set_kernel_form(KernelForm f, int value);
+const char* kernel_form_name(KernelForm f);
+
+
 // norm.hip
 void launch_rmsnorm(uint16_t* out, uint16_t* resid, const uint16_t* delta, const uint16_t* w,
                     float eps, int64_t rows, int H, int64_t in_stride, int64_t out_stride,
@@ -185,12 +203,8 @@ struct SkinnyGemmParams {
   int wnt;             // 1: weight DMA with the non-temporal cache policy (streamed once)
 };
 int skinny_gemm_cfg_count();
-void skinny_gemm_cfg_info(int cfg, int* info);   // {BN, BM, WN, WM, NSTAGE, kind}: 6 ints
+void skinny_gemm_cfg_info(int cfg, int* info);   // {BN, BM, WN, WM, NSTAGE}
 void launch_skinny_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t stream);
-// gemm_wreg.hip: the weight-in-registers tile family (IDs after gemm_skinny.hip's)
-int wreg_gemm_cfg_count();
-bool wreg_gemm_cfg_info(int cfg, int* info);
-bool launch_wreg_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t stream);
 void launch_splitk_swiglu(const float* P, int S, int M, int F, uint16_t* out, int64_t ldo,
                           hipStream_t stream);
 void launch_splitk_reduce(const float* P, int S, int M, int N, uint16_t* out, int64_t ldo,

@@ -175,9 +175,8 @@ void launch_rmsnorm(uint16_t* out, uint16_t* resid, const uint16_t* delta, const
   // The wave-per-row form measured slower than the row-per-block one at every step size of the
   // headline (add + RMSNorm, 4,096 wide: 1,426 rows 7.2 vs 6.7 us, 4,352 rows 22.5 vs 21.3 us,
   // 256 rows 3.9 both; profiles/r3_decode_step/kb_norm.json), so it is opt-in for A/B runs:
-  // NGA_RMSNORM_WAVE=1 (read per call).
-  const char* we = getenv("NGA_RMSNORM_WAVE");
-  const bool wave_on = we && atoi(we) != 0;
+  // form KF_RMSNORM_WAVE (NGA_RMSNORM_WAVE=1).
+  const bool wave_on = kernel_form(KF_RMSNORM_WAVE) != 0;
   if (wave_on && H % 512 == 0 && H <= 8192 && in_stride % 8 == 0 && out_stride % 8 == 0) {
     dim3 g4((unsigned)((rows + 3) / 4)), b4(256);
 #define NGA_RMSW(NV)                                                                               \

@@ -776,8 +776,7 @@ __global__ void __launch_bounds__(256, 1) score_topk_dma_kernel(
 int score_topk_kmax(int nq_per_item) { return nq_per_item <= 32 ? 16 : 8; }
 
 int score_topk_dma_ok(int D, int max_q_per_item) {
-  const char* e = getenv("NGA_SEARCH_DMA");   // A/B knob, read per call (kernel_bench)
-  return (e == nullptr || atoi(e) != 0) && max_q_per_item <= 16 && D % 256 == 0 && D >= 256 && D <= 2048;
+  return kernel_form(KF_SEARCH_DMA) != 0 && max_q_per_item <= 16 && D % 256 == 0 && D >= 256 && D <= 2048;
 }
 
 void launch_score_topk(const uint16_t* Q, int nq, const uint16_t* X, int64_t N, int D,
@@ -818,8 +817,7 @@ void launch_score_topk(const uint16_t* Q, int nq, const uint16_t* X, int64_t N, 
   const size_t mg = (size_t)64 * W * KR * 8;
   const size_t lds = qs > mg ? qs : mg;
   dim3 grid((unsigned)nblk, (unsigned)n_items);
-  const char* nte = getenv("NGA_SEARCH_NT");
-  const int nt = nte && atoi(nte) ? 1 : 0;
+  const int nt = kernel_form(KF_SEARCH_NT) ? 1 : 0;
 #define NGA_STK(NG_, W_, K_)                                                                    \
   do {                                                                                           \
     static bool attr_ = false;                                                                   \

@@ -6,6 +6,8 @@ GPU call raises (so a GPU test can never pass on an eager-PyTorch substitute).
 """
 from __future__ import annotations
 
+import contextlib
+
 from typing import Optional, Tuple
 
 import torch
@@ -354,6 +356,32 @@ class DecodeWorkspace:
         return max(1, -(-pages // self.nparts(B)))
 
 
+KERNEL_FORMS = ("decode_dma", "decode_nt", "rmsnorm_wave", "search_dma", "search_nt", "prefill_v1",
+                "prefill_ks")
+
+
+def kernel_form(name: str) -> int:
+    """Current value of an A/B kernel form (csrc/kernels/kernels.h KernelForm; starts from its
+    NGA_* environment variable, read once)."""
+    return int(kernels().kernel_form(name))
+
+
+@contextlib.contextmanager
+def kernel_forms(**forms):
+    """Select kernel forms for a block and restore them after, e.g.
+    ``with ops.kernel_forms(decode_dma=2): ...`` (tests and A/B benchmarks; a hipGraph keeps the
+    form it was captured with)."""
+    C = kernels()
+    old = {k: int(C.kernel_form(k)) for k in forms}
+    try:
+        for k, v in forms.items():
+            C.set_kernel_form(k, int(v))
+        yield
+    finally:
+        for k, v in old.items():
+            C.set_kernel_form(k, v)
+
+
 def decode_attention(q, kc, vc, block_tables, ctx_lens, Hq, Hkv, max_ctx, scale,
                      out=None, ws: Optional[DecodeWorkspace] = None, window: int = 0,
                      kv_scales=(1.0, 1.0), skip_empty: bool = False):
@@ -393,10 +421,8 @@ def prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
     split-key form (few prompts: two wave groups walk alternate key tiles of the same row
     block and merge in LDS) — for tests and A/B runs; 4 picks by size for a prefill that
     runs alone (no decode attention beside it: the 32x32 kernel from one prompt up, the
-    split-key form for ~one row block per CU); 5 the 32x32 kernel's 8-wave shared-tile form
-    (2 x 32 rows of each head of a GQA group of 4 per K / V^T tile; other head ratios run
-    impl 2); 6 the 32x32 kernel with register-staged K / V^T tiles instead of LDS-DMA (GQA
-    groups of 4; A/B). fp8 e4m3fn caches (``kv_scales``) run the 16x16 kernel."""
+    split-key form for ~one row block per CU). fp8 e4m3fn caches (``kv_scales``) run the
+    16x16 kernel."""
     if not _gpu(q):
         r = ref.prefill_attention_paged(q, kc, vc, block_tables, cu_q, ctx_lens, Hq, Hkv, D,
                                         scale, causal, window, kv_scales)

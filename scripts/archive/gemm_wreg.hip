@@ -1,3 +1,9 @@
+// ARCHIVED (round 5, not built): measured slower than gemm_skinny.hip's LDS tiles on every
+// llama3-8b projection at M = 64-256, consumers included (profiles/r5_wreg/: e.g. gate/up at
+// M = 256 85-118 us vs 82.7 us, down 56-75 vs 50.8, o 25.7-38 vs 23.4). Weights in registers cut
+// the LDS traffic but not the L2 -> CU intake: with BN = M = 256 per CU and split-K to fill the
+// chip the per-CU intake still caps near 40-44 GB/s, as in the LDS form. Kept as the record of
+// the experiment (it was wired in as skinny cfg IDs 17-38 for the sweep).
 // Decode-shape projection GEMM, weight-in-registers form (K6, M <= 256 per token tile):
 //
 //   out[M, N] = x[M, K] . W[N, K]^T          (nn.Linear layout: both operands K-contiguous)

@@ -23,3 +23,21 @@ def gpu():
 
     ops.kernels()  # fail loudly if the HIP extension is missing
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def kernel_form():
+    """Select an A/B kernel form for one test (csrc/kernels/kernels.h KernelForm) and restore
+    it afterwards: ``kernel_form("decode_dma", 2)``."""
+    from nv_genai_amd import ops
+
+    saved = {}
+
+    def set_form(name, value):
+        if name not in saved:
+            saved[name] = ops.kernel_form(name)
+        ops.kernels().set_kernel_form(name, int(value))
+
+    yield set_form
+    for k, v in saved.items():
+        ops.kernels().set_kernel_form(k, v)

@@ -79,8 +79,8 @@ def _paged(ctxs, Hkv, D, dev, seed=0):
 @pytest.mark.parametrize("D,G,window,ppp", [(256, 8, 0, None), (256, 1, 0, 2), (128, 4, 200, None),
                                             (128, 4, 200, 1), (256, 8, 300, None), (128, 8, 64, None)])
 @pytest.mark.parametrize("dma", ["1", "2"])
-def test_decode_attention_dim_and_window(gpu, D, G, window, ppp, dma, monkeypatch):
-    monkeypatch.setenv("NGA_DECODE_DMA", dma)   # head_dim 128 pages: whole-page / ring DMA kernel
+def test_decode_attention_dim_and_window(gpu, D, G, window, ppp, dma, kernel_form, monkeypatch):
+    kernel_form("decode_dma", dma)   # head_dim 128 pages: whole-page / ring DMA kernel
     Hkv = 2 if G < 8 else 1
     Hq = Hkv * G
     ctxs = [1, 63, 64, 65, 199, 200, 201, 700, 1333]

@@ -46,8 +46,8 @@ def _close_rows(a, b, width=None, rel=1e-2, peak=2e-2):
 # (H = 512 NV; other widths fall back to the row form)
 @pytest.mark.parametrize("wave", ["0", "1"])
 @pytest.mark.parametrize("H", [768, 1024, 2048, 3072, 4096, 5120, 6144, 8192])
-def test_rmsnorm(gpu, H, wave, monkeypatch):
-    monkeypatch.setenv("NGA_RMSNORM_WAVE", wave)   # read by the launcher per call
+def test_rmsnorm(gpu, H, wave, kernel_form, monkeypatch):
+    kernel_form("rmsnorm_wave", wave)
     torch.manual_seed(0)
     x, w = _bf(37, H, dev=gpu), _bf(H, dev=gpu)
     _close_rows(ops.rmsnorm(x, w, 1e-5), ref.rmsnorm(x.cpu().float(), w.cpu().float(), 1e-5))
@@ -140,12 +140,12 @@ def _paged_setup(ctxs, Hkv, D, dev, seed=0):
 @pytest.mark.parametrize("dma", ["1", "2"])
 @pytest.mark.parametrize("G", [4, 8])
 @pytest.mark.parametrize("ppp", [None, 2, 3])
-def test_decode_attention(gpu, G, ppp, dma, monkeypatch):
+def test_decode_attention(gpu, G, ppp, dma, kernel_form, monkeypatch):
     """NGA_DECODE_DMA 1: the whole-page LDS-DMA kernel, 2: its half-page ring form.
     Short, page-edge, long (4096 / 8192) contexts and contexts one key either side of a
     split-K partition boundary (ppp pages of 64 keys per partition), per-head relative error
     against the fp32 reference (computed on the GPU in fp32)."""
-    monkeypatch.setenv("NGA_DECODE_DMA", dma)
+    kernel_form("decode_dma", dma)
     Hkv, D = 8 if G == 4 else 1, 128
     Hq = Hkv * G
     part = 64 * (ppp or 2)
@@ -162,8 +162,8 @@ def test_decode_attention(gpu, G, ppp, dma, monkeypatch):
 
 
 @pytest.mark.parametrize("dma", ["1", "2"])
-def test_decode_attention_empty_rows(gpu, dma, monkeypatch):
-    monkeypatch.setenv("NGA_DECODE_DMA", dma)
+def test_decode_attention_empty_rows(gpu, dma, kernel_form, monkeypatch):
+    kernel_form("decode_dma", dma)
     Hkv, G, D = 8, 4, 128
     Hq = Hkv * G
     kc, vc, bt = _paged_setup([100, 1], Hkv, D, gpu)
@@ -219,13 +219,13 @@ def test_prefill_attention_v2_layouts(gpu, Hkv, G, window, causal):
     ctx_t = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
     scale = 1 / math.sqrt(D)
     o_ref = ref.prefill_attention_paged(q.float(), kc, vc, bt, cu_t, ctx_t, Hq, Hkv, D, scale, causal, window)
-    for impl in (2, 3, 5, 6):   # 4-wave, 8-wave split-key, 8-wave shared tiles, register-staged
+    for impl in (2, 3):   # 4-wave, 8-wave split-key
         out = ops.prefill_attention_paged(q, kc, vc, bt, cu_t, ctx_t, Hq, Hkv, D, max(qls), scale,
                                           causal=causal, window=window, impl=impl)
         _close_rows(out, o_ref, width=D)
 
 
-@pytest.mark.parametrize("impl", [0, 1, 2, 3, 5, 6])
+@pytest.mark.parametrize("impl", [0, 1, 2, 3])
 @pytest.mark.parametrize("ctxs,qls,window", [
     ([1200], [940], 0),            # one prompt after a 260-token prefix hit
     ([1200] * 6, [1200] * 6, 0),   # six prompts (the size rule picks the 32x32 kernel)
@@ -636,10 +636,10 @@ def test_prefill_attention_worklist_fp8_and_d256(gpu):
 
 
 @pytest.mark.parametrize("dma", ["1", "2"])
-def test_decode_attention_skip_empty_rows(gpu, dma, monkeypatch):
+def test_decode_attention_skip_empty_rows(gpu, dma, kernel_form, monkeypatch):
     """skip_empty: rows with ctx 0 are not written (the mixed-step graph's decode launch
     covers a bucket of rows whose tail belongs to the prefill tokens)."""
-    monkeypatch.setenv("NGA_DECODE_DMA", dma)
+    kernel_form("decode_dma", dma)
     Hkv, G, D = 8, 4, 128
     Hq = Hkv * G
     ctxs = [100, 0, 700, 0]
@@ -689,16 +689,11 @@ def test_skinny_gemm_every_cfg(gpu, M):
     ref0, ref2 = _skinny_ref(x, w, 0), _skinny_ref(x, wg, 2)
     for cfg in range(C.skinny_cfg_count()):
         BN, BM = C.skinny_cfg(cfg)[:2]
-        wreg = C.skinny_cfg(cfg)[5] == 1   # weight-in-registers tiles (gemm_wreg.hip): plain x / w only
         _close_rows(ops.skinny_gemm(x, w, cfg, 1, 0), ref0, rel=1e-2)
         for s in (2, 5):
             P = ops.skinny_gemm(x, w, cfg, s, 1)
             _close_rows(P.sum(0), ref0, rel=1e-4)
             _close_rows(ops.splitk_reduce(P), ref0, rel=1e-2)
-        if wreg:
-            if 512 % (BN // 2) == 0:
-                _close_rows(ops.skinny_gemm(x, wg, cfg, 1, 2), ref2, rel=2e-2)
-            continue
         if 512 % (BN // 2) == 0:
             y2 = ops.skinny_gemm(x, wg, cfg, 1, 2)
             _close_rows(y2, ref2, rel=2e-2)
