@@ -337,7 +337,7 @@ def test_step_graphs_headline_gqa_4096_bucket(gpu, gqa_weights, pf_seq_min, monk
     _same_greedy_run(outs[True], outs[False])
 
 
-def _same_greedy_run(ga, eg, lp_tol=0.1):
+def _same_greedy_run(ga, eg, lp_tol=0.25):
     """Graphed vs eager greedy generations: the first token of every request (its prefill /
     mixed-step output) equal; then equal tokens with log-probs within ``lp_tol`` up to a
     request's first divergence, which is accepted only at a near-tie (neither run confident in
@@ -345,7 +345,9 @@ def _same_greedy_run(ga, eg, lp_tol=0.1):
     decisions on random weights, bucket-padded GEMMs (other library kernels, another fp32
     summation order) can flip an exact tie; a wrong kernel changes first tokens and log-probs.
     A smoke check only: the numerics are pinned by the teacher-forced logit comparisons
-    (test_teacher_forced_*), which feed both runs the same token histories."""
+    (test_teacher_forced_*), which feed both runs the same token histories. ``lp_tol``: with
+    the x40 test head the graphed (bucket-padded GEMMs) and eager runs differ by up to 0.18
+    nats before any divergence (profiles/r5_numerics/), 0.1 fails on that alone."""
     diverged = []
     for i, ((a, la), (b, lb)) in enumerate(zip(ga, eg)):
         assert a[0] == b[0], (i, a[:3], b[:3], la[:3], lb[:3])
@@ -537,6 +539,9 @@ def _teacher_forced_logits(make_engine, prompts_early, prompts_late, max_tokens)
 def _assert_logits_close(ga, eg, rel=2e-2):
     assert ga.keys() == eg.keys() and len(ga) > 10
     worst = max((float((ga[k] - eg[k]).norm() / eg[k].norm()), k) for k in ga)
+    lp = max(float((torch.log_softmax(ga[k], -1) - torch.log_softmax(eg[k], -1)).abs().max()) for k in ga)
+    print(f"teacher-forced rows {len(ga)}: worst per-row relative logit error {worst[0]:.5f} at {worst[1]}, "
+          f"max |log-prob delta| {lp:.4f}")
     assert worst[0] < rel, f"worst per-row relative logit error {worst[0]:.4f} at (request, token) {worst[1]}"
     return worst[0]
 
