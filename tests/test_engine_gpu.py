@@ -349,14 +349,19 @@ def _same_greedy_run(ga, eg, lp_tol=0.25):
     the x40 test head the graphed (bucket-padded GEMMs) and eager runs differ by up to 0.18
     nats before any divergence (profiles/r5_numerics/), 0.1 fails on that alone."""
     diverged = []
+    worst = 0.0
     for i, ((a, la), (b, lb)) in enumerate(zip(ga, eg)):
         assert a[0] == b[0], (i, a[:3], b[:3], la[:3], lb[:3])
         d = next((j for j, (x, y) in enumerate(zip(a, b)) if x != y), None)
         upto = len(a) if d is None else d
-        assert max(abs(x - y) for x, y in zip(la[:upto], lb[:upto])) < lp_tol, (i, la[:upto], lb[:upto])
+        delta = max(abs(x - y) for x, y in zip(la[:upto], lb[:upto]))
+        worst = max(worst, delta)
+        assert delta < lp_tol, (i, la[:upto], lb[:upto])
         if d is not None:
             assert all(-1.5 <= v <= -0.4 for v in (la[d], lb[d])), ("divergence without a near-tie", i, d, la[d], lb[d])
             diverged.append(i)
+    print(f"greedy smoke check: {len(ga)} requests, max log-prob delta before divergence {worst:.4f}, "
+          f"diverged at a near-tie: {diverged}")
     assert len(diverged) <= max(1, len(ga) // 4), diverged
 
 
