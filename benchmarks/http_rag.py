@@ -94,6 +94,13 @@ def _engine_window(m0, m1) -> dict:
                                                                  "host_wait_s", "host_finalize_s")}}
     if steps:
         out["host_ms_per_step"] = {k: round(1e3 * v / steps, 3) for k, v in out["host_s"].items()}
+    if "prefix_hit_blocks" in d and "prefill_tokens" in d:
+        # prompt tokens served from the prefix cache (64-token blocks) vs computed in prefill:
+        # the same share bench.py reports, so the two topologies are comparable
+        hit = 64 * d["prefix_hit_blocks"]
+        tot = hit + d["prefill_tokens"]
+        out["prefix_cache"] = {"hit_tokens": int(hit), "prompt_tokens_total": int(tot),
+                               "hit_share": round(hit / tot, 4) if tot else 0.0}
     return out
 
 

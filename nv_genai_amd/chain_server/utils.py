@@ -205,9 +205,21 @@ def _fill_synthetic(vs, cfg) -> None:
     vs.index.add_random(n, seed=1234)
     vs.docs = SyntheticDocStore(n)
     vs._mark_write()
+    cal = TextGen(seed=999)
+    questions = [cal.question() for _ in range(4096)]
     if cfg.embeddings.model_engine in ("local", "huggingface"):
-        cal = TextGen(seed=999)
-        get_embedding_engine().calibrate_whitening([cal.question() for _ in range(4096)])
+        get_embedding_engine().calibrate_whitening(questions)
+    elif hasattr(vs.embedder, "embed_query_tensor"):
+        # the encoder sits behind HTTP (a model server, the reference's NIM topology): whiten
+        # its query vectors here, from the same calibration questions, so the split topology
+        # retrieves as diversely as the in-process one (unwhitened random-init vectors are
+        # nearly collinear: every question would retrieve the same chunks and hit the prefix
+        # cache on the whole prompt)
+        from ..engine.embed_engine import pca_whitening
+        from ..index.vectorstore import WhitenedEmbedder
+
+        mu, W = pca_whitening(vs.embedder.embed_query_tensor(questions))
+        vs.embedder = WhitenedEmbedder(vs.embedder, mu, W, device=vs.index_device())
     log.info("filled collection %s with %d synthetic chunks", vs.name, n)
 
 

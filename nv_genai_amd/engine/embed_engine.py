@@ -25,6 +25,18 @@ from ..models.encoder import EncoderModel
 from ..utils.tokenizer import EmbedTokenizer, embed_tokenizer
 
 
+def pca_whitening(x: torch.Tensor, eps: float = 1e-4):
+    """(mu, W) of PCA whitening over calibration embeddings x [n, d]: y = normalise((x - mu) W)
+    with W = C^-1/2 (eigenvalues floored at eps * the largest), fp32 on x's device."""
+    x = x.double()
+    mu = x.mean(0)
+    xc = x - mu
+    cov = xc.T @ xc / max(1, x.shape[0] - 1)
+    lam, U = torch.linalg.eigh(cov)
+    W = U @ torch.diag(1.0 / torch.sqrt(lam.clamp_min(0) + eps * lam.max())) @ U.T
+    return mu.float(), W.float()
+
+
 class EmbeddingEngine:
     def __init__(self, model: str | EncoderConfig = "arctic-embed-l", device: Optional[str] = None,
                  max_batch_tokens: int = 65536, seed: int = 0,
@@ -69,13 +81,7 @@ class EmbeddingEngine:
         encoder's embeddings isotropic so retrieval over a synthetic index is as diverse as
         with a trained model; one [n, d] x [d, d] GEMM per call."""
         self.center, self.whiten = None, None
-        x = self.embed(texts, input_type).double()
-        mu = x.mean(0)
-        xc = x - mu
-        cov = xc.T @ xc / max(1, x.shape[0] - 1)
-        lam, U = torch.linalg.eigh(cov)
-        W = U @ torch.diag(1.0 / torch.sqrt(lam.clamp_min(0) + eps * lam.max())) @ U.T
-        self.center, self.whiten = mu.float(), W.float()
+        self.center, self.whiten = pca_whitening(self.embed(texts, input_type), eps)
 
     @property
     def name(self) -> str:

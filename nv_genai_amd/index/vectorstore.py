@@ -44,6 +44,35 @@ def _embed_queries(embedder, texts: Sequence[str]) -> torch.Tensor:
     return torch.tensor([embedder.embed_query(t) for t in texts], dtype=torch.float32)
 
 
+class WhitenedEmbedder:
+    """Another embedder's vectors mapped through y = normalise((x - mu) W) on ``device``: the
+    synthetic REST corpus's query whitening (``chain_server.utils._fill_synthetic``) for an
+    encoder the store reaches over HTTP, where the encoder itself cannot be calibrated. The
+    in-process engine applies the same transform inside ``EmbeddingEngine.embed_ids``."""
+
+    def __init__(self, inner, mu: torch.Tensor, W: torch.Tensor, device=None):
+        self.inner = inner
+        dev = torch.device(device) if device is not None else mu.device
+        self.mu, self.W = mu.to(dev), W.to(dev)
+        self.dim = int(W.shape[1])
+
+    def _apply(self, x: torch.Tensor) -> torch.Tensor:
+        y = (x.to(self.W.device, torch.float32) - self.mu) @ self.W
+        return y / y.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+
+    def embed_query_tensor(self, texts: Sequence[str]) -> torch.Tensor:
+        return self._apply(_embed_queries(self.inner, texts))
+
+    def embed_documents_tensor(self, texts: Sequence[str]) -> torch.Tensor:
+        return self._apply(_embed_docs(self.inner, texts))
+
+    def embed_query(self, text: str) -> List[float]:
+        return self.embed_query_tensor([text])[0].tolist()
+
+    def embed_documents(self, texts: Sequence[str]) -> List[List[float]]:
+        return self.embed_documents_tensor(texts).tolist()
+
+
 class _QueryBatcher:
     """Coalesces concurrent similarity searches (one per chain-server request thread) into one
     query-encoder forward and one index scan, on a dedicated HIP stream. A search therefore

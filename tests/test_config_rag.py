@@ -109,6 +109,42 @@ def test_vectorstore_flat_ivf_and_persistence(tmp_path):
         assert rel and all(s >= 0.25 for _, s in rel)
 
 
+def test_synthetic_collection_whitens_a_remote_encoder(monkeypatch):
+    """The REST benchmark corpus over an encoder behind HTTP (split topology): the chain server
+    whitens the remote query vectors (nearly collinear from a random-init encoder) so concurrent
+    questions retrieve different chunks, as the in-process engine's own whitening does."""
+    from nv_genai_amd.chain_server import utils
+    from nv_genai_amd.engine.embed_engine import pca_whitening
+    from nv_genai_amd.index.vectorstore import VectorStore, WhitenedEmbedder
+
+    class Remote:   # the EmbeddingsClient surface the store uses: collinear-ish query vectors
+        dim = 64
+
+        def __init__(self):
+            self.base = torch.randn(64)
+
+        def embed_query_tensor(self, texts):
+            g = torch.Generator().manual_seed(abs(hash(tuple(texts))) % (2 ** 31))
+            return self.base + 0.01 * torch.randn(len(texts), 64, generator=g)
+
+    cfg = AppConfig.from_dict({"index": {"synthetic_docs": 2000}, "embeddings": {"model_engine": "nim"}})
+    vs = VectorStore(Remote(), 64, "flat", "cosine", "cpu", batch_queries=False)
+    utils._fill_synthetic(vs, cfg)
+    assert isinstance(vs.embedder, WhitenedEmbedder)
+    qs = [f"question {i} about widgets" for i in range(64)]
+    y = torch.cat([vs.embedder.embed_query_tensor([q]) for q in qs])
+    assert torch.allclose(y.norm(dim=1), torch.ones(64), atol=1e-4)
+    raw = torch.cat([vs.embedder.inner.embed_query_tensor([q]) for q in qs])
+    raw = raw / raw.norm(dim=1, keepdim=True)
+    off = ~torch.eye(64, dtype=torch.bool)
+    assert (raw @ raw.T)[off].mean() > 0.99            # unwhitened: every question alike
+    assert (y @ y.T)[off].abs().mean() < 0.3           # whitened: spread out
+    firsts = {vs.similarity_search_with_score(q, 4)[0][0].page_content for q in qs}
+    assert len(firsts) > 32                             # different questions, different chunks
+    mu, W = pca_whitening(torch.randn(500, 8))
+    assert mu.shape == (8,) and W.shape == (8, 8)
+
+
 def test_flat_l2_and_ip_metrics():
     from nv_genai_amd.index.flat import FlatIndex
 
