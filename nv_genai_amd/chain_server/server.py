@@ -49,6 +49,9 @@ logger = logging.getLogger(__name__)
 
 @contextlib.asynccontextmanager
 async def _lifespan(_app):
+    from ..observability.sampler import start_from_env
+
+    start_from_env("chain")   # NGA_PY_SAMPLE_OUT: stack-sample this process (diagnostics)
     import_example()
     yield
 

@@ -492,6 +492,10 @@ def main(argv=None):
     args = ap.parse_args(argv)
     import uvicorn
 
+    from ..observability.sampler import start_from_env
+
+    start_from_env("model")   # NGA_PY_SAMPLE_OUT: stack-sample this process (diagnostics)
+
     from ..engine.embed_engine import EmbeddingEngine
     from ..engine.llm_engine import EngineConfig, LLMEngine
     from .engine_service import EngineService

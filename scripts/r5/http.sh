@@ -13,6 +13,7 @@ for spec in "$@"; do
     python -c "import json;d=json.load(open('$out/bench.json'));print('bench', d['value'], d['p50_latency_ms'], d['p50_ttft_ms'])"
     continue
   fi
+  [ -n "${PYSAMPLE:-}" ] && export NGA_PY_SAMPLE_OUT=$PWD/$out/pysample_${topo}_iv${iv}_{tag}.json
   timeout -k 10 600 python benchmarks/http_rag.py --topology $topo --stream-interval $iv --out $out/http_${topo}_iv$iv.json > $out/http_${topo}_iv$iv.log 2>&1 || { tail -30 $out/http_${topo}_iv$iv.log; tail -30 $out/server.log; exit 1; }
   python -c "import json;d=json.load(open('$out/http_${topo}_iv$iv.json'));print('$topo iv$iv', d['value'], d['p50_latency_ms'], d['p50_ttft_ms'], d['sse_gap_ms'], d['server_p50_ms'])"
 done

@@ -243,3 +243,36 @@ def test_prepared_stream_never_consumed_is_cancelled(service):
         time.sleep(0.02)
     assert service.engine.sched.num_running() == 0 and service.engine.sched.num_waiting() == 0
     s.cancel()   # idempotent once done
+
+
+def test_stack_sampler_separates_busy_and_parked_threads(tmp_path):
+    """The serving processes' stack sampler (NGA_PY_SAMPLE_OUT): a spinning thread reads as
+    busy with its hot function on top, a thread parked on an Event as idle, and the JSON
+    summary lands on disk."""
+    import json
+    import threading
+    import time
+
+    from nv_genai_amd.observability.sampler import StackSampler
+
+    stop = threading.Event()
+
+    def spin_here():
+        x = 0
+        while not stop.is_set():
+            x += 1
+
+    busy = threading.Thread(target=spin_here, name="spinner", daemon=True)
+    parked = threading.Thread(target=stop.wait, name="parked", daemon=True)
+    busy.start()
+    parked.start()
+    s = StackSampler(str(tmp_path / "s.json"), interval_s=0.002).start()
+    time.sleep(0.4)
+    stop.set()
+    s.stop()
+    d = json.load(open(tmp_path / "s.json"))
+    th = d["threads"]
+    assert d["samples"] > 20
+    assert th["spinner"]["busy_share"] > 0.5
+    assert any("spin_here" in where for where, _ in th["spinner"]["top_leaf"])
+    assert th["parked"]["busy_share"] < 0.2
