@@ -305,7 +305,8 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
             svc = _need(app.state.llm, "LLM")
             msgs = [{"role": m.role, "content": _content_text(m.content)} for m in req.messages]
             with tracer.span("chat.completions", {"model": req.model}, request.headers.get("traceparent")):
-                ids = svc.engine.apply_chat_template(msgs)
+                # off the event loop: a RAG prompt is ~1,200 tokens of encoding (GIL-free)
+                ids = await asyncio.to_thread(svc.engine.apply_chat_template, msgs)
                 handles = _submit_n(svc, ids, req)
         rid = f"chatcmpl-{uuid.uuid4().hex}"
         model = req.model or llm_name
@@ -359,8 +360,7 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
         except ValueError as e:
             return JSONResponse({"error": str(e)}, status_code=400)
         fut = app.state.batcher.submit_ids(seqs)
-        vecs = await asyncio.wrap_future(fut)
-        vecs = vecs.cpu()
+        vecs = await asyncio.wrap_future(fut)   # host tensors: the batcher waited on its own stream
         metrics.observe("embed_seconds", time.perf_counter() - t0)
         metrics.inc("embed_texts_total", len(texts))
         data = []

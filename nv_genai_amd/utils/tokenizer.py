@@ -89,6 +89,11 @@ class LLMTokenizer:
         return (self.eot_id, self.eos_id)
 
     def encode(self, text: str) -> List[int]:
+        if len(text) > 512:
+            # the Rust tokenizer's batch entry point runs without the GIL (the single-text one
+            # holds it): a serving process's event loop and engine thread keep running while a
+            # prompt of a few thousand characters is encoded on a worker thread
+            return self.tok.encode_batch([text], add_special_tokens=False)[0].ids
         return self.tok.encode(text, add_special_tokens=False).ids
 
     def encode_batch(self, texts: List[str]) -> List[List[int]]:
