@@ -77,35 +77,59 @@ class ChatClient:
                         yield delta
 
     async def astream(self, messages: Messages, coalesce: bool = False, handle=None, **kw):
-        """The same SSE stream on the caller's event loop (httpx, one pooled client per loop):
-        an async server forwards an upstream model server's tokens without parking a thread
-        per open stream. ``coalesce`` joins the deltas of frames that arrived together."""
-        client = _async_client(self.timeout)
+        """The same SSE stream on the caller's event loop (one pooled aiohttp session per
+        loop): an async server forwards an upstream model server's tokens without parking a
+        thread per open stream. ``coalesce`` joins the deltas of frames that arrived together.
+
+        aiohttp, not httpx, on this path: a chain server in front of a model server relays one
+        frame per token per stream, and httpx's anyio transport re-registers the socket with
+        the selector on every read (two epoll_ctl calls per token) and looks for sniffio on
+        every request (profiles/r5_http/: the chain server's event loop was the split
+        topology's bottleneck); aiohttp's C parser hands over whatever bytes arrived."""
         body = self._body(messages, True, **kw)
-        async with client.stream("POST", f"{self.base}/chat/completions", json=body,
-                                 headers={**_headers(self.api_key), **self.extra_headers}) as r:
+        url = f"{self.base}/chat/completions"
+        headers = {**_headers(self.api_key), **self.extra_headers}
+        session = _aiohttp_session(self.timeout)
+        if session is None:   # no aiohttp: httpx
+            async for d in self._astream_httpx(url, body, headers, coalesce):
+                yield d
+            return
+        async with session.post(url, json=body, headers=headers) as r:
+            if r.status != 200:
+                text = await r.text()
+                raise RuntimeError(f"chat/completions returned {r.status}: {text[:200]}")
+            carry = [b""]
+            while True:
+                chunk = await r.content.readany()
+                if not chunk:
+                    return
+                parts, done = _sse_deltas(carry, chunk)
+                if parts:
+                    if coalesce:
+                        yield "".join(parts)
+                    else:
+                        for p in parts:
+                            yield p
+                if done:
+                    return
+
+    async def _astream_httpx(self, url: str, body: dict, headers: dict, coalesce: bool):
+        client = _async_client(self.timeout)
+        async with client.stream("POST", url, json=body, headers=headers) as r:
             if r.status_code != 200:
                 await r.aread()
                 raise RuntimeError(f"chat/completions returned {r.status_code}: {r.text[:200]}")
-            carry = [""]
-            async for chunk in r.aiter_text():
-                parts = []
-                for line in _sse_lines(carry, chunk):
-                    if line == "[DONE]":
-                        if parts:
-                            yield "".join(parts)
-                        return
-                    for ch in json.loads(line).get("choices", []):
-                        delta = ch.get("delta", {}).get("content")
-                        if delta:
-                            parts.append(delta)
-                if not parts:
-                    continue
-                if coalesce:
-                    yield "".join(parts)
-                else:
-                    for p in parts:
-                        yield p
+            carry = [b""]
+            async for chunk in r.aiter_bytes():
+                parts, done = _sse_deltas(carry, chunk)
+                if parts:
+                    if coalesce:
+                        yield "".join(parts)
+                    else:
+                        for p in parts:
+                            yield p
+                if done:
+                    return
 
     def invoke(self, messages: Messages, **kw) -> str:
         r = requests.post(f"{self.base}/chat/completions", json=self._body(messages, False, **kw),
@@ -125,15 +149,59 @@ def _sse_lines(carry: list, text: str):
             yield line[5:].strip()
 
 
+def _sse_deltas(carry: list, chunk: bytes):
+    """(content deltas, saw [DONE]) of the complete ``data:`` lines in a byte chunk of an
+    OpenAI chat stream; the partial last line stays in ``carry[0]``. Lines are split as bytes,
+    so a UTF-8 character cut across two chunks is decoded whole."""
+    *lines, carry[0] = (carry[0] + chunk).split(b"\n")
+    parts = []
+    for line in lines:
+        if not line.startswith(b"data:"):
+            continue
+        payload = line[5:].strip()
+        if payload == b"[DONE]":
+            return parts, True
+        for ch in json.loads(payload).get("choices", []):
+            delta = ch.get("delta", {}).get("content")
+            if delta:
+                parts.append(delta)
+    return parts, False
+
+
 _ASYNC_CLIENTS = {}
+_AIOHTTP_SESSIONS = {}
+
+
+def _aiohttp_session(timeout: float):
+    """One pooled aiohttp.ClientSession per event loop (no connection cap: every open stream
+    holds one), or None without aiohttp."""
+    import asyncio
+
+    try:
+        import aiohttp
+    except ImportError:   # pragma: no cover - aiohttp ships in the image
+        return None
+    loop = asyncio.get_running_loop()
+    s = _AIOHTTP_SESSIONS.get(id(loop))
+    if s is None or s[0] is not loop or s[1].closed:
+        s = (loop, aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=0, keepalive_timeout=60),
+                                         timeout=aiohttp.ClientTimeout(total=timeout)))
+        _AIOHTTP_SESSIONS[id(loop)] = s
+    return s[1]
 
 
 def _async_client(timeout: float):
     """One pooled httpx.AsyncClient per event loop (connections are reused across streams)."""
     import asyncio
+    import importlib.util
+    import sys
 
     import httpx
 
+    if "sniffio" not in sys.modules and importlib.util.find_spec("sniffio") is None:
+        # httpcore tries `import sniffio` on every request; absent, each failed import walks
+        # sys.path. A None entry makes the import fail at once (httpcore then assumes asyncio)
+        sys.modules["sniffio"] = None
     loop = asyncio.get_running_loop()
     c = _ASYNC_CLIENTS.get(id(loop))
     if c is None or c[0] is not loop:

@@ -8,8 +8,9 @@ waits on the GIL" can be read off the output. The aggregate is written as JSON e
 ``dump_every_s`` (and at exit), so a server killed by its benchmark still leaves it.
 
 Enabled by ``NGA_PY_SAMPLE_OUT=<path>`` in the chain server and the model server
-(``NGA_PY_SAMPLE_MS`` = interval, default 5 ms). The sampler itself takes the GIL once per
-interval for a few tens of microseconds per thread.
+(``NGA_PY_SAMPLE_MS`` = interval, default 20 ms). The sampler holds the GIL once per interval
+for a few microseconds per live thread: at 5 ms with ~100 worker threads that perturbed the
+chain server measurably, so sample sparsely and run longer.
 """
 from __future__ import annotations
 
@@ -111,5 +112,5 @@ def start_from_env(tag: str = "") -> Optional[StackSampler]:
     if not path or _ACTIVE is not None:
         return _ACTIVE
     path = path.replace("{tag}", tag or "proc").replace("{pid}", str(os.getpid()))
-    _ACTIVE = StackSampler(path, float(os.environ.get("NGA_PY_SAMPLE_MS", "5")) / 1e3).start()
+    _ACTIVE = StackSampler(path, float(os.environ.get("NGA_PY_SAMPLE_MS", "20")) / 1e3).start()
     return _ACTIVE

@@ -204,7 +204,7 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
                 yield head + json.dumps(delta) + tail
             fin = {"index": 0, "finish_reason": handle.finish_reason or "stop"}
             fin.update({"delta": {}} if chat else {"text": ""})
-            yield "data: " + json.dumps({"id": rid, "object": obj, "created": int(time.time()), "model": model,
+            yield "data: " + json.dumps({"id": rid, "object": obj, "created": created, "model": model,
                                          "choices": [fin], "usage": handle.usage}) + "\n\n"
             yield "data: [DONE]\n\n"
         except asyncio.CancelledError:  # client went away: free the sequence

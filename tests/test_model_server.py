@@ -132,6 +132,12 @@ def test_http_connectors_roundtrip(http_url):
     per_tok = asyncio.run(agather(False))
     assert "".join(per_tok) == whole and len(per_tok) >= 2
     assert "".join(asyncio.run(agather(True))) == whole
+
+    async def ahttpx():   # the httpx fallback (no aiohttp) carries the same text
+        body = chat._body([("user", "hi")], True, ignore_eos=True)
+        return [d async for d in chat._astream_httpx(f"{chat.base}/chat/completions", body, {}, False)]
+
+    assert "".join(asyncio.run(ahttpx())) == whole
     emb = EmbeddingsClient(http_url, "tiny-embed")
     assert len(emb.embed_query("hello")) == 128
     assert len(emb.embed_documents(["a", "b", "c"])) == 3
@@ -273,3 +279,22 @@ def test_reference_connector_names_http_and_local(http_url):
     assert len(le.get_query_embedding("alpha")) == enc.dim
     rr = compat.NVIDIARerank(engine=EmbeddingEngine("reranker-tiny", device="cpu"), top_n=1)
     assert len(rr.compress_documents(docs, "q")) == 1
+
+
+def test_sse_delta_parser_splits_lines_and_utf8_across_chunks():
+    """The async chat stream's parser: frames cut anywhere (inside a line, inside a UTF-8
+    character) come out whole; [DONE] ends the stream; non-data lines are skipped."""
+    import json
+
+    from nv_genai_amd.connectors.http import _sse_deltas
+
+    frames = b"".join(b"data: " + json.dumps({"choices": [{"delta": {"content": t}}]}, ensure_ascii=False).encode()
+                      + b"\n\n" for t in ["hé", "llo ", "世界"]) + b": keep-alive\n\ndata: [DONE]\n\n"
+    for cut in range(1, len(frames)):
+        carry, out, done = [b""], [], False
+        for piece in (frames[:cut], frames[cut:]):
+            parts, done = _sse_deltas(carry, piece)
+            out += parts
+            if done:
+                break
+        assert "".join(out) == "héllo 世界" and done, cut
