@@ -54,6 +54,9 @@ async def _lifespan(_app):
     start_from_env("chain")   # NGA_PY_SAMPLE_OUT: stack-sample this process (diagnostics)
     import_example()
     yield
+    from ..connectors.http import aclose_clients
+
+    await aclose_clients()   # pooled upstream connections (split topology)
 
 
 app = FastAPI(title="nv_genai_amd chain server", lifespan=_lifespan)

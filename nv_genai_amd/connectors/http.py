@@ -190,6 +190,19 @@ def _aiohttp_session(timeout: float):
     return s[1]
 
 
+async def aclose_clients() -> None:
+    """Close this event loop's pooled aiohttp session / httpx client (server shutdown)."""
+    import asyncio
+
+    key = id(asyncio.get_running_loop())
+    s = _AIOHTTP_SESSIONS.pop(key, None)
+    if s is not None and not s[1].closed:
+        await s[1].close()
+    c = _ASYNC_CLIENTS.pop(key, None)
+    if c is not None:
+        await c[1].aclose()
+
+
 def _async_client(timeout: float):
     """One pooled httpx.AsyncClient per event loop (connections are reused across streams)."""
     import asyncio

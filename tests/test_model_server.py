@@ -126,8 +126,14 @@ def test_http_connectors_roundtrip(http_url):
     # same text, per token or coalesced
     import asyncio
 
+    from nv_genai_amd.connectors.http import _AIOHTTP_SESSIONS, aclose_clients
+
     async def agather(coalesce):
-        return [d async for d in chat.astream([("user", "hi")], coalesce=coalesce, ignore_eos=True)]
+        out = [d async for d in chat.astream([("user", "hi")], coalesce=coalesce, ignore_eos=True)]
+        sess = _AIOHTTP_SESSIONS[id(asyncio.get_running_loop())][1]
+        await aclose_clients()          # what the chain server's lifespan runs at shutdown
+        assert sess.closed
+        return out
 
     per_tok = asyncio.run(agather(False))
     assert "".join(per_tok) == whole and len(per_tok) >= 2
