@@ -90,6 +90,19 @@ class Request:
     # multimodal prompt: (position, features [n, hidden]) — rows whose input embeddings are
     # replaced by projected image features (models/vision.py)
     mm: Optional[list] = None
+    _hs: Optional[bool] = field(default=None, repr=False, compare=False)
+
+    @property
+    def host_sampling(self) -> bool:
+        """Sampling needs host state between steps (penalty history, JSON grammar). Fixed once
+        the request is queued (``json_state`` is set in ``add_request``), so it is computed
+        once: the step loop asks it for every row several times per step."""
+        hs = self._hs
+        if hs is None:
+            p = self.params
+            hs = self._hs = bool(p.repetition_penalty != 1.0 or p.frequency_penalty or p.presence_penalty
+                                 or self.json_state is not None)
+        return hs
 
     @property
     def ttft(self) -> Optional[float]:
@@ -270,6 +283,7 @@ class LLMEngine:
         self.d_gidx = dbuf(T, dtype=torch.int64) if self.gpu else None
         self.d_gprev = dbuf(T, dtype=torch.int64) if self.gpu else None
         self._step_reqs: List[Request] = []
+        self._step_host = (-1, False)   # (rows, any needs host sampling) of the current step
         self._faults = FaultInjector(rank=self.p.rank)   # NGA_FAULT (utils/faults.py)
         self._nstep = 0
         self._beam_of: Dict[int, BeamGroup] = {}   # live beam seq id -> its group
@@ -462,6 +476,7 @@ class LLMEngine:
         self.n_step[:n] = [len(r.output_ids) + (r.id in pending_ids) for r in reqs]
         self.n_pen[:n] = [r.params.repetition_penalty for r in reqs]
         self._step_reqs = reqs
+        self._step_host = (n, any(r.host_sampling for r in reqs))
 
     def step(self, between: Optional[Callable[[], None]] = None) -> List[Request]:
         """Run one scheduler step; returns requests that finished in it.
@@ -623,9 +638,7 @@ class LLMEngine:
 
     def _needs_penalty_reqs(self, reqs) -> bool:
         """Rows whose sampling needs host state (penalty history, JSON grammar)."""
-        return any(r is not None and (r.params.repetition_penalty != 1.0 or r.params.frequency_penalty
-                                      or r.params.presence_penalty or r.json_state is not None)
-                   for r in reqs)
+        return any(r is not None and r.host_sampling for r in reqs)
 
     def _launch(self, kind: int, n: int, ntok: int, nd: int, src) -> dict:
         """Launch a step without waiting for it. ``src = (token_idx, prev_rows)`` gathers the
@@ -1095,9 +1108,11 @@ class LLMEngine:
         return self.d_tok[:n], self.d_lp[:n]
 
     def _needs_penalty(self, n) -> bool:
-        return bool((self.h_pen[:n] != 1.0).any()) or any(
-            r.params.frequency_penalty or r.params.presence_penalty or r.json_state is not None
-            for r in self._step_reqs[:n])
+        """This step's rows need host-side sampling state; computed once per step by
+        ``_fill_params`` (the rows' repetition penalties are in ``h_pen``)."""
+        if n == self._step_host[0]:
+            return self._step_host[1]
+        return any(r.host_sampling for r in self._step_reqs[:n])
 
     def _grammar(self):
         g = getattr(self, "_json_grammar", None)
