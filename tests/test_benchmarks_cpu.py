@@ -38,6 +38,28 @@ def test_http_rag_benchmark_cpu(tmp_path):
     # the server's own phase summaries and the engine counters over the timed window
     assert {"chain", "chain_wait", "prepare", "ttft"} <= set(res["server_p50_ms"]), res["server_p50_ms"]
     assert res["engine_window"]["steps"] > 0 and "wait" in res["engine_window"]["host_s"], res["engine_window"]
+    pc = res["engine_window"]["prefix_cache"]
+    assert pc["prompt_tokens_total"] > 0 and 0.0 <= pc["hit_share"] <= 1.0, pc
+
+
+def test_http_rag_benchmark_split_topology_cpu(tmp_path):
+    """--topology split: the reference's deployment — the chain server (developer_rag, index
+    in-process) reaches the LLM and the query encoder through a separate model-server process
+    over HTTP (OpenAI chat stream, base64 embeddings, whitened on the chain side); the engine
+    counters come from the model server's /metrics."""
+    out = tmp_path / "split.json"
+    r = subprocess.run([sys.executable, "benchmarks/http_rag.py", "--llm", "llama-tiny", "--embed", "encoder-tiny",
+                        "--topology", "split", "--index-size", "3000", "--concurrency", "4", "--requests", "8",
+                        "--warmup", "2", "--max-tokens", "6", "--device", "cpu", "--out", str(out)],
+                       capture_output=True, text=True, timeout=500,
+                       env=dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=os.getcwd(),
+                                NGA_HTTP_BENCH_LOG=str(tmp_path / "server.log")))
+    assert r.returncode == 0, (r.stderr[-3000:], (tmp_path / "server.log").read_text()[-3000:])
+    res = json.loads(out.read_text())
+    assert res["topology"] == "split" and res["requests"] == 8 and res["value"] > 0
+    assert res["sse_gap_ms"]["frames"] > 0
+    ew = res["engine_window"]
+    assert ew["steps"] > 0 and ew["prefix_cache"]["prompt_tokens_total"] > 0, ew
 
 
 def test_headline_bench_two_ranks_gloo():
