@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--cfgs", default=None, help="comma list (default: all)")
     ap.add_argument("--check", action="store_true", help="numerics of the best config vs fp32")
     ap.add_argument("--all", action="store_true", help="print every (cfg, split) result")
+    ap.add_argument("--rot-mb", type=float, default=640.0,
+                    help="rotate weight copies totalling at least this many MB (640: past the 256 MB MALL; 0: one copy, cache-warm)")
     a = ap.parse_args()
     print("tuned table:", use_tuned_gemms(), flush=True)
     C = ops.kernels()
@@ -60,7 +62,7 @@ def main():
     for name in a.shapes.split(","):
         N, K, epi_full = SHAPES[name]
         wbytes = N * K * 2
-        n_rot = max(2, math.ceil(640e6 / wbytes))
+        n_rot = max(2, math.ceil(a.rot_mb * 1e6 / wbytes)) if a.rot_mb > 0 else 1
         Ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16, generator=g) * 0.02 for _ in range(n_rot)]
         for M in [int(m) for m in a.ms.split(",")]:
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
