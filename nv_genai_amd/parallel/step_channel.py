@@ -70,18 +70,26 @@ class ShmStepChannel(StepChannel):
         name = obj[0]
         if name is None:
             raise RuntimeError(f"shm step channel: the driver could not create its segment ({err!r})")
+        ok = True
         if not driver:
             # reader index: this rank's position among the replica's followers
             local = pctx.rank - pctx.mp_src
-            self.ch = rt.ShmChannel(name, False, 0, 0, 0, local - 1)
-            self._buf = np.empty(self.ch.slot_bytes(), dtype=np.uint8)
-        # every follower attached: drop the name so nothing is left in /dev/shm on a crash
-        if pctx.backend == "nccl":
-            _nccl_barrier(pctx)
-        else:
-            dist.barrier(group=pctx.mp_group)
+            try:
+                self.ch = rt.ShmChannel(name, False, 0, 0, 0, local - 1)
+                self._buf = np.empty(self.ch.slot_bytes(), dtype=np.uint8)
+            except Exception as e:  # noqa: BLE001 - e.g. ranks on different hosts after all
+                ok, err = False, e
+        # every follower attached (or not): agree, then drop the name so nothing is left in
+        # /dev/shm on a crash
+        oks = [None] * pctx.mp_size
+        dist.all_gather_object(oks, ok, group=pctx.mp_group)
         if driver:
             self.ch.unlink()
+        if not all(oks):
+            if driver:
+                self.ch.close()
+            raise ShmAttachError(f"shm step channel: {oks.count(False)} follower(s) could not attach"
+                                 + (f" ({err!r})" if not ok else ""))
         self.driver = driver
 
     def send(self, msg: np.ndarray) -> None:
@@ -100,10 +108,8 @@ class ShmStepChannel(StepChannel):
         self.ch.close()
 
 
-def _nccl_barrier(pctx: ParallelContext) -> None:
-    t = torch.zeros(1, device=pctx.device)
-    dist.all_reduce(t, group=pctx.mp_group)
-    torch.cuda.synchronize(pctx.device)
+class ShmAttachError(RuntimeError):
+    """A follower could not open the driver's segment (raised on every rank of the replica)."""
 
 
 class DistStepChannel(StepChannel):
@@ -129,11 +135,22 @@ class DistStepChannel(StepChannel):
         return self._bcast(torch.empty(n, dtype=torch.uint8)).cpu().numpy()
 
 
+def _host_key() -> tuple:
+    """(hostname, kernel boot id): containers on one host share the boot id, and two hosts that
+    happen to carry the same container hostname do not."""
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        boot = ""
+    return socket.gethostname(), boot
+
+
 def same_host(pctx: ParallelContext) -> bool:
     """Every rank of this rank's replica runs on this node (collective over the replica)."""
-    names = [None] * pctx.mp_size
-    dist.all_gather_object(names, socket.gethostname(), group=pctx.mp_group)
-    return len(set(names)) == 1
+    keys = [None] * pctx.mp_size
+    dist.all_gather_object(keys, _host_key(), group=pctx.mp_group)
+    return len(set(keys)) == 1
 
 
 def create(pctx: ParallelContext, slot_bytes: int, transport: Optional[str] = None) -> StepChannel:
@@ -143,7 +160,12 @@ def create(pctx: ParallelContext, slot_bytes: int, transport: Optional[str] = No
     if transport is None:
         transport = "shm" if same_host(pctx) else "dist"
     if transport == "shm":
-        return ShmStepChannel(pctx, slot_bytes)
+        try:
+            return ShmStepChannel(pctx, slot_bytes)
+        except ShmAttachError:
+            if os.environ.get("NGA_STEP_CHANNEL") == "shm":
+                raise          # asked for explicitly: fail loudly
+            return DistStepChannel(pctx, slot_bytes)
     if transport == "dist":
         return DistStepChannel(pctx, slot_bytes)
     raise ValueError(f"step channel transport must be shm or dist, not {transport!r}")

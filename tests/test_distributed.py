@@ -391,3 +391,51 @@ def test_sharded_random_ids_are_global():
         p.join(60)
     all_ids = sorted(i for _, ids, _ in got for i in ids)
     assert all_ids == list(range(101)) and all(n == 101 for _, _, n in got)
+
+
+def _step_channel_fallback_worker(rank, world, port, q):
+    import os
+
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import numpy as np
+
+    from nv_genai_amd.parallel import dist as pd
+    from nv_genai_amd.parallel import step_channel as sc
+
+    pctx = pd.init_distributed(tp_size=2, backend="gloo", device="cpu")
+    if rank == 1:   # this follower cannot open the driver's segment (as on another host)
+        real = sc.rt.ShmChannel
+
+        def failing(name, create, *a):
+            if not create:
+                raise OSError("no such segment")
+            return real(name, create, *a)
+
+        sc.rt = type("RT", (), {"ShmChannel": staticmethod(failing)})
+    chan = sc.create(pctx, 4096, transport="shm")
+    msg = np.arange(100, dtype=np.int64)
+    if rank == 0:
+        chan.send(msg)
+        got = None
+    else:
+        got = chan.recv().view(np.int64).tolist()
+    q.put({"rank": rank, "chan": type(chan).__name__, "got": got})
+    pd.destroy()
+
+
+def test_step_channel_falls_back_when_a_follower_cannot_attach():
+    """A replica whose follower cannot open the shared-memory segment (ranks on different hosts
+    that looked alike) agrees on the broadcast channel on every rank instead of hanging."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_step_channel_fallback_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r["rank"])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r["chan"] for r in res] == ["DistStepChannel", "DistStepChannel"]
+    assert res[1]["got"] == list(range(100))
