@@ -14,11 +14,25 @@ from __future__ import annotations
 
 import json
 import os
+import threading
 from typing import Iterator, List, Optional, Sequence
 
 import requests
 
 from .local import Messages, normalize_messages
+
+
+_TLS = threading.local()
+
+
+def _session() -> requests.Session:
+    """A keep-alive ``requests.Session`` per thread (Sessions are not thread-safe): the vector
+    store's query batcher embeds every retrieval batch over HTTP in the split topology, and a
+    fresh TCP connection per call showed in its profile (profiles/r5_http/)."""
+    s = getattr(_TLS, "s", None)
+    if s is None:
+        s = _TLS.s = requests.Session()
+    return s
 
 
 def _base(url: str) -> str:
@@ -60,7 +74,7 @@ class ChatClient:
         return b
 
     def stream(self, messages: Messages, **kw) -> Iterator[str]:
-        with requests.post(f"{self.base}/chat/completions", json=self._body(messages, True, **kw),
+        with _session().post(f"{self.base}/chat/completions", json=self._body(messages, True, **kw),
                            headers={**_headers(self.api_key), **self.extra_headers},
                            stream=True, timeout=self.timeout) as r:
             r.raise_for_status()
@@ -132,7 +146,7 @@ class ChatClient:
                     return
 
     def invoke(self, messages: Messages, **kw) -> str:
-        r = requests.post(f"{self.base}/chat/completions", json=self._body(messages, False, **kw),
+        r = _session().post(f"{self.base}/chat/completions", json=self._body(messages, False, **kw),
                           headers={**_headers(self.api_key), **self.extra_headers}, timeout=self.timeout)
         r.raise_for_status()
         return r.json()["choices"][0]["message"]["content"]
@@ -240,7 +254,7 @@ class EmbeddingsClient:
             body = {"input": list(texts[i:i + self.batch_size]), "model": self.model,
                     "input_type": input_type, "truncate": self.truncate,
                     "encoding_format": "float"}
-            r = requests.post(f"{self.base}/embeddings", json=body, headers=_headers(self.api_key),
+            r = _session().post(f"{self.base}/embeddings", json=body, headers=_headers(self.api_key),
                               timeout=self.timeout)
             r.raise_for_status()
             data = sorted(r.json()["data"], key=lambda d: d["index"])
@@ -262,7 +276,7 @@ class EmbeddingsClient:
         for i in range(0, len(texts), self.batch_size):
             body = {"input": list(texts[i:i + self.batch_size]), "model": self.model, "input_type": "query",
                     "truncate": self.truncate, "encoding_format": "base64"}
-            r = requests.post(f"{self.base}/embeddings", json=body, headers=_headers(self.api_key),
+            r = _session().post(f"{self.base}/embeddings", json=body, headers=_headers(self.api_key),
                               timeout=self.timeout)
             r.raise_for_status()
             for d in sorted(r.json()["data"], key=lambda d: d["index"]):
@@ -287,7 +301,7 @@ class RerankClient:
     def rank(self, query: str, passages: Sequence[str]) -> List[dict]:
         body = {"model": self.model, "query": {"text": query},
                 "passages": [{"text": p} for p in passages]}
-        r = requests.post(f"{self.base}/ranking", json=body, headers=_headers(self.api_key),
+        r = _session().post(f"{self.base}/ranking", json=body, headers=_headers(self.api_key),
                           timeout=self.timeout)
         r.raise_for_status()
         return r.json()["rankings"]
