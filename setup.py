@@ -37,7 +37,7 @@ setup(
     packages=find_packages(include=["nv_genai_amd", "nv_genai_amd.*"]),
     package_data={"nv_genai_amd": ["*.so", "assets/*", "assets/*/*", "csrc/*", "csrc/*/*"]},
     install_requires=["torch", "numpy", "fastapi", "uvicorn", "pydantic>=2", "tokenizers", "safetensors",
-                      "jinja2", "requests", "httpx", "pyyaml"],
+                      "jinja2", "requests", "httpx", "aiohttp", "pyyaml"],
     extras_require={"test": ["pytest", "pytest-timeout", "hypothesis"]},
     entry_points={"console_scripts": [
         "nga-model-server = nv_genai_amd.serving.model_server:main",
