@@ -52,14 +52,16 @@ def _free_port() -> int:
     return p
 
 
-def _server_quantiles(text: str) -> dict:
-    """p50 (ms) of the chain server's own request-phase summaries (whole run, warmup included):
-    chain_wait = request arrival -> retrieval + prompt queued on the engine (worker-thread
-    queueing included), chain = that work alone, ttft = arrival -> first token."""
+def _server_quantiles(text: str, prefix: str = "chain_server_") -> dict:
+    """p50 (ms) of a server's own request-phase summaries (whole run, warmup included). Chain
+    server: chain_wait = request arrival -> retrieval + prompt queued on the engine (worker-thread
+    queueing included), chain = that work alone, ttft = arrival -> first token. Model server
+    (split topology): ttft / request = its own receipt of the chat request -> first token / end,
+    embed = one /v1/embeddings call."""
     out = {}
     for line in text.splitlines():
-        if line.startswith("chain_server_") and 'quantile="0.5"' in line:
-            name = line.split("{")[0][len("chain_server_"):]
+        if line.startswith(prefix) and 'quantile="0.5"' in line:
+            name = line.split("{")[0][len(prefix):]
             if name == "retrieval_batch_size":
                 out[name] = float(line.rsplit(" ", 1)[1])
             elif name.endswith("_seconds"):
@@ -276,6 +278,8 @@ def main(argv=None):
         questions = [gen.question() for _ in range(4096)]
         results, t_start, engine_window, gaps = asyncio.run(_load(base + "/generate", args, questions))
         server_side = _server_quantiles(httpx.get(base + "/metrics", timeout=30).text)
+        model_side = (_server_quantiles(httpx.get(args.engine_metrics_url, timeout=30).text, "model_server_")
+                      if args.topology == "split" else None)
         t_end = max(r[3] for r in results)
         elapsed = t_end - t_start
         lat = sorted(r[0] for r in results)
@@ -297,6 +301,7 @@ def main(argv=None):
                           "example": args.example, "max_tokens": args.max_tokens},
                "dtype": "bf16", "data": "synthetic: random-init weights, 1M random unit-vector index, generated questions",
                "setup_s": round(setup_s, 1), "server_p50_ms": server_side,
+               **({"model_server_p50_ms": model_side} if model_side is not None else {}),
                "engine_window": engine_window}
         line = json.dumps(res)
         print(line, flush=True)

@@ -60,6 +60,7 @@ def test_http_rag_benchmark_split_topology_cpu(tmp_path):
     assert res["sse_gap_ms"]["frames"] > 0
     ew = res["engine_window"]
     assert ew["steps"] > 0 and ew["prefix_cache"]["prompt_tokens_total"] > 0, ew
+    assert "ttft" in res["model_server_p50_ms"], res["model_server_p50_ms"]   # the model server's own phases
 
 
 def test_headline_bench_two_ranks_gloo():
