@@ -48,6 +48,7 @@ setup(
         "nga-pretrain = nv_genai_amd.training.pretrain:main",
         "nga-evaluate = nv_genai_amd.tools.evaluation.__main__:main",
         "nga-ingest = nv_genai_amd.ingest.streaming:main",
+        "nga-doctor = nv_genai_amd.tools.doctor:main",
     ]},
     cmdclass={"build_py": BuildNative},
 )

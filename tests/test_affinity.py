@@ -3,6 +3,8 @@ an 8-GPU, two-socket node (GPUs 0-3 on node 0, 4-7 on node 1), visibility masks,
 share a node split its cores, and a process whose CPU set excludes the node."""
 import os
 
+import pytest
+
 from nv_genai_amd.utils import affinity
 
 
@@ -79,3 +81,31 @@ def test_bind_applies_and_sizes_pools(tmp_path, monkeypatch):
     assert pl.applied and calls == [pl.cpus] and env["RAYON_NUM_THREADS"] == "24"
     off = affinity.bind_local_rank(3, 8, root, env={"NGA_NUMA_BIND": "0"})
     assert not off.applied and len(calls) == 1
+
+
+def test_doctor_report_on_this_host(tmp_path):
+    """tools/doctor.py: the deployment report loads both native libraries, lists the code
+    objects bundled in _C (gfx950) and the kernel-form registry, and reads gfx targets from a
+    HIP binary's offload-bundle ids."""
+    from nv_genai_amd.tools import doctor
+
+    rep = doctor.collect()
+    assert rep["native_C"] and rep["native_rt"], rep["problems"]
+    assert rep["native_C_targets"] == ["gfx950"]
+    assert set(rep["kernel_forms"]) >= {"decode_dma", "prefill_ks"}
+    fake = tmp_path / "x.so"
+    fake.write_bytes(b"\0junk__CLANG_OFFLOAD_BUNDLE__hipv4-amdgcn-amd-amdhsa--gfx942\0more")
+    assert doctor._gfx_targets(str(fake)) == ["gfx942"]
+    assert doctor.main(["--json"]) == (1 if rep["problems"] else 0)
+
+
+@pytest.mark.gpu
+def test_doctor_kernel_self_test_gpu():
+    """The deployment check's GPU self-test (RMSNorm, decode-shape GEMM + SwiGLU, paged decode
+    attention against fp32) passes on the box."""
+    from nv_genai_amd.tools import doctor
+
+    rep = doctor.collect(run_kernels=True)
+    assert all(v["ok"] for v in rep["self_test"].values()), rep["self_test"]
+    assert rep["gpus"] and rep["gpus"][0]["arch"].startswith("gfx950")
+    assert not rep["problems"], rep["problems"]
