@@ -129,7 +129,7 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
                embed_name: str = "snowflake/arctic-embed-l", rerank_name: str = "nv-rerank-qa-mistral-4b:1",
                batch_delay_s: float = 0.002, vlm=None, vlm_service=None, vlm_name: str = "ai-neva-22b",
                deplot=None, deplot_names=("google/deplot", "ai-google-deplot"), reward=None,
-               reward_name: str = "nvidia/nemotron-4-340b-reward") -> FastAPI:
+               reward_name: str = "nvidia/nemotron-4-340b-reward", max_inflight: Optional[int] = None) -> FastAPI:
     """``vlm`` / ``vlm_service``: a :class:`~nv_genai_amd.models.vision.VisionLanguageModel`
     and the :class:`EngineService` over its engine; chat requests with ``image_url`` parts
     (or ``model == vlm_name``) go there — the NeVA / DePlot endpoint contract of the
@@ -139,8 +139,14 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
     text as the rendered header prompt; custom_pdf_parser.py:55-71). ``reward``: a
     :class:`~nv_genai_amd.models.reward.RewardModel`; chat requests naming ``reward_name``
     score their last user / assistant turns and answer "helpfulness:x,correctness:y,..." (the
-    reward endpoint the KG-RAG evaluation calls, evaluation.py:38-56)."""
+    reward endpoint the KG-RAG evaluation calls, evaluation.py:38-56). ``max_inflight`` (default
+    ``NGA_MAX_INFLIGHT``, 0 = no limit): load shedding — a generation request that would take the
+    LLM service past this many in-flight sequences gets 429 with ``Retry-After`` instead of
+    queueing without bound behind the running batch."""
     app = FastAPI(title="nv_genai_amd model server")
+    if max_inflight is None:
+        max_inflight = int(os.environ.get("NGA_MAX_INFLIGHT", "0"))
+    app.state.max_inflight = max_inflight
     metrics = Registry()
 
     from .engine_service import EngineError
@@ -180,6 +186,16 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
             raise ValueError("a DePlot request needs at least one image")
         futs = [deplot_batcher.submit(im, " ".join(texts) or None, min(max_tokens, 512)) for im in images]
         return "\n".join(f.result() for f in futs)
+
+    def _shed(svc, n: int = 1):
+        """429 response when admitting ``n`` more sequences would exceed ``max_inflight``."""
+        cap = app.state.max_inflight
+        if cap and len(svc.handles) + n > cap:
+            metrics.inc("shed_requests_total")
+            return JSONResponse({"error": {"message": f"server busy: {len(svc.handles)} sequences in flight "
+                                                      f"(limit {cap})", "type": "rate_limit_exceeded"}},
+                                status_code=429, headers={"Retry-After": "1"})
+        return None
 
     def _need(x, what):
         if x is None:
@@ -303,6 +319,9 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
             if _has_images(req.messages):
                 return JSONResponse({"error": "this server hosts no vision-language model"}, status_code=400)
             svc = _need(app.state.llm, "LLM")
+            busy = _shed(svc, req.n)
+            if busy is not None:
+                return busy
             msgs = [{"role": m.role, "content": _content_text(m.content)} for m in req.messages]
             with tracer.span("chat.completions", {"model": req.model}, request.headers.get("traceparent")):
                 # off the event loop: a RAG prompt is ~1,200 tokens of encoding (GIL-free)
@@ -336,6 +355,9 @@ def create_app(llm_service=None, embed_engine=None, rerank_engine=None, llm_name
         rid = f"cmpl-{uuid.uuid4().hex}"
         if req.stream and (len(prompts) != 1 or req.n > 1):
             return JSONResponse({"error": "stream supports a single prompt and n = 1"}, status_code=400)
+        busy = _shed(svc, len(prompts) * req.n)
+        if busy is not None:
+            return busy
         handles = [h for p in prompts for h in _submit_n(svc, [tok.bos_id] + tok.encode(p), req)]
         if req.stream:
             return StreamingResponse(_run_stream(handles[0], rid, model, "text_completion", False, t0),
@@ -483,6 +505,8 @@ def main(argv=None):
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=8000)
     ap.add_argument("--max-num-seqs", type=int, default=256)
+    ap.add_argument("--max-inflight", type=int, default=None,
+                    help="429 beyond this many in-flight sequences (default NGA_MAX_INFLIGHT, 0 = no limit)")
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--kv-cache-fraction", type=float, default=0.3)
     ap.add_argument("--kv-cache-dtype", default="auto", choices=("auto", "fp8"),
@@ -536,7 +560,7 @@ def main(argv=None):
 
         rw = RewardModel(args.reward, device=args.device or ("cuda" if torch.cuda.is_available() else "cpu"))
     app = create_app(svc, emb, rr, vlm=vlm, vlm_service=vsvc, vlm_name=f"ai-{args.vlm}" if args.vlm else "ai-neva-22b",
-                     deplot=dp, reward=rw)
+                     deplot=dp, reward=rw, max_inflight=args.max_inflight)
     uvicorn.run(app, host=args.host, port=args.port, log_level=os.environ.get("LOGLEVEL", "info").lower())
 
 

@@ -304,3 +304,24 @@ def test_sse_delta_parser_splits_lines_and_utf8_across_chunks():
             if done:
                 break
         assert "".join(out) == "héllo 世界" and done, cut
+
+
+def test_load_shedding_429_when_inflight_limit_reached(server, client):
+    """max_inflight (NGA_MAX_INFLIGHT / --max-inflight): a generation request that would exceed
+    the in-flight sequence limit gets 429 + Retry-After instead of an unbounded queue; n choices
+    count as n sequences; under the limit requests run normally."""
+    svc = server.state.llm
+    body = {"messages": [{"role": "user", "content": "hi"}], "max_tokens": 2, "ignore_eos": True}
+    old = server.state.max_inflight
+    try:
+        server.state.max_inflight = 2
+        svc.handles[-99] = object()          # one sequence already in flight
+        r = client.post("/v1/chat/completions", json={**body, "n": 2})
+        assert r.status_code == 429 and r.headers["retry-after"] == "1"
+        assert r.json()["error"]["type"] == "rate_limit_exceeded"
+        assert client.post("/v1/completions", json={"prompt": ["a", "b"], "max_tokens": 2}).status_code == 429
+        assert client.post("/v1/chat/completions", json=body).status_code == 200   # 1 + 1 <= 2
+        assert "model_server_shed_requests_total" in client.get("/metrics").text
+    finally:
+        svc.handles.pop(-99, None)
+        server.state.max_inflight = old
