@@ -40,10 +40,18 @@ __device__ __forceinline__ void put8(CT* dst, u16x8 v, float inv_s) {
   }
 }
 
-template <typename CT>
+template <typename CT, bool NT = false>
 __device__ __forceinline__ void put1(CT* dst, uint16_t v, float inv_s) {
-  if constexpr (sizeof(CT) == 2) *dst = v;
-  else *dst = f32_to_fp8(bf2f(v) * inv_s);
+  // NT: a non-temporal store — one token's V^T column touches a different 128-B page row per d,
+  // 2 bytes each, and those rows are not in the cache (kernel form rope_vnt, A/B)
+  if constexpr (sizeof(CT) == 2) {
+    if constexpr (NT) __builtin_nontemporal_store(v, dst);
+    else *dst = v;
+  } else {
+    const CT b = f32_to_fp8(bf2f(v) * inv_s);
+    if constexpr (NT) __builtin_nontemporal_store(b, dst);
+    else *dst = b;
+  }
 }
 
 // Source of the qkv values: the bf16 projection output, or (part != nullptr) the S fp32 K-split
@@ -92,7 +100,7 @@ __device__ __forceinline__ uint32_t ld2(const uint16_t* qkv, const QkvSrc& src, 
   return (uint32_t)f2bf(a[0]) | ((uint32_t)f2bf(a[1]) << 16);
 }
 
-template <int D, typename CT>
+template <int D, typename CT, bool NT = false>
 __global__ void rope_cache_kernel(uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos,
                                   const float* __restrict__ cos_sin,
                                   const int32_t* __restrict__ slots, CT* __restrict__ kc,
@@ -145,7 +153,7 @@ __global__ void rope_cache_kernel(uint16_t* __restrict__ qkv, const int32_t* __r
       if (slot >= 0) {
         CT* dst = vc + ((blk * Hkv + vh) * D + d0) * BS + off;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) put1(dst + (int64_t)j * BS, v[j], inv_vs);
+        for (int j = 0; j < 8; ++j) put1<CT, NT>(dst + (int64_t)j * BS, v[j], inv_vs);
       }
     }
   }
@@ -160,7 +168,7 @@ __global__ void rope_cache_kernel(uint16_t* __restrict__ qkv, const int32_t* __r
 // * v head: stages the RT tokens x D tile in LDS and writes the transposed page rows with
 //   lanes = tokens, so the consecutive slots of a prefill chunk become one store per d row
 //   instead of scattered 2-B ones per token.
-template <int D, typename CT>
+template <int D, typename CT, bool NT = false>
 __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos, const float* __restrict__ cos_sin,
     const int32_t* __restrict__ slots, CT* __restrict__ kc, CT* __restrict__ vc,
@@ -243,7 +251,7 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
   const int slot = t < T ? slots[t] : -1;
   if (slot < 0) return;
   CT* dst = vc + ((int64_t)(slot / BS) * Hkv + vh) * D * BS + slot % BS;
-  for (int d = w * PH + ph; d < D; d += nw * PH) put1(dst + (int64_t)d * BS, tile[tl * LDP + d], inv_vs);
+  for (int d = w * PH + ph; d < D; d += nw * PH) put1<CT, NT>(dst + (int64_t)d * BS, tile[tl * LDP + d], inv_vs);
 }
 
 template <typename CT>
@@ -251,6 +259,7 @@ static void rope_dispatch(uint16_t* qkv, const int32_t* pos, const float* cos_si
                           const int32_t* slots, CT* kc, CT* vc, int64_t T, int Hq, int Hkv, int D,
                           int BS, float inv_ks, float inv_vs, QkvSrc src, hipStream_t stream) {
   const int rt = 4096 / D;   // tokens per tile of the tiled kernel
+  const bool nt = kernel_form(KF_ROPE_VNT) != 0;
   if (T >= rt) {
     // rotary heads per workgroup: enough workgroups to fill the chip, up to 8 heads sharing
     // one cos/sin load
@@ -259,13 +268,21 @@ static void rope_dispatch(uint16_t* qkv, const int32_t* pos, const float* cos_si
     int hg = 8;
     while (hg > 1 && tiles * ((nrot + hg - 1) / hg) < 512) hg /= 2;
     dim3 grid((unsigned)tiles, (unsigned)((nrot + hg - 1) / hg + Hkv)), block(256);
-#define NGA_RT(DD) rope_cache_tiled_kernel<DD, CT><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS, hg, inv_ks, inv_vs, src)
+#define NGA_RT(DD)                                                                                      \
+  do {                                                                                                  \
+    if (nt) rope_cache_tiled_kernel<DD, CT, true><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS, hg, inv_ks, inv_vs, src); \
+    else rope_cache_tiled_kernel<DD, CT><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS, hg, inv_ks, inv_vs, src); \
+  } while (0)
     if (D == 128) NGA_RT(128); else if (D == 256) NGA_RT(256); else if (D == 64) NGA_RT(64);
 #undef NGA_RT
     return;
   }
   dim3 grid((unsigned)T), block(256);
-#define NGA_R1(DD) rope_cache_kernel<DD, CT><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, BS, inv_ks, inv_vs, src)
+#define NGA_R1(DD)                                                                                      \
+  do {                                                                                                  \
+    if (nt) rope_cache_kernel<DD, CT, true><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, BS, inv_ks, inv_vs, src); \
+    else rope_cache_kernel<DD, CT><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, BS, inv_ks, inv_vs, src); \
+  } while (0)
   if (D == 128) NGA_R1(128); else if (D == 256) NGA_R1(256); else if (D == 64) NGA_R1(64);
 #undef NGA_R1
 }

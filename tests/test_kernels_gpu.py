@@ -79,10 +79,12 @@ def _make_cache(nb, Hkv, D, dev):
     return kc, vc
 
 
+@pytest.mark.parametrize("vnt", [0, 1])
 @pytest.mark.parametrize("Hq,Hkv,D,T", [(32, 8, 128, 70), (32, 8, 128, 7), (32, 8, 128, 300), (4, 2, 64, 130)])
-def test_rope_cache(gpu, Hq, Hkv, D, T):
+def test_rope_cache(gpu, kernel_form, Hq, Hkv, D, T, vnt):
     """per-token kernel (T < 64) and tiled kernel (T >= 64: LDS-transposed Vt page rows),
-    random slots with a padding row (-1)."""
+    random slots with a padding row (-1); vnt: the non-temporal Vt store form (rope_vnt)."""
+    kernel_form("rope_vnt", vnt)
     torch.manual_seed(2)
     qkv = _bf(T, (Hq + 2 * Hkv) * D, dev=gpu)
     pos = torch.randint(0, 4000, (T,), dtype=torch.int32, device=gpu)
