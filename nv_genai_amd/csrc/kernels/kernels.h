@@ -17,7 +17,7 @@ enum KernelForm {
   KF_SEARCH_NT,        // NGA_SEARCH_NT: 1 non-temporal index-row loads (register search form)
   KF_PREFILL_V1,       // NGA_PREFILL_V1: 1 disables the 32x32 prefill kernel
   KF_PREFILL_KS,       // NGA_PREFILL_KS: 1 / 2 forces the 32x32 prefill kernel's wave-group count
-  KF_ROPE_VNT,         // NGA_ROPE_VNT: 1 non-temporal 2-byte V^T page stores in the RoPE / KV-write kernels
+  KF_ROPE_VNT,         // NGA_ROPE_VNT: non-temporal 2-byte V^T page stores in the RoPE / KV-write kernels: 1 all, 2 tokens with no same-page neighbour
   KF_COUNT
 };
 int kernel_form(KernelForm f);

@@ -168,7 +168,7 @@ __global__ void rope_cache_kernel(uint16_t* __restrict__ qkv, const int32_t* __r
 // * v head: stages the RT tokens x D tile in LDS and writes the transposed page rows with
 //   lanes = tokens, so the consecutive slots of a prefill chunk become one store per d row
 //   instead of scattered 2-B ones per token.
-template <int D, typename CT, bool NT = false>
+template <int D, typename CT, int NTM = 0>
 __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos, const float* __restrict__ cos_sin,
     const int32_t* __restrict__ slots, CT* __restrict__ kc, CT* __restrict__ vc,
@@ -251,7 +251,20 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
   const int slot = t < T ? slots[t] : -1;
   if (slot < 0) return;
   CT* dst = vc + ((int64_t)(slot / BS) * Hkv + vh) * D * BS + slot % BS;
-  for (int d = w * PH + ph; d < D; d += nw * PH) put1<CT, NT>(dst + (int64_t)d * BS, tile[tl * LDP + d], inv_vs);
+  // NTM 1: every V^T store non-temporal; 2: only a token with no neighbour in the same page row
+  // (a decode row: its 2-byte column would leave a dirty partial line in L2 for each of its D
+  // page rows), while runs of consecutive slots (prefill chunks) keep cached stores, which the
+  // L2 merges into whole lines
+  bool nt = NTM == 1;
+  if constexpr (NTM == 2) {
+    const int sp = t > 0 ? slots[t - 1] : -2, sn = t + 1 < T ? slots[t + 1] : -2;
+    nt = !((sp >= 0 && sp + 1 == slot && sp / BS == slot / BS) || (sn == slot + 1 && sn / BS == slot / BS));
+  }
+  if (nt) {
+    for (int d = w * PH + ph; d < D; d += nw * PH) put1<CT, true>(dst + (int64_t)d * BS, tile[tl * LDP + d], inv_vs);
+  } else {
+    for (int d = w * PH + ph; d < D; d += nw * PH) put1<CT, false>(dst + (int64_t)d * BS, tile[tl * LDP + d], inv_vs);
+  }
 }
 
 template <typename CT>
@@ -259,7 +272,7 @@ static void rope_dispatch(uint16_t* qkv, const int32_t* pos, const float* cos_si
                           const int32_t* slots, CT* kc, CT* vc, int64_t T, int Hq, int Hkv, int D,
                           int BS, float inv_ks, float inv_vs, QkvSrc src, hipStream_t stream) {
   const int rt = 4096 / D;   // tokens per tile of the tiled kernel
-  const bool nt = kernel_form(KF_ROPE_VNT) != 0;
+  const int nt = kernel_form(KF_ROPE_VNT);
   if (T >= rt) {
     // rotary heads per workgroup: enough workgroups to fill the chip, up to 8 heads sharing
     // one cos/sin load
@@ -270,7 +283,8 @@ static void rope_dispatch(uint16_t* qkv, const int32_t* pos, const float* cos_si
     dim3 grid((unsigned)tiles, (unsigned)((nrot + hg - 1) / hg + Hkv)), block(256);
 #define NGA_RT(DD)                                                                                      \
   do {                                                                                                  \
-    if (nt) rope_cache_tiled_kernel<DD, CT, true><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS, hg, inv_ks, inv_vs, src); \
+    if (nt == 1) rope_cache_tiled_kernel<DD, CT, 1><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS, hg, inv_ks, inv_vs, src); \
+    else if (nt == 2) rope_cache_tiled_kernel<DD, CT, 2><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS, hg, inv_ks, inv_vs, src); \
     else rope_cache_tiled_kernel<DD, CT><<<grid, block, 0, stream>>>(qkv, pos, cos_sin, slots, kc, vc, T, Hq, Hkv, BS, hg, inv_ks, inv_vs, src); \
   } while (0)
     if (D == 128) NGA_RT(128); else if (D == 256) NGA_RT(256); else if (D == 64) NGA_RT(64);

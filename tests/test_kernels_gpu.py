@@ -79,7 +79,7 @@ def _make_cache(nb, Hkv, D, dev):
     return kc, vc
 
 
-@pytest.mark.parametrize("vnt", [0, 1])
+@pytest.mark.parametrize("vnt", [0, 1, 2])
 @pytest.mark.parametrize("Hq,Hkv,D,T", [(32, 8, 128, 70), (32, 8, 128, 7), (32, 8, 128, 300), (4, 2, 64, 130)])
 def test_rope_cache(gpu, kernel_form, Hq, Hkv, D, T, vnt):
     """per-token kernel (T < 64) and tiled kernel (T >= 64: LDS-transposed Vt page rows),
