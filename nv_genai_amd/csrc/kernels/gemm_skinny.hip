@@ -57,6 +57,13 @@ __device__ __forceinline__ void sk_wait_vm() {
 }
 
 __device__ __forceinline__ float sk_silu(float x) { return x / (1.f + __expf(-x)); }
+
+// a 16-B slab read: plain, or non-temporal (NT: the slabs are read once, kernel form skinny_snt 2)
+template <bool NT>
+__device__ __forceinline__ f32x4 sk_ld4(const float* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  else return *reinterpret_cast<const f32x4*>(p);
+}
 }  // namespace
 
 template <int BN, int BM, int WN, int WM, int NSTAGE, int EPI>
@@ -224,7 +231,8 @@ __global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmPar
       for (int nt = 0; nt < NTW; ++nt) {
         const int n = n_base + nt * 16 + 4 * h;
         if (n >= P.N) continue;
-        *reinterpret_cast<f32x4*>(op + n) = acc[nt][mt];
+        if (P.snt) __builtin_nontemporal_store(acc[nt][mt], reinterpret_cast<f32x4*>(op + n));
+        else *reinterpret_cast<f32x4*>(op + n) = acc[nt][mt];
       }
     } else {
       uint16_t* op = reinterpret_cast<uint16_t*>(P.out) + (int64_t)t * P.ldo;
@@ -241,6 +249,7 @@ __global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmPar
 }
 
 // out[m, n] = bf16(sum_s P[s, m, n]); 8 features per thread
+template <bool NT>
 __global__ void splitk_reduce_kernel(const float* __restrict__ P, int S, int M, int N,
                                      uint16_t* __restrict__ out, int64_t ldo) {
   const int nv = N / 8;
@@ -251,10 +260,10 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ P, int S, int M, 
     const int64_t m = i / nv;
     const int c = (int)(i - m * nv) * 8;
     const float* p = P + m * N + c;
-    f32x4 a0 = *reinterpret_cast<const f32x4*>(p), a1 = *reinterpret_cast<const f32x4*>(p + 4);
+    f32x4 a0 = sk_ld4<NT>(p), a1 = sk_ld4<NT>(p + 4);
     for (int s = 1; s < S; ++s) {
-      a0 += *reinterpret_cast<const f32x4*>(p + s * slab);
-      a1 += *reinterpret_cast<const f32x4*>(p + s * slab + 4);
+      a0 += sk_ld4<NT>(p + s * slab);
+      a1 += sk_ld4<NT>(p + s * slab + 4);
     }
     u16x8 o;
 #pragma unroll
@@ -268,6 +277,7 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ P, int S, int M, 
 
 // out[m, f] = bf16(silu(sum_s P[s, m, f]) * sum_s P[s, m, F + f]): the K-split gate / up
 // projection (slabs in the standard [gate | up] column order) summed by its SwiGLU consumer
+template <bool NT>
 __global__ void splitk_swiglu_kernel(const float* __restrict__ P, int S, int M, int F,
                                      uint16_t* __restrict__ out, int64_t ldo) {
   const int nv = F / 8;
@@ -278,14 +288,14 @@ __global__ void splitk_swiglu_kernel(const float* __restrict__ P, int S, int M, 
     const int64_t m = i / nv;
     const int c = (int)(i - m * nv) * 8;
     const float* p = P + m * 2 * F + c;
-    f32x4 g0 = *reinterpret_cast<const f32x4*>(p), g1 = *reinterpret_cast<const f32x4*>(p + 4);
-    f32x4 u0 = *reinterpret_cast<const f32x4*>(p + F), u1 = *reinterpret_cast<const f32x4*>(p + F + 4);
+    f32x4 g0 = sk_ld4<NT>(p), g1 = sk_ld4<NT>(p + 4);
+    f32x4 u0 = sk_ld4<NT>(p + F), u1 = sk_ld4<NT>(p + F + 4);
     for (int s = 1; s < S; ++s) {
       const float* q = p + s * slab;
-      g0 += *reinterpret_cast<const f32x4*>(q);
-      g1 += *reinterpret_cast<const f32x4*>(q + 4);
-      u0 += *reinterpret_cast<const f32x4*>(q + F);
-      u1 += *reinterpret_cast<const f32x4*>(q + F + 4);
+      g0 += sk_ld4<NT>(q);
+      g1 += sk_ld4<NT>(q + 4);
+      u0 += sk_ld4<NT>(q + F);
+      u1 += sk_ld4<NT>(q + F + 4);
     }
     u16x8 o;
 #pragma unroll
@@ -300,6 +310,7 @@ __global__ void splitk_swiglu_kernel(const float* __restrict__ P, int S, int M, 
 // resid += sum_s P[s] (one rounding to the bf16 residual); out = rmsnorm(resid) * w.
 // One workgroup per row, 8 features per lane (the add_rmsnorm kernel with the split-K sum of
 // the producing GEMM folded into its load).
+template <bool NT>
 __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(const float* __restrict__ P, int S,
                                                                   int M, uint16_t* __restrict__ resid,
                                                                   const uint16_t* __restrict__ w,
@@ -314,10 +325,10 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(const float* _
   float ss = 0.f;
   if (active) {
     const float* p = P + row * H + c;
-    f32x4 a0 = *reinterpret_cast<const f32x4*>(p), a1 = *reinterpret_cast<const f32x4*>(p + 4);
+    f32x4 a0 = sk_ld4<NT>(p), a1 = sk_ld4<NT>(p + 4);
     for (int s = 1; s < S; ++s) {
-      a0 += *reinterpret_cast<const f32x4*>(p + s * slab);
-      a1 += *reinterpret_cast<const f32x4*>(p + s * slab + 4);
+      a0 += sk_ld4<NT>(p + s * slab);
+      a1 += sk_ld4<NT>(p + s * slab + 4);
     }
     const u16x8 v = load8(resid + row * H + c);
     u16x8 st;
@@ -410,7 +421,8 @@ void launch_splitk_reduce(const float* P, int S, int M, int N, uint16_t* out, in
   if (M == 0) return;
   int64_t g = ((int64_t)M * (N / 8) + 255) / 256;
   if (g > 2048) g = 2048;
-  splitk_reduce_kernel<<<(unsigned)g, 256, 0, stream>>>(P, S, M, N, out, ldo);
+  if (kernel_form(KF_SKINNY_SNT) == 2) splitk_reduce_kernel<true><<<(unsigned)g, 256, 0, stream>>>(P, S, M, N, out, ldo);
+  else splitk_reduce_kernel<false><<<(unsigned)g, 256, 0, stream>>>(P, S, M, N, out, ldo);
 }
 
 void launch_splitk_swiglu(const float* P, int S, int M, int F, uint16_t* out, int64_t ldo,
@@ -418,7 +430,8 @@ void launch_splitk_swiglu(const float* P, int S, int M, int F, uint16_t* out, in
   if (M == 0) return;
   int64_t g = ((int64_t)M * (F / 8) + 255) / 256;
   if (g > 2048) g = 2048;
-  splitk_swiglu_kernel<<<(unsigned)g, 256, 0, stream>>>(P, S, M, F, out, ldo);
+  if (kernel_form(KF_SKINNY_SNT) == 2) splitk_swiglu_kernel<true><<<(unsigned)g, 256, 0, stream>>>(P, S, M, F, out, ldo);
+  else splitk_swiglu_kernel<false><<<(unsigned)g, 256, 0, stream>>>(P, S, M, F, out, ldo);
 }
 
 void launch_splitk_add_rmsnorm(const float* P, int S, int M, uint16_t* resid, const uint16_t* w,
@@ -426,7 +439,8 @@ void launch_splitk_add_rmsnorm(const float* P, int S, int M, uint16_t* resid, co
   if (M == 0) return;
   int t = (H / 8 + 63) / 64 * 64;
   if (t < 64) t = 64;
-  splitk_add_rmsnorm_kernel<<<M, t, 0, stream>>>(P, S, M, resid, w, eps, H, out);
+  if (kernel_form(KF_SKINNY_SNT) == 2) splitk_add_rmsnorm_kernel<true><<<M, t, 0, stream>>>(P, S, M, resid, w, eps, H, out);
+  else splitk_add_rmsnorm_kernel<false><<<M, t, 0, stream>>>(P, S, M, resid, w, eps, H, out);
 }
 
 }  // namespace nga

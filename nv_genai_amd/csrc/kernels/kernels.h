@@ -18,6 +18,7 @@ enum KernelForm {
   KF_PREFILL_V1,       // NGA_PREFILL_V1: 1 disables the 32x32 prefill kernel
   KF_PREFILL_KS,       // NGA_PREFILL_KS: 1 / 2 forces the 32x32 prefill kernel's wave-group count
   KF_ROPE_VNT,         // NGA_ROPE_VNT: non-temporal 2-byte V^T page stores in the RoPE / KV-write kernels: 1 all, 2 tokens with no same-page neighbour
+  KF_SKINNY_SNT,       // NGA_SKINNY_SNT: decode-shape GEMM fp32 K-split slabs: 1 non-temporal stores, 2 also non-temporal loads in the split-K consumers
   KF_COUNT
 };
 int kernel_form(KernelForm f);
@@ -202,6 +203,7 @@ struct SkinnyGemmParams {
   int wpack;           // 1: w is tile-packed [nN][K/64][BN][64] for this cfg's BN (pack_weight)
   int xpack;           // 1: x is tile-packed [nM][K/64][BM][64] for this cfg's BM (pack_rows)
   int wnt;             // 1: weight DMA with the non-temporal cache policy (streamed once)
+  int snt;             // 1: fp32 slab stores (epi 1) non-temporal (kernel form skinny_snt)
 };
 int skinny_gemm_cfg_count();
 void skinny_gemm_cfg_info(int cfg, int* info);   // {BN, BM, WN, WM, NSTAGE}

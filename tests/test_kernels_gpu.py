@@ -727,8 +727,10 @@ def test_gemv(gpu, M, N, K):
     _close_rows(ops.gemv(x, w, 2), sw, rel=1e-2)
 
 
-def test_splitk_swiglu(gpu):
-    """silu(sum of gate slabs) * sum of up slabs, against fp32."""
+@pytest.mark.parametrize("snt", [0, 2])
+def test_splitk_swiglu(gpu, kernel_form, snt):
+    """silu(sum of gate slabs) * sum of up slabs, against fp32 (snt 2: non-temporal slab loads)."""
+    kernel_form("skinny_snt", snt)
     torch.manual_seed(4)
     S, M, F = 3, 45, 1024
     P = torch.randn(S, M, 2 * F, device=gpu)
@@ -738,7 +740,9 @@ def test_splitk_swiglu(gpu):
     _close_rows(y, y_ref, rel=1e-2)
 
 
-def test_splitk_add_rmsnorm(gpu):
+@pytest.mark.parametrize("snt", [0, 2])
+def test_splitk_add_rmsnorm(gpu, kernel_form, snt):
+    kernel_form("skinny_snt", snt)
     torch.manual_seed(3)
     S, M, H = 4, 77, 4096
     P = torch.randn(S, M, H, device=gpu) * 0.3
@@ -830,3 +834,17 @@ def test_skinny_table_production_shapes(gpu):
             del ref
         del w
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("snt", [1, 2])
+def test_skinny_slab_nontemporal_stores_bitwise(gpu, kernel_form, snt):
+    """skinny_snt: the fp32 K-split slabs written with non-temporal stores are bit-identical to
+    the cached-store form (only the cache policy differs)."""
+    torch.manual_seed(6)
+    x, w = _bf(96, 4096, dev=gpu), _bf(4096, 4096, dev=gpu)
+    kernel_form("skinny_snt", 0)
+    a = ops.skinny_gemm(x, w, 1, 4, 1).clone()
+    kernel_form("skinny_snt", snt)
+    b = ops.skinny_gemm(x, w, 1, 4, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
