@@ -873,7 +873,7 @@ const FormSpec kForms[KF_COUNT] = {
     {"rmsnorm_wave", "NGA_RMSNORM_WAVE", 0}, {"search_dma", "NGA_SEARCH_DMA", 1},
     {"search_nt", "NGA_SEARCH_NT", 0}, {"prefill_v1", "NGA_PREFILL_V1", 0},
     {"prefill_ks", "NGA_PREFILL_KS", 0}, {"rope_vnt", "NGA_ROPE_VNT", 2},
-    {"skinny_snt", "NGA_SKINNY_SNT", 0}};
+    {"skinny_snt", "NGA_SKINNY_SNT", 0}, {"decode_dma_aux", "NGA_DECODE_DMA_AUX", 2}};
 std::atomic<int>* forms() {
   static std::atomic<int> v[KF_COUNT];
   static const bool init = [] {

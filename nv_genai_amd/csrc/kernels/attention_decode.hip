@@ -304,7 +304,9 @@ __device__ __forceinline__ int dvswz(int row) { return (row >> 1) & 7; }
 // goes out once this K is in registers and the next V^T once this V^T is, so one 16-KiB DMA is
 // always in flight. (A half-page ring, 32-key units, read each V^T row's 128-B line in two
 // 64-B halves and ran at 4.7 TB/s against 6.7.)
-template <bool RING>
+// AUX: cache policy of the KV-page DMA loads (form decode_dma_aux): 2 = nt (each page is read
+// once per step), 0 = default policy
+template <bool RING, int AUX>
 __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
     uint16_t* __restrict__ out, int64_t out_stride, const uint16_t* __restrict__ q,
     int64_t q_stride, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
@@ -354,13 +356,13 @@ __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
     for (int i = 0; i < 16; ++i) {
       const int key = 4 * i + (lane >> 4);
       __builtin_amdgcn_global_load_lds((gptr_t)(kp + key * 256 + (((lane & 15) ^ dkswz(key)) << 4)),
-                                       (lptr_t)(ks + i * 512), 16, 0, 2);
+                                       (lptr_t)(ks + i * 512), 16, 0, AUX);
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int row = 8 * i + (lane >> 3);
       __builtin_amdgcn_global_load_lds((gptr_t)(vp + row * 128 + (((lane & 7) ^ dvswz(row)) << 4)),
-                                       (lptr_t)(vs + i * 512), 16, 0, 2);
+                                       (lptr_t)(vs + i * 512), 16, 0, AUX);
     }
   };
 
@@ -387,7 +389,7 @@ __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
       for (int i = 0; i < 16; ++i) {
         const int key = 4 * i + (lane >> 4);
         __builtin_amdgcn_global_load_lds((gptr_t)(kp + key * 256 + (((lane & 15) ^ dkswz(key)) << 4)),
-                                         (lptr_t)(ks + i * 512), 16, 0, 2);
+                                         (lptr_t)(ks + i * 512), 16, 0, AUX);
       }
     };
     auto issue_v = [&](int64_t blk) {
@@ -396,7 +398,7 @@ __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
       for (int i = 0; i < 16; ++i) {
         const int row = 8 * i + (lane >> 3);
         __builtin_amdgcn_global_load_lds((gptr_t)(vp + row * 128 + (((lane & 7) ^ dvswz(row)) << 4)),
-                                         (lptr_t)(vs + i * 512), 16, 0, 2);
+                                         (lptr_t)(vs + i * 512), 16, 0, AUX);
       }
     };
     if (my_pages > 0) {
@@ -728,14 +730,17 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
     const int dma = kernel_form(KF_DECODE_DMA);
     if (kv_fp8) NGA_DEC(128, uint8_t);
     else if (dma && (pages + nparts - 1) / nparts <= DMA_MAX_PAGES) {
-      if (dma == 2)
-        decode_attn_dma_kernel<true><<<grid, 256, 0, stream>>>(
-            out, out_stride, q, q_stride, static_cast<const uint16_t*>(kc), static_cast<const uint16_t*>(vc),
-            block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, part_ml, part_o, window, skip_empty ? 1 : 0);
-      else
-        decode_attn_dma_kernel<false><<<grid, 256, 0, stream>>>(
-            out, out_stride, q, q_stride, static_cast<const uint16_t*>(kc), static_cast<const uint16_t*>(vc),
-            block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, part_ml, part_o, window, skip_empty ? 1 : 0);
+#define NGA_DMA(RING, AUX)                                                                                   \
+  decode_attn_dma_kernel<RING, AUX><<<grid, 256, 0, stream>>>(                                              \
+      out, out_stride, q, q_stride, static_cast<const uint16_t*>(kc), static_cast<const uint16_t*>(vc), \
+      block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, part_ml, part_o, window, skip_empty ? 1 : 0)
+      const bool cached = kernel_form(KF_DECODE_DMA_AUX) == 0;
+      if (dma == 2) {
+        if (cached) NGA_DMA(true, 0); else NGA_DMA(true, 2);
+      } else {
+        if (cached) NGA_DMA(false, 0); else NGA_DMA(false, 2);
+      }
+#undef NGA_DMA
     } else NGA_DEC(128, uint16_t);
     if (nparts > 1)
       decode_attn_reduce_kernel<128><<<g2, 128, 0, stream>>>(out, out_stride, part_ml, part_o, Hq, nparts,

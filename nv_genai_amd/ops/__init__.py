@@ -357,7 +357,7 @@ class DecodeWorkspace:
 
 
 KERNEL_FORMS = ("decode_dma", "decode_nt", "rmsnorm_wave", "search_dma", "search_nt", "prefill_v1",
-                "prefill_ks", "rope_vnt", "skinny_snt")
+                "prefill_ks", "rope_vnt", "skinny_snt", "decode_dma_aux")
 
 
 def kernel_form(name: str) -> int:

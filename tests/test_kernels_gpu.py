@@ -139,15 +139,18 @@ def _paged_setup(ctxs, Hkv, D, dev, seed=0):
     return kc, vc, bt.to(dev)
 
 
+@pytest.mark.parametrize("aux", ["2", "0"])
 @pytest.mark.parametrize("dma", ["1", "2"])
 @pytest.mark.parametrize("G", [4, 8])
 @pytest.mark.parametrize("ppp", [None, 2, 3])
-def test_decode_attention(gpu, G, ppp, dma, kernel_form, monkeypatch):
-    """NGA_DECODE_DMA 1: the whole-page LDS-DMA kernel, 2: its half-page ring form.
+def test_decode_attention(gpu, G, ppp, dma, aux, kernel_form, monkeypatch):
+    """NGA_DECODE_DMA 1: the whole-page LDS-DMA kernel, 2: its half-page ring form (KV loads
+    nt, or with NGA_DECODE_DMA_AUX=0 the default cache policy).
     Short, page-edge, long (4096 / 8192) contexts and contexts one key either side of a
     split-K partition boundary (ppp pages of 64 keys per partition), per-head relative error
     against the fp32 reference (computed on the GPU in fp32)."""
     kernel_form("decode_dma", dma)
+    kernel_form("decode_dma_aux", aux)
     Hkv, D = 8 if G == 4 else 1, 128
     Hq = Hkv * G
     part = 64 * (ppp or 2)
