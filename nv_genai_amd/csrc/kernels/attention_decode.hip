@@ -706,8 +706,11 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
   dim3 grid(num_seqs, Hkv, nparts);
   dim3 g2(num_seqs, Hq);
   if (!kv_fp8) k_scale = v_scale = 1.f;
-  // A/B form: non-temporal KV loads (each page is streamed once per step)
-  const int nt = kernel_form(KF_DECODE_NT) ? 1 : 0;
+  // form decode_nt: nt KV loads (each page is streamed once per step) — 1 always, 2 (default)
+  // bf16 pages only: a bf16 decode step on this kernel runs 0.6-1.2 % faster with them, the
+  // fp8-KV headline 0.5-0.9 % slower (profiles/r5_decode_nt/)
+  const int ntf = kernel_form(KF_DECODE_NT);
+  const int nt = ntf == 1 || (ntf == 2 && !kv_fp8) ? 1 : 0;
   const float sc = scale * k_scale;
 #define NGA_DEC(DD, CT)                                                                        \
   decode_attn_kernel<DD, CT><<<grid, 256, 0, stream>>>(                                        \

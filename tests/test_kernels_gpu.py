@@ -166,6 +166,25 @@ def test_decode_attention(gpu, G, ppp, dma, aux, kernel_form, monkeypatch):
     _close_rows(out, o_ref, width=D)
 
 
+@pytest.mark.parametrize("nt", ["0", "1"])
+@pytest.mark.parametrize("D", [128, 256])
+def test_decode_attention_register_kernel(gpu, D, nt, kernel_form, monkeypatch):
+    """The register decode kernel (NGA_DECODE_DMA=0; head_dim 256 always runs it) with its KV
+    loads on the default cache policy or nt (form decode_nt), against the fp32 reference."""
+    kernel_form("decode_dma", 0)
+    kernel_form("decode_nt", nt)
+    Hkv, G = 4, 4
+    Hq = Hkv * G
+    ctxs = [1, 63, 65, 700, 3001, 4096]
+    kc, vc, bt = _paged_setup(ctxs, Hkv, D, gpu, seed=5)
+    q = _bf(len(ctxs), Hq * D, dev=gpu)
+    ctx = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
+    scale = 1 / math.sqrt(D)
+    out = ops.decode_attention(q, kc, vc, bt, ctx, Hq, Hkv, max(ctxs), scale)
+    o_ref = ref.decode_attention(q.float(), kc, vc, bt, ctx, Hq, Hkv, scale, D=D)
+    _close_rows(out, o_ref, width=D)
+
+
 @pytest.mark.parametrize("dma", ["1", "2"])
 def test_decode_attention_empty_rows(gpu, dma, kernel_form, monkeypatch):
     kernel_form("decode_dma", dma)
