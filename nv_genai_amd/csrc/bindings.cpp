@@ -869,7 +869,7 @@ struct FormSpec {
   int dflt;
 };
 const FormSpec kForms[KF_COUNT] = {
-    {"decode_dma", "NGA_DECODE_DMA", 1}, {"decode_nt", "NGA_DECODE_NT", 2},
+    {"decode_dma", "NGA_DECODE_DMA", 2}, {"decode_nt", "NGA_DECODE_NT", 2},
     {"rmsnorm_wave", "NGA_RMSNORM_WAVE", 0}, {"search_dma", "NGA_SEARCH_DMA", 1},
     {"search_nt", "NGA_SEARCH_NT", 0}, {"prefill_v1", "NGA_PREFILL_V1", 0},
     {"prefill_ks", "NGA_PREFILL_KS", 0}, {"rope_vnt", "NGA_ROPE_VNT", 2},

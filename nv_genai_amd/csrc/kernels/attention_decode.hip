@@ -728,8 +728,8 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
     // register kernel's ~2,048 (graph replay, profiles/r3_search_dma/kb_decode_small_sweep.json):
     // 16 x 1,400 22.1 -> 18.6 us (2 partitions), 64 x 1,400 81.5 -> 59.6 us (1 partition),
     // 4 x 1,400 9.6 -> 8.1 us, the 70B TP=8 rank's 32 x 1,400 9.9 -> 8.8 us; 256 x 1,400
-    // 257 -> 224 us (profiles/r3_dma). Form KF_DECODE_DMA (NGA_DECODE_DMA): 0 / 1 forces the
-    // register / DMA kernel, 2 the half-page ring form of the DMA kernel.
+    // 257 -> 224 us (profiles/r3_dma). Form KF_DECODE_DMA (NGA_DECODE_DMA): 0 forces the register
+    // kernel, 1 the whole-page DMA form, 2 (default) its K / V^T refill ring (profiles/r5_dma_ring/).
     const int dma = kernel_form(KF_DECODE_DMA);
     if (kv_fp8) NGA_DEC(128, uint8_t);
     else if (dma && (pages + nparts - 1) / nparts <= DMA_MAX_PAGES) {

@@ -10,7 +10,7 @@ namespace nga {
 // variable, read ONCE (first use); launchers read the table, never the environment, and
 // tests / benchmarks switch forms explicitly through ops.kernel_forms (no per-launch getenv).
 enum KernelForm {
-  KF_DECODE_DMA = 0,   // NGA_DECODE_DMA: 1 whole-page LDS-DMA decode kernel (default), 2 its ring form, 0 register kernel
+  KF_DECODE_DMA = 0,   // NGA_DECODE_DMA: 2 ring form of the LDS-DMA decode kernel (default), 1 its whole-page form, 0 register kernel
   KF_DECODE_NT,        // NGA_DECODE_NT: register decode kernel's KV loads nt: 1 always, 2 bf16 pages only (default), 0 never
   KF_RMSNORM_WAVE,     // NGA_RMSNORM_WAVE: 1 wave-per-row RMSNorm
   KF_SEARCH_DMA,       // NGA_SEARCH_DMA: 0 forces the register form of the fused search kernel
