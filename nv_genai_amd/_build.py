@@ -139,7 +139,7 @@ def build_runtime(force: bool = False, jobs: int = 8, out_dir: Path | None = Non
     objdir.mkdir(parents=True, exist_ok=True)
     srcs = sorted((CSRC / "runtime").glob("*.cpp"))
     cxx = os.environ.get("CXX", "g++")
-    flags = ["-O2", "-fPIC", "-std=c++17", "-fvisibility=hidden", *_py_inc(), *_pybind_inc()]
+    flags = ["-O2", "-fPIC", "-std=c++17", "-pthread", "-fvisibility=hidden", *_py_inc(), *_pybind_inc()]
     extra = os.environ.get("NGA_RT_CXXFLAGS", "").split() + list(extra_flags or [])
     jobs_list, objs = [], []
     for s in srcs:
@@ -151,7 +151,7 @@ def build_runtime(force: bool = False, jobs: int = 8, out_dir: Path | None = Non
         list(ex.map(_run, jobs_list))
     if force or jobs_list or not out.exists():
         tmp = out.with_suffix(".tmp.so")
-        _run([cxx, "-shared", *map(str, objs), *extra, "-o", str(tmp), "-lrt"])
+        _run([cxx, "-shared", "-pthread", *map(str, objs), *extra, "-o", str(tmp), "-lrt"])
         os.replace(tmp, out)
     return out
 

@@ -103,12 +103,12 @@ class ChatClient:
         body = self._body(messages, True, **kw)
         url = f"{self.base}/chat/completions"
         headers = {**_headers(self.api_key), **self.extra_headers}
-        session = _aiohttp_session(self.timeout)
+        session = _aiohttp_session()
         if session is None:   # no aiohttp: httpx
             async for d in self._astream_httpx(url, body, headers, coalesce):
                 yield d
             return
-        async with session.post(url, json=body, headers=headers) as r:
+        async with session.post(url, json=body, headers=headers, timeout=_aiohttp_timeout(self.timeout)) as r:
             if r.status != 200:
                 text = await r.text()
                 raise RuntimeError(f"chat/completions returned {r.status}: {text[:200]}")
@@ -186,9 +186,19 @@ _ASYNC_CLIENTS = {}
 _AIOHTTP_SESSIONS = {}
 
 
-def _aiohttp_session(timeout: float):
+def _aiohttp_timeout(timeout: float):
+    """Per-request aiohttp timeout with the same meaning as the requests / httpx paths: the
+    limit applies to connecting and to each read, never to the whole stream (a long generation
+    relayed token by token must not be cut off at ``timeout`` seconds)."""
+    import aiohttp
+
+    return aiohttp.ClientTimeout(total=None, sock_connect=timeout, sock_read=timeout)
+
+
+def _aiohttp_session():
     """One pooled aiohttp.ClientSession per event loop (no connection cap: every open stream
-    holds one), or None without aiohttp."""
+    holds one), or None without aiohttp. Timeouts are per request (:func:`_aiohttp_timeout`),
+    so clients with different timeouts can share the session."""
     import asyncio
 
     try:
@@ -199,7 +209,7 @@ def _aiohttp_session(timeout: float):
     s = _AIOHTTP_SESSIONS.get(id(loop))
     if s is None or s[0] is not loop or s[1].closed:
         s = (loop, aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=0, keepalive_timeout=60),
-                                         timeout=aiohttp.ClientTimeout(total=timeout)))
+                                         timeout=aiohttp.ClientTimeout(total=None)))
         _AIOHTTP_SESSIONS[id(loop)] = s
     return s[1]
 

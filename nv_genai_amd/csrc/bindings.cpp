@@ -822,6 +822,8 @@ struct CustomAR {
   int64_t error() const { return impl->error(); }
   int64_t capacity() const { return impl->capacity(); }
   void set_two_shot_threshold(int64_t b) { impl->set_two_shot_threshold(b); }
+  void set_max_blocks(int64_t b) { impl->set_max_blocks((int)b); }
+  int64_t max_blocks() const { return impl->max_blocks(); }
 };
 
 // ---- debug launch checking (SURVEY.md §5.2 "stream-ordering asserts in debug builds"):
@@ -953,5 +955,7 @@ PYBIND11_MODULE(_C, m) {
       .def("all_gather", &CustomAR::all_gather)
       .def("error", &CustomAR::error)
       .def("capacity", &CustomAR::capacity)
-      .def("set_two_shot_threshold", &CustomAR::set_two_shot_threshold);
+      .def("set_two_shot_threshold", &CustomAR::set_two_shot_threshold)
+      .def("set_max_blocks", &CustomAR::set_max_blocks)
+      .def("max_blocks", &CustomAR::max_blocks);
 }

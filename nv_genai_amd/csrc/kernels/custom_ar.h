@@ -33,8 +33,15 @@ class CustomAllReduce {
   // out[row][r * row_bytes ...] = rank r's in[row] (all-gather along the last dim; `in` is
   // [rows, row_bytes] bytes, `out` [rows, world * row_bytes]; row_bytes % 16 == 0).
   void run_gather(const void* in, void* out, int64_t rows, int64_t row_bytes, hipStream_t stream);
-  // Sticky barrier-timeout flag (synchronous read; call outside graph capture).
+  // Sticky barrier-timeout code (synchronous read; call outside graph capture): 0 = every
+  // call met its peers in time, else which barrier first timed out (1 one-shot, 2 / 3
+  // two-shot start / mid, 4 all-reduce + RMSNorm, 5 all-gather).
   int error() const;
+  // Cap on workgroups per call (default kArMaxBlocks). Ranks that SHARE one device (the
+  // one-GPU rehearsals) must keep every rank's spinning blocks co-resident at once, so they
+  // lower it; on a node with one GPU per rank the default stands.
+  void set_max_blocks(int b) { max_blocks_ = b < 1 ? 1 : (b > kArMaxBlocks ? kArMaxBlocks : b); }
+  int max_blocks() const { return max_blocks_; }
 
   int64_t capacity() const { return cap_; }
   int world() const { return world_; }
@@ -47,6 +54,7 @@ class CustomAllReduce {
   int rank_, world_, device_ = 0;
   int64_t cap_;
   int64_t two_shot_threshold_ = 512 * 1024;
+  int max_blocks_ = kArMaxBlocks;
   uint64_t timeout_ticks_ = 0;
   void* mine_ = nullptr;
   void* peers_[kArMaxRanks];

@@ -46,7 +46,7 @@ struct Signal {
   uint32_t mid[kArMaxBlocks][kArMaxRanks];
   uint32_t calls;  // completed calls; read by every block at start, bumped by the last block
   uint32_t done;   // blocks finished in the current call
-  uint32_t error;  // sticky: 1 = a barrier timed out
+  uint32_t error;  // sticky: != 0 = a barrier timed out (code of the first barrier that did)
   uint32_t pad[29];
 };
 static_assert(sizeof(Signal) % 128 == 0, "Signal must keep the staging buffers 128-B aligned");
@@ -152,11 +152,18 @@ __device__ __forceinline__ bool begin_call(const ArArgs& a, uint32_t& flag) {
   return bad == 0u;
 }
 
-__device__ __forceinline__ void end_call(const ArArgs& a, uint32_t flag, bool ok) {
+// timeout codes (CustomAllReduce::error)
+constexpr uint32_t kErrOneShot = 1, kErrTwoShotStart = 2, kErrTwoShotMid = 3, kErrAddNorm = 4, kErrGather = 5;
+
+__device__ __forceinline__ void end_call(const ArArgs& a, uint32_t flag, uint32_t err) {
   Signal* me = sig_of(a, a.rank);
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (!ok) __hip_atomic_store(&me->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (err) {
+      uint32_t zero = 0u;   // keep the first code
+      __hip_atomic_compare_exchange_strong(&me->error, &zero, err, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     const uint32_t d = __hip_atomic_fetch_add(&me->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (d == gridDim.x - 1) {
       __hip_atomic_store(&me->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -179,7 +186,7 @@ __global__ __launch_bounds__(kThreads) void ar_one_shot(ArArgs a) {
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < a.nvec; i += stride)
       out[i] = reduce_at(a, par, i);
   }
-  end_call(a, flag, ok);
+  end_call(a, flag, ok ? 0u : kErrOneShot);
 }
 
 __global__ __launch_bounds__(kThreads) void ar_two_shot(ArArgs a) {
@@ -198,6 +205,7 @@ __global__ __launch_bounds__(kThreads) void ar_two_shot(ArArgs a) {
       if (e < a.nvec) mine[e] = in[e];
     }
   bool ok = block_barrier(a, offsetof(Signal, start), flag);
+  uint32_t err = ok ? 0u : kErrTwoShotStart;
   if (ok) {
     // B: reduce my chunk (sub-range b) from every rank, in place into my staging
     for (int64_t i = i0; i < chunk; i += stride) {
@@ -205,6 +213,7 @@ __global__ __launch_bounds__(kThreads) void ar_two_shot(ArArgs a) {
       if (e < a.nvec) mine[e] = reduce_at(a, par, e);
     }
     ok = block_barrier(a, offsetof(Signal, mid), flag);
+    if (!ok) err = kErrTwoShotMid;
   }
   if (ok) {
     // C: gather chunk r (sub-range b) from its owner r
@@ -217,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void ar_two_shot(ArArgs a) {
       }
     }
   }
-  end_call(a, flag, ok);
+  end_call(a, flag, err);
 }
 
 // Fused TP epilogue: resid += all_reduce(in); out = rmsnorm(resid) * w  (one-shot, bf16).
@@ -280,7 +289,7 @@ __global__ __launch_bounds__(kThreads) void ar_add_rmsnorm(ArArgs a, uint16_t* _
       __syncthreads();  // red[] is reused by the next row
     }
   }
-  end_call(a, flag, ok);
+  end_call(a, flag, ok ? 0u : kErrAddNorm);
 }
 
 // All-gather along the last dim: out[row][r * cols + c] = in_r[row][c] for every rank r (the
@@ -308,7 +317,7 @@ __global__ __launch_bounds__(kThreads) void ag_last_dim(ArArgs a, int64_t rows, 
       }
     }
   }
-  end_call(a, flag, ok);
+  end_call(a, flag, ok ? 0u : kErrGather);
 }
 
 void check(hipError_t e, const char* what) {
@@ -366,7 +375,7 @@ int CustomAllReduce::grid_for(int64_t nvec, bool two_shot) const {
   const int64_t work = two_shot ? (nvec + world_ - 1) / world_ : nvec;
   int64_t g = (work + kThreads - 1) / kThreads;
   if (g < 1) g = 1;
-  if (g > kArMaxBlocks) g = kArMaxBlocks;
+  if (g > max_blocks_) g = max_blocks_;
   return (int)g;
 }
 
@@ -414,7 +423,7 @@ void CustomAllReduce::run_add_rmsnorm(const void* in, uint16_t* resid, const uin
   a.rank = rank_;
   a.world = world_;
   a.is_bf16 = 1;
-  const int g = rows < kArMaxBlocks ? rows : kArMaxBlocks;
+  const int g = rows < max_blocks_ ? rows : max_blocks_;
   hipLaunchKernelGGL(ar_add_rmsnorm, dim3(g), dim3(kThreads), 0, stream, a, resid, w, out, rows, H, eps);
 }
 

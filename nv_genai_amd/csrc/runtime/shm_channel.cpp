@@ -6,33 +6,54 @@
 // driver's host blocks until the GPU drains and a follower cannot launch step k + 1 before
 // step k finishes — the TP engine could not pipeline its steps. Over gloo it is a TCP round
 // trip per step. Here a step is a memcpy into a ring slot of a POSIX shared-memory segment
-// and a release store; followers spin (then yield, then sleep) on the slot's sequence word.
+// and a release store.
 //
 // Layout: Header | nslots x Slot. Message s (1, 2, ...) goes to slot s % nslots. The writer
 // waits until every reader has consumed message s - nslots (their per-reader `done` words),
 // writes length + payload, then publishes slot.seq = s (release). A reader waiting for s
 // acquires slot.seq == s, copies the payload out, then stores done[r] = s (release).
-// `closed` (set by either side) makes every wait return at once — no rank can hang on a peer
-// that went away; waits are also bounded by the caller's timeout.
+//
+// Waiting: spin (pause) for a few microseconds — the pipelined engine publishes step k + 1
+// while the followers still launch step k, so a follower usually finds its message at once —
+// then yield briefly, then sleep on a futex: readers on `pub_gen`, which the writer bumps
+// after every publish and wakes only when someone sleeps (`sleepers`, a Dekker pair of
+// seq_cst operations so a publish can never slip between a reader's check and its sleep);
+// the writer (ring full) likewise on `done_gen`. Wake-up is a syscall away, not the next tick
+// of a sleep loop (round 5's 200 us sleeps), and an idle replica costs no CPU.
+//
+// Liveness, not deadlines: every participant runs a heartbeat thread (C++, no GIL) that
+// stamps its word in the header every 100 ms. A wait ends with "peer dead" once the peer it
+// waits on (the writer, for a reader; any attached reader, for the writer) has not stamped
+// for `liveness_s`, so an idle replica waits for its next step indefinitely while a crashed
+// driver is noticed within seconds. `closed` (set by either side) makes every wait return at
+// once, and a caller may still pass a hard timeout.
 //
 // Lifetime: the creator makes the segment; readers attach by name; once every reader has
 // attached the creator unlinks the name (`unlink()`), so a crash never leaves /dev/shm
 // entries behind — the mapping lives until the last process unmaps it.
 #include <fcntl.h>
+#include <linux/futex.h>
 #include <pybind11/pybind11.h>
 #include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <climits>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <thread>
+#include <vector>
 
 namespace py = pybind11;
 
@@ -40,6 +61,16 @@ namespace {
 
 constexpr uint64_t kMagic = 0x6e67615f73746570ull;   // "nga_step"
 constexpr int kMaxReaders = 64;
+constexpr int64_t kBeatNs = 100'000'000;             // heartbeat period
+
+// wait outcomes (also the Python return codes)
+constexpr int kOk = 1, kTimeout = -1, kClosed = -2, kPeerDead = -3;
+
+int64_t now_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (int64_t)ts.tv_sec * 1'000'000'000 + ts.tv_nsec;
+}
 
 struct alignas(64) Header {
   uint64_t magic;
@@ -48,12 +79,18 @@ struct alignas(64) Header {
   uint64_t nreaders;
   alignas(64) std::atomic<uint32_t> closed;
   alignas(64) std::atomic<uint32_t> attached;
-  alignas(64) std::atomic<uint64_t> done[kMaxReaders];   // last message each reader consumed
+  alignas(64) std::atomic<uint32_t> pub_gen;      // futex word: bumped after every publish / close
+  std::atomic<uint32_t> sleepers;                 // readers inside a futex wait on pub_gen
+  alignas(64) std::atomic<uint32_t> done_gen;     // futex word: bumped after every consume / close
+  std::atomic<uint32_t> writer_sleeping;
+  alignas(64) std::atomic<int64_t> beat[kMaxReaders + 1];   // [0] writer, [1 + r] reader r; 0 = never
+  alignas(64) std::atomic<uint64_t> done[kMaxReaders];      // last message each reader consumed
 };
 
 struct alignas(64) SlotHead {
   std::atomic<uint64_t> seq;
   uint64_t len;
+  int64_t pub_ns;    // writer's clock at publish: the reader's wake-up latency
 };
 
 inline void cpu_relax() {
@@ -62,27 +99,50 @@ inline void cpu_relax() {
 #endif
 }
 
-// spin -> yield -> short sleeps; returns false when `stop()` or the deadline says so
-template <typename Ready, typename Stop>
-bool wait_until(Ready ready, Stop stop, double timeout_s) {
-  using clk = std::chrono::steady_clock;
-  const auto t0 = clk::now();
-  for (uint64_t i = 0;; ++i) {
-    if (ready()) return true;
-    if (stop()) return false;
-    if (i < 4096) {
-      cpu_relax();
-      continue;
+// shared (not PRIVATE) futex ops: the word lives in a MAP_SHARED segment of several processes
+inline void futex_wait(std::atomic<uint32_t>* w, uint32_t expect, int64_t ns) {
+  timespec ts{(time_t)(ns / 1'000'000'000), (long)(ns % 1'000'000'000)};
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAIT, expect, &ts, nullptr, 0);
+}
+inline void futex_wake_all(std::atomic<uint32_t>* w) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAKE, INT_MAX, nullptr, nullptr, 0);
+}
+
+struct WaitStats {
+  uint64_t spins = 0, yields = 0, sleeps = 0;
+};
+
+// spin -> yield -> futex sleep on `gen` (registering in `sleepers`); returns kOk, kClosed,
+// kPeerDead (from `dead()`) or kTimeout (timeout_s >= 0 elapsed)
+template <typename Ready, typename Closed, typename Dead>
+int wait_until(Ready ready, Closed closed, Dead dead, std::atomic<uint32_t>* gen, std::atomic<uint32_t>* sleepers,
+               double timeout_s, WaitStats& st) {
+  for (int i = 0; i < 8192; ++i) {   // ~20-60 us
+    if (ready()) { ++st.spins; return kOk; }
+    if (closed()) return kClosed;
+    cpu_relax();
+  }
+  for (int i = 0; i < 64; ++i) {
+    if (ready()) { ++st.yields; return kOk; }
+    if (closed()) return kClosed;
+    sched_yield();
+  }
+  const int64_t t0 = now_ns();
+  const int64_t limit = timeout_s >= 0 ? (int64_t)(timeout_s * 1e9) : INT64_MAX;
+  for (;;) {
+    sleepers->fetch_add(1, std::memory_order_seq_cst);
+    const uint32_t g = gen->load(std::memory_order_seq_cst);
+    if (ready()) {
+      sleepers->fetch_sub(1, std::memory_order_seq_cst);
+      ++st.sleeps;
+      return kOk;
     }
-    if (i < 8192) {
-      sched_yield();
-      continue;
-    }
-    if ((i & 63) == 0 && timeout_s >= 0 &&
-        std::chrono::duration<double>(clk::now() - t0).count() > timeout_s)
-      return false;
-    timespec ts{0, i < 16384 ? 20000 : 200000};   // 20 us, then 200 us while idle
-    nanosleep(&ts, nullptr);
+    if (!closed()) futex_wait(gen, g, 20'000'000);   // 20 ms slices: liveness / deadline checks
+    sleepers->fetch_sub(1, std::memory_order_seq_cst);
+    if (ready()) { ++st.sleeps; return kOk; }
+    if (closed()) return kClosed;
+    if (dead()) return kPeerDead;
+    if (now_ns() - t0 > limit) return kTimeout;
   }
 }
 
@@ -90,8 +150,8 @@ class ShmChannel {
  public:
   // create = true: make the segment (the writer); otherwise attach as reader `reader`
   ShmChannel(const std::string& name, bool create, int64_t nslots, int64_t slot_bytes, int64_t nreaders,
-             int64_t reader)
-      : name_(name), creator_(create), reader_(reader) {
+             int64_t reader, double liveness_s)
+      : name_(name), creator_(create), reader_(reader), liveness_ns_((int64_t)(liveness_s * 1e9)) {
     if (name.empty() || name[0] != '/') throw std::runtime_error("shm channel: name must start with '/'");
     int fd;
     if (create) {
@@ -130,18 +190,24 @@ class ShmChannel {
       hdr_->nslots = (uint64_t)nslots;
       hdr_->slot_bytes = (uint64_t)slot_bytes;
       hdr_->nreaders = (uint64_t)nreaders;
+      hdr_->beat[0].store(now_ns(), std::memory_order_relaxed);
       std::atomic_thread_fence(std::memory_order_release);
       reinterpret_cast<std::atomic<uint64_t>*>(&hdr_->magic)->store(kMagic, std::memory_order_release);
+      beat_idx_ = 0;
     } else {
       if (reinterpret_cast<std::atomic<uint64_t>*>(&hdr_->magic)->load(std::memory_order_acquire) != kMagic)
         throw std::runtime_error("shm channel: not an initialised channel segment");
       if (reader < 0 || (uint64_t)reader >= hdr_->nreaders) throw std::runtime_error("shm channel: reader index out of range");
       slot_stride_ = (sizeof(SlotHead) + hdr_->slot_bytes + 63) / 64 * 64;
+      beat_idx_ = 1 + (int)reader;
+      hdr_->beat[beat_idx_].store(now_ns(), std::memory_order_release);
       hdr_->attached.fetch_add(1, std::memory_order_acq_rel);
     }
+    beater_ = std::thread([this] { beat_loop(); });
   }
 
   ~ShmChannel() {
+    stop_beating();
     if (creator_ && !unlinked_) shm_unlink(name_.c_str());
     if (base_) munmap(base_, bytes_);
   }
@@ -149,7 +215,13 @@ class ShmChannel {
   int64_t slot_bytes() const { return (int64_t)hdr_->slot_bytes; }
   int64_t attached() const { return hdr_->attached.load(std::memory_order_acquire); }
   bool closed() const { return hdr_->closed.load(std::memory_order_acquire) != 0; }
-  void close_channel() { hdr_->closed.store(1, std::memory_order_release); }
+  void close_channel() {
+    hdr_->closed.store(1, std::memory_order_seq_cst);
+    hdr_->pub_gen.fetch_add(1, std::memory_order_seq_cst);
+    hdr_->done_gen.fetch_add(1, std::memory_order_seq_cst);
+    futex_wake_all(&hdr_->pub_gen);
+    futex_wake_all(&hdr_->done_gen);
+  }
 
   // Remove the name (every reader attached); the segment lives on in the mappings.
   void unlink() {
@@ -159,88 +231,164 @@ class ShmChannel {
     }
   }
 
-  // Publish one message; false on timeout or a closed channel.
-  bool write(py::buffer buf, double timeout_s) {
+  // Stop this participant's heartbeat (tests: a peer that hangs without exiting).
+  void stop_beating() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (stopping_) return;
+      stopping_ = true;
+    }
+    cv_.notify_all();
+    if (beater_.joinable()) beater_.join();
+  }
+
+  // Publish one message: 1, or -1 timeout, -2 closed, -3 a reader died.
+  int write(py::buffer buf, double timeout_s) {
     if (!creator_) throw std::runtime_error("shm channel: only the creator writes");
     py::buffer_info bi = buf.request();
     if (!bi.strides.empty() && bi.strides.back() != bi.itemsize)
       throw std::runtime_error("shm channel: the message must be a contiguous buffer");
     const size_t len = (size_t)bi.size * (size_t)bi.itemsize;
     if (len > hdr_->slot_bytes) throw std::runtime_error("shm channel: message exceeds the slot size");
-    const uint64_t s = ++wseq_;
+    const uint64_t s = wseq_ + 1;
     const uint64_t nr = hdr_->nreaders;
     const uint64_t need = s > hdr_->nslots ? s - hdr_->nslots : 0;
-    bool ok;
+    int rc;
     {
       py::gil_scoped_release nogil;
-      ok = wait_until(
+      rc = wait_until(
           [&] {
             for (uint64_t r = 0; r < nr; ++r)
               if (hdr_->done[r].load(std::memory_order_acquire) < need) return false;
             return true;
           },
-          [&] { return closed(); }, timeout_s);
+          [&] { return closed(); },
+          [&] {
+            for (uint64_t r = 0; r < nr; ++r)
+              if (hdr_->done[r].load(std::memory_order_acquire) < need && stale(1 + (int)r)) return true;
+            return false;
+          },
+          &hdr_->done_gen, &hdr_->writer_sleeping, timeout_s, wstats_);
     }
-    if (!ok) {
-      --wseq_;
-      return false;
-    }
+    if (rc != kOk) return rc;
+    wseq_ = s;
     SlotHead* sh = slot(s);
     sh->len = len;
     std::memcpy(reinterpret_cast<uint8_t*>(sh) + sizeof(SlotHead), bi.ptr, len);
+    sh->pub_ns = now_ns();
     sh->seq.store(s, std::memory_order_release);
-    return true;
+    hdr_->pub_gen.fetch_add(1, std::memory_order_seq_cst);
+    if (hdr_->sleepers.load(std::memory_order_seq_cst) != 0) futex_wake_all(&hdr_->pub_gen);
+    return kOk;
   }
 
   // Wait for the next message and copy it into `out` (a writable buffer at least as large);
-  // returns its length, -1 on timeout, -2 when the channel was closed.
+  // returns its length, or -1 timeout, -2 closed by a peer, -3 the writer died.
   int64_t read(py::buffer out, double timeout_s) {
     if (creator_) throw std::runtime_error("shm channel: the creator does not read");
     py::buffer_info bi = out.request(true);
     const size_t cap = (size_t)bi.size * (size_t)bi.itemsize;
     const uint64_t s = rseq_ + 1;
     SlotHead* sh = slot(s);
-    bool ok;
+    int rc;
     {
       py::gil_scoped_release nogil;
       auto ready = [&] { return sh->seq.load(std::memory_order_acquire) == s; };
       // a message published just before the close is still delivered
-      ok = wait_until(ready, [&] { return closed() && !ready(); }, timeout_s);
+      rc = wait_until(ready, [&] { return closed() && !ready(); }, [&] { return stale(0); }, &hdr_->pub_gen,
+                      &hdr_->sleepers, timeout_s, rstats_);
     }
-    if (!ok) return closed() ? -2 : -1;
+    if (rc != kOk) return rc;
     const size_t len = sh->len;
     if (len > cap) throw std::runtime_error("shm channel: receive buffer too small");
     std::memcpy(bi.ptr, reinterpret_cast<const uint8_t*>(sh) + sizeof(SlotHead), len);
+    const int64_t lat = now_ns() - sh->pub_ns;
     rseq_ = s;
     hdr_->done[reader_].store(s, std::memory_order_release);
+    hdr_->done_gen.fetch_add(1, std::memory_order_seq_cst);
+    if (hdr_->writer_sleeping.load(std::memory_order_seq_cst) != 0) futex_wake_all(&hdr_->done_gen);
+    if (lat_.size() < kLatCap)
+      lat_.push_back(lat);
+    else
+      lat_[lat_n_ % kLatCap] = lat;
+    ++lat_n_;
     return (int64_t)len;
   }
 
+  // Receive-side wake-up latency (publish -> message copied out) over the last messages,
+  // and how each wait ended (spinning, yielding or after a futex sleep).
+  py::dict stats() const {
+    py::dict d;
+    const WaitStats& w = creator_ ? wstats_ : rstats_;
+    d["spins"] = w.spins;
+    d["yields"] = w.yields;
+    d["sleeps"] = w.sleeps;
+    d["messages"] = creator_ ? wseq_ : rseq_;
+    if (!creator_ && !lat_.empty()) {
+      std::vector<int64_t> v(lat_);
+      std::sort(v.begin(), v.end());
+      auto pct = [&](double q) { return v[std::min(v.size() - 1, (size_t)(q * (double)(v.size() - 1) + 0.5))] / 1e3; };
+      d["lat_n"] = (uint64_t)v.size();
+      d["lat_p50_us"] = pct(0.5);
+      d["lat_p99_us"] = pct(0.99);
+      d["lat_max_us"] = v.back() / 1e3;
+    }
+    return d;
+  }
+
  private:
+  static constexpr size_t kLatCap = 1 << 16;
+
   SlotHead* slot(uint64_t s) { return reinterpret_cast<SlotHead*>(base_ + sizeof(Header) + (s % hdr_->nslots) * slot_stride_); }
+
+  // participant `i` has stamped before and not within liveness_s
+  bool stale(int i) const {
+    if (liveness_ns_ <= 0) return false;
+    const int64_t b = hdr_->beat[i].load(std::memory_order_acquire);
+    return b != 0 && now_ns() - b > liveness_ns_;
+  }
+
+  void beat_loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    while (!stopping_) {
+      hdr_->beat[beat_idx_].store(now_ns(), std::memory_order_release);
+      cv_.wait_for(lk, std::chrono::nanoseconds(kBeatNs));
+    }
+  }
 
   std::string name_;
   bool creator_;
   int64_t reader_;
+  int64_t liveness_ns_;
+  int beat_idx_ = 0;
   bool unlinked_ = false;
   uint8_t* base_ = nullptr;
   Header* hdr_ = nullptr;
   size_t bytes_ = 0, slot_stride_ = 0;
   uint64_t wseq_ = 0, rseq_ = 0;
+  WaitStats wstats_, rstats_;
+  std::vector<int64_t> lat_;
+  uint64_t lat_n_ = 0;
+  std::thread beater_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stopping_ = false;
 };
 
 }  // namespace
 
 void register_shm(py::module_& m) {
   py::class_<ShmChannel>(m, "ShmChannel")
-      .def(py::init<const std::string&, bool, int64_t, int64_t, int64_t, int64_t>(), py::arg("name"),
+      .def(py::init<const std::string&, bool, int64_t, int64_t, int64_t, int64_t, double>(), py::arg("name"),
            py::arg("create"), py::arg("nslots") = 4, py::arg("slot_bytes") = 1 << 20, py::arg("nreaders") = 1,
-           py::arg("reader") = 0)
+           py::arg("reader") = 0, py::arg("liveness_s") = 30.0)
       .def("write", &ShmChannel::write, py::arg("buf"), py::arg("timeout_s") = -1.0)
       .def("read", &ShmChannel::read, py::arg("out"), py::arg("timeout_s") = -1.0)
       .def("unlink", &ShmChannel::unlink)
       .def("close", &ShmChannel::close_channel)
       .def("closed", &ShmChannel::closed)
       .def("attached", &ShmChannel::attached)
-      .def("slot_bytes", &ShmChannel::slot_bytes);
+      .def("slot_bytes", &ShmChannel::slot_bytes)
+      .def("stop_beating", &ShmChannel::stop_beating)
+      .def("stats", &ShmChannel::stats);
 }

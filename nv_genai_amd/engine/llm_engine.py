@@ -292,6 +292,8 @@ class LLMEngine:
         self._chan = None
         self._msg = None
         self._tp_gathers = 0    # follower steps that gathered ids from their own previous step
+        self._follower_launch: Deque[float] = collections.deque(maxlen=8192)   # receipt -> launched (s)
+        self._launch_t0 = None
         if self.p.mp_size > 1:
             # the replica's step channel: followers rebuild every step from the driver's layout
             # (shared memory on one node: publishing never waits for the driver's GPU, so
@@ -310,8 +312,10 @@ class LLMEngine:
                 over["async_decode"] = False
             if self.p.pp_size > 1:
                 over["use_graphs"] = False   # stage-to-stage sends stay out of hipGraphs
-            elif self.gpu and self.p.backend == "gloo" and not self.model.ipc_collectives_cover(S, S):
-                # ranks sharing one GPU over gloo: a graph may hold only the IPC collectives
+            elif self.gpu and not self.model.ipc_collectives_cover(S, S):
+                # a graph holds only the IPC collectives: gloo's host-copy collectives cannot be
+                # captured, and RCCL inside a capture (a custom all-reduce that failed its
+                # self-test) is a path no test has executed, so both replay eagerly
                 over["use_graphs"] = False
             if over:
                 self.cfg = cfg = type(cfg)(**{**cfg.__dict__, **over})
@@ -328,8 +332,7 @@ class LLMEngine:
             step = max(1, cfg.graph_token_step)
             mx = cfg.max_graph_tokens or (cfg.mixed_prefill_tokens + cfg.max_num_seqs)
             self._mg_max_tokens = min(-(-mx // step) * step, T // step * step)
-            if (self.p.mp_size > 1 and self.p.backend == "gloo"
-                    and not self.model.ipc_collectives_cover(S, self._mg_max_tokens)):
+            if self.p.mp_size > 1 and not self.model.ipc_collectives_cover(S, self._mg_max_tokens):
                 self._mg_ok = False
             self._nd_buckets = sorted({b for b in (8, 16, 32, 64, 128, 256, 512) if b < S} | {S})
             cap = self._mg_max_tokens // 32 + S + 16     # >= row blocks (32 or 64 rows) of any step
@@ -897,7 +900,11 @@ class LLMEngine:
         """Non-driver TP ranks: execute every step the driver publishes, and the hook for
         each command kind (<= -3) it broadcasts (``broadcast_command``)."""
         while True:
+            if self._launch_t0 is not None:
+                self._follower_launch.append(time.perf_counter() - self._launch_t0)
+                self._launch_t0 = None
             kind, n, ntok, max_q, max_ctx, bs, nd, gb, src, pairs = self._recv_step()
+            self._launch_t0 = time.perf_counter() if kind >= 0 else None
             self._nstep += 1
             if self._faults:
                 self._faults.check(self._nstep, "follower")
@@ -933,6 +940,18 @@ class LLMEngine:
                 meta = self._meta("decode", n, n, 1, self.cfg.max_model_len)
                 h = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta)
                 self._follower_sample(None if h is None else self.model.logits(h), n)
+
+    def follower_stats(self) -> dict:
+        """Follower of a model-parallel replica: the step channel's publish -> receipt latency
+        (µs percentiles, and how many waits ended spinning / yielding / after a futex sleep)
+        and the host time from a step's receipt to the end of its launch (µs percentiles)."""
+        v = sorted(self._follower_launch)
+        out = {"channel": self._chan.stats() if self._chan is not None else {}}
+        if v:
+            out["receipt_to_launched_us"] = {q: round(1e6 * v[min(len(v) - 1, int(f * (len(v) - 1)))], 1)
+                                             for q, f in (("p50", 0.5), ("p99", 0.99), ("max", 1.0))}
+            out["steps"] = len(v)
+        return out
 
     def stop_followers(self) -> None:
         if self.p.mp_size > 1 and self.is_driver:

@@ -177,6 +177,13 @@ LLAMA_PRESETS = {
     "llama70b-tiny": LlamaConfig(name="llama70b-tiny", vocab_size=32768, hidden=256, layers=2, heads=64,
                                  kv_heads=8, head_dim=16, ffn=512, max_position=2048,
                                  bos_id=1, eos_ids=(2,)),
+    # Llama-3-70B's attention layout with its real head_dim 128 at a small width: at TP=8 each
+    # rank holds 8 q heads and 1 KV head and the q/k/v shard is 1280 wide (as 70B's), so the
+    # one-GPU TP=8 rehearsal runs the GPU kernels of a 70B rank; hidden 2048 makes a 256-token
+    # step's all-reduce 1 MiB, past the two-shot threshold
+    "llama70b-small": LlamaConfig(name="llama70b-small", vocab_size=32768, hidden=2048, layers=2, heads=64,
+                                  kv_heads=8, head_dim=128, ffn=4096, max_position=8192, bos_id=1,
+                                  eos_ids=(2,)),
     # Llama-3-8B's attention layout (32 q : 8 kv heads of 128) at a small width: the headline's
     # GQA group and work-item counts in step-graph GPU tests
     "llama3-gqa-small": LlamaConfig(name="llama3-gqa-small", vocab_size=32768, hidden=1024, layers=2, heads=32,

@@ -42,6 +42,7 @@ class StackSampler:
         self.leaf: Dict[str, collections.Counter] = collections.defaultdict(collections.Counter)
         self.stacks: Dict[str, collections.Counter] = collections.defaultdict(collections.Counter)
         self._stop = threading.Event()
+        self._lock = threading.Lock()    # one sample and one summary never interleave
         self._thread = threading.Thread(target=self._run, name="nga-stack-sampler", daemon=True)
         self.t0 = time.time()
 
@@ -53,6 +54,9 @@ class StackSampler:
     def stop(self) -> None:
         if not self._stop.is_set():
             self._stop.set()
+            # the sampler thread may be inside a sample: let it finish before summarising
+            if self._thread.is_alive() and self._thread is not threading.current_thread():
+                self._thread.join(timeout=1.0)
             self.dump()
 
     def _run(self) -> None:
@@ -60,28 +64,36 @@ class StackSampler:
         last = time.monotonic()
         while not self._stop.wait(self.interval_s):
             names = {t.ident: t.name for t in threading.enumerate()}
-            for ident, frame in sys._current_frames().items():
-                if ident == me:
-                    continue
-                name = names.get(ident, str(ident))
-                # thread pools: one bucket per pool, not per worker
-                key = name.rstrip("0123456789_-") or name
-                leaf = frame.f_code.co_name
-                idle = leaf in _IDLE
-                self.per_thread[key]["idle" if idle else "busy"] += 1
-                if not idle:
-                    self.leaf[key][_where(frame)] += 1
-                    st, f = [], frame
-                    while f is not None and len(st) < self.depth:
-                        st.append(_where(f))
-                        f = f.f_back
-                    self.stacks[key][" <- ".join(st)] += 1
-            self.samples += 1
+            with self._lock:
+                self._sample(me, names)
             if time.monotonic() - last > self.dump_every_s:
                 last = time.monotonic()
                 self.dump()
 
+    def _sample(self, me: int, names: dict) -> None:
+        for ident, frame in sys._current_frames().items():
+            if ident == me:
+                continue
+            name = names.get(ident, str(ident))
+            # thread pools: one bucket per pool, not per worker
+            key = name.rstrip("0123456789_-") or name
+            leaf = frame.f_code.co_name
+            idle = leaf in _IDLE
+            self.per_thread[key]["idle" if idle else "busy"] += 1
+            if not idle:
+                self.leaf[key][_where(frame)] += 1
+                st, f = [], frame
+                while f is not None and len(st) < self.depth:
+                    st.append(_where(f))
+                    f = f.f_back
+                self.stacks[key][" <- ".join(st)] += 1
+        self.samples += 1
+
     def summary(self, top: int = 25) -> dict:
+        with self._lock:
+            return self._summary(top)
+
+    def _summary(self, top: int) -> dict:
         out = {"samples": self.samples, "interval_ms": self.interval_s * 1e3,
                "wall_s": round(time.time() - self.t0, 1), "threads": {}}
         for k, c in sorted(self.per_thread.items(), key=lambda kv: -kv[1]["busy"]):
@@ -97,7 +109,7 @@ class StackSampler:
             with open(tmp, "w") as f:
                 json.dump(self.summary(), f, indent=1)
             os.replace(tmp, self.path)
-        except OSError:
+        except (OSError, RuntimeError):   # unwritable path; a summary raced by interpreter exit
             pass
 
 

@@ -27,6 +27,7 @@ log = logging.getLogger(__name__)
 
 ALGO_AUTO, ALGO_ONE_SHOT, ALGO_TWO_SHOT = 0, 1, 2
 TWO_SHOT_THRESHOLD_BYTES = 512 * 1024   # the kernel's default (custom_ar.h)
+MAX_BLOCKS = 80                          # kArMaxBlocks (custom_ar.h): the grid cap per call
 # per staging buffer (x2 for the call-parity double buffer, uncached HBM): the largest message
 # a step graph may hold — a 4,352-token mixed step of a hidden-8,192 model (71 MB bf16) and
 # 256 rows of an 8B model's half vocabulary at TP=2 (66 MB fp32 logits)
@@ -77,6 +78,15 @@ class CustomAllReduce:
             err = e
         if not self._agree(err is None):
             raise RuntimeError(f"custom all-reduce: mapping peer buffers failed on some rank ({err!r})")
+        # ranks sharing one device (one-GPU rehearsals): every rank's spinning blocks must be
+        # resident at once, so each call gets a share of the grid cap
+        self.ranks_per_device = self._ranks_per_device()
+        blocks = os.environ.get("NGA_CUSTOM_AR_BLOCKS")
+        if blocks:
+            self.impl.set_max_blocks(int(blocks))
+        elif self.ranks_per_device > 1:
+            self.impl.set_max_blocks(max(4, MAX_BLOCKS // self.ranks_per_device))
+        self.max_blocks = int(self.impl.max_blocks())
         self.enabled = True
         if self_test:
             self.enabled = self._self_test()
@@ -134,7 +144,20 @@ class CustomAllReduce:
         return out
 
     def error(self) -> int:
+        """0, or the code of the first barrier that timed out (1 one-shot, 2 / 3 two-shot
+        start / mid, 4 all-reduce + RMSNorm, 5 all-gather)."""
         return int(self.impl.error())
+
+    def _ranks_per_device(self) -> int:
+        """How many ranks of the group run on this rank's physical device (host, PCI id)."""
+        from ..parallel.step_channel import _host_key
+
+        pr = torch.cuda.get_device_properties(torch.cuda.current_device())
+        key = (_host_key(), getattr(pr, "pci_domain_id", None), getattr(pr, "pci_bus_id", None),
+               getattr(pr, "pci_device_id", None), str(getattr(pr, "uuid", "")))
+        keys = [None] * self.world
+        dist.all_gather_object(keys, key, group=self.group)
+        return sum(k == key for k in keys)
 
     def _agree(self, ok: bool) -> bool:
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
@@ -197,6 +220,8 @@ def status() -> dict:
     counts of the Python entry point (calls recorded into a hipGraph count once, at capture)."""
     s = dict(_STATUS)
     if _LAST is not None:
+        s["max_blocks"] = _LAST.max_blocks
+        s["ranks_per_device"] = _LAST.ranks_per_device
         try:   # the kernels' sticky barrier-timeout flag (0: every call met its peers in time)
             s["timeout_flag"] = _LAST.error()
         except Exception as e:  # noqa: BLE001

@@ -35,6 +35,28 @@ from .dist import ParallelContext
 DEFAULT_SLOTS = 4
 
 
+def _env_float(name: str, default: float) -> float:
+    v = os.environ.get(name)
+    return float(v) if v not in (None, "") else default
+
+
+def step_timeout_s() -> float:
+    """Hard limit on one channel wait (``NGA_STEP_TIMEOUT_S``; default -1 = none). An idle
+    replica publishes no steps, so followers wait for the next one indefinitely; a dead peer
+    is found by its heartbeat instead (:func:`step_liveness_s`)."""
+    return _env_float("NGA_STEP_TIMEOUT_S", -1.0)
+
+
+def step_liveness_s() -> float:
+    """A peer whose heartbeat (stamped every 100 ms by a native thread of its channel) is this
+    old is dead (``NGA_STEP_LIVENESS_S``, default 30 s; <= 0 turns the check off)."""
+    return _env_float("NGA_STEP_LIVENESS_S", 30.0)
+
+
+class PeerDiedError(RuntimeError):
+    """The peer a channel wait depends on stopped its heartbeat (process gone or frozen)."""
+
+
 class StepChannel:
     pipelined = False   # True: publishing never waits for the driver's GPU
 
@@ -44,6 +66,9 @@ class StepChannel:
     def recv(self) -> np.ndarray:
         raise NotImplementedError
 
+    def stats(self) -> dict:
+        return {}
+
     def close(self) -> None:
         pass
 
@@ -52,9 +77,10 @@ class ShmStepChannel(StepChannel):
     pipelined = True
 
     def __init__(self, pctx: ParallelContext, slot_bytes: int, nslots: int = DEFAULT_SLOTS,
-                 timeout_s: float = 600.0):
+                 timeout_s: Optional[float] = None, liveness_s: Optional[float] = None):
         self.p = pctx
-        self.timeout = float(timeout_s)
+        self.timeout = float(step_timeout_s() if timeout_s is None else timeout_s)
+        liveness = float(step_liveness_s() if liveness_s is None else liveness_s)
         self.slot_bytes = int(slot_bytes)
         driver = pctx.tp_rank == 0 and pctx.pp_rank == 0
         name = None
@@ -62,7 +88,7 @@ class ShmStepChannel(StepChannel):
         if driver:
             name = f"/nga_step_{os.getpid()}_{uuid.uuid4().hex[:12]}"
             try:
-                self.ch = rt.ShmChannel(name, True, nslots, self.slot_bytes, pctx.mp_size - 1, 0)
+                self.ch = rt.ShmChannel(name, True, nslots, self.slot_bytes, pctx.mp_size - 1, 0, liveness)
             except Exception as e:  # noqa: BLE001
                 err, name = e, None
         obj = [name]
@@ -75,7 +101,7 @@ class ShmStepChannel(StepChannel):
             # reader index: this rank's position among the replica's followers
             local = pctx.rank - pctx.mp_src
             try:
-                self.ch = rt.ShmChannel(name, False, 0, 0, 0, local - 1)
+                self.ch = rt.ShmChannel(name, False, 0, 0, 0, local - 1, liveness)
                 self._buf = np.empty(self.ch.slot_bytes(), dtype=np.uint8)
             except Exception as e:  # noqa: BLE001 - e.g. ranks on different hosts after all
                 ok, err = False, e
@@ -93,16 +119,28 @@ class ShmStepChannel(StepChannel):
         self.driver = driver
 
     def send(self, msg: np.ndarray) -> None:
-        if not self.ch.write(np.ascontiguousarray(msg), self.timeout):
-            raise RuntimeError("step channel: followers stopped consuming (timeout or closed)")
+        rc = self.ch.write(np.ascontiguousarray(msg), self.timeout)
+        if rc == -3:
+            raise PeerDiedError("step channel: a follower stopped its heartbeat")
+        if rc == -2:
+            raise RuntimeError("step channel closed")
+        if rc != 1:
+            raise TimeoutError("step channel: followers stopped consuming")
 
     def recv(self) -> np.ndarray:
         n = self.ch.read(self._buf, self.timeout)
         if n == -2:
             raise RuntimeError("step channel closed by the driver")
+        if n == -3:
+            raise PeerDiedError("step channel: the driver stopped its heartbeat")
         if n < 0:
             raise TimeoutError("step channel: no step from the driver")
         return self._buf[:n]
+
+    def stats(self) -> dict:
+        """Follower: publish -> receipt latency percentiles (µs) over the last messages and how
+        its waits ended (spin / yield / futex sleep); driver: its own waits for ring space."""
+        return dict(self.ch.stats())
 
     def close(self) -> None:
         self.ch.close()

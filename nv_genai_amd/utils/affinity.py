@@ -38,11 +38,16 @@ class Placement:
     gpu: Optional[GpuInfo] = None
     numa_node: int = -1
     cpus: List[int] = field(default_factory=list)
+    physical_cores: int = 0          # whole cores given to the rank (every SMT sibling included)
+    l3_domains: List[str] = field(default_factory=list)   # L3 domains (shared_cpu_list) it touches
+    whole_l3: bool = False           # every touched L3 domain belongs to this rank alone
     applied: bool = False
     reason: str = ""
 
     def record(self) -> dict:
         return {"numa_node": self.numa_node, "cpu_affinity": _ranges(self.cpus),
+                "physical_cores": self.physical_cores, "l3_domains": self.l3_domains,
+                "whole_l3": self.whole_l3,
                 "pci_bus_id_sysfs": self.gpu.pci if self.gpu else None,
                 "affinity_applied": self.applied, **({"affinity_note": self.reason} if self.reason else {})}
 
@@ -114,7 +119,10 @@ def visible_gpus(root: str = "/", env=None) -> List[GpuInfo]:
     """The KFD GPUs after the runtime's visibility masks, re-indexed as HIP numbers them."""
     env = os.environ if env is None else env
     gpus = kfd_gpus(root)
-    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+    # ROCR's mask applies first (it hides agents from the HIP runtime); HIP then applies
+    # HIP_VISIBLE_DEVICES, and CUDA_VISIBLE_DEVICES only when HIP's own variable is unset
+    hip_var = "HIP_VISIBLE_DEVICES" if env.get("HIP_VISIBLE_DEVICES") else "CUDA_VISIBLE_DEVICES"
+    for var in ("ROCR_VISIBLE_DEVICES", hip_var):
         v = env.get(var)
         if v is None or v == "":
             continue
@@ -126,10 +134,76 @@ def visible_gpus(root: str = "/", env=None) -> List[GpuInfo]:
     return [GpuInfo(index=i, pci=g.pci, numa_node=g.numa_node) for i, g in enumerate(gpus)]
 
 
+@dataclass
+class _Core:
+    cpus: List[int]       # logical CPUs of one physical core (SMT siblings), allowed ones only
+    l3: str               # the core's L3 domain (its shared_cpu_list; "" when unknown)
+
+
+def cpu_topology(cpus: List[int], root: str = "/") -> List[_Core]:
+    """Group logical CPUs into physical cores (``topology/thread_siblings_list``, else
+    (``physical_package_id``, ``core_id``)) tagged with their L3 domain
+    (``cache/index3/shared_cpu_list``), ordered by L3 domain and then by first CPU. A CPU with
+    no topology in sysfs is a core of its own."""
+    base = os.path.join(root, "sys/devices/system/cpu")
+    want = set(cpus)
+    cores: dict = {}
+    for c in cpus:
+        d = os.path.join(base, f"cpu{c}")
+        sib = _read(os.path.join(d, "topology/thread_siblings_list"))
+        if sib and sib.strip():
+            key = ("sib", _ranges(parse_cpulist(sib)))
+        else:
+            pkg, cid = _read(os.path.join(d, "topology/physical_package_id")), _read(os.path.join(d, "topology/core_id"))
+            key = ("id", pkg.strip(), cid.strip()) if pkg and cid else ("cpu", c)
+        l3 = _read(os.path.join(d, "cache/index3/shared_cpu_list"))
+        core = cores.setdefault(key, _Core(cpus=[], l3=_ranges(parse_cpulist(l3)) if l3 and l3.strip() else ""))
+        if c in want:
+            core.cpus.append(c)
+    out = [k for k in cores.values() if k.cpus]
+    l3_first = {}
+    for k in out:
+        l3_first[k.l3] = min(l3_first.get(k.l3, 1 << 30), min(k.cpus))
+    out.sort(key=lambda k: (l3_first[k.l3], min(k.cpus)))
+    return out
+
+
+def split_cores(cores: List[_Core], k: int) -> List[List[_Core]]:
+    """Split cores among ``k`` ranks: whole L3 domains per rank when there are at least ``k``
+    of them (domains dealt out contiguously, balanced by core count), else contiguous runs of
+    whole cores in L3 order, so no two ranks share a physical core and each rank's cores sit
+    in as few L3 domains as possible."""
+    if k <= 0 or not cores:
+        return [[] for _ in range(max(k, 0))]
+    domains: List[List[_Core]] = []
+    for c in cores:
+        if domains and domains[-1][0].l3 == c.l3:
+            domains[-1].append(c)
+        else:
+            domains.append([c])
+    if len(domains) >= k and all(d[0].l3 for d in domains):
+        parts: List[List[_Core]] = [[] for _ in range(k)]
+        total, acc, r = len(cores), 0, 0
+        for i, d in enumerate(domains):
+            # move on to the next rank once this one holds its share of cores, leaving at
+            # least one domain for every rank still to come
+            if parts[r] and r < k - 1 and (acc >= (r + 1) * total / k or len(domains) - i <= k - 1 - r):
+                r += 1
+            parts[r].extend(d)
+            acc += len(d)
+        return parts
+    n = len(cores)
+    if n < k:   # fewer cores than ranks: ranks share cores round-robin
+        return [[cores[i % n]] for i in range(k)]
+    return [cores[i * n // k:(i + 1) * n // k] for i in range(k)]
+
+
 def plan(local_rank: int, local_world: int, root: str = "/", env=None,
          allowed: Optional[List[int]] = None) -> Placement:
     """Cores for ``local_rank``: its GPU's NUMA node's CPUs (intersected with the CPUs this
-    process may use), split evenly among the local ranks whose GPUs share that node."""
+    process may use), split among the local ranks whose GPUs share that node in whole
+    physical cores (all SMT siblings of a core go to one rank) and, where the node has at
+    least one L3 domain per rank, in whole L3 domains."""
     pl = Placement(local_rank=local_rank)
     gpus = visible_gpus(root, env)
     if allowed is None:
@@ -154,9 +228,13 @@ def plan(local_rank: int, local_world: int, root: str = "/", env=None,
         return pl
     peers = [r for r in range(local_world) if gpus[gpu_of[r]].numa_node == g.numa_node]
     k, i = len(peers), peers.index(local_rank)
-    per = max(1, len(node_cpus) // k)
-    lo = min(i * per, len(node_cpus) - 1)
-    pl.cpus = node_cpus[lo: lo + per] if i < k - 1 else node_cpus[lo:]
+    parts = split_cores(cpu_topology(node_cpus, root), k)
+    mine = parts[i]
+    pl.cpus = sorted(c for core in mine for c in core.cpus)
+    pl.physical_cores = len(mine)
+    pl.l3_domains = sorted({core.l3 for core in mine if core.l3}, key=lambda t: parse_cpulist(t)[0])
+    others = {core.l3 for j, p in enumerate(parts) if j != i for core in p}
+    pl.whole_l3 = bool(pl.l3_domains) and not (set(pl.l3_domains) & others)
     return pl
 
 

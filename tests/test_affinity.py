@@ -109,3 +109,67 @@ def test_doctor_kernel_self_test_gpu():
     assert all(v["ok"] for v in rep["self_test"].values()), rep["self_test"]
     assert rep["gpus"] and rep["gpus"][0]["arch"].startswith("gfx950")
     assert not rep["problems"], rep["problems"]
+
+
+def _smt_topology(root, ncpu=192, smt_offset=96, ccd_cores=12):
+    """Fake cpu topology for _tree's node: CPU c and c + 96 are SMT siblings of one physical
+    core; each CCD (L3 domain) holds 12 physical cores (24 logical CPUs), 4 CCDs per socket."""
+    for c in range(ncpu):
+        core = c % smt_offset
+        sibs = f"{core},{core + smt_offset}"
+        ccd = core // ccd_cores
+        lo = ccd * ccd_cores
+        l3 = f"{lo}-{lo + ccd_cores - 1},{lo + smt_offset}-{lo + smt_offset + ccd_cores - 1}"
+        d = root / f"sys/devices/system/cpu/cpu{c}"
+        (d / "topology").mkdir(parents=True)
+        (d / "topology/thread_siblings_list").write_text(sibs + "\n")
+        (d / "topology/core_id").write_text(f"{core % 48}\n")
+        (d / "topology/physical_package_id").write_text(f"{core // 48}\n")
+        (d / "cache/index3").mkdir(parents=True)
+        (d / "cache/index3/shared_cpu_list").write_text(l3 + "\n")
+
+
+def test_smt_siblings_and_l3_domains_stay_with_one_rank(tmp_path):
+    """The round-5 plan sliced the node's cpulist contiguously, so on `0-47,96-143` rank 2 got
+    96-119, the SMT siblings of rank 0's 0-23. Now every rank gets whole physical cores and,
+    with one L3 domain (CCD) or more per rank, whole L3 domains."""
+    root = _tree(tmp_path)
+    _smt_topology(tmp_path)
+    allowed = list(range(192))
+    core_of = {c: c % 96 for c in range(192)}
+    owner = {}
+    for r in range(8):
+        pl = affinity.plan(r, 8, root, env={}, allowed=allowed)
+        assert len(pl.cpus) == 24 and pl.physical_cores == 12
+        for c in pl.cpus:                          # both siblings of each core, no core shared
+            assert owner.setdefault(core_of[c], r) == r
+            assert (c + 96 if c < 96 else c - 96) in pl.cpus
+        assert len(pl.l3_domains) == 1 and pl.whole_l3
+        rec = pl.record()
+        assert rec["physical_cores"] == 12 and rec["whole_l3"] and rec["l3_domains"] == pl.l3_domains
+    # 8 ranks on one socket's 4 CCDs: whole cores (6 each), two ranks per CCD
+    env = {"HIP_VISIBLE_DEVICES": "0,1,2,3"}
+    owner = {}
+    for r in range(8):
+        pl = affinity.plan(r, 8, root, env=env, allowed=allowed)
+        assert pl.numa_node == 0 and pl.physical_cores == 6 and len(pl.cpus) == 12
+        assert len(pl.l3_domains) == 1 and not pl.whole_l3
+        for c in pl.cpus:
+            assert owner.setdefault(core_of[c], r) == r
+    # 3 ranks over 4 CCDs: whole domains, balanced 2/1/1 by cores
+    parts = affinity.split_cores(affinity.cpu_topology(affinity.parse_cpulist("0-47,96-143"), root), 3)
+    assert [len(p) for p in parts] == [24, 12, 12]
+    assert [len({c.l3 for c in p}) for p in parts] == [2, 1, 1]
+    assert not ({c.l3 for c in parts[0]} & {c.l3 for c in parts[1]})
+
+
+def test_visible_devices_hip_overrides_cuda(tmp_path):
+    """HIP applies CUDA_VISIBLE_DEVICES only when HIP_VISIBLE_DEVICES is unset (not on top of
+    it); ROCR_VISIBLE_DEVICES always filters first."""
+    root = _tree(tmp_path)
+    both = affinity.visible_gpus(root, env={"HIP_VISIBLE_DEVICES": "6,1", "CUDA_VISIBLE_DEVICES": "1"})
+    assert [g.pci for g in both] == ["0000:65:00.0", "0000:15:00.0"]
+    cuda = affinity.visible_gpus(root, env={"CUDA_VISIBLE_DEVICES": "1"})
+    assert [g.pci for g in cuda] == ["0000:15:00.0"]
+    rocr = affinity.visible_gpus(root, env={"ROCR_VISIBLE_DEVICES": "4,5,6", "HIP_VISIBLE_DEVICES": "2"})
+    assert [g.pci for g in rocr] == ["0000:65:00.0"]

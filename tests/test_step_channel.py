@@ -1,0 +1,178 @@
+"""Shared-memory step channel (csrc/runtime/shm_channel.cpp): ordering under a ring that wraps,
+a slow writer (followers sleep on the futex and wake within a bound, no 200 µs sleep tail), an
+idle driver that outlives any timeout (followers keep waiting), a driver that stops its
+heartbeat (followers raise PeerDiedError within the liveness limit) and a reader that dies
+(the writer stops instead of waiting forever). Processes are forked, so no torch.distributed
+is needed; the Python wrapper's error mapping is checked through ShmStepChannel's methods."""
+import multiprocessing as mp
+import os
+import time
+import uuid
+
+import numpy as np
+import pytest
+
+from nv_genai_amd._native import rt
+from nv_genai_amd.parallel import step_channel as sc
+
+
+def _name():
+    return f"/nga_test_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+
+
+def _reader(name, idx, n, q, liveness=30.0, timeout=-1.0):
+    ch = rt.ShmChannel(name, False, 0, 0, 0, idx, liveness)
+    buf = np.empty(ch.slot_bytes(), dtype=np.uint8)
+    got = []
+    for _ in range(n):
+        k = ch.read(buf, timeout)
+        if k < 0:
+            got.append(int(k))
+            break
+        got.append(int(buf[:k].view(np.int64)[0]))
+    q.put((idx, got, dict(ch.stats())))
+
+
+def _wait_attached(ch, n, limit=30.0):
+    t0 = time.time()
+    while ch.attached() < n:
+        assert time.time() - t0 < limit, "readers did not attach"
+        time.sleep(0.01)
+
+
+def test_ring_wraps_in_order_with_seven_readers():
+    """The TP = 8 shape: one writer, seven readers, 4 slots, 500 messages of varying size."""
+    name, n, nr = _name(), 500, 7
+    w = rt.ShmChannel(name, True, 4, 4096, nr, 0, 30.0)
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_reader, args=(name, i, n, q)) for i in range(nr)]
+    for p in ps:
+        p.start()
+    _wait_attached(w, nr)
+    w.unlink()
+    for s in range(n):
+        msg = np.full(1 + s % 37, s, dtype=np.int64)
+        assert w.write(msg, 30.0) == 1
+    res = [q.get(timeout=60) for _ in range(nr)]
+    for p in ps:
+        p.join(30)
+        assert p.exitcode == 0
+    for idx, got, st in res:
+        assert got == list(range(n)), idx
+        assert st["messages"] == n and st["lat_n"] == n
+    assert w.stats()["messages"] == n
+
+
+def test_slow_writer_wakes_sleeping_followers_quickly():
+    """Messages 20 ms apart: every follower has left its spin phase and sleeps on the futex;
+    the writer's wake brings each receipt within a few hundred µs of the publish (the old
+    sleep loop woke up to 200 µs late on top of the scheduler's latency)."""
+    name, n, nr = _name(), 40, 3
+    w = rt.ShmChannel(name, True, 4, 256, nr, 0, 30.0)
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_reader, args=(name, i, n, q)) for i in range(nr)]
+    for p in ps:
+        p.start()
+    _wait_attached(w, nr)
+    for s in range(n):
+        time.sleep(0.02)
+        assert w.write(np.array([s], dtype=np.int64), 30.0) == 1
+    res = [q.get(timeout=60) for _ in range(nr)]
+    for p in ps:
+        p.join(30)
+    for idx, got, st in res:
+        print("follower", idx, st)
+        assert got == list(range(n))
+        assert st["sleeps"] >= n // 2, st          # they really slept on the futex
+        # generous bound for a shared 8-CPU CI container; typical p50 is 10-60 us
+        assert st["lat_p50_us"] < 2000, st
+
+
+def test_idle_driver_does_not_time_out_followers():
+    """followers used to give up after a hard 600 s with no step. Now the wait has
+    no deadline while the driver's heartbeat is fresh: with a 0.5 s liveness limit, a driver
+    idle for 2 s (four limits) still delivers its next message."""
+    name = _name()
+    w = rt.ShmChannel(name, True, 2, 256, 1, 0, 0.5)
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    p = ctx.Process(target=_reader, args=(name, 0, 1, q, 0.5, -1.0))
+    p.start()
+    _wait_attached(w, 1)
+    time.sleep(2.0)
+    assert w.write(np.array([42], dtype=np.int64), 5.0) == 1
+    idx, got, _ = q.get(timeout=30)
+    p.join(10)
+    assert got == [42]
+
+
+def test_dead_driver_is_detected_by_heartbeat():
+    """A driver that stops beating (a crashed or frozen process) ends the followers' wait with
+    -3, which ShmStepChannel.recv turns into PeerDiedError; a hard timeout still returns -1."""
+    name = _name()
+    w = rt.ShmChannel(name, True, 2, 256, 1, 0, 0.5)
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    p = ctx.Process(target=_reader, args=(name, 0, 2, q, 0.5, -1.0))
+    p.start()
+    _wait_attached(w, 1)
+    assert w.write(np.array([7], dtype=np.int64), 5.0) == 1
+    t0 = time.time()
+    w.stop_beating()
+    idx, got, _ = q.get(timeout=30)
+    p.join(10)
+    assert got == [7, -3]
+    assert time.time() - t0 < 10
+
+    t0 = time.time()
+    rr_name = _name()
+    rw = rt.ShmChannel(rr_name, True, 2, 256, 1, 0, 30.0)
+    rd = rt.ShmChannel(rr_name, False, 0, 0, 0, 0, 30.0)
+    buf = np.empty(256, dtype=np.uint8)
+    assert rd.read(buf, 0.2) == -1                          # nothing published: timeout
+    assert 0.15 < time.time() - t0 < 5
+    del rw, rd
+
+
+def test_dead_reader_stops_the_writer():
+    """The ring is full and one reader stopped beating: the writer's wait ends with -3 (the
+    Python wrapper raises PeerDiedError) instead of waiting out a timeout."""
+    name = _name()
+    w = rt.ShmChannel(name, True, 2, 256, 1, 0, 0.5)
+    rd = rt.ShmChannel(name, False, 0, 0, 0, 0, 0.5)
+    for s in range(2):
+        assert w.write(np.array([s], dtype=np.int64), 5.0) == 1
+    rd.stop_beating()
+    t0 = time.time()
+    assert w.write(np.array([2], dtype=np.int64), -1.0) == -3
+    assert time.time() - t0 < 10
+    # close wakes everyone at once
+    w2n = _name()
+    w2 = rt.ShmChannel(w2n, True, 2, 256, 1, 0, 30.0)
+    r2 = rt.ShmChannel(w2n, False, 0, 0, 0, 0, 30.0)
+    w2.close()
+    assert r2.read(np.empty(256, dtype=np.uint8), -1.0) == -2
+
+
+def test_wrapper_maps_codes_to_exceptions():
+    class _Ch:
+        def __init__(self, rc):
+            self.rc = rc
+
+        def write(self, msg, t):
+            return self.rc
+
+        def read(self, buf, t):
+            return self.rc
+
+    c = sc.ShmStepChannel.__new__(sc.ShmStepChannel)
+    c.timeout, c._buf = -1.0, np.empty(8, dtype=np.uint8)
+    for rc, exc in ((-3, sc.PeerDiedError), (-2, RuntimeError), (-1, TimeoutError)):
+        c.ch = _Ch(rc)
+        with pytest.raises(exc):
+            c.send(np.zeros(1))
+        with pytest.raises(exc):
+            c.recv()
+    assert sc.step_timeout_s() == float(os.environ.get("NGA_STEP_TIMEOUT_S", -1.0))
