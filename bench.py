@@ -233,6 +233,11 @@ class ReplicaSearch:
         self.dim = index.dim
 
     def search(self, q, k):
+        payload = self.index.query_payload(q)
+        if payload.nbytes <= self.llm.command_payload_capacity():
+            # the query block travels in the command itself: one collective per search
+            self.llm.broadcast_command(SEARCH_CMD, int(q.shape[0]), payload)
+            return self.index.search(q, k, have_queries=True)
         self.llm.broadcast_command(SEARCH_CMD, int(q.shape[0]))
         return self.index.search(q, k, src=self.src)
 
@@ -274,6 +279,7 @@ def run_agent(args, world: int, shared: bool = False) -> None:
         **{k: res[k] for k in ("p50_latency_ms", "p95_latency_ms", "llm_calls_per_s", "searches_per_s",
                                "mean_prompt_tokens", "output_tokens_per_s", "setup_s")},
         "world_size": world, "backend": res.get("backend"), "shared_devices": shared,
+        **({"search": res["search"]} if res.get("search") else {}),
         **({"devices": res["devices"]} if res.get("devices") else {}),
     }
     s = json.dumps(line)
@@ -363,8 +369,11 @@ def main(argv=None):
         # the timing barriers; leave when the driver stops the replica
         hooks = {BARRIER_CMD: lambda n: (torch.cuda.synchronize() if gpu else None, pd.barrier())}
         if sharded:
-            hooks[SEARCH_CMD] = lambda n: shard.search(torch.zeros(n, dim, device=shard.comm_dev), args.top_k,
-                                                       src=pctx.mp_src)
+            def search_hook(n, payload=None):
+                if payload is not None:   # the driver's query block, from the command
+                    return shard.search(shard.queries_from_payload(n, payload), args.top_k, have_queries=True)
+                return shard.search(torch.zeros(n, dim, device=shard.comm_dev), args.top_k, src=pctx.mp_src)
+            hooks[SEARCH_CMD] = search_hook
         llm.run_follower(hooks=hooks)
         pd.all_reduce_max(0.0)
         pd.all_gather_objects(None)
@@ -480,6 +489,11 @@ def main(argv=None):
         v.clear()
     for k in getattr(rag, "submit_host_s", {}):
         rag.submit_host_s[k] = 0.0
+    from nv_genai_amd import ops
+
+    # the timed window on the GPU timeline: marker kernels a kernel trace can be cut at
+    # (scripts/summarize_prof.py: busy time and idle gaps of exactly this window)
+    ops.region_marker(pctx.device, end=False)
     t0 = time.perf_counter()
     results = []
     if args.mode == "wave":
@@ -487,6 +501,7 @@ def main(argv=None):
             results += one_step()
     else:
         results = closed_loop(args.steps * R, ramping=False, st_name="timed")
+    ops.region_marker(pctx.device, end=True)
     world_barrier()
     elapsed = time.perf_counter() - t0
     llm.stop_followers()

@@ -60,6 +60,10 @@ def parse(argv=None):
     ap.add_argument("--kv-cache-fraction", type=float, default=0.5)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--fp8", action="store_true", help="W8A8 FP8 projections (70B: 70 GB of weights)")
+    ap.add_argument("--search-legacy", action="store_true",
+                    help="A/B: the round-5 search path (query block broadcast as its own collective, "
+                         "results gathered over the process group) instead of queries in the step-channel "
+                         "command + the IPC all-gather")
     ap.add_argument("--out", default=None)
     return ap.parse_args(argv)
 
@@ -87,13 +91,18 @@ def main(argv=None, emit: bool = True, record_devices=None):
     from nv_genai_amd.models.config import encoder_config
 
     dim = encoder_config(args.embed_model).hidden
-    index = ShardedIndex(dim, "cosine", dev, pctx=pctx,
-                         capacity=max(1024, args.index_size // max(1, pctx.world_size) + 1))
+    index = ShardedIndex(dim, "cosine", dev, pctx=pctx, group=pctx.mp_group if pctx.mp_size > 1 else None,
+                         capacity=max(1024, args.index_size // max(1, pctx.world_size) + 1),
+                         ipc_gather=not args.search_legacy)
     index.add_random(args.index_size, seed=1234)
     k = args.top_k
     if not eng.is_driver:
         comm_dev = index.comm_dev
-        eng.run_follower(hooks={SEARCH_CMD: lambda n: index.search(torch.zeros(n, dim, device=comm_dev), k)})
+        def search_hook(n, payload=None):
+            if payload is not None:   # the driver's query block, from the command
+                return index.search(index.queries_from_payload(n, payload), k, have_queries=True)
+            return index.search(torch.zeros(n, dim, device=comm_dev), k)
+        eng.run_follower(hooks={SEARCH_CMD: search_hook})
         pd.destroy()
         return None
 
@@ -112,6 +121,7 @@ def main(argv=None, emit: bool = True, record_devices=None):
     tmpl = jinja2.Environment().from_string(TEMPLATE)
     setup_s = time.time() - t0
     stats = {"llm_calls": 0, "searches": 0, "prompt_tokens": 0, "output_tokens": 0}
+    search_ms = []
     slock = threading.Lock()
 
     def llm(prompt: str, max_tokens: int) -> str:
@@ -130,9 +140,22 @@ def main(argv=None, emit: bool = True, record_devices=None):
         qv = q.to(index.comm_dev if not gpu else dev).float()
 
         def run():
-            eng.broadcast_command(SEARCH_CMD, qv.shape[0])
-            return index.search(qv, k)
-        _, ids = svc.call(run).result()
+            # on the engine thread, between steps: every rank of the replica joins
+            t = time.perf_counter()
+            if index.world == 1:
+                out = index.search(qv, k)
+            elif args.search_legacy:
+                eng.broadcast_command(SEARCH_CMD, qv.shape[0])
+                out = index.search(qv, k)
+            else:
+                # the query block rides in the command: the search's only collective is the
+                # packed (score, id) all-gather
+                eng.broadcast_command(SEARCH_CMD, qv.shape[0], index.query_payload(qv))
+                out = index.search(qv, k, have_queries=True)
+            ids = out[1].cpu()        # the replica's decode waits behind this search
+            search_ms.append(1e3 * (time.perf_counter() - t))
+            return ids
+        ids = svc.call(run).result()
         with slock:
             stats["searches"] += 1
         return [docs.get(int(i)) for i in ids[0].tolist() if int(i) >= 0]
@@ -165,6 +188,7 @@ def main(argv=None, emit: bool = True, record_devices=None):
         run(args.warmup, 10_000)
     for key in stats:
         stats[key] = 0
+    search_ms.clear()
     t1 = time.perf_counter()
     lat = run(args.queries, 20_000)
     elapsed = time.perf_counter() - t1
@@ -176,6 +200,7 @@ def main(argv=None, emit: bool = True, record_devices=None):
            "n_gpus": pctx.world_size if gpu else 0, "parallelism": f"tp{pctx.tp_size}",
            "model": args.model, "embed_model": args.embed_model, "index_size": args.index_size,
            "concurrency": args.concurrency, "queries": args.queries, "elapsed_s": round(elapsed, 3),
+           "search_path": "legacy" if args.search_legacy else "command-payload+ipc-gather",
            "p50_latency_ms": round(1e3 * statistics.median(lat), 1),
            "p95_latency_ms": round(1e3 * lat[min(len(lat) - 1, int(0.95 * len(lat)))], 1),
            "llm_calls_per_s": round(stats["llm_calls"] / elapsed, 2),
@@ -185,6 +210,11 @@ def main(argv=None, emit: bool = True, record_devices=None):
            "dtype": "fp8-w8a8" if args.fp8 else "bf16",
            "data": "synthetic: random-init weights, random unit-vector index, generated questions",
            "setup_s": round(setup_s, 1), "backend": pctx.backend,
+           "search": {**{k_: v for k_, v in index.stats.items() if k_ != "host_s"},
+                      "host_ms_per_search": round(1e3 * index.stats["host_s"] / max(1, index.stats["searches"]), 3),
+                      **({"p50_ms": round(sorted(search_ms)[len(search_ms) // 2], 3),
+                          "p95_ms": round(sorted(search_ms)[int(0.95 * (len(search_ms) - 1))], 3)}
+                         if search_ms else {})},
            **({"devices": devices} if devices else {})}
     line = json.dumps(res)
     if emit:

@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--iters", type=int, default=25)
     ap.add_argument("--out", default=None, help="table file (default: the shipped asset)")
     ap.add_argument("--merge", default=None, help="update this table file with the measured shapes only")
+    ap.add_argument("--cfgs", default=None, help="comma list of tile configurations to try (default: all)")
+    ap.add_argument("--all", action="store_true", help="also print every (cfg, split) time")
     ap.add_argument("--tp", type=int, default=1, help="per-rank shapes of a TP group of this size "
                     "(column-parallel q/k/v, gate/up, LM head; row-parallel o, down)")
     a = ap.parse_args()
@@ -61,7 +63,7 @@ def main():
     shapes = {"qkv": ((cfg.heads + 2 * cfg.kv_heads) // tp * D, H), "o": (H, cfg.heads // tp * D),
               "gate_up": (2 * F, H), "down": (H, F), "lm_head": (-(-cfg.vocab_size // tp), H)}
     C = ops.kernels()
-    cfgs = list(range(C.skinny_cfg_count()))
+    cfgs = [int(c) for c in a.cfgs.split(",")] if a.cfgs else list(range(C.skinny_cfg_count()))
     info = {c: C.skinny_cfg(c) for c in cfgs}
     dev = torch.device("cuda")
     g = torch.Generator(device=dev)
@@ -139,6 +141,8 @@ def main():
                             fn = (lambda i, out=out, c=c, s=s, qb=qb: (
                                 C.skinny_gemm(out, x, Ws[i], 1, s, c, 0, 0, 0, 0, 0), rope(qb, out)))
                     t = timeit(fn, n_rot, a.iters)
+                    if a.all:
+                        print(json.dumps({"shape": name, "M": M, "cfg": c, "split": s, "us": round(t, 2)}), flush=True)
                     if best is None or t < best[0]:
                         best = (t, c, s, blocks)
             row = {"shape": name, "N": N, "K": K, "M": M, "lib_us": round(lib, 2)}

@@ -246,10 +246,10 @@ void moe_combine(Tensor y, Tensor inv, int64_t T, int64_t k, Tensor out) {
 }
 
 // ------------------------------------------------------------------ decode-shape GEMM
-std::vector<int64_t> skinny_cfg(int64_t cfg) {
-  int info[5];
+std::vector<int64_t> skinny_cfg(int64_t cfg) {   // {BN, BM, WN, WM, NSTAGE, BK}
+  int info[6];
   nga::skinny_gemm_cfg_info((int)cfg, info);
-  return {info[0], info[1], info[2], info[3], info[4]};
+  return {info[0], info[1], info[2], info[3], info[4], info[5]};
 }
 
 // epi 0: out [M, N] bf16 = x @ w^T; 1: out fp32 [split, M, N] partial slabs; 2: out [M, F] bf16 =
@@ -269,9 +269,10 @@ void skinny_gemm(Tensor out, Tensor x, Tensor w, int64_t epi, int64_t split, int
   TORCH_CHECK(K % 64 == 0 && K >= 64, "skinny_gemm: K must be a multiple of 64");
   TORCH_CHECK(wpack || w.size(1) == K, "skinny_gemm: K must match");
   TORCH_CHECK(M >= 1 && M <= 65536, "skinny_gemm: 1 <= M <= 65536");
-  int info[5];
+  int info[6];
   nga::skinny_gemm_cfg_info((int)cfg, info);
   TORCH_CHECK(info[0] > 0, "skinny_gemm: unknown tile configuration ", cfg);
+  TORCH_CHECK(info[5] == 64 || (!wpack && !xpack), "skinny_gemm: packed operands are 64-deep tiles (BK 64 configurations only)");
   const int BN = info[0], BM = info[1];
   TORCH_CHECK(epi >= 0 && epi <= 2, "skinny_gemm: epi 0, 1 or 2");
   TORCH_CHECK(split >= 1 && split <= K / 64 && (epi == 1 || split == 1), "skinny_gemm: 1 <= split <= K / 64 (> 1 only for epi 1)");
@@ -694,6 +695,12 @@ void topk(Tensor in, c10::optional<Tensor> in_idx, int64_t seg_len, int64_t k, T
                    out_i.data_ptr<int64_t>(), cur_stream(in));
 }
 
+// a begin / end marker kernel on the current stream (kernel-trace window delimiters)
+void region_marker(Tensor sink, int64_t end) {
+  CHECK_DEV(sink); CHECK_DT(sink, at::kInt);
+  nga::launch_region_marker((int)end, sink.data_ptr<int32_t>(), cur_stream(sink));
+}
+
 void pool_l2norm(Tensor hidden, Tensor cu, int64_t mode, bool normalize, Tensor out) {
   CHECK_BF16(hidden); CHECK_CONTIG(hidden);
   CHECK_DEV(cu); CHECK_DT(cu, at::kInt);
@@ -940,6 +947,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("score_topk_kmax", [](int64_t q) { return (int64_t)nga::score_topk_kmax((int)q); });
   m.def("score_topk_dma_ok", [](int64_t d, int64_t q) { return (bool)nga::score_topk_dma_ok((int)d, (int)q); });
   m.def("pool_l2norm", checked("pool_l2norm", &pool_l2norm));
+  m.def("region_marker", checked("region_marker", &region_marker));
   m.def("row_sqnorm", checked("row_sqnorm", &row_sqnorm));
   m.def("fir_c64", checked("fir_c64", &fir_c64));
   m.def("fm_demod", checked("fm_demod", &fm_demod));

@@ -42,10 +42,17 @@
 namespace nga {
 
 namespace {
-constexpr int SBK = 64;   // K per stage (one 128-B row of bf16)
+// K per stage, SBK = 64 (one 128-B row of bf16 per operand row) or 32 (64-B rows: half the LDS
+// per stage, so a 256 x 256 tile keeps 4 stages in 128 KiB instead of 2)
 
-__device__ __forceinline__ int sk_swz(int row, int ch) {  // 16-B chunk position in a 128-B LDS row
-  return row * SBK + ((ch ^ ((row >> 1) & 7)) << 3);
+// 16-B chunk position in an LDS row of SBK bf16: the XOR key changes every 256 B of rows (2
+// rows of 128 B, 4 rows of 64 B), so the 16 lanes of one ds_read_b128 pass (16 rows, one
+// logical chunk) land in 16 distinct 16-B bank groups
+template <int SBK>
+__device__ __forceinline__ int sk_swz(int row, int ch) {
+  constexpr int CPR = SBK / 8;             // 16-B chunks per row
+  constexpr int RSH = SBK == 64 ? 1 : 2;   // log2(rows per 256 B)
+  return row * SBK + ((ch ^ ((row >> RSH) & (CPR - 1))) << 3);
 }
 
 // s_waitcnt vmcnt(N) alone (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[15:14];
@@ -66,17 +73,21 @@ __device__ __forceinline__ f32x4 sk_ld4(const float* p) {
 }
 }  // namespace
 
-template <int BN, int BM, int WN, int WM, int NSTAGE, int EPI>
+template <int BN, int BM, int WN, int WM, int NSTAGE, int EPI, int SBK>
 __global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmParams P) {
   constexpr int NW = WN * WM;   // waves per workgroup (4 or 8)
   constexpr int RW = BN / WN;   // weight rows per wave
   constexpr int CW = BM / WM;   // token rows per wave
   constexpr int NTW = RW / 16, MTW = CW / 16;
+  constexpr int CPR = SBK / 8;          // 16-B chunks per LDS row
+  constexpr int RPI = 64 / CPR;         // rows per 1-KiB DMA instruction (8 or 16)
+  constexpr int KSS = SBK / 32;         // 32-deep MFMA k-steps per stage (2 or 1)
+  static_assert(SBK == 64 || SBK == 32, "stage depth");
   static_assert((NW == 4 || NW == 8) && NTW >= 1 && MTW >= 1, "tile");
-  static_assert(BN % (8 * NW) == 0 && BM % (8 * NW) == 0, "every wave stages whole 8-row DMA pieces");
+  static_assert(BN % (RPI * NW) == 0 && BM % (RPI * NW) == 0, "every wave stages whole DMA pieces");
   static_assert(EPI != 2 || NTW % 2 == 0, "SwiGLU pairs gate / up tiles inside a wave");
   static_assert(NSTAGE >= 2 && NSTAGE <= 4, "stage count");
-  constexpr int W_GL = BN / (8 * NW), X_GL = BM / (8 * NW);   // DMA instructions per wave per stage
+  constexpr int W_GL = BN / (RPI * NW), X_GL = BM / (RPI * NW);   // DMA instructions per wave per stage
   constexpr int NPS = W_GL + X_GL;
   constexpr int STAGE = (BN + BM) * SBK;          // uint16 elements per stage
   __shared__ __attribute__((aligned(16))) uint16_t smem[NSTAGE * STAGE];
@@ -97,13 +108,14 @@ __global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmPar
   const int col = lane & 15, h = lane >> 4;
 
   // per-lane DMA sources (fixed over K): instruction i of wave wv fills LDS rows
-  // [8 (wv * N + i), +8) lane-linearly; lane l lands in row + l/8, physical chunk l%8, which
-  // holds logical chunk (l%8) ^ swizzle(row)
+  // [RPI (wv * N + i), +RPI) lane-linearly; lane l lands in row + l / CPR, physical chunk
+  // l % CPR, which holds logical chunk (l % CPR) ^ swizzle(row)
+  constexpr int RSH = SBK == 64 ? 1 : 2;
   const uint16_t* wsrc[W_GL];
 #pragma unroll
   for (int i = 0; i < W_GL; ++i) {
-    const int r = (wv * W_GL + i) * 8 + (lane >> 3);
-    const int ch = (lane & 7) ^ ((r >> 1) & 7);
+    const int r = (wv * W_GL + i) * RPI + lane / CPR;
+    const int ch = (lane % CPR) ^ ((r >> RSH) & (CPR - 1));
     int wrow;
     if constexpr (EPI == 2) {
       const int rr = r % RW;
@@ -121,8 +133,8 @@ __global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmPar
   const uint16_t* xsrc[X_GL];
 #pragma unroll
   for (int i = 0; i < X_GL; ++i) {
-    const int r = (wv * X_GL + i) * 8 + (lane >> 3);
-    const int ch = (lane & 7) ^ ((r >> 1) & 7);
+    const int r = (wv * X_GL + i) * RPI + lane / CPR;
+    const int ch = (lane % CPR) ^ ((r >> RSH) & (CPR - 1));
     int t = mi * BM + r;
     if (t >= P.M) t = P.M - 1;           // padding token rows: any valid row (not stored)
     if (P.xpack)   // tile-packed activations [nM][K/64][BM][64] (rows past M are zero padding)
@@ -143,14 +155,14 @@ __global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmPar
     if (P.wnt) {
 #pragma unroll
       for (int i = 0; i < W_GL; ++i)
-        __builtin_amdgcn_global_load_lds((gptr_t)(wsrc[i] + wk0), (lptr_t)(base + (wv * W_GL + i) * 8 * SBK), 16, 0, 2);
+        __builtin_amdgcn_global_load_lds((gptr_t)(wsrc[i] + wk0), (lptr_t)(base + (wv * W_GL + i) * RPI * SBK), 16, 0, 2);
     } else {
 #pragma unroll
-      for (int i = 0; i < W_GL; ++i) glds16(wsrc[i] + wk0, base + (wv * W_GL + i) * 8 * SBK);
+      for (int i = 0; i < W_GL; ++i) glds16(wsrc[i] + wk0, base + (wv * W_GL + i) * RPI * SBK);
     }
     const int64_t xk0 = P.xpack ? (int64_t)ke * (BM * SBK) : (int64_t)k0;
 #pragma unroll
-    for (int i = 0; i < X_GL; ++i) glds16(xsrc[i] + xk0, base + BN * SBK + (wv * X_GL + i) * 8 * SBK);
+    for (int i = 0; i < X_GL; ++i) glds16(xsrc[i] + xk0, base + BN * SBK + (wv * X_GL + i) * RPI * SBK);
   };
 
   f32x4 acc[NTW][MTW];
@@ -165,10 +177,10 @@ __global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmPar
     const int ch = 4 * s + h;
 #pragma unroll
     for (int mt = 0; mt < MTW; ++mt)
-      bfr[s][mt] = as_bf16x8(*reinterpret_cast<const u16x8*>(&xs[sk_swz(wm * CW + mt * 16 + col, ch)]));
+      bfr[s][mt] = as_bf16x8(*reinterpret_cast<const u16x8*>(&xs[sk_swz<SBK>(wm * CW + mt * 16 + col, ch)]));
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt)
-      af[s][nt] = as_bf16x8(*reinterpret_cast<const u16x8*>(&ws[sk_swz(wn * RW + nt * 16 + col, ch)]));
+      af[s][nt] = as_bf16x8(*reinterpret_cast<const u16x8*>(&ws[sk_swz<SBK>(wn * RW + nt * 16 + col, ch)]));
   };
   auto mfmas = [&](int s) {
 #pragma unroll
@@ -192,18 +204,25 @@ __global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmPar
     __builtin_amdgcn_s_barrier();
     const uint16_t* ws = smem + (kt % NSTAGE) * STAGE;
     if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
-    // k-step 0's fragments first; then its MFMAs with k-step 1's reads interleaved
-    read_frags(ws, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    read_frags(ws, 1);
-    mfmas(0);
+    if constexpr (KSS == 2) {
+      // k-step 0's fragments first; then its MFMAs with k-step 1's reads interleaved
+      read_frags(ws, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      read_frags(ws, 1);
+      mfmas(0);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      __builtin_amdgcn_sched_group_barrier(0x008, GM, 0);   // MFMA
-      __builtin_amdgcn_sched_group_barrier(0x100, GR, 0);   // DS read
+      for (int g = 0; g < 4; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, GM, 0);   // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, GR, 0);   // DS read
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(1);
+    } else {
+      // one 32-deep k-step per stage: its fragments, then its MFMAs
+      read_frags(ws, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(0);
     }
-    __builtin_amdgcn_sched_barrier(0);
-    mfmas(1);
   }
   sk_wait_vm<0>();   // no DMA may still target this CU's LDS when the workgroup ends
 
@@ -357,44 +376,50 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(const float* _
 // {128,64,2,4,2} — 10-70 % slower than the table's picks (profiles/r4_skinny/sweep_more_waves.jsonl); the
 // next stage's DMA pieces spread one by one between the MFMAs instead of issued together at the
 // barrier (5-30 % slower at every tile; 256 x 256 collapsed; profiles/r4_headline_ab/sweep_il.jsonl)
-#define NGA_SKINNY_CFGS(X)     \
-  X(0, 256, 128, 2, 2, 3)   \
-  X(1, 128, 128, 2, 2, 3)   \
-  X(2, 128, 64, 2, 2, 3)    \
-  X(3, 64, 64, 2, 2, 4)     \
-  X(4, 128, 256, 2, 2, 2)   \
-  X(5, 64, 256, 1, 4, 3)    \
-  X(6, 256, 64, 4, 1, 3)    \
-  X(7, 128, 32, 4, 1, 4)    \
-  X(8, 256, 32, 4, 1, 3)    \
-  X(9, 64, 128, 1, 4, 3)    \
-  X(10, 128, 128, 2, 2, 4)  \
-  X(11, 128, 128, 2, 2, 2)  \
-  X(12, 256, 256, 4, 2, 2)  \
-  X(13, 256, 128, 4, 2, 3)  \
-  X(14, 128, 256, 2, 4, 2)  \
-  X(15, 64, 64, 2, 2, 2)    \
-  X(16, 256, 128, 2, 4, 3)
+#define NGA_SKINNY_CFGS(X)       \
+  X(0, 256, 128, 2, 2, 3, 64)   \
+  X(1, 128, 128, 2, 2, 3, 64)   \
+  X(2, 128, 64, 2, 2, 3, 64)    \
+  X(3, 64, 64, 2, 2, 4, 64)     \
+  X(4, 128, 256, 2, 2, 2, 64)   \
+  X(5, 64, 256, 1, 4, 3, 64)    \
+  X(6, 256, 64, 4, 1, 3, 64)    \
+  X(7, 128, 32, 4, 1, 4, 64)    \
+  X(8, 256, 32, 4, 1, 3, 64)    \
+  X(9, 64, 128, 1, 4, 3, 64)    \
+  X(10, 128, 128, 2, 2, 4, 64)  \
+  X(11, 128, 128, 2, 2, 2, 64)  \
+  X(12, 256, 256, 4, 2, 2, 64)  \
+  X(13, 256, 128, 4, 2, 3, 64)  \
+  X(14, 128, 256, 2, 4, 2, 64)  \
+  X(15, 64, 64, 2, 2, 2, 64)    \
+  X(16, 256, 128, 2, 4, 3, 64)  \
+  X(17, 256, 256, 4, 2, 4, 32)  \
+  X(18, 256, 256, 2, 4, 4, 32)  \
+  X(19, 256, 256, 4, 2, 3, 32)  \
+  X(20, 256, 128, 4, 2, 4, 32)  \
+  X(21, 128, 256, 2, 4, 4, 32)
 
 int skinny_gemm_cfg_count() {
   int n = 0;
-#define NGA_COUNT(ID, BN, BM, WN, WM, NS) ++n;
+#define NGA_COUNT(ID, BN, BM, WN, WM, NS, BK) ++n;
   NGA_SKINNY_CFGS(NGA_COUNT)
 #undef NGA_COUNT
   return n;
 }
 
-// {BN, BM, WN, WM, NSTAGE} of a configuration, or zeros
+// {BN, BM, WN, WM, NSTAGE, BK} of a configuration, or zeros
 void skinny_gemm_cfg_info(int cfg, int* info) {
-  info[0] = info[1] = info[2] = info[3] = info[4] = 0;
-#define NGA_INFO(ID, BN, BM, WN, WM, NS) \
-  if (cfg == ID) {                       \
-    info[0] = BN;                        \
-    info[1] = BM;                        \
-    info[2] = WN;                        \
-    info[3] = WM;                        \
-    info[4] = NS;                        \
-    return;                              \
+  info[0] = info[1] = info[2] = info[3] = info[4] = info[5] = 0;
+#define NGA_INFO(ID, BN, BM, WN, WM, NS, BK) \
+  if (cfg == ID) {                           \
+    info[0] = BN;                            \
+    info[1] = BM;                            \
+    info[2] = WN;                            \
+    info[3] = WM;                            \
+    info[4] = NS;                            \
+    info[5] = BK;                            \
+    return;                                  \
   }
   NGA_SKINNY_CFGS(NGA_INFO)
 #undef NGA_INFO
@@ -403,14 +428,14 @@ void skinny_gemm_cfg_info(int cfg, int* info) {
 void launch_skinny_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t stream) {
   const int nblk = p.nN * p.nM * p.split;
   dim3 grid(nblk);
-#define NGA_LAUNCH(ID, BN, BM, WN, WM, NS)                                                        \
-  if (cfg == ID) {                                                                                    \
-    if (nblk == 0) return;                                                                            \
-    const dim3 block(64 * WN * WM);                                                                   \
-    if (epi == 0) skinny_gemm_kernel<BN, BM, WN, WM, NS, 0><<<grid, block, 0, stream>>>(p);       \
-    else if (epi == 1) skinny_gemm_kernel<BN, BM, WN, WM, NS, 1><<<grid, block, 0, stream>>>(p);  \
-    else skinny_gemm_kernel<BN, BM, WN, WM, NS, 2><<<grid, block, 0, stream>>>(p);                \
-    return;                                                                                           \
+#define NGA_LAUNCH(ID, BN, BM, WN, WM, NS, BK)                                                        \
+  if (cfg == ID) {                                                                                        \
+    if (nblk == 0) return;                                                                                \
+    const dim3 block(64 * WN * WM);                                                                       \
+    if (epi == 0) skinny_gemm_kernel<BN, BM, WN, WM, NS, 0, BK><<<grid, block, 0, stream>>>(p);       \
+    else if (epi == 1) skinny_gemm_kernel<BN, BM, WN, WM, NS, 1, BK><<<grid, block, 0, stream>>>(p);  \
+    else skinny_gemm_kernel<BN, BM, WN, WM, NS, 2, BK><<<grid, block, 0, stream>>>(p);                \
+    return;                                                                                               \
   }
   NGA_SKINNY_CFGS(NGA_LAUNCH)
 #undef NGA_LAUNCH

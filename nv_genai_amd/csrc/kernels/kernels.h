@@ -207,7 +207,8 @@ struct SkinnyGemmParams {
   int snt;             // 1: fp32 slab stores (epi 1) non-temporal (kernel form skinny_snt)
 };
 int skinny_gemm_cfg_count();
-void skinny_gemm_cfg_info(int cfg, int* info);   // {BN, BM, WN, WM, NSTAGE}
+void launch_region_marker(int end, int* sink, hipStream_t stream);
+void skinny_gemm_cfg_info(int cfg, int* info);   // {BN, BM, WN, WM, NSTAGE, BK}
 void launch_skinny_gemm(const SkinnyGemmParams& p, int cfg, int epi, hipStream_t stream);
 void launch_splitk_swiglu(const float* P, int S, int M, int F, uint16_t* out, int64_t ldo,
                           hipStream_t stream);

@@ -84,4 +84,16 @@ void launch_row_sqnorm(const uint16_t* X, int64_t N, int D, float* out, hipStrea
   row_sqnorm_kernel<<<(unsigned)((N + 3) / 4), 256, 0, stream>>>(X, N, D, out);
 }
 
+// Timeline markers: one-thread kernels whose names bracket a region in a kernel trace
+// (bench.py's timed window; scripts/summarize_prof.py restricts its busy / gap accounting to
+// the span between the end of the begin marker and the start of the end marker). The store
+// keeps the kernel from being empty; `sink` is a 4-byte device scratch word.
+__global__ void region_begin_marker_kernel(int* sink) { *sink = 1; }
+__global__ void region_end_marker_kernel(int* sink) { *sink = 2; }
+
+void launch_region_marker(int end, int* sink, hipStream_t stream) {
+  if (end) region_end_marker_kernel<<<1, 1, 0, stream>>>(sink);
+  else region_begin_marker_kernel<<<1, 1, 0, stream>>>(sink);
+}
+
 }  // namespace nga

@@ -760,14 +760,25 @@ class LLMEngine:
                 self._finalize(pend)
             return fn()
 
-    def broadcast_command(self, kind: int, n: int = 0) -> None:
+    def broadcast_command(self, kind: int, n: int = 0, payload: Optional[np.ndarray] = None) -> None:
         """Driver of a model-parallel replica: announce a non-step command (kind <= -3) to
         the followers, which run the hook registered for it in :meth:`run_follower` —
-        the same ordered channel as the step layouts, so collectives line up."""
+        the same ordered channel as the step layouts, so collectives line up. ``payload``: host
+        bytes that travel inside the message (e.g. a sharded search's query block, so the
+        search needs no broadcast collective); the hook receives them as a uint8 array."""
         if kind > -3:
             raise ValueError("command kinds are <= -3 (-1 stop, -2 copy-on-fork are reserved)")
         if self.p.mp_size > 1:
-            self._sync_step(kind, n, 0, 0, 0, 0, 0)
+            pl = None
+            if payload is not None:
+                pl = np.ascontiguousarray(payload).view(np.uint8).reshape(-1)
+                if 8 * self._HDR + pl.size > self._msg.size:
+                    raise ValueError(f"command payload of {pl.size} B exceeds the step message slot")
+            self._sync_step(kind, n, 0, 0, 0, 0, 0, payload=pl)
+
+    def command_payload_capacity(self) -> int:
+        """Largest ``broadcast_command`` payload in bytes (0 on a single-rank engine)."""
+        return 0 if self._msg is None else int(self._msg.size - 8 * self._HDR)
 
     def drain(self) -> List[Request]:
         """Settle the in-flight pipelined step (if any)."""
@@ -797,19 +808,20 @@ class LLMEngine:
                 + S * (4 + 4 + 4 + 8 + 8) + 16 * T + 64)
 
     def _sync_step(self, kind: int, n: int, ntok: int, max_q: int, max_ctx: int, bs: int, nd: int = 0,
-                   gb: int = 0, src=None, pairs=None) -> None:
+                   gb: int = 0, src=None, pairs=None, payload=None) -> None:
         """Driver: publish a step (or a command, kind < 0) to the replica's ranks. ``gb``: token
         bucket of a graph-captured prefill / mixed step (its padded token rows travel too, so
         followers replay the same graph on the same inputs); ``src``: the pipelined id gather
         (token rows, rows of the in-flight step) — every follower applies it to its own sampled
         tokens; the sampling parameters travel so followers sample exactly what the driver
-        samples. ``pairs``: [2, k] copy-on-fork pages (kind -2)."""
+        samples. ``pairs``: [2, k] copy-on-fork pages (kind -2); ``payload``: a command's bytes
+        (kind <= -3; their count travels in the pairs field)."""
         if self.p.mp_size == 1:
             return
         rows, toks = max(n, bs), max(ntok, bs, gb)
         prow = max(rows, self.cfg.max_num_seqs if gb else 0) if kind >= 0 else 0
         nsrc = 0 if src is None else len(src[0])
-        npairs = 0 if pairs is None else int(pairs.shape[1])
+        npairs = int(payload.size) if payload is not None else (0 if pairs is None else int(pairs.shape[1]))
         m = self._msg
         m[:8 * self._HDR].view(np.int64)[:] = (kind, n, ntok, max_q, max_ctx, bs, nd, gb, nsrc, prow, npairs, 0)
         o = 8 * self._HDR
@@ -830,6 +842,8 @@ class LLMEngine:
             if nsrc:
                 put(np.asarray(src[0], dtype=np.int64))
                 put(np.asarray(src[1], dtype=np.int64))
+        elif payload is not None:
+            put(payload)
         elif npairs:
             put(np.asarray(pairs, dtype=np.int32))
         self._chan.send(m[:o])
@@ -850,7 +864,10 @@ class LLMEngine:
             return a
 
         if kind < 0:
-            pairs = take(np.int32, 2 * npairs).reshape(2, npairs).copy() if npairs else None
+            if kind <= -3:   # a command: its payload bytes (or None)
+                pairs = take(np.uint8, npairs).copy() if npairs else None
+            else:
+                pairs = take(np.int32, 2 * npairs).reshape(2, npairs).copy() if npairs else None
             return kind, n, 0, 0, 0, 0, 0, 0, None, pairs
         rows, toks = max(n, bs), max(ntok, bs, gb)
         if self._up_ev is not None:
@@ -911,7 +928,10 @@ class LLMEngine:
             if kind <= -3:
                 if not hooks or kind not in hooks:
                     raise RuntimeError(f"follower has no hook for command {kind}")
-                hooks[kind](n)
+                if pairs is None:
+                    hooks[kind](n)
+                else:          # the command's payload bytes
+                    hooks[kind](n, pairs)
                 continue
             if kind == -2:   # copy-on-fork pages (beam search)
                 self.model.copy_kv_blocks(torch.from_numpy(pairs[0]), torch.from_numpy(pairs[1]))

@@ -3,10 +3,12 @@ index of the query-decomposition config split over the 8 GPUs of a node.
 
 * ``add``: every rank sees the same (vectors, ids) and keeps its stripe (row i -> rank
   i % world), so no data moves at build time;
-* ``search``: the driver's query block is broadcast (RCCL broadcast, CC7), each rank runs the
-  MFMA score + top-k kernels on its local shard, the per-shard (score, id) lists are
-  all-gathered (CC8) and merged by the same top-k kernel over the world*k candidates (K15).
-At 1.25M x 1024 bf16 per GPU a shard is 2.5 GB of HBM; each collective moves a few KB.
+* ``search``: the driver's query block reaches every rank (inside the replica's step-channel
+  command, or by a broadcast, CC7), each rank runs the MFMA score + top-k kernels on its local
+  shard, the per-shard (score, id) lists are packed into one tensor and all-gathered in one
+  collective — the IPC all-gather kernel of the TP group when it has one (CC8) — and merged by
+  the same top-k kernel over the world*k candidates (K15).
+At 1.25M x 1024 bf16 per GPU a shard is 2.5 GB of HBM; the gather moves 48 B per query and rank.
 
 Snapshot / restore (the Milvus-volume / FAISS ``save_local`` persistence of
 the reference, ``docker-compose-vectordb.yaml:27,46,64``): ``save`` writes one safetensors
@@ -24,6 +26,8 @@ import time
 from pathlib import Path
 from typing import Optional, Tuple
 
+import numpy as np  # noqa: F401  (query_payload's return type)
+
 import torch
 import torch.distributed as dist
 
@@ -34,7 +38,8 @@ from .flat import FlatIndex
 
 class ShardedIndex:
     def __init__(self, dim: int, metric: str = "cosine", device: Optional[str] = None,
-                 pctx: Optional[ParallelContext] = None, group=None, capacity: int = 1024):
+                 pctx: Optional[ParallelContext] = None, group=None, capacity: int = 1024,
+                 ipc_gather: bool = True):
         self.p = pctx or get_context()
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -42,6 +47,10 @@ class ShardedIndex:
         self.dim, self.metric = dim, metric
         self.local = FlatIndex(dim, metric, device, capacity=capacity)
         self.comm_dev = self.local.device if self.p.backend == "nccl" else torch.device("cpu")
+        # searches, how their results were gathered, host time inside search() (launch-side:
+        # the merge is left on the stream)
+        self.stats = {"searches": 0, "broadcasts": 0, "ipc_gathers": 0, "pg_gathers": 0, "host_s": 0.0}
+        self._car = self._make_ipc_gather() if ipc_gather else None
 
     def __len__(self):
         n = torch.tensor([len(self.local)], dtype=torch.int64, device=self.comm_dev)
@@ -133,30 +142,89 @@ class ShardedIndex:
                 idx.local.add(shard.X[:n][sel], shard.ids[:n][sel])
         return idx
 
+    def _make_ipc_gather(self):
+        """This index's own IPC communicator (parallel/custom_ar.py: Signal block + staging
+        buffers mapped by every rank of the group), used only for the search gather. Its own,
+        not the TP group's: a search may run on another stream than the model's all-reduces
+        (bench.py's retrieval stream), and two kernels of one communicator must never run at
+        once on a rank (they share its call counter). Collective over the group; None on the
+        CPU, at world 1, with NGA_CUSTOM_AR=0, or when it fails its self-test."""
+        if (self.world <= 1 or self.world > 8 or self.local.device.type != "cuda"
+                or os.environ.get("NGA_CUSTOM_AR", "1") == "0"):
+            return None
+        from ..parallel.custom_ar import CustomAllReduce
+
+        try:
+            car = CustomAllReduce(self.group, capacity_mb=4.0)
+        except RuntimeError:        # raised on every rank alike (the constructor agrees first)
+            return None
+        return car if car.enabled else None
+
+    def _custom_gather(self):
+        return self._car
+
+    def query_payload(self, q: torch.Tensor) -> "np.ndarray":
+        """The query block as host bytes for the replica's step channel (fp32 [n, dim]): the
+        followers receive it inside the search command instead of through a broadcast."""
+        return q.detach().to(torch.float32).reshape(-1, self.dim).cpu().contiguous().numpy()
+
+    def queries_from_payload(self, n: int, payload) -> torch.Tensor:
+        return torch.from_numpy(payload).view(torch.float32).view(n, self.dim).to(self.local.device)
+
     @torch.inference_mode()
-    def search(self, q: torch.Tensor, k: int, src: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    def search(self, q: torch.Tensor, k: int, src: int = 0,
+               have_queries: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Top-``k`` over every shard (collective over the group). ``have_queries``: every rank
+        already holds ``q`` (it travelled in the step-channel command, ``query_payload``), so no
+        broadcast is needed; otherwise rank ``src``'s block is broadcast first (CC7).
+
+        Each rank's (score, id) list is packed into one int32 row per query — the k fp32 score
+        bit patterns, then the k int64 ids as 2k words — and gathered in ONE collective (CC8): the replica's
+        IPC all-gather kernel when the group has one (ranks read each other's staging buffers
+        over xGMI; no host round trip), else one process-group all-gather. The world x k
+        candidates are merged by the top-k kernel (K15)."""
         if q.dim() == 1:
             q = q.unsqueeze(0)
         if self.world == 1:
             return self.local.search(q, k)
-        qd = q.to(self.comm_dev, torch.float32).contiguous()
-        dist.broadcast(qd, src=src, group=self.group)
+        t0 = time.perf_counter()
+        if have_queries:
+            qd = q.to(self.local.device, torch.float32).contiguous()
+        else:
+            qd = q.to(self.comm_dev, torch.float32).contiguous()
+            dist.broadcast(qd, src=src, group=self.group)
+            self.stats["broadcasts"] += 1
         vals, ids = self.local.search(qd.to(self.local.device), k)
         nq = qd.shape[0]
         kk = vals.shape[1]
         if kk < k:  # pad a short shard
             vals = torch.cat([vals, torch.full((nq, k - kk), float("-inf"), device=vals.device)], 1)
             ids = torch.cat([ids, torch.full((nq, k - kk), -1, dtype=torch.int64, device=ids.device)], 1)
-        v_all = [torch.empty(nq, k, dtype=torch.float32, device=self.comm_dev) for _ in range(self.world)]
-        i_all = [torch.empty(nq, k, dtype=torch.int64, device=self.comm_dev) for _ in range(self.world)]
-        dist.all_gather(v_all, vals.to(self.comm_dev).float().contiguous(), group=self.group)
-        dist.all_gather(i_all, ids.to(self.comm_dev).contiguous(), group=self.group)
-        cv = torch.cat(v_all, 1).to(self.local.device).contiguous()
-        ci = torch.cat(i_all, 1).to(self.local.device).contiguous()
+        width = -(-3 * k // 4) * 4              # k scores + 2k id words, padded to 16-B rows
+        # int32 words throughout, so no float path ever touches the id bits (a -1 id is a NaN
+        # pattern as fp32)
+        packed = torch.zeros(nq, width, dtype=torch.int32, device=vals.device)
+        packed[:, :k] = vals.float().contiguous().view(torch.int32)
+        packed[:, k:3 * k] = ids.to(torch.int64).contiguous().view(torch.int32)
+        car = self._custom_gather() if packed.is_cuda else None
+        if car is not None and car.gather_eligible(packed):
+            g = car.all_gather(packed)                                   # [nq, world * width]
+            self.stats["ipc_gathers"] += 1
+        else:
+            parts = [torch.empty(nq, width, dtype=torch.int32, device=self.comm_dev) for _ in range(self.world)]
+            dist.all_gather(parts, packed.to(self.comm_dev), group=self.group)
+            g = torch.cat(parts, 1).to(self.local.device)
+            self.stats["pg_gathers"] += 1
+        g = g.view(nq, self.world, width)
+        cv = g[:, :, :k].contiguous().view(torch.float32).reshape(nq, self.world * k).contiguous()
+        ci = g[:, :, k:3 * k].contiguous().view(torch.int64).reshape(nq, self.world * k).contiguous()
         if cv.is_cuda:
             mv = torch.empty(nq, k, dtype=torch.float32, device=cv.device)
             mi = torch.empty(nq, k, dtype=torch.int64, device=cv.device)
             ops.kernels().topk(cv, ci, cv.shape[1], k, mv, mi)
-            return mv, mi
-        mv, pos = torch.topk(cv, k, dim=1)
-        return mv, torch.gather(ci, 1, pos)
+        else:
+            mv, pos = torch.topk(cv, k, dim=1)
+            mi = torch.gather(ci, 1, pos)
+        self.stats["searches"] += 1
+        self.stats["host_s"] += time.perf_counter() - t0
+        return mv, mi

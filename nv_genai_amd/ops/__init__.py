@@ -820,6 +820,23 @@ def pool_l2norm(hidden, cu, mode: int = 0, normalize: bool = True, out=None):
     return out
 
 
+_MARKER_SINK = {}
+
+
+def region_marker(device, end: bool) -> None:
+    """Launch the begin (``end=False``) or end marker kernel on ``device``'s current stream:
+    a kernel trace (rocprofv3 --kernel-trace) then shows where a region such as bench.py's timed
+    window starts and ends on the GPU timeline (scripts/summarize_prof.py uses them). No-op on
+    the CPU."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        return
+    sink = _MARKER_SINK.get(device)
+    if sink is None:
+        sink = _MARKER_SINK[device] = torch.zeros(1, dtype=torch.int32, device=device)
+    kernels().region_marker(sink, 1 if end else 0)
+
+
 def row_sqnorm(X, out=None):
     if not _gpu(X):
         return ref.row_sqnorm(X)

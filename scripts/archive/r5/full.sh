@@ -9,5 +9,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --time
 rc=$?
 tail -25 $out/pytest_gpu.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc    # 1 = test failures (read them); anything else: stop
-if [ "${2:-}" = "headline" ]; then bash scripts/r5/headline.sh ${1:-r5_full}_headline; fi
+if [ "${2:-}" = "headline" ]; then bash scripts/archive/r5/headline.sh ${1:-r5_full}_headline; fi
 exit $rc

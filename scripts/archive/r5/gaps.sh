@@ -12,6 +12,6 @@ HIP_FORCE_DEV_KERNARG=1 timeout -k 10 300 python benchmarks/decode_step.py --bat
 tail -1 $out/decode_devkernarg.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $R/$out/raw -o run -- python3 $R/benchmarks/decode_step.py --batch 256 --ctx 1400 --steps 16 > $R/$out/prof.log 2>&1 || { tail -20 $R/$out/prof.log; exit 1; }
-python3 $R/scripts/r5/graph_gaps.py $R/$out/raw > $R/$out/gaps.txt 2>&1
+python3 $R/scripts/archive/r5/graph_gaps.py $R/$out/raw > $R/$out/gaps.txt 2>&1
 rm -rf $R/$out/raw
 cat $R/$out/gaps.txt

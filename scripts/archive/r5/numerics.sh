@@ -16,4 +16,4 @@ timeout -k 10 400 python -u -m pytest -s -v -p no:cacheprovider --timeout 200 --
 rc=$?
 grep -E "PASSED|FAILED|ERROR|worst|delta|smoke|passed|failed" $out/numerics.log | tail -40
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-bash scripts/r5/full.sh r5_numerics_full
+bash scripts/archive/r5/full.sh r5_numerics_full

@@ -18,6 +18,7 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 import torch
 import torch.multiprocessing as mp
@@ -253,3 +254,48 @@ def test_custom_all_reduce_auto_routes_two_shot_through_comm():
     assert car.impl.algos == [ALGO_TWO_SHOT, ALGO_ONE_SHOT]
     assert car.algo_counts == {ALGO_ONE_SHOT: 1, ALGO_TWO_SHOT: 1}
     assert float(big[0]) == 8.0 and float(small[0]) == 8.0
+
+
+def _shard_payload_worker(rank, world, port, q):
+    """The search command's path: the driver's query block arrives as channel payload bytes
+    (query_payload -> queries_from_payload), no broadcast; ids past 2^31 and short shards
+    (-1 padding) survive the packed int32 gather."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from nv_genai_amd.index.flat import FlatIndex
+    from nv_genai_amd.index.sharded import ShardedIndex
+    from nv_genai_amd.parallel import dist as pd
+
+    pctx = pd.init_distributed(tp_size=1, backend="gloo", device="cpu")
+    g = torch.Generator().manual_seed(9)
+    X = torch.randn(21, 32, generator=g)          # 21 rows over 4 ranks: shards of 6/5/5/5 < k
+    Q = torch.randn(3, 32, generator=g)
+    ids = torch.arange(21, dtype=torch.int64) * 3_000_000_019 + 5    # up to 6e10 > 2^31
+    sh = ShardedIndex(32, "cosine", "cpu", pctx=pctx)
+    sh.add(X, ids)
+    payload = sh.query_payload(Q)                 # what the driver puts in the command
+    qq = sh.queries_from_payload(3, payload.view(np.uint8).reshape(-1))
+    vals, out_ids = sh.search(qq, 8, have_queries=True)
+    if rank == 0:
+        full = FlatIndex(32, "cosine", "cpu")
+        full.add(X, ids)
+        rv, ri = full.search(Q, 8)
+        q.put((vals.numpy(), out_ids.numpy(), rv.numpy(), ri.numpy(), dict(sh.stats)))
+    pd.destroy()
+
+
+def test_sharded_search_from_command_payload_packed_gather():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_payload_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    vals, ids, rv, ri, st = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert torch.allclose(torch.from_numpy(vals), torch.from_numpy(rv), atol=1e-5)
+    assert torch.equal(torch.from_numpy(ids), torch.from_numpy(ri))
+    assert st["broadcasts"] == 0 and st["pg_gathers"] == 1 and st["searches"] == 1

@@ -713,6 +713,7 @@ def test_skinny_gemm_every_cfg(gpu, M):
     ref0, ref2 = _skinny_ref(x, w, 0), _skinny_ref(x, wg, 2)
     for cfg in range(C.skinny_cfg_count()):
         BN, BM = C.skinny_cfg(cfg)[:2]
+        BK = C.skinny_cfg(cfg)[5]     # 64, or 32 (64-B LDS rows, twice the stages per KiB)
         _close_rows(ops.skinny_gemm(x, w, cfg, 1, 0), ref0, rel=1e-2)
         for s in (2, 5):
             P = ops.skinny_gemm(x, w, cfg, s, 1)
@@ -723,7 +724,13 @@ def test_skinny_gemm_every_cfg(gpu, M):
             _close_rows(y2, ref2, rel=2e-2)
             # tile-packed weights and the rotated K walk: the same products (fp32 sums in
             # another order for krot)
-            assert torch.equal(ops.skinny_gemm(x, ops.pack_weight(wg, BN, 2), cfg, 1, 2, n_out=512), y2)
+            if BK == 64:
+                assert torch.equal(ops.skinny_gemm(x, ops.pack_weight(wg, BN, 2), cfg, 1, 2, n_out=512), y2)
+        if BK != 64:   # packed operands are 64-deep tiles: refused for BK 32 tiles
+            with pytest.raises(RuntimeError, match="packed operands"):
+                ops.skinny_gemm(x, ops.pack_weight(w, BN), cfg, 1, 0, n_out=1000)
+            _close_rows(ops.skinny_gemm(x, w, cfg, 3, 1, krot=1).sum(0), ref0, rel=1e-4)
+            continue
         y0 = ops.skinny_gemm(x, w, cfg, 1, 0)
         assert torch.equal(ops.skinny_gemm(x, ops.pack_weight(w, BN), cfg, 1, 0, n_out=1000), y0)
         assert torch.equal(ops.skinny_gemm(ops.pack_rows(x, BM), ops.pack_weight(w, BN), cfg, 1, 0, n_out=1000,

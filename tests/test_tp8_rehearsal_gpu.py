@@ -13,10 +13,10 @@ experimental/fm-asr-streaming-rag/nim/configs/mistral-7b.yaml:32-36):
 * the same run with ``NGA_CUSTOM_AR=0``: every collective over gloo, graphs off (a graph may
   hold only IPC collectives), and the same tokens.
 
-Tokens must equal a synchronous (unpipelined) W = 8 run with the same graphs, and agree on >= 90 %
-of positions with an eager W = 8 run (no bucket padding, so the library GEMMs may pick other
-kernels and near-tied greedy choices can differ) and with TP = 1 (bf16 partial sums round
-differently). Every all-reduce / all-gather meets its peers in time (sticky timeout code 0).
+Tokens must equal a synchronous (unpipelined) W = 8 run with the same graphs, and match an eager
+W = 8 run (no bucket padding, so the library GEMMs may pick other kernels) and TP = 1 (bf16
+partial sums round differently) up to near-tie divergences (test_engine_gpu._same_greedy_run).
+Every all-reduce / all-gather meets its peers in time (sticky timeout code 0).
 
 Found by this rehearsal: with every rank's grid at the 80-block cap, the eight ranks' spinning
 all-reduce blocks were not all resident at once beside the engine's other kernels and the
@@ -67,7 +67,7 @@ def _worker(rank, port, q, custom_ar, over=None):
         # 120 + 60 + 140 + 90 prompt tokens: a 410-token prefill step (bucket 512: a 2 MiB
         # all-reduce), then decode steps of 4 rows (16 KiB: one-shot, fused add + RMSNorm)
         prompts = [[5, 6, 7, 8] * 30, [9, 10, 11] * 20, [12, 13] * 70, [21, 22, 23] * 30]
-        greedy = SamplingParams(temperature=0.0, max_tokens=16, ignore_eos=True)
+        greedy = SamplingParams(temperature=0.0, max_tokens=16, ignore_eos=True, logprobs=True)
         hot = SamplingParams(temperature=0.8, top_p=0.9, max_tokens=12, ignore_eos=True, seed=3)
         ecfg = EngineConfig(model="llama70b-small", max_num_seqs=4, max_batched_tokens=1024, max_model_len=1024,
                             kv_cache_blocks=64, use_graphs=True, mixed_graphs=True, graph_token_step=128,
@@ -77,7 +77,7 @@ def _worker(rank, port, q, custom_ar, over=None):
         if rank == 0:
             e1 = LLMEngine(dataclasses.replace(ecfg, use_graphs=False, mixed_graphs=False), device="cuda",
                            pctx=pd.ParallelContext(), weights=full)
-            res["ref"] = [r.output_ids for r in e1.generate(prompts, greedy)]
+            res["ref"] = [(r.output_ids, r.logprobs) for r in e1.generate(prompts, greedy)]
             del e1
             torch.cuda.empty_cache()
         pctx = pd.init_distributed(tp_size=WORLD, backend="gloo", device="cuda")
@@ -94,7 +94,7 @@ def _worker(rank, port, q, custom_ar, over=None):
         torch.cuda.synchronize()
         res["ar_error_init"] = car.error() if car is not None else 0
         if eng.is_driver:
-            res["out"] = [r.output_ids for r in eng.generate(prompts, greedy)]
+            res["out"] = [(r.output_ids, r.logprobs) for r in eng.generate(prompts, greedy)]
             res["hot"] = [r.output_ids for r in eng.generate(prompts, hot)]
             res["unpipelined"] = eng.stats["unpipelined_steps"]
             res["graph_steps"] = eng.stats["graph_steps"]
@@ -121,7 +121,7 @@ def _worker(rank, port, q, custom_ar, over=None):
             e2 = LLMEngine(dataclasses.replace(ecfg, **o), device="cuda", pctx=pctx, model=eng.model,
                            tokenizer=eng.tok, model_cfg=eng.mcfg)
             if e2.is_driver:
-                res[key] = [r.output_ids for r in e2.generate(prompts, greedy)]
+                res[key] = [(r.output_ids, r.logprobs) for r in e2.generate(prompts, greedy)]
                 e2.stop_followers()
             else:
                 e2.run_follower()
@@ -157,17 +157,19 @@ def _run(custom_ar: bool, over=None, check=True):
     return results
 
 
-def _agree(a, b) -> float:
-    return sum(x == y for o, r in zip(a, b) for x, y in zip(o, r)) / max(1, sum(len(r) for r in b))
-
-
 def _check_tokens(results):
+    from test_engine_gpu import _same_greedy_run
+
     drv = results[0]
     assert drv["hq_hkv"] == (8, 1), drv
-    assert all(len(o) == 16 for o in drv["out"])
-    assert drv["out"] == drv["sync"], (drv["out"], drv["sync"])
-    assert _agree(drv["out"], drv["eager"]) >= 0.9, (drv["out"], drv["eager"])
-    assert _agree(drv["out"], drv["ref"]) >= 0.9, (drv["out"], drv["ref"])
+    assert all(len(o) == 16 for o, _ in drv["out"])
+    # pipelined vs synchronous steps over the same graphs: identical tokens
+    assert [o for o, _ in drv["out"]] == [o for o, _ in drv["sync"]], (drv["out"], drv["sync"])
+    # vs eager W = 8 and vs TP = 1: equal first tokens, log-probs close until a divergence, and
+    # a divergence only at a near-tie (random weights: bucket padding or another partial-sum
+    # order can flip an exact tie, after which a greedy sequence follows another path)
+    _same_greedy_run(drv["out"], drv["eager"])
+    _same_greedy_run(drv["out"], drv["ref"])
     assert all(len(o) == 12 for o in drv["hot"])
     # after temperature sampling every rank holds the driver's tokens
     assert all(r["last_tok"] == drv["last_tok"] for r in results), [r["last_tok"] for r in results]
