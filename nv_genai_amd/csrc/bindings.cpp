@@ -695,6 +695,26 @@ void topk(Tensor in, c10::optional<Tensor> in_idx, int64_t seg_len, int64_t k, T
                    out_i.data_ptr<int64_t>(), cur_stream(in));
 }
 
+// packed step-input upload: scatter segments of the device staging buffer `src` (uint8) to
+// raw device addresses (the engine's fixed step buffers), one kernel for every segment
+void scatter_segments(Tensor src, const std::vector<int64_t>& dst, const std::vector<int64_t>& off,
+                      const std::vector<int64_t>& bytes) {
+  CHECK_DEV(src); CHECK_CONTIG(src); CHECK_DT(src, at::kByte);
+  TORCH_CHECK(dst.size() == off.size() && off.size() == bytes.size() && dst.size() <= (size_t)nga::kMaxSegments,
+              "scatter_segments: matching dst / off / bytes lists of at most 32 segments");
+  nga::SegmentTable t{};
+  t.n = (int)dst.size();
+  for (size_t i = 0; i < dst.size(); ++i) {
+    TORCH_CHECK(off[i] % 16 == 0 && dst[i] % 16 == 0 && bytes[i] % 4 == 0 && bytes[i] >= 0 &&
+                    off[i] + bytes[i] <= src.numel(),
+                "scatter_segments: 16-B aligned segments of whole 4-B words inside the staging buffer");
+    t.dst[i] = dst[i];
+    t.off[i] = off[i];
+    t.bytes[i] = bytes[i];
+  }
+  nga::launch_scatter_segments(reinterpret_cast<const uint8_t*>(src.data_ptr()), t, cur_stream(src));
+}
+
 // a begin / end marker kernel on the current stream (kernel-trace window delimiters)
 void region_marker(Tensor sink, int64_t end) {
   CHECK_DEV(sink); CHECK_DT(sink, at::kInt);
@@ -948,6 +968,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("score_topk_dma_ok", [](int64_t d, int64_t q) { return (bool)nga::score_topk_dma_ok((int)d, (int)q); });
   m.def("pool_l2norm", checked("pool_l2norm", &pool_l2norm));
   m.def("region_marker", checked("region_marker", &region_marker));
+  m.def("scatter_segments", checked("scatter_segments", &scatter_segments));
   m.def("row_sqnorm", checked("row_sqnorm", &row_sqnorm));
   m.def("fir_c64", checked("fir_c64", &fir_c64));
   m.def("fm_demod", checked("fm_demod", &fm_demod));

@@ -206,6 +206,17 @@ struct SkinnyGemmParams {
   int wnt;             // 1: weight DMA with the non-temporal cache policy (streamed once)
   int snt;             // 1: fp32 slab stores (epi 1) non-temporal (kernel form skinny_snt)
 };
+// scatter of packed step inputs (staging.hip): segment s = bytes [off, off + bytes) of the
+// device staging buffer -> dst (16-B aligned offsets / destinations, bytes % 4 == 0)
+constexpr int kMaxSegments = 32;
+struct SegmentTable {
+  int n;
+  int64_t dst[kMaxSegments];
+  int64_t off[kMaxSegments];
+  int64_t bytes[kMaxSegments];
+};
+void launch_scatter_segments(const uint8_t* src, const SegmentTable& t, hipStream_t stream);
+
 int skinny_gemm_cfg_count();
 void launch_region_marker(int end, int* sink, hipStream_t stream);
 void skinny_gemm_cfg_info(int cfg, int* info);   // {BN, BM, WN, WM, NSTAGE, BK}

@@ -290,6 +290,7 @@ class ShmChannel {
     const size_t cap = (size_t)bi.size * (size_t)bi.itemsize;
     const uint64_t s = rseq_ + 1;
     SlotHead* sh = slot(s);
+    const int64_t t_wait = now_ns();
     int rc;
     {
       py::gil_scoped_release nogil;
@@ -302,21 +303,30 @@ class ShmChannel {
     const size_t len = sh->len;
     if (len > cap) throw std::runtime_error("shm channel: receive buffer too small");
     std::memcpy(bi.ptr, reinterpret_cast<const uint8_t*>(sh) + sizeof(SlotHead), len);
-    const int64_t lat = now_ns() - sh->pub_ns;
+    const int64_t t_got = now_ns();
+    const int64_t lat = t_got - sh->pub_ns;
+    // wake-up latency: from the later of (message published, reader started waiting) to
+    // receipt; the plain publish -> receipt latency also counts time the reader spent busy
+    // with the previous step, when the message was already there
+    const int64_t wake = t_got - std::max(sh->pub_ns, t_wait);
     rseq_ = s;
     hdr_->done[reader_].store(s, std::memory_order_release);
     hdr_->done_gen.fetch_add(1, std::memory_order_seq_cst);
     if (hdr_->writer_sleeping.load(std::memory_order_seq_cst) != 0) futex_wake_all(&hdr_->done_gen);
-    if (lat_.size() < kLatCap)
+    if (lat_.size() < kLatCap) {
       lat_.push_back(lat);
-    else
+      wake_.push_back(wake);
+    } else {
       lat_[lat_n_ % kLatCap] = lat;
+      wake_[lat_n_ % kLatCap] = wake;
+    }
     ++lat_n_;
     return (int64_t)len;
   }
 
-  // Receive-side wake-up latency (publish -> message copied out) over the last messages,
-  // and how each wait ended (spinning, yielding or after a futex sleep).
+  // Receive side, over the last messages: publish -> receipt latency (lat_*), wake-up latency
+  // (wake_*: from the later of publish and the start of the wait), and how each wait ended
+  // (spinning, yielding or after a futex sleep).
   py::dict stats() const {
     py::dict d;
     const WaitStats& w = creator_ ? wstats_ : rstats_;
@@ -325,13 +335,16 @@ class ShmChannel {
     d["sleeps"] = w.sleeps;
     d["messages"] = creator_ ? wseq_ : rseq_;
     if (!creator_ && !lat_.empty()) {
-      std::vector<int64_t> v(lat_);
-      std::sort(v.begin(), v.end());
-      auto pct = [&](double q) { return v[std::min(v.size() - 1, (size_t)(q * (double)(v.size() - 1) + 0.5))] / 1e3; };
-      d["lat_n"] = (uint64_t)v.size();
-      d["lat_p50_us"] = pct(0.5);
-      d["lat_p99_us"] = pct(0.99);
-      d["lat_max_us"] = v.back() / 1e3;
+      for (int which = 0; which < 2; ++which) {
+        std::vector<int64_t> v(which ? wake_ : lat_);
+        std::sort(v.begin(), v.end());
+        auto pct = [&](double q) { return v[std::min(v.size() - 1, (size_t)(q * (double)(v.size() - 1) + 0.5))] / 1e3; };
+        const std::string k = which ? "wake" : "lat";
+        d[(k + "_p50_us").c_str()] = pct(0.5);
+        d[(k + "_p99_us").c_str()] = pct(0.99);
+        d[(k + "_max_us").c_str()] = v.back() / 1e3;
+      }
+      d["lat_n"] = (uint64_t)lat_.size();
     }
     return d;
   }
@@ -367,7 +380,7 @@ class ShmChannel {
   size_t bytes_ = 0, slot_stride_ = 0;
   uint64_t wseq_ = 0, rseq_ = 0;
   WaitStats wstats_, rstats_;
-  std::vector<int64_t> lat_;
+  std::vector<int64_t> lat_, wake_;
   uint64_t lat_n_ = 0;
   std::thread beater_;
   std::mutex mu_;

@@ -340,6 +340,17 @@ class LLMEngine:
             self.h_sidx, self.d_sidx = hbuf(S, dtype=torch.int64), dbuf(S, dtype=torch.int64)
             self.h_items, self.d_items = hbuf(cap, 2), dbuf(cap, 2)
             self.h_nitems, self.d_nitems = hbuf(1), dbuf(1)
+        # every step's inputs in one pinned -> device copy + one scatter kernel (ops/staging.py)
+        self._stager = None
+        self._staged_src = None
+        if self.gpu and os.environ.get("NGA_PACKED_UPLOAD", "1") != "0":   # 0: per-buffer copies (A/B)
+            from ..ops.staging import PackedUpload
+
+            bufs = [self.h_ids, self.h_pos, self.h_slots, self.h_cu, self.h_ctx, self.h_bt, self.h_temp,
+                    self.h_topk, self.h_topp, self.h_seed, self.h_step, self.h_pen, self.h_gidx, self.h_gprev]
+            if self._mg_ok:
+                bufs += [self.h_ctxd, self.h_items, self.h_nitems, self.h_sidx]
+            self._stager = PackedUpload(self.device, sum(b.numel() * b.element_size() + 16 for b in bufs))
         if self.gpu and cfg.use_graphs:
             self._capture_graphs()
 
@@ -542,8 +553,10 @@ class LLMEngine:
             if ok:
                 src = (ph, [rows[int(sid[i])] for i in ph.tolist()])
             else:
-                # cannot pipeline: settle the in-flight step, then run this one normally
-                self.stats["unpipelined_steps"] += 1
+                # cannot pipeline: settle the in-flight step, then run this one normally (with
+                # nothing left to schedule, kind 0, this is just the end-of-work drain)
+                if kind != 0:
+                    self.stats["unpipelined_steps"] += 1
                 done += self._finalize(pend)
                 pend = self._pending = None
                 for i in ph.tolist():
@@ -666,7 +679,7 @@ class LLMEngine:
                     self._graph_step(key, kind, n, ntok, max_q, max_ctx, nd, src)
                 else:
                     self._sync_step(kind, n, ntok, max_q, max_ctx, 0, nd, src=src)
-                    self._upload(n, ntok)
+                    self._upload(n, ntok, src=src)
                     self._gather_ids(src)
                     logits = self._prefill_forward(n, ntok, max_q, max_ctx, nd)
                     self._sample(logits, n)
@@ -688,8 +701,11 @@ class LLMEngine:
 
     def _stage_gather(self, src):
         """Device copies of the gather's (token index, previous row) lists, uploaded from the
-        pinned staging buffers; the upload event then covers them too."""
+        pinned staging buffers; the upload event then covers them too. Lists that the step's
+        packed upload already carried (``_upload(..., src=src)``) are not copied again."""
         k = len(src[0])
+        if src is self._staged_src:
+            return (self.d_gidx[:k], self.d_gprev[:k]) if self.gpu else (self.h_gidx[:k], self.h_gprev[:k])
         self.h_gidx.numpy()[:k] = src[0]
         self.h_gprev.numpy()[:k] = src[1]
         if not self.gpu:
@@ -712,7 +728,7 @@ class LLMEngine:
         if bs is not None:
             self._pad_rows(n, bs)
         self._sync_step(2, n, n, 1, self.cfg.max_model_len, bs or 0, src=src)
-        self._upload(bs or n, bs or n)
+        self._upload(bs or n, bs or n, src=src)
         self._apply_decode_src(n, src)
         if bs is not None:
             self.graphs[bs].replay()
@@ -947,15 +963,15 @@ class LLMEngine:
                     raise RuntimeError(f"follower cannot replay the driver's step graph {gb}")
                 self._graph_step(key, kind, n, ntok, max_q, max_ctx, nd, src, follower=True)
             elif kind in (1, 3):
-                self._upload(n, ntok)
+                self._upload(n, ntok, src=src)
                 self._gather_ids(src)
                 self._follower_sample(self._prefill_forward(n, ntok, max_q, max_ctx, nd), n)
             elif bs:
-                self._upload(bs, bs, nparam=prow)
+                self._upload(bs, bs, nparam=prow, src=src)
                 self._apply_decode_src(n, src)
                 self.graphs[bs].replay()
             else:
-                self._upload(n, n)
+                self._upload(n, n, src=src)
                 self._apply_decode_src(n, src)
                 meta = self._meta("decode", n, n, 1, self.cfg.max_model_len)
                 h = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta)
@@ -1101,26 +1117,31 @@ class LLMEngine:
             m.cu_q_prefill = self.d_cu[nd: n + 1] - nd
         return m
 
-    def _upload(self, n, ntok, nparam: Optional[int] = None, extra=()):
-        """Step buffers host -> device (pinned, async): ``ntok`` token rows, ``n`` sequence
-        rows, ``nparam`` (default n) sampling-parameter rows, plus ``extra`` (host, device,
-        rows) triples; one event marks the whole upload."""
-        nb = non_blocking = self.gpu
-        self.d_ids[:ntok].copy_(self.h_ids[:ntok], non_blocking=nb)
-        self.d_pos[:ntok].copy_(self.h_pos[:ntok], non_blocking=nb)
-        self.d_slots[:ntok].copy_(self.h_slots[:ntok], non_blocking=nb)
-        self.d_cu[: n + 1].copy_(self.h_cu[: n + 1], non_blocking=nb)
-        self.d_ctx[:n].copy_(self.h_ctx[:n], non_blocking=nb)
-        self.d_bt[:n].copy_(self.h_bt[:n], non_blocking=nb)
+    def _upload(self, n, ntok, nparam: Optional[int] = None, extra=(), src=None):
+        """Step buffers host -> device: ``ntok`` token rows, ``n`` sequence rows, ``nparam``
+        (default n) sampling-parameter rows, ``extra`` (host, device, rows) triples and, with
+        ``src``, the pipelined id gather's lists (then :meth:`_stage_gather` reuses them). On the
+        GPU one packed copy + one scatter kernel (ops/staging.py); the host buffers may be
+        rewritten as soon as this returns."""
         npr = n if nparam is None else nparam
-        for h, d in ((self.h_temp, self.d_temp), (self.h_topk, self.d_topk), (self.h_topp, self.d_topp),
-                     (self.h_seed, self.d_seed), (self.h_step, self.d_step), (self.h_pen, self.d_pen)):
-            d[:npr].copy_(h[:npr], non_blocking=non_blocking)
-        for h, d, rows in extra:
-            d[:rows].copy_(h[:rows], non_blocking=non_blocking)
-        if self.gpu:
-            self._up_ev = torch.cuda.Event()
-            self._up_ev.record()
+        segs = [(self.h_ids, self.d_ids, ntok), (self.h_pos, self.d_pos, ntok), (self.h_slots, self.d_slots, ntok),
+                (self.h_cu, self.d_cu, n + 1), (self.h_ctx, self.d_ctx, n), (self.h_bt, self.d_bt, n),
+                (self.h_temp, self.d_temp, npr), (self.h_topk, self.d_topk, npr), (self.h_topp, self.d_topp, npr),
+                (self.h_seed, self.d_seed, npr), (self.h_step, self.d_step, npr), (self.h_pen, self.d_pen, npr)]
+        segs += list(extra)
+        self._staged_src = None
+        if src is not None and len(src[0]):
+            k = len(src[0])
+            self.h_gidx.numpy()[:k] = src[0]
+            self.h_gprev.numpy()[:k] = src[1]
+            if self.gpu:
+                segs += [(self.h_gidx, self.d_gidx, k), (self.h_gprev, self.d_gprev, k)]
+            self._staged_src = src
+        if self._stager is not None:
+            self._stager.upload(segs)
+            return
+        for h, d, rows in segs:
+            d[:rows].copy_(h[:rows], non_blocking=self.gpu)
 
     def _tap(self, logits, rows: int) -> None:
         if self.d_tap is not None and logits is not None:
@@ -1436,7 +1457,8 @@ class LLMEngine:
             g = self._capture_step_graph(key)
         self._upload(n, tb, nparam=S, extra=((self.h_ctxd, self.d_ctxd, max(ndb, 1)),
                                              (self.h_items, self.d_items, max(len(items), 1)),
-                                             (self.h_nitems, self.d_nitems, 1), (self.h_sidx, self.d_sidx, S)))
+                                             (self.h_nitems, self.d_nitems, 1), (self.h_sidx, self.d_sidx, S)),
+                     src=src)
         self._gather_ids(src)
         self.stats["graph_steps"] += 1
         self.bucket_hist[tb] += 1

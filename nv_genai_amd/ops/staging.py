@@ -1,0 +1,91 @@
+"""One host->device copy per engine step (csrc/kernels/staging.hip).
+
+A step's inputs live in fixed device buffers (the captured hipGraphs read them in place), each
+filled from its own pinned host buffer. Copying them one by one costs a host API call and a
+~4.5 us blit dispatch on the compute stream per buffer, ~18 per step; a kernel trace of the
+headline's timed window named the copyBuffer -> copyBuffer gaps its largest idle source
+(profiles/r6_busy/). :class:`PackedUpload` packs the used rows of every buffer contiguously into
+a pinned staging area (host memcpy), issues ONE async copy into a device staging buffer and
+ONE scatter kernel to the destinations.
+
+The pinned staging area is double-buffered: the host packs step k + 1 while the copy of step k
+may still be queued behind the GPU's work; before reusing a half it waits for the copy that
+last read it (two uploads back, long done in a pipelined loop). The source host buffers can be
+rewritten as soon as :meth:`upload` returns.
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import kernels
+
+_ALIGN = 16
+MAX_SEGMENTS = 32   # kMaxSegments (kernels.h)
+
+
+class PackedUpload:
+    def __init__(self, device, capacity: int):
+        self.device = torch.device(device)
+        self.capacity = (int(capacity) + _ALIGN - 1) // _ALIGN * _ALIGN
+        self._h = [torch.empty(self.capacity, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        self._hn = [h.numpy() for h in self._h]
+        self._d = torch.empty(self.capacity, dtype=torch.uint8, device=self.device)
+        self._ev: List[Optional[torch.cuda.Event]] = [None, None]
+        self._flip = 0
+        self._meta: Dict[int, Tuple[np.ndarray, int, int, int]] = {}
+        self.uploads = 0
+        self.bytes = 0
+
+    def _info(self, h: torch.Tensor, d: torch.Tensor):
+        """(host bytes view, bytes per row, device address, device rows) of a buffer pair."""
+        key = (id(h), id(d))
+        m = self._meta.get(key)
+        if m is None:
+            if h.dtype != d.dtype or h.shape[1:] != d.shape[1:] or not (h.is_contiguous() and d.is_contiguous()):
+                raise ValueError("packed upload: host / device buffers must match in dtype and row shape")
+            row = h[0].numel() * h.element_size() if h.dim() > 1 else h.element_size()
+            if row % 4:
+                raise ValueError("packed upload: rows must be whole 4-B words")
+            m = (h.numpy().reshape(-1).view(np.uint8), row, d.data_ptr(), d.shape[0])
+            if m[2] % _ALIGN:
+                raise ValueError("packed upload: device buffers must be 16-B aligned")
+            self._meta[key] = m
+        return m
+
+    def upload(self, segs: Iterable[Tuple[torch.Tensor, torch.Tensor, int]]) -> None:
+        """Copy rows [0, rows) of every (host, device, rows) pair, in one copy + one kernel on
+        the current stream."""
+        half = self._flip
+        self._flip ^= 1
+        ev = self._ev[half]
+        if ev is not None:
+            ev.synchronize()
+        buf = self._hn[half]
+        dst, off, nbytes = [], [], []
+        o = 0
+        for h, d, rows in segs:
+            hv, row, dptr, drows = self._info(h, d)
+            if rows <= 0:
+                continue
+            if rows > drows:
+                raise ValueError(f"packed upload: {rows} rows into a {drows}-row device buffer")
+            nb = rows * row
+            if o + nb > self.capacity or len(dst) == MAX_SEGMENTS:
+                raise ValueError("packed upload: staging capacity or segment count exceeded")
+            buf[o:o + nb] = hv[:nb]
+            dst.append(dptr)
+            off.append(o)
+            nbytes.append(nb)
+            o = (o + nb + _ALIGN - 1) // _ALIGN * _ALIGN
+        if not dst:
+            return
+        self._d[:o].copy_(self._h[half][:o], non_blocking=True)
+        kernels().scatter_segments(self._d, dst, off, nbytes)
+        e = torch.cuda.Event()
+        e.record()
+        self._ev[half] = e
+        self.uploads += 1
+        self.bytes += o

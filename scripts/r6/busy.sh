@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 6: kernel-busy time over bench.py's timed window (marker kernels), 8 timed steps
+set -o pipefail
+cd "$(dirname "$0")/../.."
+R=$PWD
+out=gpurun_out/${1:-r6_busy}
+mkdir -p $out
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$out/raw -o run -- python3 $R/bench.py --steps 8 --warmup 2 --out $R/$out/bench_traced.json > $R/$out/prof.log 2>&1 || { tail -20 $R/$out/prof.log; exit 1; }
+python3 $R/scripts/summarize_prof.py $R/$out/raw > $R/$out/kernels.txt 2>&1
+rm -rf $R/$out/raw
+grep -A 20 "gpu busy" $R/$out/kernels.txt | head -24

@@ -877,3 +877,29 @@ def test_skinny_slab_nontemporal_stores_bitwise(gpu, kernel_form, snt):
     b = ops.skinny_gemm(x, w, 1, 4, 1)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+def test_packed_upload_scatters_segments(gpu):
+    """ops/staging.PackedUpload: the used rows of several pinned buffers (int32, fp32, int64,
+    2-D rows, a ragged word count) reach their device buffers through one copy + one scatter
+    kernel, rows past `rows` untouched; both staging halves in turn; oversize rows refused."""
+    from nv_genai_amd.ops.staging import PackedUpload
+
+    g = torch.Generator().manual_seed(3)
+    specs = [((1000,), torch.int32), ((77,), torch.float32), ((300,), torch.int64), ((40, 37), torch.int32),
+             ((5,), torch.float32)]
+    hs = [torch.randint(-1000, 1000, s, generator=g).to(dt).pin_memory() for s, dt in specs]
+    ds = [torch.full(s, -7, dtype=dt, device=gpu) for s, dt in specs]
+    up = PackedUpload(gpu, sum(h.numel() * h.element_size() + 16 for h in hs))
+    for it, rows in enumerate(([999, 77, 1, 13, 5], [3, 0, 300, 40, 2])):
+        for h in hs:
+            h.copy_(torch.randint(-1000, 1000, h.shape, generator=g).to(h.dtype))
+        before = [d.clone() for d in ds]
+        up.upload(list(zip(hs, ds, rows)))
+        torch.cuda.synchronize()
+        for h, d, b, r in zip(hs, ds, before, rows):
+            assert torch.equal(d[:r].cpu(), h[:r]), (it, r)
+            assert torch.equal(d[r:], b[r:])
+    assert up.uploads == 2
+    with pytest.raises(ValueError):
+        up.upload([(hs[0], ds[0], 1001)])
