@@ -207,3 +207,70 @@ def test_tp8_without_custom_all_reduce_falls_back():
         assert not r["custom_ar"], r
         assert not r["use_graphs"] and not r["mixed_graphs_ok"], r
         assert r["decode_graphs"] == 0 and r["step_graphs"] == 0, r
+
+
+def _shard_worker(rank, port, q):
+    """One rank of an 8-way sharded index on the shared GPU: the query block arrives as the
+    search command's payload bytes, the (score, id) lists meet in ONE IPC all-gather."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(WORLD), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), GPU_MAX_HW_QUEUES="2", OMP_NUM_THREADS="1", NGA_NUMA_BIND="0")
+    torch.set_num_threads(1)
+    res = {"rank": rank}
+    try:
+        from nv_genai_amd.index.flat import FlatIndex
+        from nv_genai_amd.index.sharded import ShardedIndex
+        from nv_genai_amd.parallel import dist as pd
+
+        pctx = pd.init_distributed(tp_size=1, backend="gloo", device="cuda")
+        dev = torch.device("cuda", 0)
+        g = torch.Generator().manual_seed(21)
+        X = torch.randn(20_003, 1024, generator=g)
+        Q = torch.randn(9, 1024, generator=g)
+        ids = torch.arange(20_003, dtype=torch.int64) * 7 + 3
+        sh = ShardedIndex(1024, "cosine", "cuda", pctx=pctx, capacity=20_003 // WORLD + 1)
+        sh.add(X, ids)
+        payload = sh.query_payload(Q)
+        vals, out_ids = sh.search(sh.queries_from_payload(9, payload.view("uint8").reshape(-1)), 10,
+                                  have_queries=True)
+        torch.cuda.synchronize()
+        res["stats"] = dict(sh.stats)
+        res["ipc"] = sh._car is not None
+        if rank == 0:
+            full = FlatIndex(1024, "cosine", "cuda", capacity=20_003)
+            full.add(X, ids)
+            rv, ri = full.search(Q.to(dev), 10)
+            res["vals_diff"] = float((vals - rv).abs().max())
+            res["ids_equal"] = bool(torch.equal(out_ids.cpu(), ri.cpu()))
+        res["error"] = sh._car.error() if sh._car is not None else -1
+        pd.destroy()
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        res["exc"] = traceback.format_exc()[-3000:]
+    q.put(res)
+
+
+def test_sharded_index_ipc_gather_matches_flat_eight_ranks():
+    """CC7/CC8 on the device at W = 8: no broadcast (queries from the command payload), one
+    IPC all-gather of the packed (score, id) rows, merged top-10 equal to one flat index."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    try:
+        results = sorted([q.get(timeout=300) for _ in range(WORLD)], key=lambda r: r["rank"])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in results:
+        assert "exc" not in r, (r["rank"], r["exc"])
+        assert r["ipc"] and r["error"] == 0, r
+        assert r["stats"]["broadcasts"] == 0 and r["stats"]["ipc_gathers"] == 1 and r["stats"]["pg_gathers"] == 0, r
+    r0 = results[0]
+    assert r0["ids_equal"] and r0["vals_diff"] < 1e-3, r0
