@@ -31,7 +31,6 @@ from typing import Callable, Deque, Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ..utils.runtime import capture_guard
 from .. import ops
 from ..observability.markers import gpu_range
 from .._native import rt
@@ -41,10 +40,11 @@ from ..parallel.dist import ParallelContext, get_context
 from ..utils.faults import FaultInjector
 from ..utils.tokenizer import IncrementalDetokenizer, LLMTokenizer, llm_tokenizer
 from .beam import BeamGroup, advance
+from .replica import ReplicaMixin
+from .step_graphs import StepGraphMixin
 
 log = logging.getLogger(__name__)
 _KV_SHARE_STATS = os.environ.get("NGA_KV_SHARE_STATS", "0") == "1"
-_TRACE_CAPTURE = os.environ.get("NGA_TRACE_CAPTURE", "0") == "1"   # per-rank timings of lazy captures
 
 
 @dataclass
@@ -155,7 +155,7 @@ class EngineConfig:
 _INERT = Request(id=-1, prompt_ids=[0], params=SamplingParams(temperature=0.0))
 
 
-class LLMEngine:
+class LLMEngine(ReplicaMixin, StepGraphMixin):
     def __init__(self, cfg: EngineConfig = EngineConfig(), device: Optional[str] = None,
                  pctx: Optional[ParallelContext] = None, model: Optional[LlamaModel] = None,
                  tokenizer: Optional[LLMTokenizer] = None, model_cfg: Optional[LlamaConfig] = None,
@@ -776,26 +776,6 @@ class LLMEngine:
                 self._finalize(pend)
             return fn()
 
-    def broadcast_command(self, kind: int, n: int = 0, payload: Optional[np.ndarray] = None) -> None:
-        """Driver of a model-parallel replica: announce a non-step command (kind <= -3) to
-        the followers, which run the hook registered for it in :meth:`run_follower` —
-        the same ordered channel as the step layouts, so collectives line up. ``payload``: host
-        bytes that travel inside the message (e.g. a sharded search's query block, so the
-        search needs no broadcast collective); the hook receives them as a uint8 array."""
-        if kind > -3:
-            raise ValueError("command kinds are <= -3 (-1 stop, -2 copy-on-fork are reserved)")
-        if self.p.mp_size > 1:
-            pl = None
-            if payload is not None:
-                pl = np.ascontiguousarray(payload).view(np.uint8).reshape(-1)
-                if 8 * self._HDR + pl.size > self._msg.size:
-                    raise ValueError(f"command payload of {pl.size} B exceeds the step message slot")
-            self._sync_step(kind, n, 0, 0, 0, 0, 0, payload=pl)
-
-    def command_payload_capacity(self) -> int:
-        """Largest ``broadcast_command`` payload in bytes (0 on a single-rank engine)."""
-        return 0 if self._msg is None else int(self._msg.size - 8 * self._HDR)
-
     def drain(self) -> List[Request]:
         """Settle the in-flight pipelined step (if any)."""
         with self.lock:
@@ -803,195 +783,6 @@ class LLMEngine:
                 return []
             pend, self._pending = self._pending, None
             return self._finalize(pend)
-
-    # ------------------------------------------------------------------ model parallel
-    # The replica's driver (pipeline stage 0, TP rank 0) schedules, then broadcasts the step
-    # layout (one int32 payload over RCCL) to every rank of the replica (tp x pp) so they
-    # all run the same forward; the collectives inside the model (row-parallel all-reduces,
-    # vocab all-gather, stage-to-stage sends) then line up. Followers loop in
-    # run_follower() until the driver broadcasts a stop header.
-    @property
-    def is_driver(self) -> bool:
-        return self.p.mp_size == 1 or (self.p.tp_rank == 0 and self.p.pp_rank == 0)
-
-    _HDR = 12   # int64 header: kind, n, ntok, max_q, max_ctx, bs, nd, gb, nsrc, prow, npairs, 0
-
-    def _step_msg_bytes(self, T: int, S: int) -> int:
-        """Largest step message: header, token rows (ids / positions / slots), sequence rows
-        (cu_seqlens, contexts, block tables), S rows of sampling parameters and a pipelined
-        id gather over every token row."""
-        return (8 * self._HDR + 4 * (3 * T + (S + 1) + S + S * self.max_blocks) + 8
-                + S * (4 + 4 + 4 + 8 + 8) + 16 * T + 64)
-
-    def _sync_step(self, kind: int, n: int, ntok: int, max_q: int, max_ctx: int, bs: int, nd: int = 0,
-                   gb: int = 0, src=None, pairs=None, payload=None) -> None:
-        """Driver: publish a step (or a command, kind < 0) to the replica's ranks. ``gb``: token
-        bucket of a graph-captured prefill / mixed step (its padded token rows travel too, so
-        followers replay the same graph on the same inputs); ``src``: the pipelined id gather
-        (token rows, rows of the in-flight step) — every follower applies it to its own sampled
-        tokens; the sampling parameters travel so followers sample exactly what the driver
-        samples. ``pairs``: [2, k] copy-on-fork pages (kind -2); ``payload``: a command's bytes
-        (kind <= -3; their count travels in the pairs field)."""
-        if self.p.mp_size == 1:
-            return
-        rows, toks = max(n, bs), max(ntok, bs, gb)
-        prow = max(rows, self.cfg.max_num_seqs if gb else 0) if kind >= 0 else 0
-        nsrc = 0 if src is None else len(src[0])
-        npairs = int(payload.size) if payload is not None else (0 if pairs is None else int(pairs.shape[1]))
-        m = self._msg
-        m[:8 * self._HDR].view(np.int64)[:] = (kind, n, ntok, max_q, max_ctx, bs, nd, gb, nsrc, prow, npairs, 0)
-        o = 8 * self._HDR
-
-        def put(a):
-            nonlocal o
-            b = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
-            m[o:o + b.size] = b
-            o += b.size
-
-        if kind >= 0:
-            ids, pos, sl, cu, ctx, bt = self._np[:6]
-            for a in (ids[:toks], pos[:toks], sl[:toks], cu[:rows + 1], ctx[:rows], bt[:rows]):
-                put(a)
-            o = (o + 7) & ~7
-            for a in (self.n_temp, self.n_topk, self.n_topp, self.n_seed, self.n_step):
-                put(a[:prow])
-            if nsrc:
-                put(np.asarray(src[0], dtype=np.int64))
-                put(np.asarray(src[1], dtype=np.int64))
-        elif payload is not None:
-            put(payload)
-        elif npairs:
-            put(np.asarray(pairs, dtype=np.int32))
-        self._chan.send(m[:o])
-
-    def _recv_step(self):
-        """Follower: the next message into the host step buffers. Returns (kind, n, ntok, max_q,
-        max_ctx, bs, nd, gb, src, pairs)."""
-        msg = self._chan.recv()
-        hdr = msg[:8 * self._HDR].view(np.int64).tolist()
-        kind, n, ntok, max_q, max_ctx, bs, nd, gb, nsrc, prow, npairs, _ = hdr
-        o = 8 * self._HDR
-
-        def take(dtype, count):
-            nonlocal o
-            nb = np.dtype(dtype).itemsize * count
-            a = msg[o:o + nb].view(dtype)
-            o += nb
-            return a
-
-        if kind < 0:
-            if kind <= -3:   # a command: its payload bytes (or None)
-                pairs = take(np.uint8, npairs).copy() if npairs else None
-            else:
-                pairs = take(np.int32, 2 * npairs).reshape(2, npairs).copy() if npairs else None
-            return kind, n, 0, 0, 0, 0, 0, 0, None, pairs
-        rows, toks = max(n, bs), max(ntok, bs, gb)
-        if self._up_ev is not None:
-            # the previous step's upload may still be reading the pinned buffers
-            self._up_ev.synchronize()
-        ids, pos, sl, cu, ctx, bt = self._np[:6]
-        ids[:toks] = take(np.int32, toks)
-        pos[:toks] = take(np.int32, toks)
-        sl[:toks] = take(np.int32, toks)
-        cu[:rows + 1] = take(np.int32, rows + 1)
-        ctx[:rows] = take(np.int32, rows)
-        bt[:rows] = take(np.int32, rows * self.max_blocks).reshape(rows, self.max_blocks)
-        o = (o + 7) & ~7
-        self.n_temp[:prow] = take(np.float32, prow)
-        self.n_topk[:prow] = take(np.int32, prow)
-        self.n_topp[:prow] = take(np.float32, prow)
-        self.n_seed[:prow] = take(np.int64, prow)
-        self.n_step[:prow] = take(np.int64, prow)
-        self.n_pen[:prow] = 1.0
-        src = None
-        if nsrc:
-            src = (take(np.int64, nsrc).copy(), take(np.int64, nsrc).copy())
-        return kind, n, ntok, max_q, max_ctx, bs, nd, gb, src, None
-
-    def _apply_decode_src(self, n: int, src) -> None:
-        """Pipelined decode: input ids of rows still being produced by the in-flight step."""
-        if src is not None and len(src[0]) == n:
-            _, prev = self._stage_gather(src)
-            self.d_ids[:n] = self.d_tok.index_select(0, prev)
-        else:
-            self._gather_ids(src)
-
-    def _follower_sample(self, logits, n: int) -> None:
-        """Sample the step's rows exactly as the driver does (same logits after the vocab
-        all-gather, same per-row temperature / top-k / top-p / seed / step), so the next
-        pipelined step's id gather reads the same tokens on every rank."""
-        if logits is None:   # a pipeline stage without the LM head
-            return
-        tok, lp = ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n],
-                             self.d_seed[:n], self.d_step[:n], None, None,
-                             out_tok=self.d_tok[:n], out_lp=self.d_lp[:n])
-        if tok.data_ptr() != self.d_tok.data_ptr():   # reference path returns fresh tensors
-            self.d_tok[:n].copy_(tok[:n])
-            self.d_lp[:n].copy_(lp[:n])
-
-    def run_follower(self, hooks: Optional[Dict[int, Callable[[int], None]]] = None) -> None:
-        """Non-driver TP ranks: execute every step the driver publishes, and the hook for
-        each command kind (<= -3) it broadcasts (``broadcast_command``)."""
-        while True:
-            if self._launch_t0 is not None:
-                self._follower_launch.append(time.perf_counter() - self._launch_t0)
-                self._launch_t0 = None
-            kind, n, ntok, max_q, max_ctx, bs, nd, gb, src, pairs = self._recv_step()
-            self._launch_t0 = time.perf_counter() if kind >= 0 else None
-            self._nstep += 1
-            if self._faults:
-                self._faults.check(self._nstep, "follower")
-            if kind <= -3:
-                if not hooks or kind not in hooks:
-                    raise RuntimeError(f"follower has no hook for command {kind}")
-                if pairs is None:
-                    hooks[kind](n)
-                else:          # the command's payload bytes
-                    hooks[kind](n, pairs)
-                continue
-            if kind == -2:   # copy-on-fork pages (beam search)
-                self.model.copy_kv_blocks(torch.from_numpy(pairs[0]), torch.from_numpy(pairs[1]))
-                continue
-            if kind < 0:
-                return
-            if src is not None:
-                self._tp_gathers += 1
-            prow = max(n, bs, self.cfg.max_num_seqs if gb else 0)
-            if kind in (1, 3) and gb:
-                key = self._graph_key(n, ntok, nd)
-                if key is None or key[0] != gb:
-                    raise RuntimeError(f"follower cannot replay the driver's step graph {gb}")
-                self._graph_step(key, kind, n, ntok, max_q, max_ctx, nd, src, follower=True)
-            elif kind in (1, 3):
-                self._upload(n, ntok, src=src)
-                self._gather_ids(src)
-                self._follower_sample(self._prefill_forward(n, ntok, max_q, max_ctx, nd), n)
-            elif bs:
-                self._upload(bs, bs, nparam=prow, src=src)
-                self._apply_decode_src(n, src)
-                self.graphs[bs].replay()
-            else:
-                self._upload(n, n, src=src)
-                self._apply_decode_src(n, src)
-                meta = self._meta("decode", n, n, 1, self.cfg.max_model_len)
-                h = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta)
-                self._follower_sample(None if h is None else self.model.logits(h), n)
-
-    def follower_stats(self) -> dict:
-        """Follower of a model-parallel replica: the step channel's publish -> receipt latency
-        (µs percentiles, and how many waits ended spinning / yielding / after a futex sleep)
-        and the host time from a step's receipt to the end of its launch (µs percentiles)."""
-        v = sorted(self._follower_launch)
-        out = {"channel": self._chan.stats() if self._chan is not None else {}}
-        if v:
-            out["receipt_to_launched_us"] = {q: round(1e6 * v[min(len(v) - 1, int(f * (len(v) - 1)))], 1)
-                                             for q, f in (("p50", 0.5), ("p99", 0.99), ("max", 1.0))}
-            out["steps"] = len(v)
-        return out
-
-    def stop_followers(self) -> None:
-        if self.p.mp_size > 1 and self.is_driver:
-            self._sync_step(-1, 0, 0, 0, 0, 0, 0)
 
     # ------------------------------------------------------------------ beam search
     def _beam_step(self, smp: List[int], now: float) -> List[Request]:
@@ -1292,216 +1083,6 @@ class LLMEngine:
         ops.sample(logits, self.d_temp[:bs], self.d_topk[:bs], self.d_topp[:bs],
                    self.d_seed[:bs], self.d_step[:bs], None, None,
                    out_tok=self.d_tok[:bs], out_lp=self.d_lp[:bs])
-
-    # ------------------------------------------------------------------ prefill / mixed step graphs
-    def _mixed_graphs_eligible(self) -> bool:
-        """Graph-captured prefill / mixed steps need a work-list prefill kernel (the 32x32
-        one for bf16 head_dim-128 pages with <= 1024 pages per sequence, else the 16x16 one
-        for head_dim 64 / 128 / 256 and fp8 pages), one pipeline stage and the plain stacked
-        forward (no sequence-parallel prefill, no split mixed steps, no MoE)."""
-        c, m = self.cfg, self.model
-        if not c.mixed_graphs or not (self.gpu and c.use_graphs or c.graph_eager):
-            return False
-        self._pf_impl = 2 if (m.D == 128 and m.kv_dtype == "auto" and self.max_blocks <= 1024) else 1
-        self._pf_seq_min = int(os.environ.get("NGA_PF_SEQ_MIN", "384"))   # _graph_pf_seq; 0 = off
-        return (self.p.pp_size == 1 and not c.sequence_parallel and not m.split_mixed and m.D in (64, 128, 256)
-                and not self.mcfg.is_moe)
-
-    def _graph_key(self, n: int, ntok: int, nd: int):
-        """(token bucket, decode-row bucket) of a prefill / mixed step, or None (eager)."""
-        if not self._mg_ok or self._has_mm or n > self.cfg.max_num_seqs:
-            return None
-        step = self.cfg.graph_token_step
-        tb = -(-ntok // step) * step
-        if tb > self._mg_max_tokens:
-            return None
-        ndb = 0 if nd == 0 else next(b for b in self._nd_buckets if b >= nd)
-        # the decode launch covers the first ndb rows of the bucket (fine token steps: a
-        # mostly-decode step can round to fewer tokens than its decode-row bucket)
-        tb = max(tb, -(-ndb // step) * step)
-        if tb > self._mg_max_tokens:
-            return None
-        return (tb, ndb)
-
-    def _graph_kernel(self, key):
-        """(impl, ks) of the work-list prefill kernel in the step graph of ``key``, by the
-        eager size rule: the 32x32 kernel from ~1,024 row-block workgroups up (two per CU),
-        else the 16x16 one — whose small LDS footprint also lets the decode attention of a
-        mixed step share the CUs (the 32x32 kernel's 64-128 KiB per workgroup crowds it out).
-        The 8-wave split-key form only for a lone prompt with no decode rows beside it."""
-        tb, ndb = key
-        if self._pf_impl != 2:
-            return 1, 1
-        if self._graph_pf_seq(key):
-            return 2, 1
-        G = self.model.hq // self.model.hkv
-        hpw = 4 if G % 4 == 0 else 2 if G % 2 == 0 else 1
-        items = (tb - ndb) // ops.prefill_rows_per_block(self.model.hq, self.model.hkv) * self.model.hkv * (G // hpw)
-        if items >= 1024:
-            return 2, 1
-        if ndb == 0:   # no decode attention beside it: the standalone size rule (impl 4)
-            return (2, 2) if items <= 320 else (2, 1)
-        return 1, 1
-
-    def _graph_pf_seq(self, key) -> bool:
-        """Mixed steps with a large prefill (NGA_PF_SEQ_MIN <= work items < 1,024, decode rows
-        beside it): the 32x32 prefill kernel after the decode attention instead of the 16x16
-        one concurrently. Beside a 60-150 us prefill the decode kernel stretches from 229 to
-        331 us (profiles/r3_prof_bins/attn_overlap.json)."""
-        tb, ndb = key
-        if self._pf_impl != 2 or ndb == 0 or self._pf_seq_min <= 0:
-            return False
-        G = self.model.hq // self.model.hkv
-        hpw = 4 if G % 4 == 0 else 2 if G % 2 == 0 else 1
-        items = (tb - ndb) // ops.prefill_rows_per_block(self.model.hq, self.model.hkv) * self.model.hkv * (G // hpw)
-        return self._pf_seq_min <= items < 1024
-
-    def _graph_meta(self, key) -> AttnMeta:
-        tb, ndb = key
-        impl, ks = self._graph_kernel(key)
-        S = self.cfg.max_num_seqs
-        return AttnMeta(kind="graph", slots=self.d_slots[:tb], cu_q=self.d_cu[: S + 1], ctx_lens=self.d_ctx[:S],
-                        block_tables=self.d_bt[:S], max_q_len=0, max_ctx=self.cfg.max_model_len,
-                        decode_ws=self.decode_ws, n_decode=ndb, decode_ctx=self.d_ctxd[:max(ndb, 1)],
-                        items=self.d_items, n_items=self.d_nitems, pf_grid=256 if ks == 2 else 512, pf_ks=ks,
-                        pf_impl=impl, pf_seq=self._graph_pf_seq(key))
-
-    def _graph_body(self, key) -> None:
-        """One prefill / mixed step over the bucket: forward of tb token rows, logits of the
-        S = max_num_seqs sampling rows (d_sidx), sampling into d_tok / d_lp."""
-        tb, _ = key
-        S = self.cfg.max_num_seqs
-        h = self.model.forward(self.d_ids[:tb], self.d_pos[:tb], self._graph_meta(key), self.d_sidx[:S])
-        logits = self.model.logits(h)
-        self._tap(logits, S)
-        tok, lp = ops.sample(logits, self.d_temp[:S], self.d_topk[:S], self.d_topp[:S], self.d_seed[:S],
-                             self.d_step[:S], None, None, out_tok=self.d_tok[:S], out_lp=self.d_lp[:S])
-        if tok.data_ptr() != self.d_tok.data_ptr():   # reference path returns fresh tensors
-            self.d_tok[:S].copy_(tok[:S])
-            self.d_lp[:S].copy_(lp[:S])
-
-    def _capture_step_graph(self, key) -> "torch.cuda.CUDAGraph":
-        """Capture the step graph of ``key`` (first use). The device is drained first; the
-        warm-up and capture run on inert inputs (no KV writes or reads: slots -1, no decode
-        rows, an empty work list) and the sampled tokens of the step in flight are kept."""
-        tb, ndb = key
-        dev = self.device
-        t0 = time.perf_counter()
-        trace = _TRACE_CAPTURE and (lambda m: print(f"[capture rank{self.p.rank} {key}] {m} "
-                                                    f"+{time.perf_counter() - t0:.3f}s", file=sys.stderr, flush=True))
-        torch.cuda.synchronize(dev)
-        if trace:
-            trace("drained")
-        keep = (self.d_tok.clone(), self.d_lp.clone())
-        self.d_ids[:tb].zero_()
-        self.d_pos[:tb].zero_()
-        self.d_slots[:tb].fill_(-1)
-        self.d_ctxd.zero_()
-        self.d_nitems.zero_()
-        self.d_sidx.zero_()
-        if self._cap_stream is None:
-            self._cap_stream = torch.cuda.Stream(dev)
-        stream = self._cap_stream
-        stream.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(stream):
-            self._graph_body(key)
-            if trace:
-                stream.synchronize()
-                trace("warm-up done")
-            g = torch.cuda.CUDAGraph()
-            with capture_guard(), torch.cuda.graph(g, pool=self._graph_pool, stream=stream,
-                                                   capture_error_mode="thread_local"):
-                self._graph_body(key)
-        torch.cuda.current_stream(dev).wait_stream(stream)
-        torch.cuda.synchronize(dev)
-        if trace:
-            trace("captured")
-        self._graph_pool = g.pool()
-        self.d_tok.copy_(keep[0])
-        self.d_lp.copy_(keep[1])
-        self.mgraphs[key] = g
-        self.stats["graph_captures"] += 1
-        self.stats["graph_capture_s"] += time.perf_counter() - t0
-        return g
-
-    def _graph_step(self, key, kind, n, ntok, max_q, max_ctx, nd, src, follower: bool = False) -> None:
-        """Launch a prefill / mixed step through its graph: pad the token rows to the bucket,
-        fill the step's device layout (decode-row contexts, prefill work list, sampling rows
-        and parameters), upload, gather pipelined ids, replay."""
-        tb, ndb = key
-        S = self.cfg.max_num_seqs
-        if not follower:
-            self.h_ids[ntok:tb] = 0
-            self.h_pos[ntok:tb] = 0
-            self.h_slots[ntok:tb] = -1
-        cu, ctx = self._np[3], self._np[4]
-        self.h_ctxd[:nd] = self.h_ctx[:nd]
-        self.h_ctxd[nd:max(ndb, nd)] = 0
-        items = ops.plan_prefill_items(cu, ctx, nd, n, self.model.hq, self.model.hkv, self.model.window,
-                                       out=self.h_items.numpy(),
-                                       rw=ops.worklist_rows(self._graph_kernel(key)[0], self.model.hq,
-                                                            self.model.hkv))
-        self.h_nitems[0] = len(items)
-        sidx = self.h_sidx.numpy()
-        sidx[:n] = cu[1:n + 1] - 1
-        sidx[n:S] = 0
-        self._pad_params(n, S)
-        if not follower:
-            self._sync_step(kind, n, ntok, max_q, max_ctx, 0, nd, gb=tb, src=src)
-        # lazy capture only after the step header and payload went out: under TP the warm-up
-        # and captured forwards issue all-reduces, which the followers (blocked in _recv_step
-        # until the broadcast) must meet in the same order. The capture leaves the host-side
-        # step layout alone and the upload below refills every device input it zeroed.
-        g = self.mgraphs.get(key)
-        if g is None and self.gpu and not self.cfg.graph_eager:
-            g = self._capture_step_graph(key)
-        self._upload(n, tb, nparam=S, extra=((self.h_ctxd, self.d_ctxd, max(ndb, 1)),
-                                             (self.h_items, self.d_items, max(len(items), 1)),
-                                             (self.h_nitems, self.d_nitems, 1), (self.h_sidx, self.d_sidx, S)),
-                     src=src)
-        self._gather_ids(src)
-        self.stats["graph_steps"] += 1
-        self.bucket_hist[tb] += 1
-        self.ntok_hist[ntok // 128 * 128] += 1
-        if g is not None:
-            g.replay()
-        else:
-            self._graph_body(key)
-
-    def _pad_params(self, n: int, rows: int) -> None:
-        """Sampling-parameter rows [n, rows) of a padded launch: greedy, no penalty."""
-        self.h_temp[n:rows] = 0.0
-        self.h_topk[n:rows] = 0
-        self.h_topp[n:rows] = 1.0
-        self.h_seed[n:rows] = 0
-        self.h_step[n:rows] = 0
-        self.h_pen[n:rows] = 1.0
-
-    def _capture_graphs(self):
-        sizes = [b for b in self.cfg.graph_batch_sizes if b <= self.cfg.max_num_seqs]
-        # inert inputs for capture: no cache writes, empty contexts
-        self.d_slots.fill_(-1)
-        self.d_ctx.zero_()
-        self.d_temp.zero_()
-        self.d_topp.fill_(1.0)
-        pool = None
-        stream = torch.cuda.Stream(self.device)
-        stream.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(stream):
-            for bs in sorted(sizes, reverse=True):
-                for _ in range(2):
-                    self._decode_body(bs)
-                g = torch.cuda.CUDAGraph()
-                # thread_local: other threads of a serving process (retrieval, embeddings, other
-                # engines) keep launching on their own streams while this one captures
-                with capture_guard(), torch.cuda.graph(g, pool=pool, stream=stream,
-                                                       capture_error_mode="thread_local"):
-                    self._decode_body(bs)
-                pool = g.pool()
-                self.graphs[bs] = g
-        self._graph_pool = pool     # step graphs captured later share the pool
-        torch.cuda.current_stream(self.device).wait_stream(stream)
-        torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ convenience
     def run_until_done(self, reqs: Optional[List[Request]] = None) -> None:

@@ -405,6 +405,18 @@ def test_skinny_gemm_path_matches_library_path(gpu, weights, tmp_path, monkeypat
     assert torch.allclose(res["1lg"], res["0lg"], rtol=0.02, atol=0.05 * float(res["0lg"].abs().max()))
     _same_greedy_run(res["1"], res["0"])
 
+    # the numerics pin: the same token histories through the skinny path (graphed decode and
+    # mixed steps) and the library path (eager), teacher-forced, fp32 logits per row at bf16
+    # tolerance — no near-tie escape
+    def make(graphs):
+        monkeypatch.setenv("NGA_SKINNY", "1" if graphs else "0")
+        e = _engine(weights, "cuda", use_graphs=graphs, mixed_graphs=graphs, mixed_prefill_tokens=512,
+                    max_graph_tokens=1536, async_decode=False, logits_tap=True)
+        assert e.model.skinny == graphs
+        return e
+
+    _assert_logits_close(*_teacher_forced_logits(make, PROMPTS[:2], PROMPTS[2:], 16))
+
 
 def test_step_graph_capture_beside_reward_thread(gpu, weights):
     """As below with the model server's reward endpoint: RewardModel.score runs library GEMMs
