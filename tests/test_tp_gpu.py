@@ -231,3 +231,72 @@ def test_tp2_graphs_pipelined_match_tp1():
     assert all(len(o) == 12 for o in drv["hot"])
     assert fol["gathers"] > 0, fol
     assert drv["last_tok"] == fol["last_tok"]
+
+
+def _ep_worker(rank, port, q):
+    """Mixtral (mixtral-small: 8 experts, top-2) at TP = 2 with EXPERT parallelism: each rank
+    holds 4 whole experts (its own routing slice), runs the grouped MFMA expert GEMMs
+    (csrc/kernels/moe.hip) for the tokens routed to them, and the expert outputs meet in the
+    all-reduce."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    res = {"rank": rank}
+    try:
+        from nv_genai_amd.engine.llm_engine import EngineConfig, LLMEngine, SamplingParams
+        from nv_genai_amd.models.config import llama_config
+        from nv_genai_amd.models.llama import LlamaModel
+        from nv_genai_amd.parallel import dist as pd
+
+        cfg = llama_config("mixtral-small")
+        full = LlamaModel(cfg, "cpu", dtype=torch.bfloat16, pctx=pd.ParallelContext(), seed=7).state_dict()
+        full["lm_head.weight"] = full["lm_head.weight"] * 40.0
+        prompts = [[5, 6, 7, 8] * 30, [9, 10, 11] * 20]
+        greedy = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True, logprobs=True)
+        ecfg = EngineConfig(model="mixtral-small", max_num_seqs=4, max_batched_tokens=1024, max_model_len=1024,
+                            kv_cache_blocks=64, use_graphs=False)
+        if rank == 0:
+            e1 = LLMEngine(ecfg, device="cuda", pctx=pd.ParallelContext(), weights=full)
+            res["ref"] = [(r.output_ids, r.logprobs) for r in e1.generate(prompts, greedy)]
+            del e1
+            torch.cuda.empty_cache()
+        pctx = pd.init_distributed(tp_size=2, backend="gloo", device="cuda")
+        eng = LLMEngine(ecfg, device="cuda", pctx=pctx, weights=full)
+        res["ep"] = eng.model.expert_parallel
+        res["experts"] = (eng.model.expert0, eng.model.n_experts)
+        if eng.is_driver:
+            res["out"] = [(r.output_ids, r.logprobs) for r in eng.generate(prompts, greedy)]
+            eng.stop_followers()
+        else:
+            eng.run_follower()
+        torch.cuda.synchronize()
+        pd.destroy()
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        res["exc"] = traceback.format_exc()[-3000:]
+    q.put(res)
+
+
+def test_tp2_mixtral_expert_parallel_matches_tp1():
+    """EP on the device: the two ranks hold experts [0, 4) and [4, 8); greedy tokens match one
+    rank up to near-ties (test_engine_gpu._same_greedy_run)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from test_engine_gpu import _same_greedy_run
+
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ep_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = sorted([q.get(timeout=300) for _ in range(2)], key=lambda r: r["rank"])
+    for p in procs:
+        p.join(timeout=60)
+    for r in results:
+        assert "exc" not in r, r["exc"]
+        assert r["ep"], r
+    assert [r["experts"] for r in results] == [(0, 4), (4, 4)]
+    drv = results[0]
+    assert all(len(o) == 10 for o, _ in drv["out"])
+    _same_greedy_run(drv["out"], drv["ref"])
