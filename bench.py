@@ -370,8 +370,8 @@ def main(argv=None):
         hooks = {BARRIER_CMD: lambda n: (torch.cuda.synchronize() if gpu else None, pd.barrier())}
         if sharded:
             def search_hook(n, payload=None):
-                if payload is not None:   # the driver's query block, from the command
-                    return shard.search(shard.queries_from_payload(n, payload), args.top_k, have_queries=True)
+                if payload is not None:   # the driver's query block, from the command: side stream
+                    return shard.search_side(payload, n, args.top_k, wait=False)
                 return shard.search(torch.zeros(n, dim, device=shard.comm_dev), args.top_k, src=pctx.mp_src)
             hooks[SEARCH_CMD] = search_hook
         llm.run_follower(hooks=hooks)

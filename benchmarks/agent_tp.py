@@ -36,6 +36,7 @@ import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
 
+import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -99,8 +100,8 @@ def main(argv=None, emit: bool = True, record_devices=None):
     if not eng.is_driver:
         comm_dev = index.comm_dev
         def search_hook(n, payload=None):
-            if payload is not None:   # the driver's query block, from the command
-                return index.search(index.queries_from_payload(n, payload), k, have_queries=True)
+            if payload is not None:   # the driver's query block, from the command: side stream
+                return index.search_side(payload, n, k, wait=False)
             return index.search(torch.zeros(n, dim, device=comm_dev), k)
         eng.run_follower(hooks={SEARCH_CMD: search_hook})
         pd.destroy()
@@ -149,10 +150,11 @@ def main(argv=None, emit: bool = True, record_devices=None):
                 out = index.search(qv, k)
             else:
                 # the query block rides in the command: the search's only collective is the
-                # packed (score, id) all-gather
-                eng.broadcast_command(SEARCH_CMD, qv.shape[0], index.query_payload(qv))
-                out = index.search(qv, k, have_queries=True)
-            ids = out[1].cpu()        # the replica's decode waits behind this search
+                # packed (score, id) all-gather, on the index's own stream on every rank
+                payload = index.query_payload(qv)
+                eng.broadcast_command(SEARCH_CMD, qv.shape[0], payload)
+                out = index.search_side(payload.view(np.uint8).reshape(-1), qv.shape[0], k)
+            ids = out[1].cpu()
             search_ms.append(1e3 * (time.perf_counter() - t))
             return ids
         ids = svc.call(run).result()

@@ -51,6 +51,10 @@ class ShardedIndex:
         # the merge is left on the stream)
         self.stats = {"searches": 0, "broadcasts": 0, "ipc_gathers": 0, "pg_gathers": 0, "host_s": 0.0}
         self._car = self._make_ipc_gather() if ipc_gather else None
+        # searches whose query block comes from the host (the step-channel command) run on
+        # their own stream: they start beside the replica's in-flight step instead of queueing
+        # behind it, and the engine's stream never waits for them (search_side)
+        self._stream = torch.cuda.Stream(self.local.device) if self.local.device.type == "cuda" else None
 
     def __len__(self):
         n = torch.tensor([len(self.local)], dtype=torch.int64, device=self.comm_dev)
@@ -170,6 +174,22 @@ class ShardedIndex:
 
     def queries_from_payload(self, n: int, payload) -> torch.Tensor:
         return torch.from_numpy(payload).view(torch.float32).view(n, self.dim).to(self.local.device)
+
+    def search_side(self, payload, n: int, k: int, wait: bool = True):
+        """A search whose query block every rank holds as host bytes (``query_payload``, sent in
+        the step-channel command), run start to finish on the index's own stream: nothing on
+        the engine's stream waits for it and it does not wait for the engine's in-flight step.
+        ``wait``: return (scores, ids) on the host (the driver); else return None at once (a
+        follower joins the collective and moves on)."""
+        if self._stream is None:
+            v, i = self.search(self.queries_from_payload(n, payload), k, have_queries=True)
+            return (v.cpu(), i.cpu()) if wait else None
+        with torch.cuda.stream(self._stream):
+            v, i = self.search(self.queries_from_payload(n, payload), k, have_queries=True)
+            if not wait:
+                return None
+            out = (v.cpu(), i.cpu())   # synchronises this stream only
+        return out
 
     @torch.inference_mode()
     def search(self, q: torch.Tensor, k: int, src: int = 0,
