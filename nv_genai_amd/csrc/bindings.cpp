@@ -715,6 +715,23 @@ void scatter_segments(Tensor src, const std::vector<int64_t>& dst, const std::ve
   nga::launch_scatter_segments(reinterpret_cast<const uint8_t*>(src.data_ptr()), t, cur_stream(src));
 }
 
+// the whole packed step upload in one call: `nbytes` of the pinned host staging buffer -> the
+// device staging buffer (one async copy), then the scatter kernel, back to back on the current
+// stream (no host work between the two dispatches)
+void packed_upload(Tensor dev, Tensor host, int64_t nbytes, const std::vector<int64_t>& dst,
+                   const std::vector<int64_t>& off, const std::vector<int64_t>& bytes) {
+  CHECK_DEV(dev); CHECK_CONTIG(dev); CHECK_DT(dev, at::kByte);
+  TORCH_CHECK(!host.is_cuda() && host.is_contiguous() && host.scalar_type() == at::kByte && host.is_pinned(),
+              "packed_upload: host staging must be a pinned uint8 CPU tensor");
+  TORCH_CHECK(nbytes >= 0 && nbytes <= dev.numel() && nbytes <= host.numel(), "packed_upload: size");
+  hipStream_t st = cur_stream(dev);
+  if (nbytes > 0) {
+    hipError_t e = hipMemcpyAsync(dev.data_ptr(), host.data_ptr(), (size_t)nbytes, hipMemcpyHostToDevice, st);
+    TORCH_CHECK(e == hipSuccess, "packed_upload: hipMemcpyAsync: ", hipGetErrorString(e));
+  }
+  scatter_segments(dev, dst, off, bytes);
+}
+
 // a begin / end marker kernel on the current stream (kernel-trace window delimiters)
 void region_marker(Tensor sink, int64_t end) {
   CHECK_DEV(sink); CHECK_DT(sink, at::kInt);
@@ -969,6 +986,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("pool_l2norm", checked("pool_l2norm", &pool_l2norm));
   m.def("region_marker", checked("region_marker", &region_marker));
   m.def("scatter_segments", checked("scatter_segments", &scatter_segments));
+  m.def("packed_upload", checked("packed_upload", &packed_upload));
   m.def("row_sqnorm", checked("row_sqnorm", &row_sqnorm));
   m.def("fir_c64", checked("fir_c64", &fir_c64));
   m.def("fm_demod", checked("fm_demod", &fm_demod));

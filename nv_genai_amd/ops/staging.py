@@ -82,8 +82,8 @@ class PackedUpload:
             o = (o + nb + _ALIGN - 1) // _ALIGN * _ALIGN
         if not dst:
             return
-        self._d[:o].copy_(self._h[half][:o], non_blocking=True)
-        kernels().scatter_segments(self._d, dst, off, nbytes)
+        # the async copy and the scatter kernel, issued back to back from C++
+        kernels().packed_upload(self._d, self._h[half], o, dst, off, nbytes)
         e = torch.cuda.Event()
         e.record()
         self._ev[half] = e
