@@ -203,11 +203,19 @@ class ShmChannel {
       hdr_->beat[beat_idx_].store(now_ns(), std::memory_order_release);
       hdr_->attached.fetch_add(1, std::memory_order_acq_rel);
     }
-    beater_ = std::thread([this] { beat_loop(); });
+    owner_pid_ = getpid();
+    beater_ = new std::thread([this] { beat_loop(); });
   }
 
   ~ShmChannel() {
+    if (getpid() != owner_pid_) {
+      // a copy inherited across fork(): the heartbeat thread and the name belong to the parent;
+      // leave both alone (the thread object is leaked: it has no thread in this process)
+      if (base_) munmap(base_, bytes_);
+      return;
+    }
     stop_beating();
+    delete beater_;
     if (creator_ && !unlinked_) shm_unlink(name_.c_str());
     if (base_) munmap(base_, bytes_);
   }
@@ -233,13 +241,14 @@ class ShmChannel {
 
   // Stop this participant's heartbeat (tests: a peer that hangs without exiting).
   void stop_beating() {
+    if (getpid() != owner_pid_) return;   // no heartbeat thread in a forked copy
     {
       std::lock_guard<std::mutex> lk(mu_);
       if (stopping_) return;
       stopping_ = true;
     }
     cv_.notify_all();
-    if (beater_.joinable()) beater_.join();
+    if (beater_ && beater_->joinable()) beater_->join();
   }
 
   // Publish one message: 1, or -1 timeout, -2 closed, -3 a reader died.
@@ -382,7 +391,8 @@ class ShmChannel {
   WaitStats wstats_, rstats_;
   std::vector<int64_t> lat_, wake_;
   uint64_t lat_n_ = 0;
-  std::thread beater_;
+  std::thread* beater_ = nullptr;
+  pid_t owner_pid_ = 0;
   std::mutex mu_;
   std::condition_variable cv_;
   bool stopping_ = false;

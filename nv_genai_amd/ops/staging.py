@@ -15,7 +15,7 @@ rewritten as soon as :meth:`upload` returns.
 """
 from __future__ import annotations
 
-from typing import Dict, Iterable, List, Optional, Tuple
+from typing import Dict, Iterable, List, Optional, Tuple  # noqa: F401
 
 import numpy as np
 import torch
@@ -35,7 +35,9 @@ class PackedUpload:
         self._d = torch.empty(self.capacity, dtype=torch.uint8, device=self.device)
         self._ev: List[Optional[torch.cuda.Event]] = [None, None]
         self._flip = 0
-        self._meta: Dict[int, Tuple[np.ndarray, int, int, int]] = {}
+        # (host, device) -> (host, device, host bytes view, bytes per row, device address, rows);
+        # the entry holds both tensors, so their ids cannot be reused by other tensors
+        self._meta: Dict[Tuple[int, int], tuple] = {}
         self.uploads = 0
         self.bytes = 0
 
@@ -43,17 +45,19 @@ class PackedUpload:
         """(host bytes view, bytes per row, device address, device rows) of a buffer pair."""
         key = (id(h), id(d))
         m = self._meta.get(key)
+        if m is not None and (m[0] is not h or m[1] is not d or m[4] != d.data_ptr()):
+            m = None
         if m is None:
             if h.dtype != d.dtype or h.shape[1:] != d.shape[1:] or not (h.is_contiguous() and d.is_contiguous()):
                 raise ValueError("packed upload: host / device buffers must match in dtype and row shape")
             row = h[0].numel() * h.element_size() if h.dim() > 1 else h.element_size()
             if row % 4:
                 raise ValueError("packed upload: rows must be whole 4-B words")
-            m = (h.numpy().reshape(-1).view(np.uint8), row, d.data_ptr(), d.shape[0])
-            if m[2] % _ALIGN:
+            m = (h, d, h.numpy().reshape(-1).view(np.uint8), row, d.data_ptr(), d.shape[0])
+            if m[4] % _ALIGN:
                 raise ValueError("packed upload: device buffers must be 16-B aligned")
             self._meta[key] = m
-        return m
+        return m[2:]
 
     def upload(self, segs: Iterable[Tuple[torch.Tensor, torch.Tensor, int]]) -> None:
         """Copy rows [0, rows) of every (host, device, rows) pair, in one copy + one kernel on

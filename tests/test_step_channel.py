@@ -176,3 +176,28 @@ def test_wrapper_maps_codes_to_exceptions():
         with pytest.raises(exc):
             c.recv()
     assert sc.step_timeout_s() == float(os.environ.get("NGA_STEP_TIMEOUT_S", -1.0))
+
+
+def test_forked_copy_leaves_the_parents_channel_alone():
+    """A process forked after the writer was created inherits a copy of the object; destroying
+    that copy must neither join the parent's heartbeat thread (it has none in the child) nor
+    unlink the segment's name under the parent."""
+    import gc
+
+    name = _name()
+    w = rt.ShmChannel(name, True, 2, 256, 1, 0, 30.0)
+    pid = os.fork()
+    if pid == 0:   # child: drop the inherited copy, exit without running anything else
+        code = 0
+        try:
+            del w                  # the child's only reference: its copy is destroyed here
+            gc.collect()
+        except BaseException:  # noqa: BLE001
+            code = 1
+        os._exit(code)
+    _, status = os.waitpid(pid, 0)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0
+    rd = rt.ShmChannel(name, False, 0, 0, 0, 0, 30.0)     # the name is still there
+    assert w.write(np.array([5], dtype=np.int64), 5.0) == 1
+    buf = np.empty(256, dtype=np.uint8)
+    assert rd.read(buf, 5.0) == 8 and int(buf[:8].view(np.int64)[0]) == 5
