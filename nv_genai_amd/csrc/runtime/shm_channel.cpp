@@ -204,18 +204,21 @@ class ShmChannel {
       hdr_->attached.fetch_add(1, std::memory_order_acq_rel);
     }
     owner_pid_ = getpid();
-    beater_ = new std::thread([this] { beat_loop(); });
+    beat_ = new Beat();
+    beat_->th = std::thread([this] { beat_loop(); });
   }
 
   ~ShmChannel() {
     if (getpid() != owner_pid_) {
       // a copy inherited across fork(): the heartbeat thread and the name belong to the parent;
-      // leave both alone (the thread object is leaked: it has no thread in this process)
+      // leave both alone. The heartbeat state is leaked on purpose: its thread does not exist
+      // here, and its condition variable may record the parent thread as a waiter, which
+      // pthread_cond_destroy would wait for forever.
       if (base_) munmap(base_, bytes_);
       return;
     }
     stop_beating();
-    delete beater_;
+    delete beat_;
     if (creator_ && !unlinked_) shm_unlink(name_.c_str());
     if (base_) munmap(base_, bytes_);
   }
@@ -241,14 +244,14 @@ class ShmChannel {
 
   // Stop this participant's heartbeat (tests: a peer that hangs without exiting).
   void stop_beating() {
-    if (getpid() != owner_pid_) return;   // no heartbeat thread in a forked copy
+    if (getpid() != owner_pid_ || beat_ == nullptr) return;   // no heartbeat thread in a forked copy
     {
-      std::lock_guard<std::mutex> lk(mu_);
-      if (stopping_) return;
-      stopping_ = true;
+      std::lock_guard<std::mutex> lk(beat_->mu);
+      if (beat_->stopping) return;
+      beat_->stopping = true;
     }
-    cv_.notify_all();
-    if (beater_ && beater_->joinable()) beater_->join();
+    beat_->cv.notify_all();
+    if (beat_->th.joinable()) beat_->th.join();
   }
 
   // Publish one message: 1, or -1 timeout, -2 closed, -3 a reader died.
@@ -371,12 +374,19 @@ class ShmChannel {
   }
 
   void beat_loop() {
-    std::unique_lock<std::mutex> lk(mu_);
-    while (!stopping_) {
+    std::unique_lock<std::mutex> lk(beat_->mu);
+    while (!beat_->stopping) {
       hdr_->beat[beat_idx_].store(now_ns(), std::memory_order_release);
-      cv_.wait_for(lk, std::chrono::nanoseconds(kBeatNs));
+      beat_->cv.wait_for(lk, std::chrono::nanoseconds(kBeatNs));
     }
   }
+
+  struct Beat {   // heartbeat thread and its wake-up (heap: a forked copy must not destroy it)
+    std::mutex mu;
+    std::condition_variable cv;
+    bool stopping = false;
+    std::thread th;
+  };
 
   std::string name_;
   bool creator_;
@@ -391,11 +401,8 @@ class ShmChannel {
   WaitStats wstats_, rstats_;
   std::vector<int64_t> lat_, wake_;
   uint64_t lat_n_ = 0;
-  std::thread* beater_ = nullptr;
+  Beat* beat_ = nullptr;
   pid_t owner_pid_ = 0;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  bool stopping_ = false;
 };
 
 }  // namespace
