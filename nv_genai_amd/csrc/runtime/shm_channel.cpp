@@ -45,10 +45,8 @@
 #include <atomic>
 #include <chrono>
 #include <climits>
-#include <condition_variable>
 #include <cstdint>
 #include <cstring>
-#include <mutex>
 #include <new>
 #include <stdexcept>
 #include <string>
@@ -212,8 +210,7 @@ class ShmChannel {
     if (getpid() != owner_pid_) {
       // a copy inherited across fork(): the heartbeat thread and the name belong to the parent;
       // leave both alone. The heartbeat state is leaked on purpose: its thread does not exist
-      // here, and its condition variable may record the parent thread as a waiter, which
-      // pthread_cond_destroy would wait for forever.
+      // here (destroying a joinable std::thread would terminate the process).
       if (base_) munmap(base_, bytes_);
       return;
     }
@@ -245,12 +242,8 @@ class ShmChannel {
   // Stop this participant's heartbeat (tests: a peer that hangs without exiting).
   void stop_beating() {
     if (getpid() != owner_pid_ || beat_ == nullptr) return;   // no heartbeat thread in a forked copy
-    {
-      std::lock_guard<std::mutex> lk(beat_->mu);
-      if (beat_->stopping) return;
-      beat_->stopping = true;
-    }
-    beat_->cv.notify_all();
+    if (beat_->stop.exchange(1) != 0) return;
+    futex_wake_all(&beat_->stop);
     if (beat_->th.joinable()) beat_->th.join();
   }
 
@@ -373,18 +366,16 @@ class ShmChannel {
     return b != 0 && now_ns() - b > liveness_ns_;
   }
 
+  // stamp every kBeatNs until stop_beating() sets the stop word (a futex: it wakes the sleep)
   void beat_loop() {
-    std::unique_lock<std::mutex> lk(beat_->mu);
-    while (!beat_->stopping) {
+    while (beat_->stop.load(std::memory_order_acquire) == 0) {
       hdr_->beat[beat_idx_].store(now_ns(), std::memory_order_release);
-      beat_->cv.wait_for(lk, std::chrono::nanoseconds(kBeatNs));
+      futex_wait(&beat_->stop, 0, kBeatNs);
     }
   }
 
-  struct Beat {   // heartbeat thread and its wake-up (heap: a forked copy must not destroy it)
-    std::mutex mu;
-    std::condition_variable cv;
-    bool stopping = false;
+  struct Beat {   // heartbeat thread and its stop word (heap: a forked copy must not destroy it)
+    std::atomic<uint32_t> stop{0};
     std::thread th;
   };
 

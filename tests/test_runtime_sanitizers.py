@@ -157,13 +157,41 @@ TSAN_WORKLOAD = textwrap.dedent(r'''
         h.add(rng.standard_normal((1500, 16)).astype(np.float32), np.arange(2500, 4000, dtype=np.int64), 8)
         h.remove(list(range(0, 4000, 5)))
         h.search(rng.standard_normal((400, 16)).astype(np.float32), 10, 64, 8)
+    # the step channel: one writer and two readers on three threads (the GIL is released in
+    # write / read), each object with its heartbeat thread; futex sleeps and wake-ups
+    import os, threading, time
+    name = f"/nga_tsan_{os.getpid()}"
+    w = rt.ShmChannel(name, True, 4, 256, 2, 0, 30.0)
+    rds = [rt.ShmChannel(name, False, 0, 0, 0, i, 30.0) for i in range(2)]
+    w.unlink()
+    got = [[], []]
+    def reader(i):
+        buf = np.empty(256, np.uint8)
+        for _ in range(3000):
+            n = rds[i].read(buf, 30.0)
+            assert n == 8, n
+            got[i].append(int(buf[:8].view(np.int64)[0]))
+    ts = [threading.Thread(target=reader, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for s in range(3000):
+        if s % 500 == 0:
+            time.sleep(0.05)    # readers fall asleep on the futex now and then
+        assert w.write(np.array([s], np.int64), 30.0) == 1
+    for t in ts:
+        t.join()
+    assert got[0] == got[1] == list(range(3000))
+    rds[0].stats(); w.stats()
+    w.close()
+    del rds, w
     print("TSAN_OK")
 ''')
 
 
 @pytest.mark.timeout(600)
 def test_hnsw_parallel_build_under_tsan(tmp_path):
-    """ThreadSanitizer build of _rt driving the only multi-threaded native code path (HNSW)."""
+    """ThreadSanitizer build of _rt driving its multi-threaded native code: the HNSW parallel
+    build / search and the step channel (writer, readers and heartbeat threads)."""
     if shutil.which("g++") is None:
         pytest.skip("no g++")
     libtsan = subprocess.run(["g++", "-print-file-name=libtsan.so"], capture_output=True,
