@@ -1,5 +1,5 @@
 """ASan + UBSan build of the native host runtime (_rt: paged-KV block manager, continuous-
-batching scheduler, BM25 index, splitters, HNSW graph index), driven by a randomized stress workload in a
+batching scheduler, BM25 index, splitters, HNSW graph index, step channel), driven by a randomized stress workload in a
 child interpreter (the reference has no sanitizer coverage at all).
 
 The instrumented module is built into a temp dir (the in-tree _rt stays uninstrumented) and
@@ -108,6 +108,28 @@ STRESS = textwrap.dedent(r'''
                 bad()
             except (RuntimeError, ValueError):
                 pass
+    # step channel: ring wrap with varying message sizes, every error path, close
+    name = f"/nga_asan_{os.getpid()}"
+    w = rt.ShmChannel(name, True, 3, 512, 1, 0, 30.0)
+    rd = rt.ShmChannel(name, False, 0, 0, 0, 0, 30.0)
+    buf = np.empty(512, np.uint8)
+    for i in range(2000):
+        msg = nr.integers(0, 255, int(nr.integers(1, 513)), dtype=np.uint8)
+        assert w.write(msg, 5.0) == 1
+        n = rd.read(buf, 5.0)
+        assert n == msg.size and bytes(buf[:n]) == msg.tobytes()
+    for bad in (lambda: w.write(np.zeros(513, np.uint8), 1.0), lambda: rd.write(np.zeros(1, np.uint8), 1.0),
+                lambda: w.read(buf, 1.0), lambda: rd.read(np.empty(4, np.uint8), 0.01),
+                lambda: rt.ShmChannel(name, False, 0, 0, 0, 5, 30.0), lambda: rt.ShmChannel("bad", True, 2, 64, 1, 0, 1.0)):
+        try:
+            bad()
+        except (RuntimeError, ValueError):
+            pass
+    assert rd.read(buf, 0.01) == -1
+    w.unlink(); w.close()
+    assert rd.read(buf, 1.0) == -2
+    rd.stats(); w.stats()
+    del w, rd
     print("STRESS_OK")
 ''')
 
