@@ -22,6 +22,8 @@
 // sizes the grid), so the split adapts to each sequence's real context length.
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -305,7 +307,7 @@ __device__ __forceinline__ int dvswz(int row) { return (row >> 1) & 7; }
 // always in flight. (A half-page ring, 32-key units, read each V^T row's 128-B line in two
 // 64-B halves and ran at 4.7 TB/s against 6.7.)
 // AUX: cache policy of the KV-page DMA loads (form decode_dma_aux): 2 = nt (each page is read
-// once per step), 0 = default policy
+// once per step), 0 = default policy, 3 = nt except each sequence's first page (ring form only)
 template <bool RING, int AUX>
 __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
     uint16_t* __restrict__ out, int64_t out_stride, const uint16_t* __restrict__ q,
@@ -383,27 +385,40 @@ __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
     // k's scores and softmax; V(k+1) as soon as V(k) is, during page k's P.V
     const int my_pages = p_begin + w < p_end ? (p_end - 1 - (p_begin + w)) / NW + 1 : 0;
     auto blk_of = [&](int k) { return (int64_t)sbt[w + NW * k]; };
-    auto issue_k = [&](int64_t blk) {
+    // AUX 3: nt loads, except a sequence's FIRST page (its position 0), which every sequence
+    // of a prompt template shares through the prefix cache: with the default policy the
+    // sequences after the first on an XCD find it in L2 instead of HBM
+    auto shared_page = [&](int k) { return AUX == 3 && p_begin + w + NW * k == 0; };
+    auto issue_k_as = [&](auto aux, int64_t blk) {
       const char* kp = reinterpret_cast<const char*>(kc + (blk * Hkv + kvh) * (int64_t)(BS * D));
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int key = 4 * i + (lane >> 4);
         __builtin_amdgcn_global_load_lds((gptr_t)(kp + key * 256 + (((lane & 15) ^ dkswz(key)) << 4)),
-                                         (lptr_t)(ks + i * 512), 16, 0, AUX);
+                                         (lptr_t)(ks + i * 512), 16, 0, decltype(aux)::value);
       }
     };
-    auto issue_v = [&](int64_t blk) {
+    auto issue_v_as = [&](auto aux, int64_t blk) {
       const char* vp = reinterpret_cast<const char*>(vc + (blk * Hkv + kvh) * (int64_t)(D * BS));
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int row = 8 * i + (lane >> 3);
         __builtin_amdgcn_global_load_lds((gptr_t)(vp + row * 128 + (((lane & 7) ^ dvswz(row)) << 4)),
-                                         (lptr_t)(vs + i * 512), 16, 0, AUX);
+                                         (lptr_t)(vs + i * 512), 16, 0, decltype(aux)::value);
       }
     };
+    constexpr int AUX_PAGE = AUX == 3 ? 2 : AUX;
+    auto issue_k = [&](int k) {
+      if (shared_page(k)) issue_k_as(std::integral_constant<int, 0>{}, blk_of(k));
+      else issue_k_as(std::integral_constant<int, AUX_PAGE>{}, blk_of(k));
+    };
+    auto issue_v = [&](int k) {
+      if (shared_page(k)) issue_v_as(std::integral_constant<int, 0>{}, blk_of(k));
+      else issue_v_as(std::integral_constant<int, AUX_PAGE>{}, blk_of(k));
+    };
     if (my_pages > 0) {
-      issue_k(blk_of(0));
-      issue_v(blk_of(0));
+      issue_k(0);
+      issue_v(0);
     }
     bf16x8 qf[DS];
     {
@@ -432,7 +447,7 @@ __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
           kf[ti][s] = *reinterpret_cast<const u16x8*>(ks + key * D + (((4 * s + h) ^ dkswz(key)) << 3));
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // K buffer free
-      if (more) issue_k(blk_of(k + 1));
+      if (more) issue_k(k + 1);
 
       const int kbase = (p_begin + w + NW * k) * BS;
       const bool full = kbase + BS <= ctx && kbase >= key_lo;
@@ -492,7 +507,7 @@ __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
           vf[g][dt] = *reinterpret_cast<const u16x8*>(vs + row * BS + (((4 * g + h) ^ dvswz(row)) << 3));
         }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // V buffer free
-      if (more) issue_v(blk_of(k + 1));
+      if (more) issue_v(k + 1);
 #pragma unroll
       for (int g = 0; g < 2; ++g)
 #pragma unroll
@@ -737,9 +752,10 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
   decode_attn_dma_kernel<RING, AUX><<<grid, 256, 0, stream>>>(                                              \
       out, out_stride, q, q_stride, static_cast<const uint16_t*>(kc), static_cast<const uint16_t*>(vc), \
       block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, part_ml, part_o, window, skip_empty ? 1 : 0)
-      const bool cached = kernel_form(KF_DECODE_DMA_AUX) == 0;
+      const int aux = kernel_form(KF_DECODE_DMA_AUX);
+      const bool cached = aux == 0;
       if (dma == 2) {
-        if (cached) NGA_DMA(true, 0); else NGA_DMA(true, 2);
+        if (cached) NGA_DMA(true, 0); else if (aux == 3) NGA_DMA(true, 3); else NGA_DMA(true, 2);
       } else {
         if (cached) NGA_DMA(false, 0); else NGA_DMA(false, 2);
       }

@@ -98,9 +98,16 @@ def test_ivf_recall_property(nlist, seed, k):
     ivf = IVFFlatIndex(32, nlist=nlist, nprobe=nlist, metric="cosine", device="cpu")
     ivf.train(X, seed=seed)
     ivf.add(X, ids)
-    _, ie = flat.search(Q, k)
-    _, ia = ivf.search(Q, k, nprobe=nlist)
-    assert torch.equal(torch.sort(ia, 1).values, torch.sort(ie, 1).values)
+    ve, ie = flat.search(Q, k)
+    va, ia = ivf.search(Q, k, nprobe=nlist)
+    # exact: the same top-k scores; the same ids wherever the k-th score is not tied with the
+    # next one (the two indexes sum the dot products in different orders, so an fp32 tie at
+    # the cut can fall either way)
+    assert torch.allclose(va, ve, atol=1e-5), (va, ve)
+    v1, _ = flat.search(Q, k + 1)
+    for qi in range(Q.shape[0]):
+        if v1.shape[1] <= k or float(v1[qi, k - 1] - v1[qi, k]) > 1e-5:
+            assert set(ia[qi].tolist()) == set(ie[qi].tolist()), qi
     _, ih = ivf.search(Q, k, nprobe=max(1, nlist // 2))
     rec = np.mean([len(set(a.tolist()) & set(e.tolist())) / k for a, e in zip(ih, ie)])
     assert rec >= 0.9, rec
