@@ -156,9 +156,20 @@ def build_runtime(force: bool = False, jobs: int = 8, out_dir: Path | None = Non
     return out
 
 
+def check_loadable() -> None:
+    """Import both extensions in a fresh interpreter: a link that leaves a symbol undefined
+    (e.g. a kernel template whose host stub the compiler did not emit) only shows at load
+    time, and must fail the build, not the first GPU run."""
+    r = subprocess.run([sys.executable, "-c", "import nv_genai_amd._rt, nv_genai_amd._C"],
+                       cwd=str(PKG.parent), capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("built extensions do not load:\n" + r.stderr[-2000:])
+
+
 def build_all(force: bool = False) -> None:
     build_runtime(force=force)
     build_kernels(force=force)
+    check_loadable()
 
 
 if __name__ == "__main__":

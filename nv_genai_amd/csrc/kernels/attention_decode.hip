@@ -22,8 +22,6 @@
 // sizes the grid), so the split adapts to each sequence's real context length.
 #include <cstdlib>
 
-#include <type_traits>
-
 #include "common.h"
 #include "kernels.h"
 
@@ -298,6 +296,30 @@ constexpr int DSLOT = 2 * BS * 128;   // elements of one wave's slot: K page + V
 constexpr int DMA_MAX_PAGES = 1024;   // block ids of a workgroup's partition staged in LDS
 __device__ __forceinline__ int dkswz(int row) { return (row & 3) | (((row >> 3) & 3) << 2); }
 __device__ __forceinline__ int dvswz(int row) { return (row >> 1) & 7; }
+
+// one page's K (16 x 1 KiB DMA: keys 4i .. 4i+3) / V^T (rows 8i .. 8i+7) into a wave's slot,
+// cache policy A (the aux immediate of global_load_lds)
+template <int A>
+__device__ __forceinline__ void dma_k_page(const uint16_t* kc, int64_t blk, int Hkv, int kvh, int lane, uint16_t* ks) {
+  const char* kp = reinterpret_cast<const char*>(kc + (blk * Hkv + kvh) * (int64_t)(BS * 128));
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int key = 4 * i + (lane >> 4);
+    __builtin_amdgcn_global_load_lds((gptr_t)(kp + key * 256 + (((lane & 15) ^ dkswz(key)) << 4)),
+                                     (lptr_t)(ks + i * 512), 16, 0, A);
+  }
+}
+
+template <int A>
+__device__ __forceinline__ void dma_v_page(const uint16_t* vc, int64_t blk, int Hkv, int kvh, int lane, uint16_t* vs) {
+  const char* vp = reinterpret_cast<const char*>(vc + (blk * Hkv + kvh) * (int64_t)(128 * BS));
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = 8 * i + (lane >> 3);
+    __builtin_amdgcn_global_load_lds((gptr_t)(vp + row * 128 + (((lane & 7) ^ dvswz(row)) << 4)),
+                                     (lptr_t)(vs + i * 512), 16, 0, A);
+  }
+}
 }  // namespace
 
 // RING = true (NGA_DECODE_DMA=2): the wave's K and V^T buffers are refilled separately. With
@@ -389,32 +411,16 @@ __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
     // of a prompt template shares through the prefix cache: with the default policy the
     // sequences after the first on an XCD find it in L2 instead of HBM
     auto shared_page = [&](int k) { return AUX == 3 && p_begin + w + NW * k == 0; };
-    auto issue_k_as = [&](auto aux, int64_t blk) {
-      const char* kp = reinterpret_cast<const char*>(kc + (blk * Hkv + kvh) * (int64_t)(BS * D));
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = 4 * i + (lane >> 4);
-        __builtin_amdgcn_global_load_lds((gptr_t)(kp + key * 256 + (((lane & 15) ^ dkswz(key)) << 4)),
-                                         (lptr_t)(ks + i * 512), 16, 0, decltype(aux)::value);
-      }
-    };
-    auto issue_v_as = [&](auto aux, int64_t blk) {
-      const char* vp = reinterpret_cast<const char*>(vc + (blk * Hkv + kvh) * (int64_t)(D * BS));
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = 8 * i + (lane >> 3);
-        __builtin_amdgcn_global_load_lds((gptr_t)(vp + row * 128 + (((lane & 7) ^ dvswz(row)) << 4)),
-                                         (lptr_t)(vs + i * 512), 16, 0, decltype(aux)::value);
-      }
-    };
     constexpr int AUX_PAGE = AUX == 3 ? 2 : AUX;
     auto issue_k = [&](int k) {
-      if (shared_page(k)) issue_k_as(std::integral_constant<int, 0>{}, blk_of(k));
-      else issue_k_as(std::integral_constant<int, AUX_PAGE>{}, blk_of(k));
+      const int64_t blk = blk_of(k);
+      if (shared_page(k)) dma_k_page<0>(kc, blk, Hkv, kvh, lane, ks);
+      else dma_k_page<AUX_PAGE>(kc, blk, Hkv, kvh, lane, ks);
     };
     auto issue_v = [&](int k) {
-      if (shared_page(k)) issue_v_as(std::integral_constant<int, 0>{}, blk_of(k));
-      else issue_v_as(std::integral_constant<int, AUX_PAGE>{}, blk_of(k));
+      const int64_t blk = blk_of(k);
+      if (shared_page(k)) dma_v_page<0>(vc, blk, Hkv, kvh, lane, vs);
+      else dma_v_page<AUX_PAGE>(vc, blk, Hkv, kvh, lane, vs);
     };
     if (my_pages > 0) {
       issue_k(0);
