@@ -329,14 +329,15 @@ __device__ __forceinline__ void dma_v_page(const uint16_t* vc, int64_t blk, int 
 // always in flight. (A half-page ring, 32-key units, read each V^T row's 128-B line in two
 // 64-B halves and ran at 4.7 TB/s against 6.7.)
 // AUX: cache policy of the KV-page DMA loads (form decode_dma_aux): 2 = nt (each page is read
-// once per step), 0 = default policy, 3 = nt except each sequence's first page (ring form only)
+// once per step), 0 = default policy, 3 = nt except each sequence's first `cached_pages` pages
+// (ring form only; the launcher passes form value - 2 pages)
 template <bool RING, int AUX>
 __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
     uint16_t* __restrict__ out, int64_t out_stride, const uint16_t* __restrict__ q,
     int64_t q_stride, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int max_blocks,
     const int32_t* __restrict__ ctx_lens, int Hq, int Hkv, float scale,
-    float* __restrict__ part_ml, float* __restrict__ part_o, int window, int skip_empty) {
+    float* __restrict__ part_ml, float* __restrict__ part_o, int window, int skip_empty, int cached_pages) {
   constexpr int D = 128, DS = 4, DT = 8;
   // ONE LDS object (a second one makes the compiler drain the DMA before fragment reads):
   // the waves' page slots, reused by the wave combine after the loop
@@ -407,10 +408,10 @@ __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
     // k's scores and softmax; V(k+1) as soon as V(k) is, during page k's P.V
     const int my_pages = p_begin + w < p_end ? (p_end - 1 - (p_begin + w)) / NW + 1 : 0;
     auto blk_of = [&](int k) { return (int64_t)sbt[w + NW * k]; };
-    // AUX 3: nt loads, except a sequence's FIRST page (its position 0), which every sequence
-    // of a prompt template shares through the prefix cache: with the default policy the
-    // sequences after the first on an XCD find it in L2 instead of HBM
-    auto shared_page = [&](int k) { return AUX == 3 && p_begin + w + NW * k == 0; };
+    // AUX 3: nt loads, except a sequence's first `cached_pages` pages, which every sequence of
+    // a prompt template shares through the prefix cache (the RAG template fills pages 0-1):
+    // with the default policy the sequences after the first on an XCD find them in L2
+    auto shared_page = [&](int k) { return AUX == 3 && p_begin + w + NW * k < cached_pages; };
     constexpr int AUX_PAGE = AUX == 3 ? 2 : AUX;
     auto issue_k = [&](int k) {
       const int64_t blk = blk_of(k);
@@ -757,11 +758,12 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
 #define NGA_DMA(RING, AUX)                                                                                   \
   decode_attn_dma_kernel<RING, AUX><<<grid, 256, 0, stream>>>(                                              \
       out, out_stride, q, q_stride, static_cast<const uint16_t*>(kc), static_cast<const uint16_t*>(vc), \
-      block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, part_ml, part_o, window, skip_empty ? 1 : 0)
+      block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, part_ml, part_o, window, skip_empty ? 1 : 0, \
+      aux >= 3 ? aux - 2 : 0)
       const int aux = kernel_form(KF_DECODE_DMA_AUX);
       const bool cached = aux == 0;
       if (dma == 2) {
-        if (cached) NGA_DMA(true, 0); else if (aux == 3) NGA_DMA(true, 3); else NGA_DMA(true, 2);
+        if (cached) NGA_DMA(true, 0); else if (aux >= 3) NGA_DMA(true, 3); else NGA_DMA(true, 2);
       } else {
         if (cached) NGA_DMA(false, 0); else NGA_DMA(false, 2);
       }
