@@ -296,30 +296,6 @@ constexpr int DSLOT = 2 * BS * 128;   // elements of one wave's slot: K page + V
 constexpr int DMA_MAX_PAGES = 1024;   // block ids of a workgroup's partition staged in LDS
 __device__ __forceinline__ int dkswz(int row) { return (row & 3) | (((row >> 3) & 3) << 2); }
 __device__ __forceinline__ int dvswz(int row) { return (row >> 1) & 7; }
-
-// one page's K (16 x 1 KiB DMA: keys 4i .. 4i+3) / V^T (rows 8i .. 8i+7) into a wave's slot,
-// cache policy A (the aux immediate of global_load_lds)
-template <int A>
-__device__ __forceinline__ void dma_k_page(const uint16_t* kc, int64_t blk, int Hkv, int kvh, int lane, uint16_t* ks) {
-  const char* kp = reinterpret_cast<const char*>(kc + (blk * Hkv + kvh) * (int64_t)(BS * 128));
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int key = 4 * i + (lane >> 4);
-    __builtin_amdgcn_global_load_lds((gptr_t)(kp + key * 256 + (((lane & 15) ^ dkswz(key)) << 4)),
-                                     (lptr_t)(ks + i * 512), 16, 0, A);
-  }
-}
-
-template <int A>
-__device__ __forceinline__ void dma_v_page(const uint16_t* vc, int64_t blk, int Hkv, int kvh, int lane, uint16_t* vs) {
-  const char* vp = reinterpret_cast<const char*>(vc + (blk * Hkv + kvh) * (int64_t)(128 * BS));
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int row = 8 * i + (lane >> 3);
-    __builtin_amdgcn_global_load_lds((gptr_t)(vp + row * 128 + (((lane & 7) ^ dvswz(row)) << 4)),
-                                     (lptr_t)(vs + i * 512), 16, 0, A);
-  }
-}
 }  // namespace
 
 // RING = true (NGA_DECODE_DMA=2): the wave's K and V^T buffers are refilled separately. With
@@ -329,15 +305,14 @@ __device__ __forceinline__ void dma_v_page(const uint16_t* vc, int64_t blk, int 
 // always in flight. (A half-page ring, 32-key units, read each V^T row's 128-B line in two
 // 64-B halves and ran at 4.7 TB/s against 6.7.)
 // AUX: cache policy of the KV-page DMA loads (form decode_dma_aux): 2 = nt (each page is read
-// once per step), 0 = default policy, 3 = nt except each sequence's first `cached_pages` pages
-// (ring form only; the launcher passes form value - 2 pages)
+// once per step), 0 = default policy
 template <bool RING, int AUX>
 __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
     uint16_t* __restrict__ out, int64_t out_stride, const uint16_t* __restrict__ q,
     int64_t q_stride, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int max_blocks,
     const int32_t* __restrict__ ctx_lens, int Hq, int Hkv, float scale,
-    float* __restrict__ part_ml, float* __restrict__ part_o, int window, int skip_empty, int cached_pages) {
+    float* __restrict__ part_ml, float* __restrict__ part_o, int window, int skip_empty) {
   constexpr int D = 128, DS = 4, DT = 8;
   // ONE LDS object (a second one makes the compiler drain the DMA before fragment reads):
   // the waves' page slots, reused by the wave combine after the loop
@@ -408,24 +383,27 @@ __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
     // k's scores and softmax; V(k+1) as soon as V(k) is, during page k's P.V
     const int my_pages = p_begin + w < p_end ? (p_end - 1 - (p_begin + w)) / NW + 1 : 0;
     auto blk_of = [&](int k) { return (int64_t)sbt[w + NW * k]; };
-    // AUX 3: nt loads, except a sequence's first `cached_pages` pages, which every sequence of
-    // a prompt template shares through the prefix cache (the RAG template fills pages 0-1):
-    // with the default policy the sequences after the first on an XCD find them in L2
-    auto shared_page = [&](int k) { return AUX == 3 && p_begin + w + NW * k < cached_pages; };
-    constexpr int AUX_PAGE = AUX == 3 ? 2 : AUX;
-    auto issue_k = [&](int k) {
-      const int64_t blk = blk_of(k);
-      if (shared_page(k)) dma_k_page<0>(kc, blk, Hkv, kvh, lane, ks);
-      else dma_k_page<AUX_PAGE>(kc, blk, Hkv, kvh, lane, ks);
+    auto issue_k = [&](int64_t blk) {
+      const char* kp = reinterpret_cast<const char*>(kc + (blk * Hkv + kvh) * (int64_t)(BS * D));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = 4 * i + (lane >> 4);
+        __builtin_amdgcn_global_load_lds((gptr_t)(kp + key * 256 + (((lane & 15) ^ dkswz(key)) << 4)),
+                                         (lptr_t)(ks + i * 512), 16, 0, AUX);
+      }
     };
-    auto issue_v = [&](int k) {
-      const int64_t blk = blk_of(k);
-      if (shared_page(k)) dma_v_page<0>(vc, blk, Hkv, kvh, lane, vs);
-      else dma_v_page<AUX_PAGE>(vc, blk, Hkv, kvh, lane, vs);
+    auto issue_v = [&](int64_t blk) {
+      const char* vp = reinterpret_cast<const char*>(vc + (blk * Hkv + kvh) * (int64_t)(D * BS));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = 8 * i + (lane >> 3);
+        __builtin_amdgcn_global_load_lds((gptr_t)(vp + row * 128 + (((lane & 7) ^ dvswz(row)) << 4)),
+                                         (lptr_t)(vs + i * 512), 16, 0, AUX);
+      }
     };
     if (my_pages > 0) {
-      issue_k(0);
-      issue_v(0);
+      issue_k(blk_of(0));
+      issue_v(blk_of(0));
     }
     bf16x8 qf[DS];
     {
@@ -454,7 +432,7 @@ __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
           kf[ti][s] = *reinterpret_cast<const u16x8*>(ks + key * D + (((4 * s + h) ^ dkswz(key)) << 3));
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // K buffer free
-      if (more) issue_k(k + 1);
+      if (more) issue_k(blk_of(k + 1));
 
       const int kbase = (p_begin + w + NW * k) * BS;
       const bool full = kbase + BS <= ctx && kbase >= key_lo;
@@ -514,7 +492,7 @@ __global__ void __launch_bounds__(256, 1) decode_attn_dma_kernel(
           vf[g][dt] = *reinterpret_cast<const u16x8*>(vs + row * BS + (((4 * g + h) ^ dvswz(row)) << 3));
         }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // V buffer free
-      if (more) issue_v(k + 1);
+      if (more) issue_v(blk_of(k + 1));
 #pragma unroll
       for (int g = 0; g < 2; ++g)
 #pragma unroll
@@ -758,12 +736,10 @@ void launch_decode_attention(uint16_t* out, int64_t out_stride, const uint16_t* 
 #define NGA_DMA(RING, AUX)                                                                                   \
   decode_attn_dma_kernel<RING, AUX><<<grid, 256, 0, stream>>>(                                              \
       out, out_stride, q, q_stride, static_cast<const uint16_t*>(kc), static_cast<const uint16_t*>(vc), \
-      block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, part_ml, part_o, window, skip_empty ? 1 : 0, \
-      aux >= 3 ? aux - 2 : 0)
-      const int aux = kernel_form(KF_DECODE_DMA_AUX);
-      const bool cached = aux == 0;
+      block_tables, max_blocks, ctx_lens, Hq, Hkv, sc, part_ml, part_o, window, skip_empty ? 1 : 0)
+      const bool cached = kernel_form(KF_DECODE_DMA_AUX) == 0;
       if (dma == 2) {
-        if (cached) NGA_DMA(true, 0); else if (aux >= 3) NGA_DMA(true, 3); else NGA_DMA(true, 2);
+        if (cached) NGA_DMA(true, 0); else NGA_DMA(true, 2);
       } else {
         if (cached) NGA_DMA(false, 0); else NGA_DMA(false, 2);
       }

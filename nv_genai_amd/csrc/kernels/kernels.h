@@ -19,7 +19,7 @@ enum KernelForm {
   KF_PREFILL_KS,       // NGA_PREFILL_KS: 1 / 2 forces the 32x32 prefill kernel's wave-group count
   KF_ROPE_VNT,         // NGA_ROPE_VNT: non-temporal 2-byte V^T page stores in the RoPE / KV-write kernels: 1 all, 2 tokens with no same-page neighbour
   KF_SKINNY_SNT,       // NGA_SKINNY_SNT: decode-shape GEMM fp32 K-split slabs: 1 non-temporal stores, 2 also non-temporal loads in the split-K consumers
-  KF_DECODE_DMA_AUX,   // NGA_DECODE_DMA_AUX: cache policy of the LDS-DMA decode kernel's KV loads: 2 nt (default), 0 default policy, n >= 3: nt except each sequence's first n - 2 pages
+  KF_DECODE_DMA_AUX,   // NGA_DECODE_DMA_AUX: cache policy of the LDS-DMA decode kernel's KV loads: 2 nt (default), 0 default policy
   KF_COUNT
 };
 int kernel_form(KernelForm f);

@@ -139,15 +139,13 @@ def _paged_setup(ctxs, Hkv, D, dev, seed=0):
     return kc, vc, bt.to(dev)
 
 
-@pytest.mark.parametrize("aux", ["2", "0", "4"])
+@pytest.mark.parametrize("aux", ["2", "0"])
 @pytest.mark.parametrize("dma", ["1", "2"])
 @pytest.mark.parametrize("G", [4, 8])
 @pytest.mark.parametrize("ppp", [None, 2, 3])
 def test_decode_attention(gpu, G, ppp, dma, aux, kernel_form, monkeypatch):
     """NGA_DECODE_DMA 1: the whole-page LDS-DMA kernel, 2: its half-page ring form (KV loads
-    nt, or with NGA_DECODE_DMA_AUX=0 the default cache policy, 4 nt except each sequence's
-    first two pages, which the sequences then share, as a prompt template's pages are shared
-    through the prefix cache).
+    nt, or with NGA_DECODE_DMA_AUX=0 the default cache policy).
     Short, page-edge, long (4096 / 8192) contexts and contexts one key either side of a
     split-K partition boundary (ppp pages of 64 keys per partition), per-head relative error
     against the fp32 reference (computed on the GPU in fp32)."""
@@ -158,10 +156,6 @@ def test_decode_attention(gpu, G, ppp, dma, aux, kernel_form, monkeypatch):
     part = 64 * (ppp or 2)
     ctxs = [1, 63, 64, 65, 700, 3001, 128, 4096, 8192, part - 1, part + 1, 3 * part, 5 * part + 1]
     kc, vc, bt = _paged_setup(ctxs, Hkv, D, gpu)
-    if aux == "4":      # the first two pages shared by every sequence that has them
-        bt[:, 0] = bt[0, 0]
-        two = torch.tensor([c > 64 for c in ctxs], device=bt.device)
-        bt[:, 1] = torch.where(two, bt[-1, 1], bt[:, 1])
     B = len(ctxs)
     q = _bf(B, Hq * D, dev=gpu)
     ctx = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
