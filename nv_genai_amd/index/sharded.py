@@ -164,9 +164,6 @@ class ShardedIndex:
             return None
         return car if car.enabled else None
 
-    def _custom_gather(self):
-        return self._car
-
     def query_payload(self, q: torch.Tensor) -> "np.ndarray":
         """The query block as host bytes for the replica's step channel (fp32 [n, dim]): the
         followers receive it inside the search command instead of through a broadcast."""
@@ -199,10 +196,10 @@ class ShardedIndex:
         broadcast is needed; otherwise rank ``src``'s block is broadcast first (CC7).
 
         Each rank's (score, id) list is packed into one int32 row per query — the k fp32 score
-        bit patterns, then the k int64 ids as 2k words — and gathered in ONE collective (CC8): the replica's
-        IPC all-gather kernel when the group has one (ranks read each other's staging buffers
-        over xGMI; no host round trip), else one process-group all-gather. The world x k
-        candidates are merged by the top-k kernel (K15)."""
+        bit patterns, then the k int64 ids as 2k words — and gathered in ONE collective (CC8):
+        the index's own IPC all-gather kernel (ranks read each other's staging buffers over
+        xGMI; no host round trip), else one process-group all-gather. The world x k candidates
+        are merged by the top-k kernel (K15)."""
         if q.dim() == 1:
             q = q.unsqueeze(0)
         if self.world == 1:
@@ -226,7 +223,7 @@ class ShardedIndex:
         packed = torch.zeros(nq, width, dtype=torch.int32, device=vals.device)
         packed[:, :k] = vals.float().contiguous().view(torch.int32)
         packed[:, k:3 * k] = ids.to(torch.int64).contiguous().view(torch.int32)
-        car = self._custom_gather() if packed.is_cuda else None
+        car = self._car if packed.is_cuda else None
         if car is not None and car.gather_eligible(packed):
             g = car.all_gather(packed)                                   # [nq, world * width]
             self.stats["ipc_gathers"] += 1
