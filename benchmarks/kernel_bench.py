@@ -97,19 +97,14 @@ def main():
             return
     if args.only in ("", "norm"):
         # residual add + RMSNorm at decode / mixed / full-budget step sizes (Llama-3-8B width):
-        # wave-per-row kernel vs the row-per-workgroup form
+        # add + RMSNorm at the headline's step sizes
         w = torch.randn(4096, device=dev).to(torch.bfloat16)
         for T in (256, 1426, 4352):
             r = torch.randn(T, 4096, device=dev).to(torch.bfloat16)
             dlt = torch.randn(T, 4096, device=dev).to(torch.bfloat16)
             o = torch.empty_like(r)
-            res = {}
-            for tag, env in (("wave", "1"), ("row_block", "0")):
-                ops.kernels().set_kernel_form("rmsnorm_wave", int(env))
-                us = timeit(lambda: ops.add_rmsnorm(r, dlt, w, 1e-5, out=o))
-                res[tag] = {"us": round(us, 1), "TBps": round(4 * T * 4096 * 2 / us / 1e6, 2)}
-            ops.kernels().set_kernel_form("rmsnorm_wave", 0)   # back to the default (row-per-block)
-            out[f"add_rmsnorm_{T}x4096"] = res
+            us = timeit(lambda: ops.add_rmsnorm(r, dlt, w, 1e-5, out=o))
+            out[f"add_rmsnorm_{T}x4096"] = {"us": round(us, 1), "TBps": round(4 * T * 4096 * 2 / us / 1e6, 2)}
         if args.only == "norm":
             print(json.dumps(out))
             return
@@ -137,14 +132,10 @@ def main():
             us_f = timeit(lambda: ops.search_topk(Q, X, bias, 1.0, 4))
             ops.kernels().set_kernel_form("search_dma", 0)    # the register-load form
             us_reg = timeit(lambda: ops.search_topk(Q, X, bias, 1.0, 4))
-            ops.kernels().set_kernel_form("search_nt", 1)
-            us_nt = timeit(lambda: ops.search_topk(Q, X, bias, 1.0, 4))
-            ops.kernels().set_kernel_form("search_nt", 0)
             ops.kernels().set_kernel_form("search_dma", 1)
             out[f"search_1Mx1024_q{nq}"] = {"reg_us": round(us_reg, 1),
                                              "reg_TBps": round(N * Dx * 2 / us_reg / 1e6, 2),
-                                             "fused_nt_us": round(us_nt, 1),
-                                             "fused_nt_TBps": round(N * Dx * 2 / us_nt / 1e6, 2),"score_us": round(us, 1), "score_TBps": round(N * Dx * 2 / us / 1e6, 2),
+                                             "score_us": round(us, 1), "score_TBps": round(N * Dx * 2 / us / 1e6, 2),
                                              "score_topk_us": round(us_all, 1),
                                              "fused_us": round(us_f, 1),
                                              "fused_TBps": round(N * Dx * 2 / us_f / 1e6, 2),

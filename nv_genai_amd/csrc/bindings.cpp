@@ -286,8 +286,6 @@ void skinny_gemm(Tensor out, Tensor x, Tensor w, int64_t epi, int64_t split, int
   p.krot = krot ? 1 : 0;
   p.wpack = wpack ? 1 : 0;
   p.xpack = xpack ? 1 : 0;
-  p.wnt = 0;   // non-temporal weight DMA: measured within noise (NGA_SKINNY_WNT, removed)
-  p.snt = nga::kernel_form(nga::KF_SKINNY_SNT) != 0 ? 1 : 0;
   if (xpack) {
     const int64_t nm = (M + info[1] - 1) / info[1];
     TORCH_CHECK(x.size(1) == 64 && x.size(0) == nm * (K / 64) * info[1],
@@ -916,10 +914,9 @@ struct FormSpec {
 };
 const FormSpec kForms[KF_COUNT] = {
     {"decode_dma", "NGA_DECODE_DMA", 2}, {"decode_nt", "NGA_DECODE_NT", 2},
-    {"rmsnorm_wave", "NGA_RMSNORM_WAVE", 0}, {"search_dma", "NGA_SEARCH_DMA", 1},
-    {"search_nt", "NGA_SEARCH_NT", 0}, {"prefill_v1", "NGA_PREFILL_V1", 0},
+    {"search_dma", "NGA_SEARCH_DMA", 1}, {"prefill_v1", "NGA_PREFILL_V1", 0},
     {"prefill_ks", "NGA_PREFILL_KS", 0}, {"rope_vnt", "NGA_ROPE_VNT", 2},
-    {"skinny_snt", "NGA_SKINNY_SNT", 0}, {"decode_dma_aux", "NGA_DECODE_DMA_AUX", 2}};
+    {"decode_dma_aux", "NGA_DECODE_DMA_AUX", 2}};
 std::atomic<int>* forms() {
   static std::atomic<int> v[KF_COUNT];
   static const bool init = [] {

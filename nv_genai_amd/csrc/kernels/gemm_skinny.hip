@@ -65,12 +65,10 @@ __device__ __forceinline__ void sk_wait_vm() {
 
 __device__ __forceinline__ float sk_silu(float x) { return x / (1.f + __expf(-x)); }
 
-// a 16-B slab read: plain, or non-temporal (NT: the slabs are read once, kernel form skinny_snt 2)
-template <bool NT>
-__device__ __forceinline__ f32x4 sk_ld4(const float* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-  else return *reinterpret_cast<const f32x4*>(p);
-}
+// a 16-B slab read. The slabs are read once, but non-temporal slab stores / loads measured no
+// faster (the very next kernel reads them back; headline 40.08 / 39.82 QPS with nt stores vs
+// 40.24 / 40.25 cached, profiles/r5_skinny_snt/) and were removed.
+__device__ __forceinline__ f32x4 sk_ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 }  // namespace
 
 template <int BN, int BM, int WN, int WM, int NSTAGE, int EPI, int SBK>
@@ -152,14 +150,9 @@ __global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmPar
     if (ke >= nk) ke -= nk;
     const int k0 = ke * SBK;
     const int64_t wk0 = P.wpack ? (int64_t)ke * (BN * SBK) : (int64_t)k0;
-    if (P.wnt) {
+    // weights with the default cache policy: non-temporal weight DMA measured within noise
 #pragma unroll
-      for (int i = 0; i < W_GL; ++i)
-        __builtin_amdgcn_global_load_lds((gptr_t)(wsrc[i] + wk0), (lptr_t)(base + (wv * W_GL + i) * RPI * SBK), 16, 0, 2);
-    } else {
-#pragma unroll
-      for (int i = 0; i < W_GL; ++i) glds16(wsrc[i] + wk0, base + (wv * W_GL + i) * RPI * SBK);
-    }
+    for (int i = 0; i < W_GL; ++i) glds16(wsrc[i] + wk0, base + (wv * W_GL + i) * RPI * SBK);
     const int64_t xk0 = P.xpack ? (int64_t)ke * (BM * SBK) : (int64_t)k0;
 #pragma unroll
     for (int i = 0; i < X_GL; ++i) glds16(xsrc[i] + xk0, base + BN * SBK + (wv * X_GL + i) * RPI * SBK);
@@ -250,8 +243,7 @@ __global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmPar
       for (int nt = 0; nt < NTW; ++nt) {
         const int n = n_base + nt * 16 + 4 * h;
         if (n >= P.N) continue;
-        if (P.snt) __builtin_nontemporal_store(acc[nt][mt], reinterpret_cast<f32x4*>(op + n));
-        else *reinterpret_cast<f32x4*>(op + n) = acc[nt][mt];
+        *reinterpret_cast<f32x4*>(op + n) = acc[nt][mt];
       }
     } else {
       uint16_t* op = reinterpret_cast<uint16_t*>(P.out) + (int64_t)t * P.ldo;
@@ -268,7 +260,6 @@ __global__ void __launch_bounds__(64 * WN * WM) skinny_gemm_kernel(SkinnyGemmPar
 }
 
 // out[m, n] = bf16(sum_s P[s, m, n]); 8 features per thread
-template <bool NT>
 __global__ void splitk_reduce_kernel(const float* __restrict__ P, int S, int M, int N,
                                      uint16_t* __restrict__ out, int64_t ldo) {
   const int nv = N / 8;
@@ -279,10 +270,10 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ P, int S, int M, 
     const int64_t m = i / nv;
     const int c = (int)(i - m * nv) * 8;
     const float* p = P + m * N + c;
-    f32x4 a0 = sk_ld4<NT>(p), a1 = sk_ld4<NT>(p + 4);
+    f32x4 a0 = sk_ld4(p), a1 = sk_ld4(p + 4);
     for (int s = 1; s < S; ++s) {
-      a0 += sk_ld4<NT>(p + s * slab);
-      a1 += sk_ld4<NT>(p + s * slab + 4);
+      a0 += sk_ld4(p + s * slab);
+      a1 += sk_ld4(p + s * slab + 4);
     }
     u16x8 o;
 #pragma unroll
@@ -296,7 +287,6 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ P, int S, int M, 
 
 // out[m, f] = bf16(silu(sum_s P[s, m, f]) * sum_s P[s, m, F + f]): the K-split gate / up
 // projection (slabs in the standard [gate | up] column order) summed by its SwiGLU consumer
-template <bool NT>
 __global__ void splitk_swiglu_kernel(const float* __restrict__ P, int S, int M, int F,
                                      uint16_t* __restrict__ out, int64_t ldo) {
   const int nv = F / 8;
@@ -307,14 +297,14 @@ __global__ void splitk_swiglu_kernel(const float* __restrict__ P, int S, int M, 
     const int64_t m = i / nv;
     const int c = (int)(i - m * nv) * 8;
     const float* p = P + m * 2 * F + c;
-    f32x4 g0 = sk_ld4<NT>(p), g1 = sk_ld4<NT>(p + 4);
-    f32x4 u0 = sk_ld4<NT>(p + F), u1 = sk_ld4<NT>(p + F + 4);
+    f32x4 g0 = sk_ld4(p), g1 = sk_ld4(p + 4);
+    f32x4 u0 = sk_ld4(p + F), u1 = sk_ld4(p + F + 4);
     for (int s = 1; s < S; ++s) {
       const float* q = p + s * slab;
-      g0 += sk_ld4<NT>(q);
-      g1 += sk_ld4<NT>(q + 4);
-      u0 += sk_ld4<NT>(q + F);
-      u1 += sk_ld4<NT>(q + F + 4);
+      g0 += sk_ld4(q);
+      g1 += sk_ld4(q + 4);
+      u0 += sk_ld4(q + F);
+      u1 += sk_ld4(q + F + 4);
     }
     u16x8 o;
 #pragma unroll
@@ -329,7 +319,6 @@ __global__ void splitk_swiglu_kernel(const float* __restrict__ P, int S, int M, 
 // resid += sum_s P[s] (one rounding to the bf16 residual); out = rmsnorm(resid) * w.
 // One workgroup per row, 8 features per lane (the add_rmsnorm kernel with the split-K sum of
 // the producing GEMM folded into its load).
-template <bool NT>
 __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(const float* __restrict__ P, int S,
                                                                   int M, uint16_t* __restrict__ resid,
                                                                   const uint16_t* __restrict__ w,
@@ -344,10 +333,10 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(const float* _
   float ss = 0.f;
   if (active) {
     const float* p = P + row * H + c;
-    f32x4 a0 = sk_ld4<NT>(p), a1 = sk_ld4<NT>(p + 4);
+    f32x4 a0 = sk_ld4(p), a1 = sk_ld4(p + 4);
     for (int s = 1; s < S; ++s) {
-      a0 += sk_ld4<NT>(p + s * slab);
-      a1 += sk_ld4<NT>(p + s * slab + 4);
+      a0 += sk_ld4(p + s * slab);
+      a1 += sk_ld4(p + s * slab + 4);
     }
     const u16x8 v = load8(resid + row * H + c);
     u16x8 st;
@@ -451,8 +440,7 @@ void launch_splitk_reduce(const float* P, int S, int M, int N, uint16_t* out, in
   if (M == 0) return;
   int64_t g = ((int64_t)M * (N / 8) + 255) / 256;
   if (g > 2048) g = 2048;
-  if (kernel_form(KF_SKINNY_SNT) == 2) splitk_reduce_kernel<true><<<(unsigned)g, 256, 0, stream>>>(P, S, M, N, out, ldo);
-  else splitk_reduce_kernel<false><<<(unsigned)g, 256, 0, stream>>>(P, S, M, N, out, ldo);
+  splitk_reduce_kernel<<<(unsigned)g, 256, 0, stream>>>(P, S, M, N, out, ldo);
 }
 
 void launch_splitk_swiglu(const float* P, int S, int M, int F, uint16_t* out, int64_t ldo,
@@ -460,8 +448,7 @@ void launch_splitk_swiglu(const float* P, int S, int M, int F, uint16_t* out, in
   if (M == 0) return;
   int64_t g = ((int64_t)M * (F / 8) + 255) / 256;
   if (g > 2048) g = 2048;
-  if (kernel_form(KF_SKINNY_SNT) == 2) splitk_swiglu_kernel<true><<<(unsigned)g, 256, 0, stream>>>(P, S, M, F, out, ldo);
-  else splitk_swiglu_kernel<false><<<(unsigned)g, 256, 0, stream>>>(P, S, M, F, out, ldo);
+  splitk_swiglu_kernel<<<(unsigned)g, 256, 0, stream>>>(P, S, M, F, out, ldo);
 }
 
 void launch_splitk_add_rmsnorm(const float* P, int S, int M, uint16_t* resid, const uint16_t* w,
@@ -469,8 +456,7 @@ void launch_splitk_add_rmsnorm(const float* P, int S, int M, uint16_t* resid, co
   if (M == 0) return;
   int t = (H / 8 + 63) / 64 * 64;
   if (t < 64) t = 64;
-  if (kernel_form(KF_SKINNY_SNT) == 2) splitk_add_rmsnorm_kernel<true><<<M, t, 0, stream>>>(P, S, M, resid, w, eps, H, out);
-  else splitk_add_rmsnorm_kernel<false><<<M, t, 0, stream>>>(P, S, M, resid, w, eps, H, out);
+  splitk_add_rmsnorm_kernel<<<M, t, 0, stream>>>(P, S, M, resid, w, eps, H, out);
 }
 
 }  // namespace nga

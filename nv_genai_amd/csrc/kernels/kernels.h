@@ -12,13 +12,10 @@ namespace nga {
 enum KernelForm {
   KF_DECODE_DMA = 0,   // NGA_DECODE_DMA: 2 ring form of the LDS-DMA decode kernel (default), 1 its whole-page form, 0 register kernel
   KF_DECODE_NT,        // NGA_DECODE_NT: register decode kernel's KV loads nt: 1 always, 2 bf16 pages only (default), 0 never
-  KF_RMSNORM_WAVE,     // NGA_RMSNORM_WAVE: 1 wave-per-row RMSNorm
   KF_SEARCH_DMA,       // NGA_SEARCH_DMA: 0 forces the register form of the fused search kernel
-  KF_SEARCH_NT,        // NGA_SEARCH_NT: 1 non-temporal index-row loads (register search form)
   KF_PREFILL_V1,       // NGA_PREFILL_V1: 1 disables the 32x32 prefill kernel
   KF_PREFILL_KS,       // NGA_PREFILL_KS: 1 / 2 forces the 32x32 prefill kernel's wave-group count
   KF_ROPE_VNT,         // NGA_ROPE_VNT: non-temporal 2-byte V^T page stores in the RoPE / KV-write kernels: 1 all, 2 tokens with no same-page neighbour
-  KF_SKINNY_SNT,       // NGA_SKINNY_SNT: decode-shape GEMM fp32 K-split slabs: 1 non-temporal stores, 2 also non-temporal loads in the split-K consumers
   KF_DECODE_DMA_AUX,   // NGA_DECODE_DMA_AUX: cache policy of the LDS-DMA decode kernel's KV loads: 2 nt (default), 0 default policy
   KF_COUNT
 };
@@ -203,8 +200,6 @@ struct SkinnyGemmParams {
   int krot;            // 1: each block starts its K walk at a block-dependent step
   int wpack;           // 1: w is tile-packed [nN][K/64][BN][64] for this cfg's BN (pack_weight)
   int xpack;           // 1: x is tile-packed [nM][K/64][BM][64] for this cfg's BM (pack_rows)
-  int wnt;             // 1: weight DMA with the non-temporal cache policy (streamed once)
-  int snt;             // 1: fp32 slab stores (epi 1) non-temporal (kernel form skinny_snt)
 };
 // scatter of packed step inputs (staging.hip): segment s = bytes [off, off + bytes) of the
 // device staging buffer -> dst (16-B aligned offsets / destinations, bytes % 4 == 0)

@@ -112,57 +112,6 @@ __global__ void __launch_bounds__(1024) layernorm_kernel(uint16_t* __restrict__ 
   }
 }
 
-// Wave-per-row form for the decoder widths (H = 512 NV): a row lives in one wave's registers
-// (NV 16-B vectors per lane, all loads of the row in flight at once), the reduction is a wave
-// reduction with no barrier, and a 256-thread workgroup takes 4 rows. The one-workgroup-per-
-// row form above issues one 16-B load per lane and then two barriers, so a mixed step's
-// ~1,400 rows took ~10 us for 46 MB (4.5 TB/s).
-template <bool ADD, int NV>
-__global__ void __launch_bounds__(256) rmsnorm_wave_kernel(uint16_t* __restrict__ out,
-                                                           uint16_t* __restrict__ resid,
-                                                           const uint16_t* __restrict__ delta,
-                                                           const uint16_t* __restrict__ w, float eps,
-                                                           int64_t rows, int64_t in_stride,
-                                                           int64_t out_stride) {
-  constexpr int H = 512 * NV;
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  uint16_t* rp = resid + row * in_stride;
-  u16x8 v[NV], d[NV];
-#pragma unroll
-  for (int j = 0; j < NV; ++j) v[j] = load8(rp + 512 * j + 8 * lane);
-  if (ADD) {
-    const uint16_t* dp = delta + row * in_stride;
-#pragma unroll
-    for (int j = 0; j < NV; ++j) d[j] = load8(dp + 512 * j + 8 * lane);
-  }
-  float ss = 0.f;
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    if (ADD) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[j][i] = f2bf(bf2f(v[j][i]) + bf2f(d[j][i]));
-      store8(rp + 512 * j + 8 * lane, v[j]);   // normalise what is stored (bf16 residual stream)
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float x = bf2f(v[j][i]);
-      ss += x * x;
-    }
-  }
-  const float r = rsqrtf(wave_sum(ss) / (float)H + eps);
-  uint16_t* op = out + row * out_stride;
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const u16x8 wv = load8(w + 512 * j + 8 * lane);
-    u16x8 o;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = f2bf(bf2f(v[j][i]) * r * bf2f(wv[i]));
-    store8(op + 512 * j + 8 * lane, o);
-  }
-}
-
 static int row_threads(int H) {
   int t = (H / 8 + 63) / 64 * 64;
   return t < 64 ? 64 : t;
@@ -172,34 +121,10 @@ void launch_rmsnorm(uint16_t* out, uint16_t* resid, const uint16_t* delta, const
                     float eps, int64_t rows, int H, int64_t in_stride, int64_t out_stride,
                     hipStream_t stream) {
   if (rows == 0) return;
-  // The wave-per-row form measured slower than the row-per-block one at every step size of the
-  // headline (add + RMSNorm, 4,096 wide: 1,426 rows 7.2 vs 6.7 us, 4,352 rows 22.5 vs 21.3 us,
-  // 256 rows 3.9 both; profiles/r3_decode_step/kb_norm.json), so it is opt-in for A/B runs:
-  // form KF_RMSNORM_WAVE (NGA_RMSNORM_WAVE=1).
-  const bool wave_on = kernel_form(KF_RMSNORM_WAVE) != 0;
-  if (wave_on && H % 512 == 0 && H <= 8192 && in_stride % 8 == 0 && out_stride % 8 == 0) {
-    dim3 g4((unsigned)((rows + 3) / 4)), b4(256);
-#define NGA_RMSW(NV)                                                                               \
-  do {                                                                                             \
-    if (delta)                                                                                     \
-      rmsnorm_wave_kernel<true, NV><<<g4, b4, 0, stream>>>(out, resid, delta, w, eps, rows, in_stride, \
-                                                           out_stride);                            \
-    else                                                                                           \
-      rmsnorm_wave_kernel<false, NV><<<g4, b4, 0, stream>>>(out, resid, delta, w, eps, rows,        \
-                                                            in_stride, out_stride);                \
-    return;                                                                                        \
-  } while (0)
-    switch (H / 512) {
-      case 4: NGA_RMSW(4);
-      case 6: NGA_RMSW(6);
-      case 8: NGA_RMSW(8);
-      case 10: NGA_RMSW(10);
-      case 12: NGA_RMSW(12);
-      case 16: NGA_RMSW(16);
-      default: break;
-    }
-#undef NGA_RMSW
-  }
+  // One workgroup per row. A wave-per-row form (a row in one wave's registers, 4 rows per
+  // workgroup) measured slower at every step size of the headline (add + RMSNorm, 4,096 wide:
+  // 1,426 rows 7.2 vs 6.7 us, 4,352 rows 22.5 vs 21.3 us, 256 rows 3.9 both;
+  // profiles/r3_decode_step/kb_norm.json) and was removed.
   dim3 grid((unsigned)rows), block(row_threads(H));
   if (delta)
     rmsnorm_kernel<true><<<grid, block, 0, stream>>>(out, resid, delta, w, eps, H, in_stride,

@@ -356,8 +356,8 @@ class DecodeWorkspace:
         return max(1, -(-pages // self.nparts(B)))
 
 
-KERNEL_FORMS = ("decode_dma", "decode_nt", "rmsnorm_wave", "search_dma", "search_nt", "prefill_v1",
-                "prefill_ks", "rope_vnt", "skinny_snt", "decode_dma_aux")
+KERNEL_FORMS = ("decode_dma", "decode_nt", "search_dma", "prefill_v1", "prefill_ks", "rope_vnt",
+                "decode_dma_aux")
 
 
 def kernel_form(name: str) -> int:

@@ -42,12 +42,8 @@ def _close_rows(a, b, width=None, rel=1e-2, peak=2e-2):
     assert pk <= peak * b.abs().max().item() + 1e-6, f"max abs err {pk:.4g} > {peak} x max|ref|"
 
 
-# default: one workgroup per row at every width; wave = "1": the opt-in wave-per-row kernel
-# (H = 512 NV; other widths fall back to the row form)
-@pytest.mark.parametrize("wave", ["0", "1"])
 @pytest.mark.parametrize("H", [768, 1024, 2048, 3072, 4096, 5120, 6144, 8192])
-def test_rmsnorm(gpu, H, wave, kernel_form, monkeypatch):
-    kernel_form("rmsnorm_wave", wave)
+def test_rmsnorm(gpu, H):
     torch.manual_seed(0)
     x, w = _bf(37, H, dev=gpu), _bf(H, dev=gpu)
     _close_rows(ops.rmsnorm(x, w, 1e-5), ref.rmsnorm(x.cpu().float(), w.cpu().float(), 1e-5))
@@ -756,10 +752,8 @@ def test_gemv(gpu, M, N, K):
     _close_rows(ops.gemv(x, w, 2), sw, rel=1e-2)
 
 
-@pytest.mark.parametrize("snt", [0, 2])
-def test_splitk_swiglu(gpu, kernel_form, snt):
-    """silu(sum of gate slabs) * sum of up slabs, against fp32 (snt 2: non-temporal slab loads)."""
-    kernel_form("skinny_snt", snt)
+def test_splitk_swiglu(gpu):
+    """silu(sum of gate slabs) * sum of up slabs, against fp32."""
     torch.manual_seed(4)
     S, M, F = 3, 45, 1024
     P = torch.randn(S, M, 2 * F, device=gpu)
@@ -769,9 +763,7 @@ def test_splitk_swiglu(gpu, kernel_form, snt):
     _close_rows(y, y_ref, rel=1e-2)
 
 
-@pytest.mark.parametrize("snt", [0, 2])
-def test_splitk_add_rmsnorm(gpu, kernel_form, snt):
-    kernel_form("skinny_snt", snt)
+def test_splitk_add_rmsnorm(gpu):
     torch.manual_seed(3)
     S, M, H = 4, 77, 4096
     P = torch.randn(S, M, H, device=gpu) * 0.3
@@ -863,20 +855,6 @@ def test_skinny_table_production_shapes(gpu):
             del ref
         del w
         torch.cuda.empty_cache()
-
-
-@pytest.mark.parametrize("snt", [1, 2])
-def test_skinny_slab_nontemporal_stores_bitwise(gpu, kernel_form, snt):
-    """skinny_snt: the fp32 K-split slabs written with non-temporal stores are bit-identical to
-    the cached-store form (only the cache policy differs)."""
-    torch.manual_seed(6)
-    x, w = _bf(96, 4096, dev=gpu), _bf(4096, 4096, dev=gpu)
-    kernel_form("skinny_snt", 0)
-    a = ops.skinny_gemm(x, w, 1, 4, 1).clone()
-    kernel_form("skinny_snt", snt)
-    b = ops.skinny_gemm(x, w, 1, 4, 1)
-    torch.cuda.synchronize()
-    assert torch.equal(a, b)
 
 
 def test_packed_upload_scatters_segments(gpu):
