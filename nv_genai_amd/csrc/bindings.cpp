@@ -713,21 +713,41 @@ void scatter_segments(Tensor src, const std::vector<int64_t>& dst, const std::ve
   nga::launch_scatter_segments(reinterpret_cast<const uint8_t*>(src.data_ptr()), t, cur_stream(src));
 }
 
-// the whole packed step upload in one call: `nbytes` of the pinned host staging buffer -> the
-// device staging buffer (one async copy), then the scatter kernel, back to back on the current
-// stream (no host work between the two dispatches)
-void packed_upload(Tensor dev, Tensor host, int64_t nbytes, const std::vector<int64_t>& dst,
-                   const std::vector<int64_t>& off, const std::vector<int64_t>& bytes) {
-  CHECK_DEV(dev); CHECK_CONTIG(dev); CHECK_DT(dev, at::kByte);
-  TORCH_CHECK(!host.is_cuda() && host.is_contiguous() && host.scalar_type() == at::kByte && host.is_pinned(),
-              "packed_upload: host staging must be a pinned uint8 CPU tensor");
-  TORCH_CHECK(nbytes >= 0 && nbytes <= dev.numel() && nbytes <= host.numel(), "packed_upload: size");
-  hipStream_t st = cur_stream(dev);
-  if (nbytes > 0) {
-    hipError_t e = hipMemcpyAsync(dev.data_ptr(), host.data_ptr(), (size_t)nbytes, hipMemcpyHostToDevice, st);
-    TORCH_CHECK(e == hipSuccess, "packed_upload: hipMemcpyAsync: ", hipGetErrorString(e));
+// Host staging the GPU reads in place: pinned, mapped, portable and coherent (fine-grained) host
+// memory, so a kernel can take a step's packed inputs straight from it, with no copy dispatch
+// before it
+Tensor host_staging(int64_t nbytes) {
+  TORCH_CHECK(nbytes > 0, "host_staging: size");
+  void* p = nullptr;
+  hipError_t e = hipHostMalloc(&p, (size_t)nbytes, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable);
+  TORCH_CHECK(e == hipSuccess && p, "host_staging: hipHostMalloc: ", hipGetErrorString(e));
+  return torch::from_blob(p, {nbytes}, [](void* q) { (void)hipHostFree(q); },
+                          torch::TensorOptions().dtype(torch::kUInt8));
+}
+
+// the scatter kernel reading a host_staging buffer through its device mapping, on `device`'s
+// current stream
+void scatter_host(Tensor host, int64_t device, const std::vector<int64_t>& dst, const std::vector<int64_t>& off,
+                  const std::vector<int64_t>& bytes) {
+  TORCH_CHECK(!host.is_cuda() && host.is_contiguous() && host.scalar_type() == at::kByte,
+              "scatter_host: host staging must be a uint8 CPU tensor from host_staging()");
+  TORCH_CHECK(dst.size() == off.size() && off.size() == bytes.size() && dst.size() <= (size_t)nga::kMaxSegments,
+              "scatter_host: matching dst / off / bytes lists of at most 32 segments");
+  void* dp = nullptr;
+  hipError_t e = hipHostGetDevicePointer(&dp, host.data_ptr(), 0);
+  TORCH_CHECK(e == hipSuccess && dp, "scatter_host: not a mapped host buffer: ", hipGetErrorString(e));
+  nga::SegmentTable t{};
+  t.n = (int)dst.size();
+  for (size_t i = 0; i < dst.size(); ++i) {
+    TORCH_CHECK(off[i] % 16 == 0 && dst[i] % 16 == 0 && bytes[i] % 4 == 0 && bytes[i] >= 0 &&
+                    off[i] + bytes[i] <= host.numel(),
+                "scatter_host: 16-B aligned segments of whole 4-B words inside the staging buffer");
+    t.dst[i] = dst[i];
+    t.off[i] = off[i];
+    t.bytes[i] = bytes[i];
   }
-  scatter_segments(dev, dst, off, bytes);
+  nga::launch_scatter_segments(reinterpret_cast<const uint8_t*>(dp), t,
+                               c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream());
 }
 
 // a begin / end marker kernel on the current stream (kernel-trace window delimiters)
@@ -983,7 +1003,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("pool_l2norm", checked("pool_l2norm", &pool_l2norm));
   m.def("region_marker", checked("region_marker", &region_marker));
   m.def("scatter_segments", checked("scatter_segments", &scatter_segments));
-  m.def("packed_upload", checked("packed_upload", &packed_upload));
+  m.def("host_staging", &host_staging);
+  m.def("scatter_host", checked("scatter_host", &scatter_host));
   m.def("row_sqnorm", checked("row_sqnorm", &row_sqnorm));
   m.def("fir_c64", checked("fir_c64", &fir_c64));
   m.def("fm_demod", checked("fm_demod", &fm_demod));

@@ -1,16 +1,19 @@
-"""One host->device copy per engine step (csrc/kernels/staging.hip).
+"""One dispatch per engine step for the step's host inputs (csrc/kernels/staging.hip).
 
 A step's inputs live in fixed device buffers (the captured hipGraphs read them in place), each
 filled from its own pinned host buffer. Copying them one by one costs a host API call and a
 ~4.5 us blit dispatch on the compute stream per buffer, ~18 per step; a kernel trace of the
 headline's timed window named the copyBuffer -> copyBuffer gaps its largest idle source
 (profiles/r6_busy/). :class:`PackedUpload` packs the used rows of every buffer contiguously into
-a pinned staging area (host memcpy), issues ONE async copy into a device staging buffer and
-ONE scatter kernel to the destinations.
+a host staging area (host memcpy) and launches ONE scatter kernel that reads the staging area
+in place, over its device mapping (pinned, mapped, coherent host memory: `_C.host_staging`),
+and writes the destinations. No copy is dispatched: back to back, one upload of 24 KB costs
+3.6 us of device time against 19.2 for one async copy into a device staging buffer plus the
+scatter (`profiles/r6_h2d/probe.json`).
 
-The pinned staging area is double-buffered: the host packs step k + 1 while the copy of step k
-may still be queued behind the GPU's work; before reusing a half it waits for the copy that
-last read it (two uploads back, long done in a pipelined loop). The source host buffers can be
+The staging area is double-buffered: the host packs step k + 1 while the scatter of step k may
+still be queued behind the GPU's work; before reusing a half it waits for the scatter that last
+read it (two uploads back, long done in a pipelined loop). The source host buffers can be
 rewritten as soon as :meth:`upload` returns.
 """
 from __future__ import annotations
@@ -30,9 +33,10 @@ class PackedUpload:
     def __init__(self, device, capacity: int):
         self.device = torch.device(device)
         self.capacity = (int(capacity) + _ALIGN - 1) // _ALIGN * _ALIGN
-        self._h = [torch.empty(self.capacity, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        with torch.cuda.device(self.device):
+            self._h = [kernels().host_staging(self.capacity) for _ in range(2)]
         self._hn = [h.numpy() for h in self._h]
-        self._d = torch.empty(self.capacity, dtype=torch.uint8, device=self.device)
+        self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self._ev: List[Optional[torch.cuda.Event]] = [None, None]
         self._flip = 0
         # (host, device) -> (host, device, host bytes view, bytes per row, device address, rows);
@@ -60,8 +64,8 @@ class PackedUpload:
         return m[2:]
 
     def upload(self, segs: Iterable[Tuple[torch.Tensor, torch.Tensor, int]]) -> None:
-        """Copy rows [0, rows) of every (host, device, rows) pair, in one copy + one kernel on
-        the current stream."""
+        """Copy rows [0, rows) of every (host, device, rows) pair, in one kernel on the current
+        stream."""
         half = self._flip
         self._flip ^= 1
         ev = self._ev[half]
@@ -86,8 +90,7 @@ class PackedUpload:
             o = (o + nb + _ALIGN - 1) // _ALIGN * _ALIGN
         if not dst:
             return
-        # the async copy and the scatter kernel, issued back to back from C++
-        kernels().packed_upload(self._d, self._h[half], o, dst, off, nbytes)
+        kernels().scatter_host(self._h[half], self._dev_index, dst, off, nbytes)
         e = torch.cuda.Event()
         e.record()
         self._ev[half] = e

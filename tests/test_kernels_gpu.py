@@ -859,8 +859,11 @@ def test_skinny_table_production_shapes(gpu):
 
 def test_packed_upload_scatters_segments(gpu):
     """ops/staging.PackedUpload: the used rows of several pinned buffers (int32, fp32, int64,
-    2-D rows, a ragged word count) reach their device buffers through one copy + one scatter
-    kernel, rows past `rows` untouched; both staging halves in turn; oversize rows refused."""
+    2-D rows, a ragged word count) reach their device buffers through one scatter kernel that
+    reads the mapped host staging in place, rows past `rows` untouched; both staging halves in
+    turn; oversize rows refused. Then three uploads queued behind a busy stream, the sources
+    rewritten after each: the third reuses the first's staging half only after the first
+    kernel has read it."""
     from nv_genai_amd.ops.staging import PackedUpload
 
     g = torch.Generator().manual_seed(3)
@@ -881,3 +884,13 @@ def test_packed_upload_scatters_segments(gpu):
     assert up.uploads == 2
     with pytest.raises(ValueError):
         up.upload([(hs[0], ds[0], 1001)])
+    want = []
+    torch.cuda._sleep(20_000_000)
+    for i in range(3):
+        for h in hs:
+            h.copy_(torch.randint(-1000, 1000, h.shape, generator=g).to(h.dtype))
+        want.append(hs[i][:5].clone())
+        up.upload([(hs[i], ds[i], 5)])
+    torch.cuda.synchronize()
+    for i in range(3):
+        assert torch.equal(ds[i][:5].cpu(), want[i]), i
