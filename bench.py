@@ -78,6 +78,8 @@ def parse(argv=None):
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    ap.add_argument("--timeline-out", default=None,
+                    help="write the engine's last 4,096 scheduler steps (kind, rows, tokens, decode rows) here")
     ap.add_argument("--no-step-timing", dest="step_timing", action="store_false",
                     help="skip the GPU events around every engine step (in-step time vs idle between "
                          "steps, reported as gpu_step_timing; on by default, two event records per step)")
@@ -602,6 +604,9 @@ def main(argv=None):
         if args.out:
             with open(args.out, "w") as f:
                 f.write(s + "\n")
+        if args.timeline_out:
+            with open(args.timeline_out, "w") as f:
+                json.dump(llm.timeline(4096), f)
     pd.destroy()
 
 

@@ -81,6 +81,41 @@ def test_scheduler_prefix_cache_hit_and_preemption():
     assert s2.preemptions() >= 1
 
 
+def test_scheduler_token_alignment_leaves_no_short_tail():
+    """Mixed steps round their token count down to the alignment by shortening the last prefill
+    chunk, but not when that would leave its prompt a tail shorter than one alignment unit (the
+    old rule then fed such a tail 256 - nd tokens a step). 6 decode rows + a 13-token prompt at
+    alignment 8 run as one 19-token step; a 40-token prompt under a 26-token budget beside 7
+    decode rows is cut to 25 (32 tokens, its 15-token rest >= 8), and the rest then runs whole
+    (22 tokens: aligning to 16 would leave a 6-token tail)."""
+    s = rt.Scheduler(64, 16, 8, 256, 256, False)
+    s.set_mixed_prefill_tokens(64)
+    s.set_token_alignment(8)
+    b = _bufs()
+    for i in range(6):
+        s.add(i + 1, [10 + i] * 4, 8)
+    kind, n, ntok = s.schedule(*b)
+    assert kind == 1 and ntok == 24
+    for i in range(6):
+        s.append_token(i + 1, 1)
+    s.add(9, list(range(1, 14)), 8)
+    kind, n, ntok = s.schedule(*b)
+    assert kind == 3 and n == 7 and ntok == 19 and s.last_num_decode() == 6
+    ids, pos, sl, cu, ctx, bt, sid, smp = b
+    assert sid[6] == 9 and smp[6] == 1 and ctx[6] == 13
+    for i in range(6):
+        s.append_token(i + 1, 1)
+    s.append_token(9, 1)
+    s.set_mixed_prefill_tokens(26)
+    s.add(10, list(range(1, 41)), 8)
+    kind, n, ntok = s.schedule(*b)
+    assert kind == 3 and ntok == 32 and s.last_num_decode() == 7   # 7 decode + 25, aligned to 32
+    for i in list(range(1, 7)) + [9]:
+        s.append_token(i, 1)
+    kind, n, ntok = s.schedule(*b)
+    assert kind == 3 and ntok == 7 + 15                             # the 15-token rest, kept whole
+
+
 def test_bm25_ranking_and_delete():
     b = rt.BM25Index()
     b.add(1, "the mi355x gpu has 288 gb of hbm3e memory")
