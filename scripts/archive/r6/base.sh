@@ -2,7 +2,7 @@
 # Round 6 baseline: the whole GPU test suite, then the driver's bench configuration and the
 # 256 x 1,400 decode step on this box.
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_base}
 mkdir -p $out
 export PYTHONUNBUFFERED=1

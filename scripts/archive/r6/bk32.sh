@@ -2,7 +2,7 @@
 # Round 6: the 32-deep-stage decode-shape GEMM tiles (cfgs 17-21): numerics of every cfg, then
 # each llama3-8b projection at M = 128-256 with its consumer, every (cfg, split) printed
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_bk32}
 mkdir -p $out
 export PYTHONUNBUFFERED=1

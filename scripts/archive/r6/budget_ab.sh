@@ -2,7 +2,7 @@
 # Round 6: mixed-step prefill budget (--mixed-prefill-tokens) with the no-short-tail alignment,
 # interleaved on one box: headline (8 steps)
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_budget}
 mkdir -p $out
 export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD

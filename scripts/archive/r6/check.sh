@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6: smoke(), the packed-upload / TP / TP=8 GPU tests, and the 256 x 1,400 decode step
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_check}
 mkdir -p $out
 export PYTHONUNBUFFERED=1

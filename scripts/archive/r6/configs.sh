@@ -3,7 +3,7 @@
 # the agent with Llama-3-8B over a 10M-vector index, the REST path in the reference's split
 # topology. Mode "70b": the agent with Llama-3-70B at TP = 1.
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/${1:-r6_configs}; mkdir -p $O
 export PYTHONUNBUFFERED=1
 val() { python3 -c "import json;d=json.load(open('$1'));print(d['value'], d.get('p50_latency_ms'), d.get('p50_ttft_ms', ''))"; }

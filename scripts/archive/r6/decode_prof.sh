@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6: kernel table of the 256 x 1,400 decode step (graph replays)
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 R=$PWD
 out=gpurun_out/${1:-r6_decode_prof}
 mkdir -p $out

@@ -2,7 +2,7 @@
 # Round 6: step-graph token bucket granularity (--graph-token-step 256 default vs 128) with the
 # no-short-tail alignment, interleaved on one box: headline (8 steps)
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_gts}
 mkdir -p $out
 export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD

@@ -4,11 +4,11 @@
 # and engine GPU tests, then interleaved against per-buffer copies (NGA_PACKED_UPLOAD=0): the
 # 256 x 1,400 decode step and the headline (8 steps)
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_h2d}
 mkdir -p $out
 export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD
-timeout -k 10 200 python -u scripts/r6/h2d_probe.py > $out/probe.log 2>&1 || { tail -20 $out/probe.log; exit 1; }
+timeout -k 10 200 python -u scripts/dev/h2d_probe.py > $out/probe.log 2>&1 || { tail -20 $out/probe.log; exit 1; }
 tail -1 $out/probe.log > $out/probe.json
 timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_engine_gpu.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -rf > $out/pytest_gpu.log 2>&1 || { tail -30 $out/pytest_gpu.log; exit 1; }
 tail -2 $out/pytest_gpu.log

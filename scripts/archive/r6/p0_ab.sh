@@ -3,7 +3,7 @@
 # policy (shared prompt-template page, L2 hits) vs nt everywhere: numerics, then interleaved
 # headline (8 steps) and the decode step
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_p0}
 mkdir -p $out
 export PYTHONUNBUFFERED=1

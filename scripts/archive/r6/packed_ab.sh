@@ -3,7 +3,7 @@
 # per-buffer copies (NGA_PACKED_UPLOAD=0), interleaved on one box: headline (8 steps) and the
 # 256 x 1,400 decode step
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_packed}
 mkdir -p $out
 export PYTHONUNBUFFERED=1

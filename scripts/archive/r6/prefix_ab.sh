@@ -4,7 +4,7 @@
 # engine, then interleaved on one box against NGA_DECODE_PREFIX=0: the 256 x 1,400 decode step
 # with a 133-token shared prompt head (the RAG template), and the headline (8 steps)
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_prefix}
 mkdir -p $out
 export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD

@@ -3,7 +3,7 @@
 # Round 6: kernel times of the shared-prefix decode pass: rocprofv3 kernel trace of the
 # 256 x 1,400 decode step with a 133-token shared head, prefix pass on and off
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_prefix_prof}
 mkdir -p $out
 export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD TMPDIR=/tmp

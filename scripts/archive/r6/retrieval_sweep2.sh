@@ -2,7 +2,7 @@
 # Round 6: retrieval batching (--retrieval-batch queries per embedding + search launch,
 # --retrieval-delay-ms max wait for the batch to fill), interleaved on one box: headline (8 steps)
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_retrieval2}
 mkdir -p $out
 export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6: the whole GPU test suite (every failure listed)
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_suite}
 mkdir -p $out
 export PYTHONUNBUFFERED=1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6: the TP = 8 one-GPU rehearsal tests (8 ranks on cuda:0)
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_tp8}
 mkdir -p $out
 export PYTHONUNBUFFERED=1

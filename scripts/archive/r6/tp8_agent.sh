@@ -4,7 +4,7 @@
 # (queries in the step-channel command + one IPC all-gather) against the round-5 one
 # (broadcast + process-group gathers), then bench.py's record of the same job
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_tp8_agent}
 mkdir -p $out
 export PYTHONUNBUFFERED=1 GPU_MAX_HW_QUEUES=2

@@ -2,7 +2,7 @@
 # Round 6: the TP = 8 rehearsal tests (with wake-up stats) + the 8-rank sharded search test,
 # then RAG with a TP = 2 replica and its sharded index (searches on the retrieval stream)
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 out=gpurun_out/${1:-r6_tp8b}
 mkdir -p $out
 export PYTHONUNBUFFERED=1

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 6: what the driver runs at round end, on this tree: smoke(), the whole GPU test suite,
-# and bench.py at the driver's configuration (20 steps, 5 warm-up)
+# What the round driver runs at round end, on this tree: smoke(), the whole GPU test suite, and
+# bench.py at the driver's configuration (20 steps, 5 warm-up). Usage: gpu_endcheck.sh [out-name]
 set -o pipefail
-cd "$(dirname "$0")/../.."
-out=gpurun_out/${1:-r6_endcheck}
+cd "$(dirname "$0")/.."
+out=gpurun_out/${1:-endcheck}
 mkdir -p $out
 export PYTHONUNBUFFERED=1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { tail -20 $out/smoke.log; exit 1; }
