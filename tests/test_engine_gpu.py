@@ -337,6 +337,10 @@ def test_step_graphs_headline_gqa_4096_bucket(gpu, gqa_weights, pf_seq_min, monk
     _same_greedy_run(outs[True], outs[False])
 
 
+def _near_tie(x: float, y: float) -> bool:
+    return -1.5 <= x <= -0.4 and -1.5 <= y <= -0.4
+
+
 def _same_greedy_run(ga, eg, lp_tol=0.25):
     """Graphed vs eager greedy generations: the first token of every request (its prefill /
     mixed-step output) equal; then equal tokens with log-probs within ``lp_tol`` up to a
@@ -347,21 +351,31 @@ def _same_greedy_run(ga, eg, lp_tol=0.25):
     A smoke check only: the numerics are pinned by the teacher-forced logit comparisons
     (test_teacher_forced_*), which feed both runs the same token histories. ``lp_tol``: with
     the x40 test head the graphed (bucket-padded GEMMs) and eager runs differ by up to 0.18
-    nats before any divergence (profiles/r5_numerics/), 0.1 fails on that alone."""
+    nats before any divergence (profiles/r5_numerics/), 0.1 fails on that alone. Near-tie
+    positions are exempt from it as from the token match: there the x40 head turns a 1 %
+    logit difference into up to 1.8 nats (the teacher-forced tests' max |log-prob delta|), e.g.
+    -0.55 vs -0.94 for the same token in the skinny vs library run (profiles/r6_endcheck2/)."""
     diverged = []
     worst = 0.0
+    ties = 0
     for i, ((a, la), (b, lb)) in enumerate(zip(ga, eg)):
         assert a[0] == b[0], (i, a[:3], b[:3], la[:3], lb[:3])
         d = next((j for j, (x, y) in enumerate(zip(a, b)) if x != y), None)
         upto = len(a) if d is None else d
-        delta = max(abs(x - y) for x, y in zip(la[:upto], lb[:upto]))
+        # a near-tie position (both runs unsure: log-probs in [-1.5, -0.4]) may move its
+        # probability between the two candidates as freely as it may flip the choice
+        deltas = [0.0 if _near_tie(x, y) else abs(x - y) for x, y in zip(la[:upto], lb[:upto])]
+        ties += sum(1 for x, y in zip(la[:upto], lb[:upto]) if _near_tie(x, y) and abs(x - y) >= lp_tol)
+        j = max(range(len(deltas)), key=deltas.__getitem__)
+        delta = deltas[j]
         worst = max(worst, delta)
-        assert delta < lp_tol, (i, la[:upto], lb[:upto])
+        assert delta < lp_tol, f"request {i}: log-prob delta {delta:.4f} at token {j} ({la[j]:.4f} vs {lb[j]:.4f}; "\
+                               f"tokens {a[j]} / {b[j]}; first divergence {d})"
         if d is not None:
-            assert all(-1.5 <= v <= -0.4 for v in (la[d], lb[d])), ("divergence without a near-tie", i, d, la[d], lb[d])
+            assert _near_tie(la[d], lb[d]), ("divergence without a near-tie", i, d, la[d], lb[d])
             diverged.append(i)
-    print(f"greedy smoke check: {len(ga)} requests, max log-prob delta before divergence {worst:.4f}, "
-          f"diverged at a near-tie: {diverged}")
+    print(f"greedy smoke check: {len(ga)} requests, max log-prob delta before divergence {worst:.4f} "
+          f"(near-tie positions above {lp_tol}: {ties}), diverged at a near-tie: {diverged}")
     assert len(diverged) <= max(1, len(ga) // 4), diverged
 
 
@@ -403,7 +417,6 @@ def test_skinny_gemm_path_matches_library_path(gpu, weights, tmp_path, monkeypat
         hs = torch.randn(3, e.model.cfg.hidden, generator=torch.Generator().manual_seed(1)).to("cuda", torch.bfloat16)
         res[on + "lg"] = e.model.logits(hs).float()
     assert torch.allclose(res["1lg"], res["0lg"], rtol=0.02, atol=0.05 * float(res["0lg"].abs().max()))
-    _same_greedy_run(res["1"], res["0"])
 
     # the numerics pin: the same token histories through the skinny path (graphed decode and
     # mixed steps) and the library path (eager), teacher-forced, fp32 logits per row at bf16
@@ -416,6 +429,7 @@ def test_skinny_gemm_path_matches_library_path(gpu, weights, tmp_path, monkeypat
         return e
 
     _assert_logits_close(*_teacher_forced_logits(make, PROMPTS[:2], PROMPTS[2:], 16))
+    _same_greedy_run(res["1"], res["0"])
 
 
 def test_step_graph_capture_beside_reward_thread(gpu, weights):
