@@ -63,18 +63,21 @@ def test_http_rag_benchmark_split_topology_cpu(tmp_path):
     assert "ttft" in res["model_server_p50_ms"], res["model_server_p50_ms"]   # the model server's own phases
 
 
-def test_headline_bench_two_ranks_gloo():
+def test_headline_bench_two_ranks_gloo(tmp_path):
     """bench.py under torch.distributed.run with 2 ranks (gloo on CPU, the driver's N>1 launch):
-    exactly one JSON line, from rank 0, with the whole-job value over both replicas."""
+    exactly one JSON line, from rank 0, with the whole-job value over both replicas; rank 0's
+    step timeline (--timeline-out) and its composition through scripts/steps_probe.py."""
     import socket
 
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
+    tl = tmp_path / "timeline.json"
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                         "--master-addr=127.0.0.1", f"--master-port={port}", "bench.py", "--gpus", "2",
                         "--steps", "1", "--warmup", "1", "--model", "llama-tiny", "--embed-model", "encoder-tiny",
-                        "--index-size", "2000", "--concurrency", "3", "--max-tokens", "4"],
+                        "--index-size", "2000", "--concurrency", "3", "--max-tokens", "4",
+                        "--timeline-out", str(tl)],
                        capture_output=True, text=True, timeout=400,
                        env=dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=os.getcwd()))
     assert r.returncode == 0, r.stderr[-3000:]
@@ -87,6 +90,13 @@ def test_headline_bench_two_ranks_gloo():
     assert abs(res["value"] - 6 / (res["ms_per_step"] / 1000)) / res["value"] < 0.01
     for k in ("metric", "unit", "higher_is_better", "scaling", "vs_baseline", "dtype", "data"):
         assert k in res
+    steps = json.loads(tl.read_text())
+    assert steps and {"kind", "rows", "tokens", "decode_rows"} <= set(steps[0])
+    assert sum(1 for st in steps if st["kind"] == "decode") > 0
+    p = subprocess.run([sys.executable, "scripts/steps_probe.py", str(tl)], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    comp = json.loads(p.stdout)
+    assert comp["decode"]["steps"] > 0
 
 
 def test_headline_bench_self_launches_for_gpus_n():
