@@ -392,7 +392,8 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(const float* _
   X(23, 128, 128, 2, 4, 4, 32)  \
   X(24, 256, 128, 4, 2, 2, 32)  \
   X(25, 256, 128, 2, 4, 3, 32)  \
-  X(26, 128, 256, 2, 4, 3, 32)
+  X(26, 128, 256, 2, 4, 3, 32)  \
+  X(27, 224, 128, 1, 4, 3, 64)
 
 int skinny_gemm_cfg_count() {
   int n = 0;

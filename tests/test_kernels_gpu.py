@@ -707,6 +707,9 @@ def test_skinny_gemm_every_cfg(gpu, M):
     w = _bf(1000, K, dev=gpu, scale=0.05)
     wg = _bf(2 * 512, K, dev=gpu, scale=0.05)
     ref0, ref2 = _skinny_ref(x, w, 0), _skinny_ref(x, wg, 2)
+    # SwiGLU for tiles whose BN / 2 does not divide 512 (BN 224: 112 features per block)
+    wg7 = _bf(2 * 448, K, dev=gpu, scale=0.05)
+    ref7 = _skinny_ref(x, wg7, 2)
     for cfg in range(C.skinny_cfg_count()):
         BN, BM = C.skinny_cfg(cfg)[:2]
         BK = C.skinny_cfg(cfg)[5]     # 64, or 32 (64-B LDS rows, twice the stages per KiB)
@@ -715,13 +718,14 @@ def test_skinny_gemm_every_cfg(gpu, M):
             P = ops.skinny_gemm(x, w, cfg, s, 1)
             _close_rows(P.sum(0), ref0, rel=1e-4)
             _close_rows(ops.splitk_reduce(P), ref0, rel=1e-2)
-        if 512 % (BN // 2) == 0:
-            y2 = ops.skinny_gemm(x, wg, cfg, 1, 2)
-            _close_rows(y2, ref2, rel=2e-2)
+        F, wgc, refc = (512, wg, ref2) if 512 % (BN // 2) == 0 else (448, wg7, ref7)
+        if F % (BN // 2) == 0:
+            y2 = ops.skinny_gemm(x, wgc, cfg, 1, 2)
+            _close_rows(y2, refc, rel=2e-2)
             # tile-packed weights and the rotated K walk: the same products (fp32 sums in
             # another order for krot)
             if BK == 64:
-                assert torch.equal(ops.skinny_gemm(x, ops.pack_weight(wg, BN, 2), cfg, 1, 2, n_out=512), y2)
+                assert torch.equal(ops.skinny_gemm(x, ops.pack_weight(wgc, BN, 2), cfg, 1, 2, n_out=F), y2)
         if BK != 64:   # packed operands are 64-deep tiles: refused for BK 32 tiles
             with pytest.raises(RuntimeError, match="packed operands"):
                 ops.skinny_gemm(x, ops.pack_weight(w, BN), cfg, 1, 0, n_out=1000)
